@@ -1,0 +1,476 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures by running the REAL reference (/root/reference) on CPU.
+
+TEST INFRASTRUCTURE ONLY.  Runs in the survey/dev container (where /root/reference exists);
+the GPU box never runs this.  It imports the reference in place (no source is copied),
+with the stand-ins of oracle/ref_stubs.py for packages that are absent here, and writes
+small data fixtures (inputs + expected outputs) under tests/golden/.
+
+    python oracle/gen_goldens.py all        # everything below
+    python oracle/gen_goldens.py llm ops codec codec_full llm_wide
+
+Reference call sites exercised (file:line in /root/reference):
+  * BaseModelArgs.from_pretrained / _from_fish_qwen3_omni     llama.py:75-143
+  * _remap_fish_qwen3_omni_keys, Attention.load_hook (wq/wk/wv) llama.py:229-246, 876-881
+  * generate / decode_one_token_ar / decode_n_tokens (top_k=1) inference.py:96-359
+  * forward_generate / forward_generate_fast (teacher forcing)  llama.py:390-466, 798-827
+  * RMSNorm, nn.RMSNorm (qk-norm), precompute_freqs_cis,
+    apply_rotary_emb                                            llama.py:989-1037
+  * logits_to_probs                                             inference.py:54-77
+  * DAC.from_indices -> DownsampleResidualVectorQuantize.decode
+    -> WindowLimitedTransformer -> upsample -> Decoder          modded_dac.py:925-927, rvq.py:352-366
+  * causal-prefix property of the codec (rvq.py:374-398 style)
+"""
+from __future__ import annotations
+
+import functools
+import json
+import os
+import sys
+import time
+from collections import OrderedDict
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+GOLD = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(REPO, "fish-speech_amd"))
+
+import ref_stubs  # noqa: E402
+
+ref_stubs.install()
+
+import torch  # noqa: E402
+from safetensors.torch import save_file  # noqa: E402
+
+from fishmi import synth  # noqa: E402
+
+torch.set_num_threads(8)
+IM_END_ID = 4
+
+
+class StubTokenizer:
+    """Only what generate()/decode_n_tokens() call: get_token_id(IM_END_TOKEN)."""
+
+    def get_token_id(self, tok):
+        assert tok == "<|im_end|>"
+        return IM_END_ID
+
+
+def bf16_tensor(x_f32: np.ndarray, shape) -> torch.Tensor:
+    bits = synth.f32_to_bf16_bits(x_f32.reshape(-1))
+    return torch.from_numpy(bits.view(np.int16).copy()).view(torch.bfloat16).reshape(shape)
+
+
+def synth_state(keys_shapes, seed, rule):
+    out = OrderedDict()
+    for k, shape in keys_shapes:
+        n = int(np.prod(shape))
+        c, e = rule(k)
+        out[k] = bf16_tensor(synth.synth_f32(seed, k, n, c, e), shape)
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# Dual-AR LLM
+# --------------------------------------------------------------------------------------
+LLM_A_CONFIG = {
+    "model_type": "fish_qwen3_omni",
+    "text_config": {
+        "vocab_size": 512, "n_layer": 4, "n_head": 4, "n_local_heads": 2, "head_dim": 32,
+        "dim": 128, "intermediate_size": 256, "rope_base": 1000000, "norm_eps": 1e-6,
+        "max_seq_len": 256, "tie_word_embeddings": True, "attention_qkv_bias": False,
+        "attention_o_bias": False, "attention_qk_norm": True,
+    },
+    "audio_decoder_config": {
+        "vocab_size": 128, "num_codebooks": 10, "n_layer": 2, "dim": 128, "n_head": 4,
+        "n_local_heads": 2, "head_dim": 32, "intermediate_size": 256,
+    },
+    "semantic_start_token_id": 200,
+    "semantic_end_token_id": 327,
+}
+
+LLM_B_CONFIG = {
+    "model_type": "dual_ar",
+    "vocab_size": 400, "n_layer": 3, "n_head": 4, "n_local_heads": 1, "head_dim": 32,
+    "dim": 128, "intermediate_size": 320, "rope_base": 10000, "norm_eps": 1e-5,
+    "max_seq_len": 192, "tie_word_embeddings": False, "attention_qkv_bias": True,
+    "attention_o_bias": True, "attention_qk_norm": False, "codebook_size": 64,
+    "num_codebooks": 6, "semantic_begin_id": 300, "semantic_end_id": 363,
+    "n_fast_layer": 2, "fast_dim": 96, "fast_n_head": 3, "fast_n_local_heads": 1,
+    "fast_head_dim": 32, "fast_intermediate_size": 192, "scale_codebook_embeddings": False,
+    "norm_fastlayer_input": False,
+}
+
+
+def to_qwen3_omni_key(k: str) -> str:
+    """Inverse of llama.py:229-246 _remap_fish_qwen3_omni_keys (to store fixtures the
+    way an S2-Pro checkpoint stores them)."""
+    if k.startswith("codebook_embeddings."):
+        return "audio_decoder." + k
+    if k.startswith("fast_"):
+        return "audio_decoder." + k[len("fast_"):]
+    return "text_model.model." + k
+
+
+def build_llm(config: dict, weights_dir: str | None, seed: int, log2_half: int):
+    from fish_speech.models.text2semantic import llama
+
+    cfg_path = os.path.join(weights_dir or "/tmp/fishmi_cfg", "config.json")
+    os.makedirs(os.path.dirname(cfg_path), exist_ok=True)
+    with open(cfg_path, "w") as f:
+        json.dump(config, f, indent=1)
+    cfg = llama.BaseModelArgs.from_pretrained(cfg_path)
+    torch.manual_seed(0)
+    model = llama.DualARTransformer(cfg)
+    keys = [(k, tuple(v.shape)) for k, v in model.state_dict().items()]
+    state = synth_state(keys, seed, functools.partial(synth.llm_rule, log2_half_linear=log2_half))
+    if weights_dir is not None:
+        # store as an S2-Pro style checkpoint: qwen3-omni key layout, 2 shards + index,
+        # and layer 0's attention split into wq/wk/wv (exercises Attention.load_hook).
+        stored = OrderedDict()
+        for k, v in state.items():
+            if k == "layers.0.attention.wqkv.weight":
+                qs = cfg.n_head * cfg.head_dim
+                ks = cfg.n_local_heads * cfg.head_dim
+                stored[to_qwen3_omni_key("layers.0.attention.wq.weight")] = v[:qs].contiguous()
+                stored[to_qwen3_omni_key("layers.0.attention.wk.weight")] = v[qs:qs + ks].contiguous()
+                stored[to_qwen3_omni_key("layers.0.attention.wv.weight")] = v[qs + ks:].contiguous()
+            else:
+                stored[to_qwen3_omni_key(k)] = v
+        names = list(stored)
+        half = len(names) // 2
+        shards = {"model-00001-of-00002.safetensors": names[:half],
+                  "model-00002-of-00002.safetensors": names[half:]}
+        wmap = {}
+        for fn, ns in shards.items():
+            save_file({n: stored[n] for n in ns}, os.path.join(weights_dir, fn))
+            wmap.update({n: fn for n in ns})
+        with open(os.path.join(weights_dir, "model.safetensors.index.json"), "w") as f:
+            json.dump({"metadata": {}, "weight_map": wmap}, f, indent=1)
+        # load back exactly the way from_pretrained does (llama.py:550-586)
+        from safetensors.torch import load_file
+
+        loaded = OrderedDict()
+        for fn in sorted(set(wmap.values())):
+            loaded.update(load_file(os.path.join(weights_dir, fn), device="cpu"))
+        loaded = llama._remap_fish_qwen3_omni_keys(loaded)
+        err = model.load_state_dict(loaded, strict=False, assign=True)
+    else:
+        err = model.load_state_dict(state, strict=False, assign=True)
+    assert not err.missing_keys and not err.unexpected_keys, err
+    model.tokenizer = StubTokenizer()
+    return model.eval()
+
+
+def make_prompt(cfg, T: int, seed: int) -> torch.Tensor:
+    """(C+1, T) int64 prompt: text tokens, an im_start, a run of semantic frames with codes,
+    and more text (covers the codebook-embedding branch in prefill, llama.py:399-420)."""
+    rng = np.random.default_rng(seed)
+    C = cfg.num_codebooks
+    p = np.zeros((C + 1, T), dtype=np.int64)
+    p[0] = rng.integers(16, cfg.semantic_begin_id, size=T)
+    p[0, 0] = 1
+    s0, s1 = T // 3, T // 3 + max(3, T // 4)
+    codes0 = rng.integers(0, cfg.codebook_size, size=s1 - s0)
+    p[0, s0:s1] = cfg.semantic_begin_id + codes0
+    p[1, s0:s1] = codes0
+    p[2:, s0:s1] = rng.integers(0, cfg.codebook_size, size=(C - 1, s1 - s0))
+    p[0, s1] = IM_END_ID
+    return torch.from_numpy(p)
+
+
+def teacher_forced(model, seq: torch.Tensor, T: int, nsteps: int, dtype):
+    """Per-frame slow logits (+ semantic bias) and fast logits, replaying decode_one_token_ar
+    (inference.py:96-181) with the reference's own emitted columns as the sampled tokens."""
+    from torch.nn.attention import SDPBackend, sdpa_kernel
+
+    cfg = model.config
+    C, V, cb = cfg.num_codebooks, cfg.vocab_size, cfg.codebook_size
+    model._cache_setup_done = False
+    model.setup_caches(1, cfg.max_seq_len, dtype=dtype)
+    with torch.inference_mode():  # zero the caches left by the free-running generate()
+        for b in list(model.layers) + list(model.fast_layers):
+            b.attention.kv_cache.k_cache.zero_()
+            b.attention.kv_cache.v_cache.zero_()
+    bias = torch.full((1, 1, V), float("-inf"), dtype=dtype)
+    bias[0, 0, cfg.semantic_begin_id: cfg.semantic_end_id + 1] = 0.0
+    bias[0, 0, IM_END_ID] = 0.0
+    slow_all, fast_all, hid_all = [], [], []
+    x = seq[:, :T].view(1, C + 1, T)
+    pos = torch.arange(T)
+    for i in range(nsteps):
+        col = seq[:, T + i]
+        ctx = sdpa_kernel(SDPBackend.MATH) if i > 0 else _nullctx()
+        with ctx, torch.inference_mode():
+            fr = model.forward_generate(x, pos)
+            slow = (fr.logits + bias)[0, -1].float().numpy().copy()
+            h = fr.hidden_states
+            hid_all.append(h.reshape(-1).float().numpy().copy())
+            model.forward_generate_fast(h, torch.tensor([0]))
+            a = torch.clamp(col[0:1] - cfg.semantic_begin_id, 0, cb - 1)
+            hs = model.fast_embeddings(a)
+            fl = []
+            for c in range(1, C):
+                lg = model.forward_generate_fast(hs, torch.tensor([c]))
+                fl.append(lg.reshape(-1).float().numpy().copy())
+                hs = model.fast_embeddings(col[c + 1: c + 2])
+        slow_all.append(slow)
+        fast_all.append(np.stack(fl))
+        x = col.view(1, C + 1, 1)
+        pos = torch.tensor([T + i])
+    return np.stack(slow_all), np.stack(fast_all), np.stack(hid_all)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def run_llm_case(name, config, weights_dir, seed, log2_half, T, n_new, dtypes, prompt_seed):
+    from fish_speech.models.text2semantic import inference
+
+    for dtype in dtypes:
+        model = build_llm(config, weights_dir, seed, log2_half).to(dtype)
+        cfg = model.config
+        prompt = make_prompt(cfg, T, prompt_seed)
+        t0 = time.time()
+        seq = inference.generate(model=model, prompt=prompt.clone(), max_new_tokens=n_new,
+                                 audio_masks=None, audio_parts=None, temperature=0.7,
+                                 top_p=0.9, top_k=1)
+        n = seq.shape[1] - T
+        slow, fast, hid = teacher_forced(model, seq, T, n, dtype)
+        tag = {torch.float32: "fp32", torch.bfloat16: "bf16"}[dtype]
+        out = os.path.join(GOLD, f"{name}_{tag}.npz")
+        np.savez_compressed(out, prompt=prompt.numpy().astype(np.int32),
+                            seq=seq.numpy().astype(np.int32), slow_logits=slow,
+                            fast_logits=fast, hidden=hid, synth_seed=seed,
+                            log2_half=log2_half, torch_version=torch.__version__,
+                            threads=torch.get_num_threads())
+        print(f"{name} {tag}: T={T} generated {n} frames in {time.time() - t0:.1f}s -> {out}")
+        print("  first columns:", seq[:, T:T + 3].T.tolist())
+
+
+def cmd_llm():
+    wdir = os.path.join(GOLD, "llm_a")
+    os.makedirs(wdir, exist_ok=True)
+    run_llm_case("llm_a", LLM_A_CONFIG, wdir, seed=11, log2_half=3, T=24, n_new=32,
+                 dtypes=[torch.float32, torch.bfloat16], prompt_seed=1)
+    bdir = os.path.join(GOLD, "llm_b")
+    os.makedirs(bdir, exist_ok=True)
+    with open(os.path.join(bdir, "config.json"), "w") as f:
+        json.dump(LLM_B_CONFIG, f, indent=1)
+    run_llm_case("llm_b", LLM_B_CONFIG, None, seed=23, log2_half=3, T=17, n_new=24,
+                 dtypes=[torch.float32, torch.bfloat16], prompt_seed=2)
+
+
+# --------------------------------------------------------------------------------------
+# Per-op goldens
+# --------------------------------------------------------------------------------------
+def cmd_ops():
+    from fish_speech.models.text2semantic import inference, llama
+
+    rng = np.random.default_rng(5)
+    out = {}
+    # RMSNorm (llama.py:989-1000): fp32 normalise, round to bf16, * bf16 weight
+    x = torch.from_numpy(rng.normal(0, 3, (6, 256)).astype(np.float32)).bfloat16()
+    m = llama.RMSNorm(256, eps=1e-6)
+    m.weight.data = torch.from_numpy(rng.normal(1, 0.2, 256).astype(np.float32)).bfloat16()
+    with torch.no_grad():
+        out["rms_x"], out["rms_w"], out["rms_y"] = x.float(), m.weight.float(), m(x).float()
+    # qk-norm nn.RMSNorm(head_dim) on bf16 (llama.py:861-863)
+    q = torch.from_numpy(rng.normal(0, 2, (2, 3, 4, 64)).astype(np.float32)).bfloat16()
+    qn = torch.nn.RMSNorm(64, 1e-6).bfloat16()
+    qn.weight.data = torch.from_numpy(rng.normal(1, 0.2, 64).astype(np.float32)).bfloat16()
+    with torch.no_grad():
+        out["qk_x"], out["qk_w"], out["qk_y"] = q.float(), qn.weight.float(), qn(q).float()
+    # RoPE (llama.py:1003-1037)
+    fc = llama.precompute_freqs_cis(64, 32, 10000)
+    out["rope_table"] = fc.float()
+    xr = torch.from_numpy(rng.normal(0, 1, (1, 5, 4, 32)).astype(np.float32)).bfloat16()
+    pos = torch.tensor([0, 3, 17, 40, 63])
+    out["rope_pos"] = pos.to(torch.int32)
+    out["rope_x"] = xr.float()
+    out["rope_y"] = llama.apply_rotary_emb(xr, fc[pos]).float()
+    fc2 = llama.precompute_freqs_cis(4096, 128, 1000000)
+    out["rope_table_big"] = fc2[::97].float()
+    # logits_to_probs (inference.py:54-77) with bf16 temperature / top_p tensors
+    cases = [(0.7, 0.9, 30), (1.0, 0.9, 30), (0.7, 0.5, 5), (0.7, 0.9, 1), (0.3, 0.99, 64),
+             (1.0, 0.9, 30)]
+    lp_in, lp_out, lp_par = [], [], []
+    for ci, (t, p, k) in enumerate(cases):
+        lg = rng.normal(0, 2.0, 300).astype(np.float32)
+        lg[rng.integers(0, 300, 8)] = lg.max()          # ties at the top
+        if ci == 5:
+            lg[:100] = -np.inf                           # constrained-bias style row
+        lgt = torch.from_numpy(lg).bfloat16()
+        probs = inference.logits_to_probs(lgt, torch.tensor(t).bfloat16(),
+                                          torch.tensor(p).bfloat16(), k)
+        lp_in.append(lgt.float().numpy())
+        lp_out.append(probs.float().numpy())
+        lp_par.append([t, p, k])
+    out["lp_logits"] = np.stack(lp_in)
+    out["lp_probs"] = np.stack(lp_out)
+    out["lp_params"] = np.array(lp_par, dtype=np.float64)
+    # argmax tie order of sample() under top_k=1 (sort order of ties)
+    lg = torch.zeros(64).bfloat16()
+    lg[[5, 9, 40]] = 3.0
+    idx, _ = inference.sample(lg.view(1, 1, -1), torch.tensor(0.7).bfloat16(),
+                              torch.tensor(0.9).bfloat16(), 1)
+    out["tie_logits"] = lg.float()
+    out["tie_idx"] = idx.to(torch.int32)
+    np.savez_compressed(os.path.join(GOLD, "ops.npz"),
+                        **{k: (v.numpy() if torch.is_tensor(v) else v) for k, v in out.items()},
+                        torch_version=torch.__version__)
+    print("ops: tie idx", int(idx), "->", os.path.join(GOLD, "ops.npz"))
+
+
+# --------------------------------------------------------------------------------------
+# Codec (modded DAC decode)
+# --------------------------------------------------------------------------------------
+CODEC_TINY = dict(encoder_dim=8, latent=128, decoder_dim=64, n_codebooks=9, codebook_size=32,
+                  semantic_codebook_size=64, codebook_dim=8, t_layers=2, t_heads=2,
+                  t_head_dim=64, t_inter=384, window=16)
+CODEC_FULL = dict(encoder_dim=64, latent=1024, decoder_dim=1536, n_codebooks=9,
+                  codebook_size=1024, semantic_codebook_size=4096, codebook_dim=8,
+                  t_layers=8, t_heads=16, t_head_dim=64, t_inter=3072, window=128)
+
+
+def build_codec(spec: dict, seed: int):
+    from fish_speech.models.dac.modded_dac import DAC, ModelArgs, WindowLimitedTransformer
+    from fish_speech.models.dac.rvq import DownsampleResidualVectorQuantize
+
+    tcfg = ModelArgs(block_size=2048, n_layer=spec["t_layers"], n_head=spec["t_heads"],
+                     dim=spec["latent"], intermediate_size=spec["t_inter"], n_local_heads=-1,
+                     head_dim=spec["t_head_dim"], rope_base=10000, norm_eps=1e-5,
+                     dropout_rate=0.1, attn_dropout_rate=0.1, channels_first=True)
+    post = WindowLimitedTransformer(causal=True, window_size=spec["window"],
+                                    input_dim=spec["latent"], config=tcfg)
+    quant = DownsampleResidualVectorQuantize(
+        input_dim=spec["latent"], n_codebooks=spec["n_codebooks"],
+        codebook_size=spec["codebook_size"], codebook_dim=spec["codebook_dim"],
+        quantizer_dropout=0.5, downsample_factor=[2, 2], post_module=post, pre_module=None,
+        semantic_codebook_size=spec["semantic_codebook_size"])
+    gen = functools.partial(ModelArgs, block_size=8192, n_local_heads=-1, head_dim=64,
+                            rope_base=10000, norm_eps=1e-5, dropout_rate=0.1,
+                            attn_dropout_rate=0.1, channels_first=True)
+    dac = DAC(encoder_dim=spec["encoder_dim"], encoder_rates=[2, 4, 8, 8],
+              decoder_dim=spec["decoder_dim"], decoder_rates=[8, 8, 4, 2], quantizer=quant,
+              sample_rate=44100, causal=True, encoder_transformer_layers=[0, 0, 0, 0],
+              decoder_transformer_layers=[0, 0, 0, 0], transformer_general_config=gen)
+    sd = dac.state_dict()
+    keys = [(k, tuple(v.shape)) for k, v in sd.items()
+            if k.startswith("decoder.") or k.startswith("quantizer.")]
+    state = synth_state(keys, seed, synth.codec_rule)
+    state = OrderedDict((k, v.float()) for k, v in state.items())
+    err = dac.load_state_dict(state, strict=False)
+    assert not err.unexpected_keys, err.unexpected_keys
+    missing = [k for k in err.missing_keys if not k.startswith("encoder.")]
+    assert not missing, missing
+    return dac.eval()
+
+
+def codec_codes(spec, T, seed):
+    rng = np.random.default_rng(seed)
+    c = np.zeros((1, spec["n_codebooks"] + 1, T), dtype=np.int64)
+    c[0, 0] = rng.integers(0, spec["semantic_codebook_size"], T)
+    c[0, 1:] = rng.integers(0, spec["codebook_size"], (spec["n_codebooks"], T))
+    return c
+
+
+def run_codec(name, spec, seed, T, clamp_test: bool):
+    dac = build_codec(spec, seed)
+    codes = codec_codes(spec, T, seed + 1)
+    if clamp_test:  # out-of-range codes are clamped in place by rvq.py:354-359
+        codes[0, 0, 3] = spec["semantic_codebook_size"] + 9
+        codes[0, 2, 5] = spec["codebook_size"] + 3
+    res = {"codes": codes.astype(np.int32), "synth_seed": seed, "spec": json.dumps(spec),
+           "torch_version": torch.__version__}
+    with torch.inference_mode():
+        t0 = time.time()
+        y32 = dac.from_indices(torch.from_numpy(codes.copy()))
+        res["wave_fp32"] = y32.float().numpy()
+        dt = time.time() - t0
+        half = T // 2
+        yp = dac.from_indices(torch.from_numpy(codes[..., :half].copy()))
+        res["prefix_T"] = half
+        res["prefix_maxdiff"] = float((yp - y32[..., :yp.shape[-1]]).abs().max())
+        # intermediate: latent after RVQ decode + post transformer + upsample (B,1024,4T)
+        z = dac.quantizer.decode(torch.from_numpy(codes.copy()))
+        res["latent_fp32"] = z.float().numpy()
+        dac_bf = dac.to(torch.bfloat16)
+        ybf = dac_bf.from_indices(torch.from_numpy(codes.copy()))
+        res["wave_bf16"] = ybf.float().numpy()
+    np.savez_compressed(os.path.join(GOLD, f"{name}.npz"), **res)
+    print(f"{name}: T={T} -> {res['wave_fp32'].shape} fp32 {dt:.1f}s; prefix maxdiff "
+          f"{res['prefix_maxdiff']:.3g}; bf16-vs-fp32 rms "
+          f"{np.sqrt(np.mean((res['wave_bf16'] - res['wave_fp32'])**2)):.3g} "
+          f"(signal rms {np.sqrt(np.mean(res['wave_fp32']**2)):.3g})")
+
+
+def cmd_codec():
+    run_codec("codec_tiny", CODEC_TINY, seed=31, T=12, clamp_test=True)
+
+
+def cmd_codec_full():
+    run_codec("codec_full", CODEC_FULL, seed=37, T=4, clamp_test=False)
+
+
+# --------------------------------------------------------------------------------------
+# LLM at the real S2-Pro widths, reduced depth (synthetic weights, nothing committed but
+# the outputs).  Shapes per SURVEY.md §2.3.
+# --------------------------------------------------------------------------------------
+LLM_WIDE_CONFIG = {
+    "model_type": "fish_qwen3_omni",
+    "text_config": {
+        "vocab_size": 155776, "n_layer": 2, "n_head": 32, "n_local_heads": 8,
+        "head_dim": 128, "dim": 2560, "intermediate_size": 9728, "rope_base": 1000000,
+        "norm_eps": 1e-6, "max_seq_len": 64, "tie_word_embeddings": True,
+        "attention_qkv_bias": False, "attention_o_bias": False, "attention_qk_norm": True,
+    },
+    "audio_decoder_config": {
+        "vocab_size": 4096, "num_codebooks": 10, "n_layer": 1, "dim": 2560, "n_head": 32,
+        "n_local_heads": 8, "head_dim": 128, "intermediate_size": 9728,
+    },
+    "semantic_start_token_id": 151678,
+    "semantic_end_token_id": 155773,
+}
+
+
+def cmd_llm_wide():
+    os.makedirs(os.path.join(GOLD, "llm_wide"), exist_ok=True)
+    with open(os.path.join(GOLD, "llm_wide", "config.json"), "w") as f:
+        json.dump(LLM_WIDE_CONFIG, f, indent=1)
+    from fish_speech.models.text2semantic import inference
+
+    model = build_llm(LLM_WIDE_CONFIG, None, seed=41, log2_half=5).to(torch.bfloat16)
+    cfg = model.config
+    prompt = make_prompt(cfg, 16, 3)
+    t0 = time.time()
+    seq = inference.generate(model=model, prompt=prompt.clone(), max_new_tokens=4,
+                             audio_masks=None, audio_parts=None, temperature=0.7, top_p=0.9,
+                             top_k=1)
+    n = seq.shape[1] - 16
+    slow, fast, hid = teacher_forced(model, seq, 16, n, torch.bfloat16)
+    # keep the constrained rows only (semantic range + im_end); the rest are -inf
+    keep = np.r_[IM_END_ID, cfg.semantic_begin_id:cfg.semantic_end_id + 1]
+    np.savez_compressed(os.path.join(GOLD, "llm_wide_bf16.npz"),
+                        prompt=prompt.numpy().astype(np.int32), seq=seq.numpy().astype(np.int32),
+                        slow_rows=keep.astype(np.int32), slow_logits=slow[:, keep],
+                        fast_logits=fast, hidden=hid, synth_seed=41, log2_half=5,
+                        torch_version=torch.__version__, threads=torch.get_num_threads())
+    print(f"llm_wide: {n} frames in {time.time() - t0:.1f}s; first cols",
+          seq[:, 16:18].T.tolist())
+
+
+if __name__ == "__main__":
+    cmds = sys.argv[1:] or ["all"]
+    if cmds == ["all"]:
+        cmds = ["ops", "llm", "codec", "codec_full", "llm_wide"]
+    for c in cmds:
+        globals()[f"cmd_{c}"]()
