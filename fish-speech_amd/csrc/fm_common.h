@@ -1,0 +1,107 @@
+// fm_common.h -- shared device helpers for the gfx950 kernels of libfishmi.
+//
+// Precision model: every kernel is templated on the storage type T of activations and
+// weights: bf16_t (production) or float (fp32 validation mode).  Arithmetic is fp32; rnd<T>()
+// rounds to the storage type at the points where the reference rounds (identity for float).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
+
+template <typename T> struct is_bf16 { static constexpr bool value = false; };
+template <> struct is_bf16<bf16_t> { static constexpr bool value = true; };
+
+__device__ __forceinline__ float bf2f(bf16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
+
+// round-to-nearest-even fp32 -> bf16 bits, NaN stays NaN
+__device__ __forceinline__ bf16_t f2bf(float x) {
+    uint32_t u = __float_as_uint(x);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40u);
+    return (bf16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bfround(float x) { return bf2f(f2bf(x)); }
+
+template <typename T> __device__ __forceinline__ float rnd(float x) {
+    if constexpr (is_bf16<T>::value) return bfround(x);
+    else return x;
+}
+template <typename T> __device__ __forceinline__ float ld(const T* p, size_t i) {
+    if constexpr (is_bf16<T>::value) return bf2f(p[i]);
+    else return p[i];
+}
+// store with rounding to T
+template <typename T> __device__ __forceinline__ void st(T* p, size_t i, float v) {
+    if constexpr (is_bf16<T>::value) p[i] = f2bf(v);
+    else p[i] = v;
+}
+
+// 8 consecutive elements (16 B for bf16, 32 B for float), p 16-byte aligned
+template <typename T> __device__ __forceinline__ void load8(const T* p, float (&o)[8]) {
+    if constexpr (is_bf16<T>::value) {
+        u32x4_t v = *reinterpret_cast<const u32x4_t*>(p);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            o[2 * j] = __uint_as_float(v[j] << 16);
+            o[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
+        }
+    } else {
+        f32x4_t a = *reinterpret_cast<const f32x4_t*>(p);
+        f32x4_t b = *reinterpret_cast<const f32x4_t*>(p + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { o[j] = a[j]; o[4 + j] = b[j]; }
+    }
+}
+
+// ---- wave (64-lane) reductions ------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+// block-wide sum for blockDim.x <= 1024; scratch: >= 16 floats of LDS
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane == 0) scratch[w] = v;
+    __syncthreads();
+    float t = 0.f;
+    for (int i = 0; i < nw; ++i) t += scratch[i];
+    return t;
+}
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wave_max(v);
+    __syncthreads();
+    if (lane == 0) scratch[w] = v;
+    __syncthreads();
+    float t = -INFINITY;
+    for (int i = 0; i < nw; ++i) t = fmaxf(t, scratch[i]);
+    return t;
+}
+
+// ---- counter-based RNG (identical formula in fishmi/synth.py and oracle/fishmi_oracle.c) --
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+// sampler uniform in [0,1), truncated to bf16, keyed by (seed, step, draw, index)
+__device__ __forceinline__ float rng_uniform_bf16(uint64_t seed, uint64_t step, uint32_t draw,
+                                                  uint32_t idx) {
+    uint64_t key = seed * 0xD1B54A32D192ED03ull + (step * 64ull + draw) * 0x9E3779B97F4A7C15ull + idx;
+    uint32_t m = (uint32_t)(splitmix64(key) >> 40);
+    float u = (float)m * (1.0f / 16777216.0f);
+    return __uint_as_float(__float_as_uint(u) & 0xffff0000u);
+}
+
+#define FM_CEIL(a, b) (((a) + (b) - 1) / (b))

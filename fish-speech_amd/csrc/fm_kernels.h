@@ -1,0 +1,103 @@
+// fm_kernels.h -- kernel argument blocks and launchers (host <-> device seam of libfishmi).
+#pragma once
+#include <algorithm>
+#include "fm_common.h"
+
+enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_F32 = 3 };
+
+template <typename T> struct LinearArgs {
+    const T* W;      // [N(padded to 16)][K] row-major (nn.Linear layout)
+    const T* W2;     // second weight for EPI_SWIGLU (w3), same shape
+    const T* bias;   // [N] or null
+    const T* X;      // [R][ldx]
+    int ldx, R, N, K;
+    T* Y;            // [R][ldy]
+    int ldy;
+    const T* res;    // residual [R][ldr] (EPI_RESID)
+    int ldr;
+    float* Yf;       // fp32 output (EPI_F32)
+};
+
+template <typename T> struct QkArgs {
+    const T* qkv;    // [R][ldqkv]
+    int ldqkv;
+    const int* row_slot;
+    const int* row_pos;
+    int fixed_pos;   // >= 0: every row at this position (fast model)
+    int nh, nkv, hd, qk_norm;
+    float eps;
+    const T* qn;
+    const T* kn;
+    const float* rope;  // [S][hd/2][2] (bf16-valued cos/sin)
+    T* qout;         // [R][nh*hd]
+    T* kc;
+    T* vc;
+    size_t slot_stride, layer_off;
+    int S;
+};
+
+template <typename T> struct AttnArgs {
+    const T* q;      // [R][nh*hd]
+    const int* row_slot;
+    const int* row_pos;
+    const T* kc;
+    const T* vc;
+    size_t slot_stride, layer_off;
+    int S, nh, nkv, hd, split, maxsplit;
+    float scale;
+    float* part;     // [R][nh][maxsplit][hd+2]
+};
+
+template <typename T> struct FastAttnArgs {
+    const T* q;
+    const int* row_slot;
+    const T* kc;
+    const T* vc;
+    size_t slot_stride, layer_off;
+    int S, nh, nkv, hd, cpos;
+    float scale;
+    T* out;
+};
+
+struct SlotParams {
+    float temperature, top_p;
+    int top_k, mask_im_end;
+    uint64_t seed;
+    int step, pad;
+};
+
+struct SampleArgs {
+    const float* logits;  // [R][ldl]
+    int ldl, Nl;
+    const int* row_slot;
+    const SlotParams* sp;
+    const int32_t* ras;   // [slot][ras_stride]
+    int ras_stride, ras_enable;
+    int slow, sb, se, im_end, cb, draw, col_idx;
+    int32_t* cols;        // [R][ldc]
+    int ldc;
+};
+
+template <typename T>
+void launch_embed(hipStream_t s, const int32_t* tok, int R, const T* emb, const T* cbemb, int d,
+                  int C, int cb, int sb, int se, int scale, T* x, const int* row_slot);
+template <typename T>
+void launch_gather_rows(hipStream_t s, const int32_t* codes, int ldc, int col, const T* table,
+                        int d, int R, T* x);
+template <typename T>
+void launch_rmsnorm(hipStream_t s, const T* x, int ldx, const T* w, int d, float eps, T* y,
+                    int ldy, int R);
+template <typename T> void launch_linear(hipStream_t s, const LinearArgs<T>& a, int epi);
+template <typename T> void launch_qk_rope_cache(hipStream_t s, const QkArgs<T>& a, int R);
+template <typename T>
+void launch_attn(hipStream_t s, const AttnArgs<T>& a, int R, int nsplit, T* out);
+template <typename T> void launch_fast_attn(hipStream_t s, const FastAttnArgs<T>& a, int R);
+template <typename T> void launch_sample(hipStream_t s, const SampleArgs& a, int R);
+void launch_finish(hipStream_t s, int R, const int* row_slot, int* row_pos, const int32_t* cols,
+                   int ldc, int32_t* tok_in, int32_t* ras, int ras_stride, int C1, int update_ras,
+                   SlotParams* sp);
+template <typename T>
+void launch_synth(hipStream_t s, T* dst, int64_t n, uint64_t seed, uint32_t tid, float center,
+                  int log2_half);
+template <typename T>
+void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* dst);

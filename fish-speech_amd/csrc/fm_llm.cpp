@@ -1,0 +1,823 @@
+// fm_llm.cpp -- host runtime of the Dual-AR decode path (C ABI in include/fishmi.h).
+//
+// One handle per GPU owns: the weights (bf16 or fp32), per-slot KV caches, per-slot sampler
+// state (temperature/top_p/top_k/seed/step + RAS window), and the activation buffers.  A
+// frame (one decode_one_token_ar for n slots, inference.py:96-181) is a fixed kernel sequence
+// that reads every dynamic value (tokens, positions, steps) from device memory, so it is
+// captured once per batch size into a hipGraph and replayed.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <algorithm>
+#include <memory>
+
+#include "fm_kernels.h"
+#include "fm_runtime.h"
+
+static thread_local std::string g_err;
+void fm_set_error(const std::string& s) { g_err = s; }
+extern "C" const char* fm_last_error(void) { return g_err.c_str(); }
+extern "C" int fm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+static constexpr int PREFILL_CHUNK = 256;
+static constexpr int ATTN_SPLIT = 64;
+
+struct LayerW {
+    void *wqkv = nullptr, *bqkv = nullptr, *wo = nullptr, *bo = nullptr, *qn = nullptr, *kn = nullptr;
+    void *w1 = nullptr, *w3 = nullptr, *w2 = nullptr, *an = nullptr, *fn = nullptr;
+};
+
+struct StackDims {
+    int n_layer, dim, nh, nkv, hd, inter, qkv_bias, o_bias, qk_norm;
+    int nq() const { return nh * hd; }
+    int nqkv() const { return (nh + 2 * nkv) * hd; }
+};
+
+struct fm_llm {
+    fm_model_config c{};
+    int device = 0, prec = FM_PREC_BF16, max_slots = 1;
+    size_t esz = 2;
+    hipStream_t stream = nullptr;
+    std::map<std::string, DTensor> w;
+    bool finalized = false;
+    StackDims sd{}, fdm{};
+    int S = 0, C = 0, C1 = 0, cb = 0, nsem = 0, Nhead = 0, maxsplit = 0, Rmax = 0;
+    std::vector<LayerW> slow, fast;
+    void *emb = nullptr, *cbemb = nullptr, *norm = nullptr, *head_c = nullptr, *fproj_w = nullptr,
+         *fproj_b = nullptr, *femb = nullptr, *fnorm = nullptr, *fout = nullptr;
+    // caches
+    void *kc = nullptr, *vc = nullptr, *fkc = nullptr, *fvc = nullptr;
+    size_t slot_stride = 0, layer_stride = 0, fslot_stride = 0, flayer_stride = 0;
+    float *rope = nullptr, *frope = nullptr;
+    // activations
+    void *x = nullptr, *h = nullptr, *xn = nullptr, *qkv = nullptr, *q = nullptr, *att = nullptr,
+         *act = nullptr;
+    void *xl = nullptr, *xnl = nullptr, *fx = nullptr, *fh = nullptr, *fxn = nullptr;
+    float *part = nullptr, *logits = nullptr, *flogits = nullptr;
+    // rows / slots
+    int *frame_slot = nullptr, *frame_pos = nullptr, *prow_slot = nullptr, *prow_pos = nullptr;
+    int32_t *tok_in = nullptr, *cols = nullptr, *ptok = nullptr, *ras = nullptr;
+    SlotParams* sp = nullptr;
+    int32_t* h_cols = nullptr;  // pinned [2][max_slots][C1]
+    std::vector<int> host_pos, host_step;
+    std::vector<int> uploaded_slots;
+    // graphs
+    bool use_graph = true;
+    std::map<int, hipGraphExec_t> graphs;
+    Profiler prof;
+    std::vector<void*> allocs;
+
+    ~fm_llm() {
+        if (device >= 0) (void)hipSetDevice(device);
+        for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
+        for (auto& kv : w)
+            if (kv.second.p) (void)hipFree(kv.second.p);
+        for (void* p : allocs) (void)hipFree(p);
+        if (h_cols) (void)hipHostFree(h_cols);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    void* dalloc(size_t bytes, bool zero = true) {
+        void* p = nullptr;
+        if (bytes == 0) bytes = 16;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess)
+            throw FmError{FM_ERR_OOM, "hipMalloc(" + std::to_string(bytes) + ") failed: " + hipGetErrorString(e)};
+        if (zero) HIPCHK(hipMemsetAsync(p, 0, bytes, stream));
+        allocs.push_back(p);
+        return p;
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// tensor inventory (names = reference state_dict keys after remap; llama.py module tree)
+// ------------------------------------------------------------------------------------------
+static void add_t(fm_llm* m, const std::string& n, int64_t rows, int64_t cols) {
+    DTensor t;
+    t.rows = rows;
+    t.cols = cols;
+    t.numel = rows * cols;
+    m->w[n] = t;
+}
+static void add_stack(fm_llm* m, const std::string& pre, const StackDims& s) {
+    for (int i = 0; i < s.n_layer; ++i) {
+        std::string p = pre + std::to_string(i) + ".";
+        add_t(m, p + "attention.wqkv.weight", s.nqkv(), s.dim);
+        if (s.qkv_bias) add_t(m, p + "attention.wqkv.bias", 1, s.nqkv());
+        add_t(m, p + "attention.wo.weight", s.dim, s.nq());
+        if (s.o_bias) add_t(m, p + "attention.wo.bias", 1, s.dim);
+        if (s.qk_norm) {
+            add_t(m, p + "attention.q_norm.weight", 1, s.hd);
+            add_t(m, p + "attention.k_norm.weight", 1, s.hd);
+        }
+        add_t(m, p + "feed_forward.w1.weight", s.inter, s.dim);
+        add_t(m, p + "feed_forward.w3.weight", s.inter, s.dim);
+        add_t(m, p + "feed_forward.w2.weight", s.dim, s.inter);
+        add_t(m, p + "ffn_norm.weight", 1, s.dim);
+        add_t(m, p + "attention_norm.weight", 1, s.dim);
+    }
+}
+
+static void build_inventory(fm_llm* m) {
+    const fm_model_config& c = m->c;
+    m->sd = StackDims{c.n_layer, c.dim, c.n_head, c.n_local_heads, c.head_dim, c.intermediate_size,
+                      c.qkv_bias, c.o_bias, c.qk_norm};
+    m->fdm = StackDims{c.n_fast_layer, c.fast_dim, c.fast_n_head, c.fast_n_local_heads, c.fast_head_dim,
+                       c.fast_intermediate_size, c.fast_qkv_bias, c.fast_o_bias, c.fast_qk_norm};
+    add_t(m, "embeddings.weight", c.vocab_size, c.dim);
+    add_t(m, "codebook_embeddings.weight", (int64_t)c.codebook_size * c.num_codebooks, c.dim);
+    add_stack(m, "layers.", m->sd);
+    add_t(m, "norm.weight", 1, c.dim);
+    if (!c.tie_word_embeddings) add_t(m, "output.weight", c.vocab_size, c.dim);
+    if (c.fast_dim != c.dim) {
+        add_t(m, "fast_project_in.weight", c.fast_dim, c.dim);
+        add_t(m, "fast_project_in.bias", 1, c.fast_dim);
+    }
+    add_t(m, "fast_embeddings.weight", c.codebook_size, c.fast_dim);
+    add_stack(m, "fast_layers.", m->fdm);
+    add_t(m, "fast_norm.weight", 1, c.fast_dim);
+    add_t(m, "fast_output.weight", c.codebook_size, c.fast_dim);
+}
+
+static DTensor& tensor_for(fm_llm* m, const char* name, int64_t numel) {
+    auto it = m->w.find(name);
+    FMCHECK(it != m->w.end(), std::string("unknown tensor: ") + name);
+    FMCHECK(it->second.numel == numel, std::string("wrong numel for ") + name + ": got " +
+                                           std::to_string(numel) + ", want " + std::to_string(it->second.numel));
+    DTensor& t = it->second;
+    if (!t.p) {
+        const int64_t rows = t.rows > 1 ? (t.rows + 15) / 16 * 16 : 1;
+        const size_t bytes = (size_t)rows * t.cols * m->esz;
+        HIPCHK(hipMalloc(&t.p, bytes));
+        HIPCHK(hipMemsetAsync(t.p, 0, bytes, m->stream));
+    }
+    return t;
+}
+
+// ------------------------------------------------------------------------------------------
+// kernels on a stack (slow or fast), templated on storage T
+// ------------------------------------------------------------------------------------------
+template <typename T> struct Run {
+    typedef T type_t;
+    fm_llm* m;
+    hipStream_t s;
+    int64_t E;  // element size
+    explicit Run(fm_llm* mm) : m(mm), s(mm->stream), E(sizeof(T)) {}
+
+    void linear(const void* W, const void* W2, const void* bias, const void* X, int ldx, int R, int N,
+                int K, void* Y, int ldy, const void* res, int ldr, float* Yf, int epi, const char* cls) {
+        LinearArgs<T> a{(const T*)W, (const T*)W2, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y,
+                        ldy, (const T*)res, ldr, Yf};
+        const int64_t wbytes = (int64_t)N * K * E * (epi == EPI_SWIGLU ? 2 : 1);
+        const int64_t bytes = wbytes + (int64_t)R * K * E + (int64_t)R * N * (epi == EPI_F32 ? 4 : E);
+        const double flops = 2.0 * R * N * K * (epi == EPI_SWIGLU ? 2 : 1);
+        m->prof.run(s, cls, bytes, flops, [&] { launch_linear<T>(s, a, epi); });
+    }
+
+    // TransformerBlock.forward (llama.py:838-843) on R rows; x is updated in place.
+    void block(const StackDims& d, const LayerW& L, int R, const int* rslot, const int* rpos,
+               int fixed_pos, bool is_fast, void* kc, void* vc, size_t sstride, size_t loff, int Sc,
+               const float* rope, void* xb, void* hb, void* xnb) {
+        const float eps = m->c.norm_eps;
+        m->prof.run(s, "norm", 0, 0, [&] {
+            launch_rmsnorm<T>(s, (const T*)xb, d.dim, (const T*)L.an, d.dim, eps, (T*)xnb, d.dim, R);
+        });
+        linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
+               nullptr, EPI_STORE, "linear");
+        QkArgs<T> qa{(const T*)m->qkv, d.nqkv(), rslot, rpos, fixed_pos, d.nh, d.nkv, d.hd, d.qk_norm,
+                     eps, (const T*)L.qn, (const T*)L.kn, rope, (T*)m->q, (T*)kc, (T*)vc, sstride, loff, Sc};
+        m->prof.run(s, "rope", 0, 0, [&] { launch_qk_rope_cache<T>(s, qa, R); });
+        const float scale = 1.0f / sqrtf((float)d.hd);
+        if (!is_fast) {
+            AttnArgs<T> aa{(const T*)m->q, rslot, rpos, (const T*)kc, (const T*)vc, sstride, loff, Sc,
+                           d.nh, d.nkv, d.hd, ATTN_SPLIT, m->maxsplit, scale, m->part};
+            m->prof.run(s, "attn", 0, 0, [&] { launch_attn<T>(s, aa, R, m->maxsplit, (T*)m->att); });
+        } else {
+            FastAttnArgs<T> fa{(const T*)m->q, rslot, (const T*)kc, (const T*)vc, sstride, loff, Sc,
+                               d.nh, d.nkv, d.hd, fixed_pos, scale, (T*)m->att};
+            m->prof.run(s, "attn", 0, 0, [&] { launch_fast_attn<T>(s, fa, R); });
+        }
+        linear(L.wo, nullptr, L.bo, m->att, d.nq(), R, d.dim, d.nq(), hb, d.dim, xb, d.dim, nullptr,
+               EPI_RESID, "linear");
+        m->prof.run(s, "norm", 0, 0, [&] {
+            launch_rmsnorm<T>(s, (const T*)hb, d.dim, (const T*)L.fn, d.dim, eps, (T*)xnb, d.dim, R);
+        });
+        linear(L.w1, L.w3, nullptr, xnb, d.dim, R, d.inter, d.dim, m->act, d.inter, nullptr, 0, nullptr,
+               EPI_SWIGLU, "linear");
+        linear(L.w2, nullptr, nullptr, m->act, d.inter, R, d.dim, d.inter, xb, d.dim, hb, d.dim, nullptr,
+               EPI_RESID, "linear");
+    }
+
+    void slow_layers(int R, const int* rslot, const int* rpos) {
+        for (int l = 0; l < m->sd.n_layer; ++l)
+            block(m->sd, m->slow[l], R, rslot, rpos, -1, false, m->kc, m->vc, m->slot_stride,
+                  (size_t)l * m->layer_stride, m->S, m->rope, m->x, m->h, m->xn);
+    }
+
+    // final norm -> constrained head logits; hidden for the fast model (llama.py:447-466, 826)
+    void head_and_hidden(const void* xlast, int n) {
+        const fm_model_config& c = m->c;
+        m->prof.run(s, "norm", 0, 0, [&] {
+            launch_rmsnorm<T>(s, (const T*)xlast, c.dim, (const T*)m->norm, c.dim, c.norm_eps, (T*)m->xnl,
+                              c.dim, n);
+        });
+        linear(m->head_c, nullptr, nullptr, m->xnl, c.dim, n, m->Nhead, c.dim, nullptr, m->Nhead,
+               nullptr, 0, m->logits, EPI_F32, "linear");
+        const void* src = c.norm_fastlayer_input ? m->xnl : xlast;
+        if (m->fproj_w)
+            linear(m->fproj_w, nullptr, m->fproj_b, src, c.dim, n, c.fast_dim, c.dim, m->fx, c.fast_dim,
+                   nullptr, 0, nullptr, EPI_STORE, "linear");
+        else
+            HIPCHK(hipMemcpyAsync(m->fx, src, (size_t)n * c.dim * E, hipMemcpyDeviceToDevice, s));
+    }
+
+    void fast_pass(int n, int cpos, bool with_head) {
+        const fm_model_config& c = m->c;
+        for (int l = 0; l < m->fdm.n_layer; ++l)
+            block(m->fdm, m->fast[l], n, m->frame_slot, nullptr, cpos, true, m->fkc, m->fvc,
+                  m->fslot_stride, (size_t)l * m->flayer_stride, m->C, m->frope, m->fx, m->fh, m->fxn);
+        if (with_head) {
+            m->prof.run(s, "norm", 0, 0, [&] {
+                launch_rmsnorm<T>(s, (const T*)m->fx, c.fast_dim, (const T*)m->fnorm, c.fast_dim,
+                                  c.norm_eps, (T*)m->fxn, c.fast_dim, n);
+            });
+            linear(m->fout, nullptr, nullptr, m->fxn, c.fast_dim, n, m->cb, c.fast_dim, nullptr, m->cb,
+                   nullptr, 0, m->flogits, EPI_F32, "linear");
+        }
+    }
+
+    SampleArgs sargs(bool slow, int ras_enable, int c) {
+        const fm_model_config& cc = m->c;
+        SampleArgs a{};
+        a.logits = slow ? m->logits : m->flogits;
+        a.ldl = slow ? m->Nhead : m->cb;
+        a.Nl = a.ldl;
+        a.row_slot = m->frame_slot;
+        a.sp = m->sp;
+        a.ras = m->ras;
+        a.ras_stride = m->C1 * 10;
+        a.ras_enable = ras_enable;
+        a.slow = slow;
+        a.sb = cc.semantic_begin_id;
+        a.se = cc.semantic_end_id;
+        a.im_end = cc.im_end_id;
+        a.cb = m->cb;
+        a.draw = 1 + c;
+        a.col_idx = c + 1;
+        a.cols = m->cols;
+        a.ldc = m->C1;
+        return a;
+    }
+
+    // tail of decode_one_token_ar after the slow forward: sample, fast AR over codebooks
+    void frame_tail(int n, bool ras_enable, bool sample) {
+        if (sample) {
+            SampleArgs a = sargs(true, ras_enable, 0);
+            m->prof.run(s, "sample", 0, 0, [&] { launch_sample<T>(s, a, n); });
+        }
+        fast_pass(n, 0, false);  // position 0: fills the fast KV cache, logits discarded
+        for (int cc = 1; cc < m->C; ++cc) {
+            m->prof.run(s, "other", 0, 0, [&] {
+                launch_gather_rows<T>(s, m->cols, m->C1, cc, (const T*)m->femb, m->c.fast_dim, n, (T*)m->fx);
+            });
+            fast_pass(n, cc, true);
+            if (sample) {
+                SampleArgs a = sargs(false, 0, cc);
+                m->prof.run(s, "sample", 0, 0, [&] { launch_sample<T>(s, a, n); });
+            }
+        }
+    }
+
+    void decode_frame(int n) {
+        m->prof.run(s, "other", 0, 0, [&] {
+            launch_embed<T>(s, m->tok_in, n, (const T*)m->emb, (const T*)m->cbemb, m->c.dim, m->C, m->cb,
+                            m->c.semantic_begin_id, m->c.semantic_end_id, m->c.scale_codebook_embeddings,
+                            (T*)m->x, m->frame_slot);
+        });
+        slow_layers(n, m->frame_slot, m->frame_pos);
+        head_and_hidden(m->x, n);
+        frame_tail(n, true, true);
+        launch_finish(s, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10,
+                      m->C1, 1, m->sp);
+    }
+
+    // runs the prompt through the slow model (chunks), leaves the last row in m->x[row]
+    const void* prefill_slow(int slot, const int32_t* tokens, int Tn, int pos0) {
+        const int C1 = m->C1;
+        std::vector<int32_t> rows((size_t)PREFILL_CHUNK * C1);
+        std::vector<int> rs(PREFILL_CHUNK, slot), rp(PREFILL_CHUNK);
+        int last = 0;
+        for (int t0 = 0; t0 < Tn; t0 += PREFILL_CHUNK) {
+            const int R = std::min(PREFILL_CHUNK, Tn - t0);
+            for (int r = 0; r < R; ++r) {
+                for (int q = 0; q < C1; ++q) rows[(size_t)r * C1 + q] = tokens[(size_t)q * Tn + t0 + r];
+                rp[r] = pos0 + t0 + r;
+            }
+            HIPCHK(hipMemcpyAsync(m->ptok, rows.data(), (size_t)R * C1 * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(m->prow_slot, rs.data(), (size_t)R * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(m->prow_pos, rp.data(), (size_t)R * 4, hipMemcpyHostToDevice, s));
+            launch_embed<T>(s, m->ptok, R, (const T*)m->emb, (const T*)m->cbemb, m->c.dim, m->C, m->cb,
+                            m->c.semantic_begin_id, m->c.semantic_end_id, m->c.scale_codebook_embeddings,
+                            (T*)m->x, nullptr);
+            slow_layers(R, m->prow_slot, m->prow_pos);
+            last = R - 1;
+            HIPCHK(hipStreamSynchronize(s));  // host vectors reused by the next chunk
+        }
+        return (const char*)m->x + (size_t)last * m->c.dim * E;
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// finalize: validate weights, derive pointers, allocate caches / buffers
+// ------------------------------------------------------------------------------------------
+static void* W(fm_llm* m, const std::string& n) {
+    auto it = m->w.find(n);
+    FMCHECK(it != m->w.end() && it->second.set, "tensor not set: " + n);
+    return it->second.p;
+}
+static void* Wopt(fm_llm* m, const std::string& n) {
+    auto it = m->w.find(n);
+    return (it != m->w.end() && it->second.set) ? it->second.p : nullptr;
+}
+
+static void finalize(fm_llm* m) {
+    if (m->finalized) return;
+    const fm_model_config& c = m->c;
+    for (auto& kv : m->w) FMCHECK(kv.second.set, "tensor not set: " + kv.first);
+    auto stack = [&](const std::string& pre, const StackDims& d, std::vector<LayerW>& out) {
+        out.resize(d.n_layer);
+        for (int i = 0; i < d.n_layer; ++i) {
+            std::string p = pre + std::to_string(i) + ".";
+            LayerW& L = out[i];
+            L.wqkv = W(m, p + "attention.wqkv.weight");
+            L.bqkv = Wopt(m, p + "attention.wqkv.bias");
+            L.wo = W(m, p + "attention.wo.weight");
+            L.bo = Wopt(m, p + "attention.wo.bias");
+            L.qn = Wopt(m, p + "attention.q_norm.weight");
+            L.kn = Wopt(m, p + "attention.k_norm.weight");
+            L.w1 = W(m, p + "feed_forward.w1.weight");
+            L.w3 = W(m, p + "feed_forward.w3.weight");
+            L.w2 = W(m, p + "feed_forward.w2.weight");
+            L.an = W(m, p + "attention_norm.weight");
+            L.fn = W(m, p + "ffn_norm.weight");
+        }
+    };
+    stack("layers.", m->sd, m->slow);
+    stack("fast_layers.", m->fdm, m->fast);
+    m->emb = W(m, "embeddings.weight");
+    m->cbemb = W(m, "codebook_embeddings.weight");
+    m->norm = W(m, "norm.weight");
+    m->fproj_w = Wopt(m, "fast_project_in.weight");
+    m->fproj_b = Wopt(m, "fast_project_in.bias");
+    m->femb = W(m, "fast_embeddings.weight");
+    m->fnorm = W(m, "fast_norm.weight");
+    m->fout = W(m, "fast_output.weight");
+    // constrained head (inference.py:308-320): only the semantic rows + <|im_end|> can be
+    // finite after the bias, so the LM head streams exactly those rows.
+    const void* outw = c.tie_word_embeddings ? m->emb : W(m, "output.weight");
+    m->nsem = c.semantic_end_id - c.semantic_begin_id + 1;
+    m->Nhead = m->nsem + 1;
+    FMCHECK(m->Nhead <= 8192, "constrained head wider than 8192 rows is not supported");
+    const size_t rowb = (size_t)c.dim * m->esz;
+    m->head_c = m->dalloc((size_t)(m->Nhead + 15) / 16 * 16 * rowb);
+    HIPCHK(hipMemcpyAsync(m->head_c, (const char*)outw + (size_t)c.semantic_begin_id * rowb,
+                          (size_t)m->nsem * rowb, hipMemcpyDeviceToDevice, m->stream));
+    HIPCHK(hipMemcpyAsync((char*)m->head_c + (size_t)m->nsem * rowb,
+                          (const char*)outw + (size_t)c.im_end_id * rowb, rowb, hipMemcpyDeviceToDevice,
+                          m->stream));
+    // caches [slot][layer][kv][S][hd]
+    const StackDims& d = m->sd;
+    m->layer_stride = (size_t)d.nkv * m->S * d.hd;
+    m->slot_stride = m->layer_stride * d.n_layer;
+    m->kc = m->dalloc(m->slot_stride * m->max_slots * m->esz);
+    m->vc = m->dalloc(m->slot_stride * m->max_slots * m->esz);
+    const StackDims& f = m->fdm;
+    m->flayer_stride = (size_t)f.nkv * m->C * f.hd;
+    m->fslot_stride = m->flayer_stride * f.n_layer;
+    m->fkc = m->dalloc(m->fslot_stride * m->max_slots * m->esz);
+    m->fvc = m->dalloc(m->fslot_stride * m->max_slots * m->esz);
+    auto rt = rope_table_host(m->S, d.hd, c.rope_base);
+    m->rope = (float*)m->dalloc(rt.size() * 4, false);
+    HIPCHK(hipMemcpy(m->rope, rt.data(), rt.size() * 4, hipMemcpyHostToDevice));
+    auto frt = rope_table_host(m->C, f.hd, c.rope_base);
+    m->frope = (float*)m->dalloc(frt.size() * 4, false);
+    HIPCHK(hipMemcpy(m->frope, frt.data(), frt.size() * 4, hipMemcpyHostToDevice));
+    // activations
+    const int R = m->Rmax = std::max(m->max_slots, PREFILL_CHUNK);
+    const int dmax = std::max(c.dim, c.fast_dim);
+    const int qkvmax = std::max(d.nqkv(), f.nqkv()), qmax = std::max(d.nq(), f.nq());
+    const int imax = std::max(d.inter, f.inter);
+    const size_t E = m->esz;
+    m->x = m->dalloc((size_t)R * dmax * E);
+    m->h = m->dalloc((size_t)R * dmax * E);
+    m->xn = m->dalloc((size_t)R * dmax * E);
+    m->qkv = m->dalloc((size_t)R * qkvmax * E);
+    m->q = m->dalloc((size_t)R * qmax * E);
+    m->att = m->dalloc((size_t)R * qmax * E);
+    m->act = m->dalloc((size_t)R * imax * E);
+    const int n = m->max_slots;
+    m->xl = m->dalloc((size_t)n * dmax * E);
+    m->xnl = m->dalloc((size_t)n * dmax * E);
+    m->fx = m->dalloc((size_t)n * dmax * E);
+    m->fh = m->dalloc((size_t)n * dmax * E);
+    m->fxn = m->dalloc((size_t)n * dmax * E);
+    m->maxsplit = FM_CEIL(m->S, ATTN_SPLIT);
+    m->part = (float*)m->dalloc((size_t)R * d.nh * m->maxsplit * (d.hd + 2) * 4, false);
+    m->logits = (float*)m->dalloc((size_t)n * m->Nhead * 4);
+    m->flogits = (float*)m->dalloc((size_t)n * m->cb * 4);
+    m->frame_slot = (int*)m->dalloc(n * 4);
+    m->frame_pos = (int*)m->dalloc(n * 4);
+    m->prow_slot = (int*)m->dalloc(PREFILL_CHUNK * 4);
+    m->prow_pos = (int*)m->dalloc(PREFILL_CHUNK * 4);
+    m->tok_in = (int32_t*)m->dalloc((size_t)n * m->C1 * 4);
+    m->cols = (int32_t*)m->dalloc((size_t)n * m->C1 * 4);
+    m->ptok = (int32_t*)m->dalloc((size_t)PREFILL_CHUNK * m->C1 * 4);
+    m->ras = (int32_t*)m->dalloc((size_t)n * m->C1 * 10 * 4);
+    m->sp = (SlotParams*)m->dalloc(sizeof(SlotParams) * n);
+    HIPCHK(hipHostMalloc((void**)&m->h_cols, (size_t)2 * n * m->C1 * 4, hipHostMallocDefault));
+    m->host_pos.assign(n, 0);
+    m->host_step.assign(n, 0);
+    HIPCHK(hipStreamSynchronize(m->stream));
+    m->finalized = true;
+}
+
+template <typename F> static int with_prec(fm_llm* m, F&& f) {
+    if (m->prec == FM_PREC_BF16) {
+        Run<bf16_t> r(m);
+        f(r);
+    } else {
+        Run<float> r(m);
+        f(r);
+    }
+    return 0;
+}
+
+static void check_tokens(fm_llm* m, const int32_t* tok, int T) {
+    const fm_model_config& c = m->c;
+    for (int t = 0; t < T; ++t) {
+        const int t0 = tok[t];
+        FMCHECK(t0 >= 0 && t0 < c.vocab_size, "token id out of range: " + std::to_string(t0));
+        for (int q = 0; q < m->C; ++q) {
+            const int v = tok[(size_t)(q + 1) * T + t];
+            FMCHECK(v >= 0 && v < m->cb, "codebook token out of range: " + std::to_string(v));
+        }
+    }
+}
+
+static void reset_slot(fm_llm* m, int slot, const fm_sampling* sp) {
+    HIPCHK(hipMemsetAsync((char*)m->ras + (size_t)slot * m->C1 * 10 * 4, 0, (size_t)m->C1 * 10 * 4, m->stream));
+    SlotParams p{};
+    if (sp) {
+        p.temperature = sp->temperature;
+        p.top_p = sp->top_p;
+        p.top_k = sp->top_k;
+        p.mask_im_end = sp->mask_im_end;
+        p.seed = sp->seed;
+    } else {
+        p.temperature = 0.7f;
+        p.top_p = 0.9f;
+        p.top_k = 1;
+    }
+    p.step = 0;
+    HIPCHK(hipMemcpyAsync(m->sp + slot, &p, sizeof p, hipMemcpyHostToDevice, m->stream));
+    HIPCHK(hipStreamSynchronize(m->stream));
+    m->host_step[slot] = 0;
+}
+
+static void upload_frame_rows(fm_llm* m, const int32_t* slots, int n) {
+    std::vector<int> s(slots, slots + n), p(n);
+    if (s == m->uploaded_slots) return;
+    for (int i = 0; i < n; ++i) p[i] = m->host_pos[s[i]];
+    HIPCHK(hipMemcpyAsync(m->frame_slot, s.data(), (size_t)n * 4, hipMemcpyHostToDevice, m->stream));
+    HIPCHK(hipMemcpyAsync(m->frame_pos, p.data(), (size_t)n * 4, hipMemcpyHostToDevice, m->stream));
+    HIPCHK(hipStreamSynchronize(m->stream));
+    m->uploaded_slots = s;
+}
+
+// one decode frame for the uploaded rows (graph replay when enabled), async
+static void launch_frame(fm_llm* m, int n) {
+    if (m->use_graph && !m->prof.on) {
+        auto it = m->graphs.find(n);
+        if (it == m->graphs.end()) {
+            hipGraph_t g;
+            HIPCHK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
+            with_prec(m, [&](auto& r) { r.decode_frame(n); });
+            HIPCHK(hipStreamEndCapture(m->stream, &g));
+            hipGraphExec_t ge;
+            HIPCHK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+            HIPCHK(hipGraphDestroy(g));
+            it = m->graphs.emplace(n, ge).first;
+        }
+        HIPCHK(hipGraphLaunch(it->second, m->stream));
+    } else {
+        with_prec(m, [&](auto& r) { r.decode_frame(n); });
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+int fm_llm_open(const fm_model_config* cfg, int device, int precision, int max_slots, fm_llm** out) {
+    return fm_guard([&] {
+        FMCHECK(cfg && out, "null argument");
+        FMCHECK(precision == FM_PREC_BF16 || precision == FM_PREC_FP32, "bad precision");
+        FMCHECK(max_slots >= 1 && max_slots <= 4096, "bad max_slots");
+        const fm_model_config& c = *cfg;
+        FMCHECK(c.dim % 32 == 0 && c.fast_dim % 32 == 0, "dims must be multiples of 32");
+        FMCHECK(c.intermediate_size % 32 == 0 && c.fast_intermediate_size % 32 == 0,
+                "intermediate sizes must be multiples of 32");
+        FMCHECK((c.n_head * c.head_dim) % 32 == 0 && (c.fast_n_head * c.fast_head_dim) % 32 == 0,
+                "n_head*head_dim must be a multiple of 32");
+        FMCHECK(c.head_dim % 8 == 0 && c.head_dim <= 256 && c.fast_head_dim <= 256, "bad head_dim");
+        FMCHECK(c.n_head % c.n_local_heads == 0 && c.fast_n_head % c.fast_n_local_heads == 0, "bad GQA");
+        FMCHECK(c.num_codebooks >= 1 && c.num_codebooks <= 63, "bad num_codebooks");
+        FMCHECK(c.codebook_size <= 8192, "codebook_size > 8192 unsupported");
+        FMCHECK(c.im_end_id >= 0 && c.im_end_id < c.vocab_size, "im_end_id must be set");
+        FMCHECK(c.semantic_begin_id >= 0 && c.semantic_end_id < c.vocab_size &&
+                    c.semantic_begin_id <= c.semantic_end_id,
+                "bad semantic id range");
+        int ndev = fm_device_count();
+        FMCHECK(ndev > 0, "no HIP device visible");
+        FMCHECK(device >= 0 && device < ndev, "bad device index");
+        HIPCHK(hipSetDevice(device));
+        std::unique_ptr<fm_llm> m(new fm_llm());
+        m->c = c;
+        m->device = device;
+        m->prec = precision;
+        m->esz = precision == FM_PREC_BF16 ? 2 : 4;
+        m->max_slots = max_slots;
+        m->S = (c.max_seq_len + 7) / 8 * 8;
+        m->C = c.num_codebooks;
+        m->C1 = c.num_codebooks + 1;
+        m->cb = c.codebook_size;
+        HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+        build_inventory(m.get());
+        *out = m.release();
+    });
+}
+
+int fm_llm_set_tensor(fm_llm* m, const char* name, const void* data, int dtype, int64_t numel) {
+    return fm_guard([&] {
+        FMCHECK(m && name && data, "null argument");
+        FMCHECK(!m->finalized, "weights are frozen after finalize");
+        HIPCHK(hipSetDevice(m->device));
+        DTensor& t = tensor_for(m, name, numel);
+        const size_t sb = dtype == FM_DT_BF16 ? 2 : 4;
+        void* tmp = nullptr;
+        HIPCHK(hipMalloc(&tmp, (size_t)numel * sb));
+        HIPCHK(hipMemcpy(tmp, data, (size_t)numel * sb, hipMemcpyHostToDevice));
+        if (m->prec == FM_PREC_BF16)
+            launch_convert<bf16_t>(m->stream, tmp, dtype == FM_DT_BF16, numel, (bf16_t*)t.p);
+        else
+            launch_convert<float>(m->stream, tmp, dtype == FM_DT_BF16, numel, (float*)t.p);
+        HIPCHK(hipStreamSynchronize(m->stream));
+        HIPCHK(hipFree(tmp));
+        t.set = true;
+    });
+}
+
+int fm_llm_synth_tensor(fm_llm* m, const char* name, int64_t numel, uint64_t seed, float center,
+                        int log2_half) {
+    return fm_guard([&] {
+        FMCHECK(m && name, "null argument");
+        FMCHECK(!m->finalized, "weights are frozen after finalize");
+        HIPCHK(hipSetDevice(m->device));
+        DTensor& t = tensor_for(m, name, numel);
+        if (m->prec == FM_PREC_BF16)
+            launch_synth<bf16_t>(m->stream, (bf16_t*)t.p, numel, seed, fnv1a32(name), center, log2_half);
+        else
+            launch_synth<float>(m->stream, (float*)t.p, numel, seed, fnv1a32(name), center, log2_half);
+        HIPCHK(hipGetLastError());
+        t.set = true;
+    });
+}
+
+int fm_llm_finalize(fm_llm* m) {
+    return fm_guard([&] {
+        FMCHECK(m, "null handle");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+    });
+}
+
+static void do_prefill(fm_llm* m, int slot, const int32_t* tokens, int T, const fm_sampling* sp,
+                       int32_t* first_col) {
+    FMCHECK(slot >= 0 && slot < m->max_slots, "bad slot");
+    FMCHECK(T >= 1 && T < m->c.max_seq_len, "prompt length must be in [1, max_seq_len)");
+    check_tokens(m, tokens, T);
+    reset_slot(m, slot, sp);
+    const int32_t one = slot;
+    m->uploaded_slots.clear();
+    HIPCHK(hipMemcpyAsync(m->frame_slot, &one, 4, hipMemcpyHostToDevice, m->stream));
+    with_prec(m, [&](auto& r) {
+        const void* last = r.prefill_slow(slot, tokens, T, 0);
+        r.head_and_hidden(last, 1);
+        r.frame_tail(1, false, true);
+    });
+    int pos = T - 1;  // finish() advances it to T: the first decode frame runs at position T
+    HIPCHK(hipMemcpyAsync(m->frame_pos, &pos, 4, hipMemcpyHostToDevice, m->stream));
+    launch_finish(m->stream, 1, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras,
+                  m->C1 * 10, m->C1, 0, m->sp);
+    HIPCHK(hipMemcpyAsync(m->h_cols, m->cols, (size_t)m->C1 * 4, hipMemcpyDeviceToHost, m->stream));
+    HIPCHK(hipStreamSynchronize(m->stream));
+    m->prof.collect();
+    m->host_pos[slot] = T;
+    m->host_step[slot] = 1;
+    m->uploaded_slots.clear();
+    if (first_col) memcpy(first_col, m->h_cols, (size_t)m->C1 * 4);
+}
+
+int fm_llm_prefill(fm_llm* m, int slot, const int32_t* tokens, int T, const fm_sampling* sp,
+                   int32_t* first_col) {
+    return fm_guard([&] {
+        FMCHECK(m && tokens, "null argument");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        do_prefill(m, slot, tokens, T, sp, first_col);
+    });
+}
+
+int fm_llm_decode(fm_llm* m, const int32_t* slots, int n, int32_t* cols) {
+    return fm_guard([&] {
+        FMCHECK(m && slots && n >= 1 && n <= m->max_slots, "bad arguments");
+        FMCHECK(m->finalized, "call fm_llm_prefill first");
+        HIPCHK(hipSetDevice(m->device));
+        for (int i = 0; i < n; ++i) {
+            FMCHECK(slots[i] >= 0 && slots[i] < m->max_slots, "bad slot");
+            FMCHECK(m->host_pos[slots[i]] < m->c.max_seq_len, "slot reached max_seq_len");
+        }
+        upload_frame_rows(m, slots, n);
+        launch_frame(m, n);
+        HIPCHK(hipMemcpyAsync(m->h_cols, m->cols, (size_t)n * m->C1 * 4, hipMemcpyDeviceToHost, m->stream));
+        HIPCHK(hipStreamSynchronize(m->stream));
+        m->prof.collect();
+        for (int i = 0; i < n; ++i) {
+            m->host_pos[slots[i]]++;
+            m->host_step[slots[i]]++;
+        }
+        if (cols) memcpy(cols, m->h_cols, (size_t)n * m->C1 * 4);
+    });
+}
+
+int fm_llm_generate(fm_llm* m, int slot, const int32_t* prompt, int T, int max_new, const fm_sampling* sp,
+                    int32_t* out, int* n_out) {
+    return fm_guard([&] {
+        FMCHECK(m && prompt && out && n_out, "null argument");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        const fm_model_config& c = m->c;
+        if (max_new <= 0 || T + max_new > c.max_seq_len) max_new = c.max_seq_len - T;
+        FMCHECK(max_new >= 1, "prompt leaves no room to generate");
+        const int C1 = m->C1;
+        int32_t col[64];
+        do_prefill(m, slot, prompt, T, sp, col);
+        for (int q = 0; q < C1; ++q) out[(size_t)q * max_new] = col[q];
+        int n = 1;
+        upload_frame_rows(m, &slot, 1);
+        // pipelined: frame k+1 is queued before frame k's column is inspected on the host
+        hipEvent_t ev[2];
+        HIPCHK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+        auto issue = [&](int k) {
+            launch_frame(m, 1);
+            HIPCHK(hipMemcpyAsync(m->h_cols + (size_t)(k & 1) * m->max_slots * C1, m->cols, (size_t)C1 * 4,
+                                  hipMemcpyDeviceToHost, m->stream));
+            HIPCHK(hipEventRecord(ev[k & 1], m->stream));
+        };
+        const int steps = max_new - 1;
+        int issued = 0;
+        if (steps > 0) issue(issued++);
+        for (int k = 0; k < steps; ++k) {
+            if (issued < steps && issued <= k + 1) issue(issued++);
+            HIPCHK(hipEventSynchronize(ev[k & 1]));
+            const int32_t* hc = m->h_cols + (size_t)(k & 1) * m->max_slots * C1;
+            for (int q = 0; q < C1; ++q) out[(size_t)q * max_new + n] = hc[q];
+            n++;
+            if (hc[0] == c.im_end_id) break;
+        }
+        HIPCHK(hipStreamSynchronize(m->stream));
+        m->prof.collect();
+        (void)hipEventDestroy(ev[0]);
+        (void)hipEventDestroy(ev[1]);
+        m->host_pos[slot] = T + issued;  // device advanced once per issued frame
+        m->host_step[slot] = 1 + issued;
+        m->uploaded_slots.clear();
+        *n_out = n;
+    });
+}
+
+int fm_llm_teacher_step(fm_llm* m, int slot, const int32_t* x, int S, int pos0, const int32_t* next_col,
+                        float* slow_logits, float* hidden, float* fast_logits) {
+    return fm_guard([&] {
+        FMCHECK(m && x && S >= 1, "bad arguments");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        FMCHECK(slot >= 0 && slot < m->max_slots, "bad slot");
+        FMCHECK(pos0 + S <= m->c.max_seq_len, "beyond max_seq_len");
+        check_tokens(m, x, S);
+        if (next_col)
+            for (int q = 1; q < m->C1; ++q)
+                FMCHECK(next_col[q] >= 0 && next_col[q] < m->cb, "next_col codebook token out of range");
+        if (pos0 == 0) reset_slot(m, slot, nullptr);
+        const fm_model_config& c = m->c;
+        const int32_t one = slot;
+        HIPCHK(hipMemcpyAsync(m->frame_slot, &one, 4, hipMemcpyHostToDevice, m->stream));
+        m->uploaded_slots.clear();
+        std::vector<float> lg(m->Nhead);
+        with_prec(m, [&](auto& r) {
+            const void* last = r.prefill_slow(slot, x, S, pos0);
+            r.head_and_hidden(last, 1);
+            HIPCHK(hipMemcpyAsync(lg.data(), m->logits, (size_t)m->Nhead * 4, hipMemcpyDeviceToHost, m->stream));
+            if (hidden) {
+                std::vector<uint8_t> hb((size_t)c.fast_dim * m->esz);
+                HIPCHK(hipMemcpyAsync(hb.data(), m->fx, hb.size(), hipMemcpyDeviceToHost, m->stream));
+                HIPCHK(hipStreamSynchronize(m->stream));
+                for (int i = 0; i < c.fast_dim; ++i) {
+                    if (m->esz == 2) {
+                        uint32_t u = ((uint32_t)((uint16_t*)hb.data())[i]) << 16;
+                        memcpy(&hidden[i], &u, 4);
+                    } else {
+                        hidden[i] = ((float*)hb.data())[i];
+                    }
+                }
+            }
+            if (next_col) {
+                HIPCHK(hipMemcpyAsync(m->cols, next_col, (size_t)m->C1 * 4, hipMemcpyHostToDevice, m->stream));
+                r.fast_pass(1, 0, false);
+                for (int cc = 1; cc < m->C; ++cc) {
+                    using TT = typename std::remove_reference_t<decltype(r)>::type_t;
+                    launch_gather_rows<TT>(m->stream, m->cols, m->C1, cc, (const TT*)m->femb, c.fast_dim, 1,
+                                           (TT*)m->fx);
+                    r.fast_pass(1, cc, true);
+                    if (fast_logits)
+                        HIPCHK(hipMemcpyAsync(fast_logits + (size_t)(cc - 1) * m->cb, m->flogits, (size_t)m->cb * 4,
+                                              hipMemcpyDeviceToHost, m->stream));
+                }
+            }
+        });
+        HIPCHK(hipStreamSynchronize(m->stream));
+        m->prof.collect();
+        m->host_pos[slot] = pos0 + S;
+        if (slow_logits) {
+            for (int i = 0; i < c.vocab_size; ++i) slow_logits[i] = -INFINITY;
+            for (int i = 0; i < m->nsem; ++i) slow_logits[c.semantic_begin_id + i] = lg[i];
+            slow_logits[c.im_end_id] = lg[m->nsem];
+        }
+    });
+}
+
+int64_t fm_llm_frame_bytes(fm_llm* m, int n, int pos) {
+    if (!m) return -1;
+    const fm_model_config& c = m->c;
+    const int64_t E = (int64_t)m->esz;
+    auto stack_bytes = [&](const StackDims& d) {
+        int64_t per = (int64_t)d.nqkv() * d.dim + (int64_t)d.dim * d.nq() + 3LL * d.inter * d.dim + 2LL * d.dim;
+        if (d.qk_norm) per += 2LL * d.hd;
+        return per * d.n_layer * E;
+    };
+    int64_t b = stack_bytes(m->sd) + (int64_t)m->Nhead * c.dim * E + (int64_t)c.dim * E;  // slow + head + norm
+    b += (int64_t)m->C * stack_bytes(m->fdm) + (int64_t)(m->C - 1) * ((int64_t)m->cb * c.fast_dim + c.fast_dim) * E;
+    if (m->fproj_w) b += (int64_t)c.fast_dim * c.dim * E;
+    // per-stream: KV reads (+ the row written), embeddings
+    int64_t per_stream = 2LL * m->sd.n_layer * m->sd.nkv * m->sd.hd * E * (pos + 1);
+    for (int cc = 0; cc < m->C; ++cc) per_stream += 2LL * m->fdm.n_layer * m->fdm.nkv * m->fdm.hd * E * (cc + 1);
+    per_stream += (int64_t)(m->C + 1) * c.dim * E + (int64_t)(m->C - 1) * c.fast_dim * E;
+    return b + per_stream * n;
+}
+
+int fm_llm_profile(fm_llm* m, int enable) {
+    return fm_guard([&] {
+        FMCHECK(m, "null handle");
+        m->prof.on = enable != 0;
+        if (enable) m->prof.acc.clear();
+    });
+}
+
+int fm_llm_profile_read(fm_llm* m, const char* cls, double* ms, int64_t* launches, int64_t* bytes) {
+    return fm_guard([&] {
+        FMCHECK(m && cls, "null argument");
+        auto it = m->prof.acc.find(cls);
+        Profiler::Acc a = it == m->prof.acc.end() ? Profiler::Acc{} : it->second;
+        if (ms) *ms = a.ms;
+        if (launches) *launches = a.n;
+        if (bytes) *bytes = a.bytes;
+    });
+}
+
+int fm_llm_use_graph(fm_llm* m, int enable) {
+    return fm_guard([&] {
+        FMCHECK(m, "null handle");
+        m->use_graph = enable != 0;
+    });
+}
+
+int fm_llm_close(fm_llm* m) {
+    return fm_guard([&] { delete m; });
+}
+
+}  // extern "C"

@@ -1,0 +1,685 @@
+// fm_llm_kernels.hip -- gfx950 kernels of the Dual-AR decode step (slow 4B llama + fast
+// codebook transformer + sampling).  Every kernel is templated on the storage type T
+// (bf16_t: production, float: fp32 validation mode) and rounds at the reference's points:
+//
+//   embed_kernel ............. llama.py:399-420   (fp32 codebook sum, 3 roundings)
+//   rmsnorm_kernel ........... llama.py:989-1000  (round(x*rstd) * w, rounded)
+//   linear_kernel ............ nn.Linear / F.linear; MFMA 16x16x32 bf16 (or f32 16x16x4),
+//                              W streamed once from HBM straight into A fragments, split-K
+//                              over 8 waves, fused epilogues (bias, residual, SwiGLU)
+//   qk_rope_cache_kernel ..... llama.py:894-910   (qk-norm, RoPE on bf16 table, cache write)
+//   attn_split/combine ....... llama.py:915-933   (SDPA over the valid prefix, split-K flash
+//                              decode; GQA heads share K/V reads, no repeat_interleave)
+//   fast_attn_kernel ......... llama.py:947-975   (matmul-softmax-matmul, rounded per op)
+//   sample_kernel ............ inference.py:43-93, 117-144 (top-k / top-p / temperature /
+//                              RAS with the reference's rounding; no full-vocab sort)
+#include "fm_kernels.h"
+
+// =========================================================================================
+// embeddings
+// =========================================================================================
+template <typename T>
+__global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ tok, int R,
+                                                    const T* __restrict__ emb,
+                                                    const T* __restrict__ cbemb, int d, int C,
+                                                    int cb, int sb, int se, int scale,
+                                                    T* __restrict__ x,
+                                                    const int* __restrict__ row_slot) {
+    const int r = blockIdx.x;
+    if (r >= R) return;
+    // prefill: tokens per row; decode: the slot's last emitted column (row_slot != null)
+    const int32_t* t = tok + (size_t)(row_slot ? row_slot[r] : r) * (C + 1);
+    const int t0 = t[0];
+    const bool sem = t0 >= sb && t0 <= se;
+    const float inv = sqrtf((float)(C + 1));
+    for (int i = threadIdx.x; i < d; i += blockDim.x) {
+        float v = 0.f;
+        if (sem) {
+            for (int q = 0; q < C; ++q) v += ld(cbemb, (size_t)(t[1 + q] + q * cb) * d + i);
+            v = rnd<T>(v);
+        }
+        float e = rnd<T>(ld(emb, (size_t)t0 * d + i) + v);
+        if (scale && sem) e = rnd<T>(e / inv);
+        st(x, (size_t)r * d + i, e);
+    }
+}
+
+// x[r] = table[codes[r * ld + col]]  (fast_embeddings lookup, inference.py:154, 173)
+template <typename T>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const int32_t* __restrict__ codes,
+                                                          int ldc, int col, const T* __restrict__ table,
+                                                          int d, T* __restrict__ x) {
+    const int r = blockIdx.x;
+    const int c = codes[(size_t)r * ldc + col];
+    for (int i = threadIdx.x; i < d; i += blockDim.x) x[(size_t)r * d + i] = table[(size_t)c * d + i];
+}
+
+// =========================================================================================
+// RMSNorm (llama.py:989-1000): fp32 mean square, round(x*rstd), * weight, round
+// =========================================================================================
+template <typename T>
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const T* __restrict__ x, int ldx,
+                                                      const T* __restrict__ w, int d, float eps,
+                                                      T* __restrict__ y, int ldy) {
+    __shared__ float scratch[16];
+    const int r = blockIdx.x;
+    const T* xr = x + (size_t)r * ldx;
+    float ss = 0.f;
+    for (int i = threadIdx.x; i < d; i += blockDim.x) {
+        float v = ld(xr, i);
+        ss += v * v;
+    }
+    ss = block_sum(ss, scratch);
+    const float rs = 1.0f / sqrtf(ss / (float)d + eps);
+    for (int i = threadIdx.x; i < d; i += blockDim.x) {
+        float v = rnd<T>(ld(xr, i) * rs);
+        st(y, (size_t)r * ldy + i, v * ld(w, i));
+    }
+}
+
+// =========================================================================================
+// linear: Y[col][n] = epi( sum_k X[col][k] * W[n][k] )
+// =========================================================================================
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16_t> {
+    typedef u32x4_t frag;  // 8 bf16 along k
+    static __device__ __forceinline__ frag load(const bf16_t* p) {
+        return *reinterpret_cast<const u32x4_t*>(p);
+    }
+    static __device__ __forceinline__ f32x4_t mma(frag a, frag b, f32x4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                       __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+    }
+};
+template <> struct Mfma<float> {
+    struct frag {
+        f32x4_t lo, hi;
+    };
+    static __device__ __forceinline__ frag load(const float* p) {
+        frag f;
+        f.lo = *reinterpret_cast<const f32x4_t*>(p);
+        f.hi = *reinterpret_cast<const f32x4_t*>(p + 4);
+        return f;
+    }
+    // lane l holds k = 8*(l>>4) + j of a 32-wide k block; MFMA j covers {8g + j}: exact f32
+    static __device__ __forceinline__ f32x4_t mma(frag a, frag b, f32x4_t c) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[j], b.lo[j], c, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[j], b.hi[j], c, 0, 0, 0);
+        return c;
+    }
+};
+
+__device__ __forceinline__ float silu_f(float a) { return a / (1.0f + expf(-a)); }
+
+template <typename T, int NCG, int EPI>
+__global__ __launch_bounds__(512) void linear_kernel(LinearArgs<T> a) {
+    using M = Mfma<T>;
+    constexpr int NACC = (EPI == EPI_SWIGLU) ? 2 : 1;
+    constexpr int U = (NCG == 1) ? 8 : 4;
+    __shared__ f32x4_t red[8][NACC * NCG][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n0 = blockIdx.x * 16;
+    const int r = lane & 15, g = lane >> 4;
+    const int nsteps = a.K >> 5;
+    const int s0 = (wave * nsteps) >> 3, s1 = ((wave + 1) * nsteps) >> 3;
+    const T* wp = a.W + (size_t)(n0 + r) * a.K + 8 * g;
+    const T* wp2 = (EPI == EPI_SWIGLU) ? a.W2 + (size_t)(n0 + r) * a.K + 8 * g : nullptr;
+
+    for (int c0 = 0; c0 < a.R; c0 += 16 * NCG) {
+        f32x4_t acc[NACC][NCG];
+        const T* xp[NCG];
+#pragma unroll
+        for (int c = 0; c < NCG; ++c) {
+            int col = c0 + 16 * c + r;
+            col = col < a.R ? col : a.R - 1;  // out-of-range columns read a valid row; discarded
+            xp[c] = a.X + (size_t)col * a.ldx + 8 * g;
+#pragma unroll
+            for (int q = 0; q < NACC; ++q) acc[q][c] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        }
+        int s = s0;
+        for (; s + U <= s1; s += U) {
+            typename M::frag fa[NACC][U], fb[NCG][U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                fa[0][u] = M::load(wp + (size_t)(s + u) * 32);
+                if constexpr (NACC == 2) fa[1][u] = M::load(wp2 + (size_t)(s + u) * 32);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int c = 0; c < NCG; ++c) fb[c][u] = M::load(xp[c] + (size_t)(s + u) * 32);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int c = 0; c < NCG; ++c)
+#pragma unroll
+                    for (int q = 0; q < NACC; ++q) acc[q][c] = M::mma(fa[q][u], fb[c][u], acc[q][c]);
+        }
+        for (; s < s1; ++s) {
+            typename M::frag fa0 = M::load(wp + (size_t)s * 32);
+            typename M::frag fa1;
+            if constexpr (NACC == 2) fa1 = M::load(wp2 + (size_t)s * 32);
+#pragma unroll
+            for (int c = 0; c < NCG; ++c) {
+                typename M::frag fb = M::load(xp[c] + (size_t)s * 32);
+                acc[0][c] = M::mma(fa0, fb, acc[0][c]);
+                if constexpr (NACC == 2) acc[1][c] = M::mma(fa1, fb, acc[1][c]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NACC; ++q)
+#pragma unroll
+            for (int c = 0; c < NCG; ++c) red[wave][q * NCG + c][lane] = acc[q][c];
+        __syncthreads();
+        // epilogue: 16 rows x (16*NCG) cols; C/D map: row = 4*(lane>>4)+i, col = lane&15
+        for (int o = threadIdx.x; o < 256 * NCG; o += 512) {
+            const int c = o >> 8, rem = o & 255, i = rem >> 6, ln = rem & 63;
+            const int n = n0 + 4 * (ln >> 4) + i;
+            const int col = c0 + 16 * c + (ln & 15);
+            float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                v0 += red[w][c][ln][i];
+                if constexpr (NACC == 2) v1 += red[w][NCG + c][ln][i];
+            }
+            if (n < a.N && col < a.R) {
+                const size_t yi = (size_t)col * a.ldy + n;
+                if (a.bias) v0 += ld(a.bias, n);
+                if constexpr (EPI == EPI_STORE) {
+                    st(a.Y, yi, v0);
+                } else if constexpr (EPI == EPI_RESID) {
+                    st(a.Y, yi, ld(a.res, (size_t)col * a.ldr + n) + rnd<T>(v0));
+                } else if constexpr (EPI == EPI_SWIGLU) {
+                    const float ga = rnd<T>(v0), ub = rnd<T>(v1);
+                    st(a.Y, yi, rnd<T>(silu_f(ga)) * ub);
+                } else {  // EPI_F32: logits as fp32 holding the T-rounded value
+                    a.Yf[yi] = rnd<T>(v0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// =========================================================================================
+// qk-norm + RoPE + KV-cache write (llama.py:894-910, 205-214).  One wave per head.
+// =========================================================================================
+template <typename T>
+__global__ __launch_bounds__(256) void qk_rope_cache_kernel(QkArgs<T> a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = blockIdx.x;
+    const int head = blockIdx.y * 4 + wave;
+    const int nheads = a.nh + 2 * a.nkv;
+    if (head >= nheads) return;
+    const int pos = a.fixed_pos >= 0 ? a.fixed_pos : a.row_pos[r];
+    const int slot = a.row_slot[r];
+    const int hd = a.hd, half = hd >> 1;
+    const T* src = a.qkv + (size_t)r * a.ldqkv + (size_t)head * hd;
+    const int kind = head < a.nh ? 0 : (head < a.nh + a.nkv ? 1 : 2);
+    float x0[2], x1[2];
+    int np = 0;
+    for (int p = lane; p < half; p += 64, ++np) {
+        x0[np] = ld(src, 2 * p);
+        x1[np] = ld(src, 2 * p + 1);
+    }
+    if (kind < 2 && a.qk_norm) {
+        float ss = 0.f;
+        for (int i = 0; i < np; ++i) ss += x0[i] * x0[i] + x1[i] * x1[i];
+        ss = wave_sum(ss);
+        const float rs = 1.0f / sqrtf(ss / (float)hd + a.eps);
+        const T* w = kind == 0 ? a.qn : a.kn;
+        for (int i = 0; i < np; ++i) {
+            const int p = lane + 64 * i;
+            x0[i] = rnd<T>((x0[i] * rs) * ld(w, 2 * p));
+            x1[i] = rnd<T>((x1[i] * rs) * ld(w, 2 * p + 1));
+        }
+    }
+    if (kind < 2) {
+        const float* tab = a.rope + (size_t)pos * hd;
+        for (int i = 0; i < np; ++i) {
+            const int p = lane + 64 * i;
+            const float c = tab[2 * p], s = tab[2 * p + 1];
+            const float y0 = x0[i] * c - x1[i] * s;
+            const float y1 = x1[i] * c + x0[i] * s;
+            x0[i] = rnd<T>(y0);
+            x1[i] = rnd<T>(y1);
+        }
+    }
+    T* dst;
+    if (kind == 0) {
+        dst = a.qout + (size_t)r * a.nh * hd + (size_t)head * hd;
+    } else {
+        const int kvh = kind == 1 ? head - a.nh : head - a.nh - a.nkv;
+        T* base = (kind == 1 ? a.kc : a.vc) + (size_t)slot * a.slot_stride + a.layer_off;
+        dst = base + ((size_t)kvh * a.S + pos) * hd;
+    }
+    for (int i = 0; i < np; ++i) {
+        const int p = lane + 64 * i;
+        st(dst, 2 * p, x0[i]);
+        st(dst, 2 * p + 1, x1[i]);
+    }
+}
+
+// =========================================================================================
+// slow attention: split-K flash decode over the valid prefix [0, pos]
+// grid (R, nkv, nsplit); each wave owns q-heads of the GQA group and the KV tile is shared.
+// =========================================================================================
+template <typename T>
+__global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs<T> a) {
+    __shared__ float qs[4][256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+    const int pos = a.row_pos[r];
+    const int j0 = sp * a.split;
+    if (j0 > pos) return;
+    const int j1 = min(j0 + a.split, pos + 1);
+    const int slot = a.row_slot[r];
+    const int hd = a.hd;
+    const T* kc = a.kc + (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
+    const T* vc = a.vc + (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
+    const int g = a.nh / a.nkv;
+    for (int qh = wave; qh < g; qh += 4) {
+        const int h = kvh * g + qh;
+        const T* q = a.q + (size_t)r * a.nh * hd + (size_t)h * hd;
+        for (int e = lane; e < hd; e += 64) qs[wave][e] = ld(q, e);
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        float m = -INFINITY, l = 0.f;
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int jc = j0; jc < j1; jc += 64) {
+            const int j = jc + lane;
+            float sc = -INFINITY;
+            if (j < j1) {
+                const T* kr = kc + (size_t)j * hd;
+                float dot = 0.f;
+                for (int e = 0; e < hd; e += 8) {
+                    float kv[8];
+                    load8(kr + e, kv);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) dot += qs[wave][e + u] * kv[u];
+                }
+                sc = dot * a.scale;
+            }
+            const float mn = fmaxf(m, wave_max(sc));
+            const float alpha = expf(m - mn);
+            const float p = (j < j1) ? expf(sc - mn) : 0.f;
+            l = l * alpha + wave_sum(p);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] *= alpha;
+            const int nv = min(64, j1 - jc);
+            for (int jj = 0; jj < nv; ++jj) {
+                const float pj = __shfl(p, jj, 64);
+                const T* vr = vc + (size_t)(jc + jj) * hd;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int e = lane + 64 * i;
+                    if (e < hd) o[i] += pj * ld(vr, e);
+                }
+            }
+            m = mn;
+        }
+        float* out = a.part + (((size_t)r * a.nh + h) * a.maxsplit + sp) * (hd + 2);
+        if (lane == 0) {
+            out[0] = m;
+            out[1] = l;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = lane + 64 * i;
+            if (e < hd) out[2 + e] = o[i];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restrict__ part,
+                                                          const int* __restrict__ row_pos, int nh,
+                                                          int hd, int split, int maxsplit,
+                                                          T* __restrict__ out) {
+    const int r = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+    const int ns = row_pos[r] / split + 1;
+    const float* p = part + ((size_t)r * nh + h) * maxsplit * (hd + 2);
+    float M = -INFINITY;
+    for (int s = 0; s < ns; ++s) M = fmaxf(M, p[(size_t)s * (hd + 2)]);
+    float L = 0.f;
+    for (int s = 0; s < ns; ++s) L += p[(size_t)s * (hd + 2) + 1] * expf(p[(size_t)s * (hd + 2)] - M);
+    for (int e = lane; e < hd; e += 64) {
+        float o = 0.f;
+        for (int s = 0; s < ns; ++s)
+            o += p[(size_t)s * (hd + 2) + 2 + e] * expf(p[(size_t)s * (hd + 2)] - M);
+        st(out, (size_t)r * nh * hd + (size_t)h * hd + e, o / L);
+    }
+}
+
+// =========================================================================================
+// fast attention (llama.py:947-975): s = round(round(q.k) * scale), masked j > cpos,
+// p = round(softmax(s)), y = round(p @ v).  grid (R, nh), one wave.
+// =========================================================================================
+template <typename T>
+__global__ __launch_bounds__(64) void fast_attn_kernel(FastAttnArgs<T> a) {
+    const int lane = threadIdx.x;
+    const int r = blockIdx.x, h = blockIdx.y;
+    const int slot = a.row_slot[r];
+    const int hd = a.hd, g = a.nh / a.nkv, kvh = h / g;
+    const T* q = a.q + (size_t)r * a.nh * hd + (size_t)h * hd;
+    const T* kc = a.kc + (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
+    const T* vc = a.vc + (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
+    float sc = -INFINITY;
+    if (lane < a.S && lane <= a.cpos) {
+        float dot = 0.f;
+        for (int e = 0; e < hd; ++e) dot += ld(q, e) * ld(kc + (size_t)lane * hd, e);
+        sc = rnd<T>(rnd<T>(dot) * a.scale);
+    }
+    __shared__ float ps[64];
+    const float mx = wave_max(sc);
+    const float ex = (sc == -INFINITY) ? 0.f : expf(sc - mx);
+    const float den = wave_sum(ex);
+    ps[lane] = rnd<T>(ex / den);
+    __syncthreads();
+    for (int e = lane; e < hd; e += 64) {
+        float o = 0.f;
+        for (int j = 0; j < a.S; ++j) o += ps[j] * ld(vc + (size_t)j * hd, e);
+        st(a.out, (size_t)r * a.nh * hd + (size_t)h * hd + e, o);
+    }
+}
+
+// =========================================================================================
+// sampling (inference.py:43-93) + RAS (117-144).  One block (4 waves) per row.
+// Candidates are (value desc, token id asc): the order of a stable sort (CUDA radix sort).
+// =========================================================================================
+struct Cand {
+    float v;
+    int id;
+};
+__device__ __forceinline__ bool better(float v, int id, float bv, int bid) {
+    return v > bv || (v == bv && id < bid);
+}
+__device__ __forceinline__ void wave_argmax(float& v, int& id) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float ov = __shfl_xor(v, o, 64);
+        int oid = __shfl_xor(id, o, 64);
+        if (better(ov, oid, v, id)) {
+            v = ov;
+            id = oid;
+        }
+    }
+}
+
+template <typename T>
+__device__ int sample_from(const Cand* cand, int K, float M, float den, float temperature,
+                           float top_p, int top_k, uint64_t seed, uint64_t step, uint32_t draw,
+                           int lane) {
+    // lane k < K holds rank k
+    const float v = lane < K ? cand[lane].v : -INFINITY;
+    const int id = lane < K ? cand[lane].id : 0x7fffffff;
+    const float p = (v == -INFINITY) ? 0.f : rnd<T>(expf(v - M) / den);
+    float cum = 0.f, mycum = 0.f;
+    for (int k = 0; k < K; ++k) {
+        cum += __shfl(p, k, 64);
+        if (lane == k) mycum = rnd<T>(cum);
+    }
+    const float t = rnd<T>(temperature), tp = rnd<T>(top_p);
+    const bool keep = lane < K && v != -INFINITY && (lane == 0 || (!(mycum > tp) && lane < top_k));
+    const float tt = fmaxf(t, 1e-5f);
+    const float lt = keep ? rnd<T>(v / tt) : -INFINITY;
+    const float m2 = wave_max(lt);
+    const float e = keep ? expf(lt - m2) : 0.f;
+    const float d2 = wave_sum(e);
+    const float prob = rnd<T>(e / d2);
+    float score = -1.f;
+    if (keep) {
+        const float u = rng_uniform_bf16(seed, step, draw, (uint32_t)id);
+        const float qv = rnd<T>(-logf(u));
+        score = rnd<T>(prob / qv);
+    }
+    int bid = keep ? id : 0x7fffffff;
+    wave_argmax(score, bid);
+    return bid;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void sample_kernel(SampleArgs a) {
+    extern __shared__ float vals[];  // [Nl]
+    __shared__ float scratch[16];
+    __shared__ Cand wl[4][64];
+    __shared__ Cand cand[64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = blockIdx.x;
+    const int slot = a.row_slot[r];
+    const SlotParams sp = a.sp[slot];
+    const float* lg = a.logits + (size_t)r * a.ldl;
+    const int Nl = a.Nl;
+    for (int i = threadIdx.x; i < Nl; i += 256) {
+        float v = lg[i];
+        if (a.slow && sp.mask_im_end && i == Nl - 1) v = -INFINITY;
+        vals[i] = v;
+    }
+    __syncthreads();
+    // token id of row i: slow head rows = [sb..se] + im_end; fast head: identity
+    auto tok_of = [&](int i) { return a.slow ? (i < Nl - 1 ? a.sb + i : a.im_end) : i; };
+    float mloc = -INFINITY;
+    for (int i = threadIdx.x; i < Nl; i += 256) mloc = fmaxf(mloc, vals[i]);
+    const float M = block_max(mloc, scratch);
+    float sloc = 0.f;
+    for (int i = threadIdx.x; i < Nl; i += 256)
+        sloc += (vals[i] == -INFINITY) ? 0.f : expf(vals[i] - M);
+    const float den = block_sum(sloc, scratch);
+    int K = sp.top_k < 1 ? 1 : sp.top_k;
+    if (K > 64) K = 64;
+    if (K > Nl) K = Nl;
+    // ---- per-wave top-K by repeated wave argmax (each lane owns i = wave*64+lane + 256*j)
+    uint32_t taken = 0;
+    const int per = (Nl + 255) / 256;  // <= 32
+    for (int k = 0; k < K; ++k) {
+        float bv = -INFINITY;
+        int bid = 0x7fffffff, bj = -1;
+        for (int j = 0; j < per; ++j) {
+            const int i = wave * 64 + lane + 256 * j;
+            if (i < Nl && !((taken >> j) & 1u)) {
+                const float v = vals[i];
+                const int id = tok_of(i);
+                if (better(v, id, bv, bid)) {
+                    bv = v;
+                    bid = id;
+                    bj = j;
+                }
+            }
+        }
+        float wv = bv;
+        int wid = bid;
+        wave_argmax(wv, wid);
+        if (bj >= 0 && wid == bid && wv == bv) taken |= 1u << bj;
+        if (lane == 0) wl[wave][k] = Cand{wv, wid};
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // merge 4 sorted lists: lane holds entries lane, lane+64, lane+128, lane+192 of wl
+        uint32_t tk = 0;
+        for (int k = 0; k < K; ++k) {
+            float bv = -INFINITY;
+            int bid = 0x7fffffff, bj = -1;
+            for (int j = 0; j < 4; ++j) {
+                const int e = lane + 64 * j;
+                const int w = e / K, kk = e % K;
+                if (e < 4 * K && !((tk >> j) & 1u) && better(wl[w][kk].v, wl[w][kk].id, bv, bid)) {
+                    bv = wl[w][kk].v;
+                    bid = wl[w][kk].id;
+                    bj = j;
+                }
+            }
+            float wv = bv;
+            int wid = bid;
+            wave_argmax(wv, wid);
+            if (bj >= 0 && wid == bid && wv == bv) tk |= 1u << bj;
+            if (lane == 0) cand[k] = Cand{wv, wid};
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t step = (uint64_t)sp.step;
+        int32_t* col = a.cols + (size_t)r * a.ldc;
+        if (a.slow) {
+            int tok = sample_from<T>(cand, K, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed,
+                                     step, 0, lane);
+            const int hi = sample_from<T>(cand, K, M, den, 1.0f, 0.9f, sp.top_k, sp.seed, step, 1,
+                                          lane);
+            if (a.ras_enable) {
+                const int32_t* prev = a.ras + (size_t)slot * a.ras_stride;  // row 0, 10 entries
+                bool inwin = false;
+                for (int j = 0; j < 10; ++j) inwin |= prev[j] == tok;
+                const bool sem = tok >= a.sb && tok <= a.se;
+                if (inwin && sem) tok = hi;
+            }
+            if (lane == 0) {
+                col[0] = tok;
+                int c = tok - a.sb;
+                c = c < 0 ? 0 : (c > a.cb - 1 ? a.cb - 1 : c);
+                col[1] = c;
+            }
+        } else {
+            const int code = sample_from<T>(cand, K, M, den, sp.temperature, sp.top_p, sp.top_k,
+                                            sp.seed, step, (uint32_t)a.draw, lane);
+            if (lane == 0) col[a.col_idx] = code;
+        }
+    }
+}
+
+// =========================================================================================
+// frame bookkeeping: RAS window roll (inference.py:227-230), next input column, pos/step++
+// =========================================================================================
+__global__ void finish_kernel(int R, const int* __restrict__ row_slot, int* __restrict__ row_pos,
+                              const int32_t* __restrict__ cols, int ldc, int32_t* __restrict__ tok_in,
+                              int32_t* __restrict__ ras, int ras_stride, int C1, int update_ras,
+                              SlotParams* __restrict__ sp) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    const int slot = row_slot[r];
+    const int32_t* col = cols + (size_t)r * ldc;
+    for (int q = 0; q < C1; ++q) tok_in[(size_t)slot * C1 + q] = col[q];
+    if (update_ras) {
+        int32_t* w = ras + (size_t)slot * ras_stride;
+        for (int q = 0; q < C1; ++q) {
+            for (int j = 0; j < 9; ++j) w[q * 10 + j] = w[q * 10 + j + 1];
+            w[q * 10 + 9] = col[q];
+        }
+    }
+    row_pos[r] += 1;
+    sp[slot].step += 1;
+}
+
+// =========================================================================================
+// synthetic weights (fishmi/synth.py formula) and small utilities
+// =========================================================================================
+template <typename T>
+__global__ void synth_kernel(T* __restrict__ dst, int64_t n, uint64_t base, float center,
+                             float scale) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t m = (int64_t)(splitmix64(base + (uint64_t)i) >> 40);
+        const float rr = (float)(2 * m - (1 << 24)) * scale;
+        const float v = __fadd_rn(center, rr);
+        st(dst, i, bfround(v));  // synthetic weights are bf16-valued in both precisions
+    }
+}
+
+template <typename T>
+__global__ void convert_kernel(const void* __restrict__ src, int src_bf16, int64_t n,
+                               T* __restrict__ dst) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float v = src_bf16 ? bf2f(((const bf16_t*)src)[i]) : ((const float*)src)[i];
+        st(dst, i, v);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------------
+template <typename T>
+void launch_embed(hipStream_t s, const int32_t* tok, int R, const T* emb, const T* cbemb, int d,
+                  int C, int cb, int sb, int se, int scale, T* x, const int* row_slot) {
+    embed_kernel<T><<<R, 256, 0, s>>>(tok, R, emb, cbemb, d, C, cb, sb, se, scale, x, row_slot);
+}
+template <typename T>
+void launch_gather_rows(hipStream_t s, const int32_t* codes, int ldc, int col, const T* table,
+                        int d, int R, T* x) {
+    gather_rows_kernel<T><<<R, 256, 0, s>>>(codes, ldc, col, table, d, x);
+}
+template <typename T>
+void launch_rmsnorm(hipStream_t s, const T* x, int ldx, const T* w, int d, float eps, T* y,
+                    int ldy, int R) {
+    rmsnorm_kernel<T><<<R, 256, 0, s>>>(x, ldx, w, d, eps, y, ldy);
+}
+
+template <typename T, int EPI>
+static void linear_dispatch(hipStream_t s, const LinearArgs<T>& a) {
+    const int grid = FM_CEIL(a.N, 16);
+    if (a.R <= 16)
+        linear_kernel<T, 1, EPI><<<grid, 512, 0, s>>>(a);
+    else if (a.R <= 32)
+        linear_kernel<T, 2, EPI><<<grid, 512, 0, s>>>(a);
+    else
+        linear_kernel<T, 4, EPI><<<grid, 512, 0, s>>>(a);
+}
+template <typename T> void launch_linear(hipStream_t s, const LinearArgs<T>& a, int epi) {
+    switch (epi) {
+        case EPI_STORE: linear_dispatch<T, EPI_STORE>(s, a); break;
+        case EPI_RESID: linear_dispatch<T, EPI_RESID>(s, a); break;
+        case EPI_SWIGLU: linear_dispatch<T, EPI_SWIGLU>(s, a); break;
+        default: linear_dispatch<T, EPI_F32>(s, a); break;
+    }
+}
+template <typename T> void launch_qk_rope_cache(hipStream_t s, const QkArgs<T>& a, int R) {
+    dim3 grid(R, FM_CEIL(a.nh + 2 * a.nkv, 4));
+    qk_rope_cache_kernel<T><<<grid, 256, 0, s>>>(a);
+}
+template <typename T> void launch_attn(hipStream_t s, const AttnArgs<T>& a, int R, int nsplit, T* out) {
+    dim3 g1(R, a.nkv, nsplit);
+    attn_split_kernel<T><<<g1, 256, 0, s>>>(a);
+    dim3 g2(R, a.nh);
+    attn_combine_kernel<T><<<g2, 64, 0, s>>>(a.part, a.row_pos, a.nh, a.hd, a.split, a.maxsplit, out);
+}
+template <typename T> void launch_fast_attn(hipStream_t s, const FastAttnArgs<T>& a, int R) {
+    dim3 g(R, a.nh);
+    fast_attn_kernel<T><<<g, 64, 0, s>>>(a);
+}
+template <typename T> void launch_sample(hipStream_t s, const SampleArgs& a, int R) {
+    sample_kernel<T><<<R, 256, sizeof(float) * a.Nl, s>>>(a);
+}
+void launch_finish(hipStream_t s, int R, const int* row_slot, int* row_pos, const int32_t* cols,
+                   int ldc, int32_t* tok_in, int32_t* ras, int ras_stride, int C1, int update_ras,
+                   SlotParams* sp) {
+    finish_kernel<<<FM_CEIL(R, 64), 64, 0, s>>>(R, row_slot, row_pos, cols, ldc, tok_in, ras,
+                                               ras_stride, C1, update_ras, sp);
+}
+template <typename T>
+void launch_synth(hipStream_t s, T* dst, int64_t n, uint64_t seed, uint32_t tid, float center,
+                  int log2_half) {
+    const uint64_t base = seed * 0xD1B54A32D192ED03ull + (uint64_t)tid * 0x9E3779B97F4A7C15ull;
+    const float scale = ldexpf(1.0f, -24 - log2_half);
+    int blocks = (int)std::min<int64_t>(FM_CEIL(n, 256), 8192);
+    synth_kernel<T><<<blocks, 256, 0, s>>>(dst, n, base, center, scale);
+}
+template <typename T>
+void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* dst) {
+    int blocks = (int)std::min<int64_t>(FM_CEIL(n, 256), 8192);
+    convert_kernel<T><<<blocks, 256, 0, s>>>(src, src_bf16, n, dst);
+}
+
+#define INST(T)                                                                                  \
+    template void launch_embed<T>(hipStream_t, const int32_t*, int, const T*, const T*, int, int, \
+                                  int, int, int, int, T*, const int*);                           \
+    template void launch_gather_rows<T>(hipStream_t, const int32_t*, int, int, const T*, int, int, \
+                                        T*);                                                     \
+    template void launch_rmsnorm<T>(hipStream_t, const T*, int, const T*, int, float, T*, int, int); \
+    template void launch_linear<T>(hipStream_t, const LinearArgs<T>&, int);                      \
+    template void launch_qk_rope_cache<T>(hipStream_t, const QkArgs<T>&, int);                   \
+    template void launch_attn<T>(hipStream_t, const AttnArgs<T>&, int, int, T*);                 \
+    template void launch_fast_attn<T>(hipStream_t, const FastAttnArgs<T>&, int);                 \
+    template void launch_sample<T>(hipStream_t, const SampleArgs&, int);                         \
+    template void launch_synth<T>(hipStream_t, T*, int64_t, uint64_t, uint32_t, float, int);    \
+    template void launch_convert<T>(hipStream_t, const void*, int, int64_t, T*);
+INST(bf16_t)
+INST(float)

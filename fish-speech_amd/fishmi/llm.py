@@ -1,0 +1,183 @@
+"""Dual-AR model on libfishmi: the drop-in for DualARTransformer + decode_one_token_ar.
+
+Mirrors the reference's seams (fish_speech/models/text2semantic/llama.py and inference.py):
+  * ``DualARModel.from_pretrained(path)``  <- BaseTransformer.from_pretrained (llama.py:479-593)
+  * ``model.generate(prompt, ...)``         <- inference.generate (inference.py:241-359)
+  * ``model.decode_one_token(...)``         <- decode_one_token_ar (inference.py:96-181), batched
+  * ``model.teacher_step(...)``             <- forward_generate + forward_generate_fast
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+from . import native
+from .checkpoint import Tensor, llm_tensor_shapes, load_llm_weights
+from .config import DualARConfig
+from .synth import llm_rule
+
+IM_END_TOKEN = "<|im_end|>"
+
+
+def resolve_im_end_id(path) -> Optional[int]:
+    """FishTokenizer.get_token_id(IM_END_TOKEN) (tokenizer.py) from tokenizer.json, offline."""
+    p = Path(path)
+    tj = p / "tokenizer.json"
+    if tj.exists():
+        with open(tj, encoding="utf-8") as f:
+            data = json.load(f)
+        for t in data.get("added_tokens", []):
+            if t.get("content") == IM_END_TOKEN:
+                return int(t["id"])
+        vocab = data.get("model", {}).get("vocab", {})
+        if isinstance(vocab, dict) and IM_END_TOKEN in vocab:
+            return int(vocab[IM_END_TOKEN])
+    return None
+
+
+class DualARModel:
+    def __init__(self, cfg: DualARConfig, device: int = 0, precision: str = "bf16",
+                 max_slots: int = 1):
+        if cfg.im_end_id < 0:
+            raise ValueError("config.im_end_id must be set (tokenizer's <|im_end|> id)")
+        self.cfg = cfg
+        self.device = device
+        self.precision = precision
+        self.max_slots = max_slots
+        self.C1 = cfg.num_codebooks + 1
+        L = native.lib()
+        if native.device_count() < 1:
+            raise native.FishMIError("no HIP device visible; libfishmi has no CPU fallback")
+        self._c = cfg.to_c()
+        h = ctypes.c_void_p()
+        prec = native.FM_PREC_BF16 if precision == "bf16" else native.FM_PREC_FP32
+        native.check(L.fm_llm_open(ctypes.byref(self._c), device, prec, max_slots, ctypes.byref(h)))
+        self.h = h
+        self._finalized = False
+
+    # ---- construction --------------------------------------------------------------
+    @classmethod
+    def from_pretrained(cls, path, device: int = 0, precision: str = "bf16", max_slots: int = 1,
+                        max_length: Optional[int] = None, im_end_id: Optional[int] = None):
+        cfg = DualARConfig.from_pretrained(path)
+        if max_length is not None:
+            cfg.max_seq_len = max_length
+        im = im_end_id if im_end_id is not None else resolve_im_end_id(path)
+        if im is None:
+            raise ValueError(f"cannot resolve <|im_end|> id: no tokenizer.json in {path}; pass im_end_id")
+        cfg.im_end_id = im
+        m = cls(cfg, device, precision, max_slots)
+        m.load_weights(load_llm_weights(path))
+        m.finalize()
+        return m
+
+    @classmethod
+    def synthetic(cls, cfg: DualARConfig, seed: int, log2_half: int = 5, device: int = 0,
+                  precision: str = "bf16", max_slots: int = 1):
+        m = cls(cfg, device, precision, max_slots)
+        m.synth(seed, log2_half)
+        m.finalize()
+        return m
+
+    def load_weights(self, weights: "dict[str, Tensor]"):
+        L = native.lib()
+        shapes = llm_tensor_shapes(self.cfg)
+        missing = [k for k in shapes if k not in weights]
+        if missing:
+            raise KeyError(f"checkpoint lacks {len(missing)} tensors, e.g. {missing[:3]}")
+        for name in shapes:
+            t = weights[name]
+            a = np.ascontiguousarray(t.data)
+            dt = native.FM_DT_BF16 if t.bf16 else native.FM_DT_F32
+            if not t.bf16:
+                a = np.ascontiguousarray(a, dtype=np.float32)
+            native.check(L.fm_llm_set_tensor(self.h, name.encode(), a.ctypes.data_as(ctypes.c_void_p),
+                                             dt, a.size))
+
+    def synth(self, seed: int, log2_half: int = 5):
+        L = native.lib()
+        for name, shape in llm_tensor_shapes(self.cfg).items():
+            c, e = llm_rule(name, log2_half)
+            native.check(L.fm_llm_synth_tensor(self.h, name.encode(), int(np.prod(shape)), seed, c, e))
+
+    def finalize(self):
+        native.check(native.lib().fm_llm_finalize(self.h))
+        self._finalized = True
+
+    def close(self):
+        if getattr(self, "h", None):
+            native.lib().fm_llm_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- decode ----------------------------------------------------------------------
+    @staticmethod
+    def sampling(temperature=0.7, top_p=0.9, top_k=30, seed=0, mask_im_end=False):
+        return native.SamplingC(float(temperature), float(top_p), int(top_k), int(seed) & (2**64 - 1),
+                                int(bool(mask_im_end)))
+
+    def prefill(self, slot: int, prompt: np.ndarray, sampling) -> np.ndarray:
+        p = np.ascontiguousarray(prompt, dtype=np.int32)
+        assert p.shape[0] == self.C1
+        col = np.zeros(self.C1, np.int32)
+        native.check(native.lib().fm_llm_prefill(self.h, slot, native.i32p(p), p.shape[1],
+                                                 ctypes.byref(sampling), native.i32p(col)))
+        return col
+
+    def decode(self, slots) -> np.ndarray:
+        s = np.ascontiguousarray(slots, dtype=np.int32)
+        out = np.zeros((s.size, self.C1), np.int32)
+        native.check(native.lib().fm_llm_decode(self.h, native.i32p(s), s.size, native.i32p(out)))
+        return out
+
+    def generate(self, prompt: np.ndarray, max_new_tokens: int, temperature=0.7, top_p=0.9,
+                 top_k=30, seed=0, slot=0, mask_im_end=False) -> np.ndarray:
+        """inference.generate: returns the emitted columns (C+1, n) (seq[:, T:])."""
+        p = np.ascontiguousarray(prompt, dtype=np.int32)
+        T = p.shape[1]
+        mx = max_new_tokens if (max_new_tokens and T + max_new_tokens <= self.cfg.max_seq_len) \
+            else self.cfg.max_seq_len - T
+        out = np.zeros((self.C1, mx), np.int32)
+        n = ctypes.c_int(0)
+        sp = self.sampling(temperature, top_p, top_k, seed, mask_im_end)
+        native.check(native.lib().fm_llm_generate(self.h, slot, native.i32p(p), T, mx,
+                                                  ctypes.byref(sp), native.i32p(out), ctypes.byref(n)))
+        return out[:, : n.value]
+
+    def teacher_step(self, x: np.ndarray, pos0: int, next_col=None, slot: int = 0):
+        xx = np.ascontiguousarray(x, dtype=np.int32)
+        lg = np.zeros(self.cfg.vocab_size, np.float32)
+        hid = np.zeros(self.cfg.fast_dim, np.float32)
+        fl = np.zeros((self.cfg.num_codebooks - 1, self.cfg.codebook_size), np.float32)
+        nc = np.ascontiguousarray(next_col, dtype=np.int32) if next_col is not None else None
+        native.check(native.lib().fm_llm_teacher_step(
+            self.h, slot, native.i32p(xx), xx.shape[1], pos0,
+            native.i32p(nc) if nc is not None else None, native.f32p(lg), native.f32p(hid),
+            native.f32p(fl) if nc is not None else None))
+        return lg, hid, (fl if nc is not None else None)
+
+    # ---- accounting / profiling --------------------------------------------------------
+    def frame_bytes(self, n: int, pos: int) -> int:
+        return int(native.lib().fm_llm_frame_bytes(self.h, n, pos))
+
+    def profile(self, enable: bool):
+        native.check(native.lib().fm_llm_profile(self.h, int(enable)))
+
+    def profile_read(self, cls: str):
+        ms, n, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+        native.check(native.lib().fm_llm_profile_read(self.h, cls.encode(), ctypes.byref(ms),
+                                                      ctypes.byref(n), ctypes.byref(b)))
+        return ms.value, n.value, b.value
+
+    def use_graph(self, enable: bool):
+        native.check(native.lib().fm_llm_use_graph(self.h, int(enable)))

@@ -1,0 +1,99 @@
+"""ctypes binding of libfishmi.so (include/fishmi.h).
+
+The product path is this library and nothing else: if it is missing or no GPU is visible,
+construction fails loudly (there is no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfishmi.so")
+
+FM_PREC_BF16, FM_PREC_FP32 = 0, 1
+FM_DT_F32, FM_DT_BF16 = 0, 1
+
+_lib = None
+
+# every symbol include/fishmi.h declares (checked by tests/test_abi.py)
+ABI_SYMBOLS = [
+    "fm_device_count", "fm_last_error", "fm_llm_open", "fm_llm_set_tensor", "fm_llm_synth_tensor",
+    "fm_llm_finalize", "fm_llm_prefill", "fm_llm_decode", "fm_llm_generate", "fm_llm_teacher_step",
+    "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_use_graph",
+    "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
+    "fm_codec_finalize", "fm_codec_decode", "fm_codec_profile_read", "fm_codec_close",
+]
+
+
+class FishMIError(RuntimeError):
+    pass
+
+
+class SamplingC(ctypes.Structure):
+    _fields_ = [("temperature", ctypes.c_float), ("top_p", ctypes.c_float),
+                ("top_k", ctypes.c_int), ("seed", ctypes.c_uint64), ("mask_im_end", ctypes.c_int)]
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FishMIError(f"{LIB_PATH} is missing: build it with `make -C fish-speech_amd` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64
+    f32 = ctypes.c_float
+    pi32 = ctypes.POINTER(ctypes.c_int32)
+    pf32 = ctypes.POINTER(ctypes.c_float)
+    L.fm_last_error.restype = ctypes.c_char_p
+    L.fm_device_count.restype = i32
+    L.fm_llm_open.argtypes = [vp, i32, i32, i32, ctypes.POINTER(vp)]
+    L.fm_llm_set_tensor.argtypes = [vp, ctypes.c_char_p, vp, i32, i64]
+    L.fm_llm_synth_tensor.argtypes = [vp, ctypes.c_char_p, i64, u64, f32, i32]
+    L.fm_llm_finalize.argtypes = [vp]
+    L.fm_llm_prefill.argtypes = [vp, i32, pi32, i32, ctypes.POINTER(SamplingC), pi32]
+    L.fm_llm_decode.argtypes = [vp, pi32, i32, pi32]
+    L.fm_llm_generate.argtypes = [vp, i32, pi32, i32, i32, ctypes.POINTER(SamplingC), pi32,
+                                  ctypes.POINTER(ctypes.c_int)]
+    L.fm_llm_teacher_step.argtypes = [vp, i32, pi32, i32, i32, pi32, pf32, pf32, pf32]
+    L.fm_llm_frame_bytes.argtypes = [vp, i32, i32]
+    L.fm_llm_frame_bytes.restype = i64
+    L.fm_llm_profile.argtypes = [vp, i32]
+    L.fm_llm_profile_read.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    L.fm_llm_use_graph.argtypes = [vp, i32]
+    L.fm_llm_close.argtypes = [vp]
+    if hasattr(L, "fm_codec_open"):
+        L.fm_codec_open.argtypes = [vp, i32, i32, i32, ctypes.POINTER(vp)]
+        L.fm_codec_set_tensor.argtypes = [vp, ctypes.c_char_p, vp, i32, i64]
+        L.fm_codec_synth_tensor.argtypes = [vp, ctypes.c_char_p, i64, u64, f32, i32]
+        L.fm_codec_finalize.argtypes = [vp]
+        L.fm_codec_decode.argtypes = [vp, pi32, i32, pf32]
+        L.fm_codec_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_int64),
+                                            ctypes.POINTER(ctypes.c_double)]
+        L.fm_codec_close.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc != 0:
+        raise FishMIError(f"libfishmi error {rc}: {lib().fm_last_error().decode()}")
+    return rc
+
+
+def device_count() -> int:
+    return lib().fm_device_count()
+
+
+def i32p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def f32p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))

@@ -1,0 +1,144 @@
+/*
+ * fishmi.h -- C ABI of libfishmi.so, the MI355X-native Fish-Speech S2-Pro hot path:
+ * the Dual-AR text->semantic decode loop and the modded-DAC codec decode.
+ *
+ * The reference has no FFI/plugin API for this path; its seams are Python
+ * callables.  Each entry point below replaces one of them (file:line in the reference,
+ * PoTaTo-Mika/fish-speech @ 2026-04-03):
+ *
+ *   fm_llm_open/set_tensor/finalize  <- DualARTransformer.from_pretrained + init_model +
+ *                                       setup_caches           (llama.py:479-593, 307-324,
+ *                                                               707-721; inference.py:362-392)
+ *   fm_llm_prefill                   <- generate() prefill: decode_one_token_ar(prompt,
+ *                                       arange(T))             (inference.py:322-335)
+ *   fm_llm_decode                    <- decode_one_token_ar per frame, batched over slots
+ *                                                              (inference.py:96-181, 209-234)
+ *   fm_llm_generate                  <- generate()             (inference.py:241-359)
+ *   fm_llm_teacher_step              <- forward_generate + forward_generate_fast with given
+ *                                       tokens (teacher forcing; parity tests)
+ *                                                              (llama.py:390-466, 798-827)
+ *   fm_codec_open/set_tensor/...     <- load_codec_model / dac.inference.load_model
+ *                                                              (inference.py:395-417;
+ *                                                               dac/inference.py:23-47)
+ *   fm_codec_decode                  <- DAC.from_indices       (modded_dac.py:925-927)
+ *
+ * Conventions: every function returns FM_OK (0) or a negative FM_ERR_*; the message of the
+ * last failure on the calling thread is fm_last_error().  Nothing throws across the ABI.
+ * Buffers are caller-owned host memory.  One handle per GPU; calls on a handle must come from
+ * one host thread at a time (the reference's single LLM worker thread, inference.py:748-799).
+ * Token matrices are (C+1) x T row-major int32, exactly the reference's prompt layout
+ * (row 0 = text/semantic token, rows 1..C = codebooks).
+ */
+#ifndef FISHMI_H
+#define FISHMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FM_OK 0
+#define FM_ERR_ARG -1
+#define FM_ERR_HIP -2
+#define FM_ERR_STATE -3
+#define FM_ERR_OOM -4
+
+/* precision of the compute path: bf16 storage + fp32 accumulation (production), or the fp32
+   validation mode (same kernels, fp32 storage) used for token-exact parity. */
+#define FM_PREC_BF16 0
+#define FM_PREC_FP32 1
+
+/* source dtype for fm_*_set_tensor */
+#define FM_DT_F32 0
+#define FM_DT_BF16 1
+
+/* == DualARModelArgs after from_pretrained (llama.py:27-193); im_end_id from the tokenizer. */
+typedef struct fm_model_config {
+    int vocab_size, dim, n_layer, n_head, n_local_heads, head_dim, intermediate_size;
+    float rope_base, norm_eps;
+    int max_seq_len;
+    int qkv_bias, o_bias, qk_norm, tie_word_embeddings;
+    int codebook_size, num_codebooks, semantic_begin_id, semantic_end_id, im_end_id;
+    int scale_codebook_embeddings, norm_fastlayer_input;
+    int n_fast_layer, fast_dim, fast_n_head, fast_n_local_heads, fast_head_dim,
+        fast_intermediate_size;
+    int fast_qkv_bias, fast_o_bias, fast_qk_norm;
+} fm_model_config;
+
+/* sampling knobs of decode_one_token_ar; temperature/top_p are applied as tensors of the
+   compute dtype like inference.py:305-306.  mask_im_end=1 forbids <|im_end|> (fixed-length
+   timing runs). */
+typedef struct fm_sampling {
+    float temperature, top_p;
+    int top_k;
+    uint64_t seed;
+    int mask_im_end;
+} fm_sampling;
+
+typedef struct fm_llm fm_llm;
+
+int fm_device_count(void);
+const char* fm_last_error(void);
+
+int fm_llm_open(const fm_model_config* cfg, int device, int precision, int max_slots,
+                fm_llm** out);
+/* name = reference state_dict key after remap (e.g. "layers.3.attention.wqkv.weight") */
+int fm_llm_set_tensor(fm_llm* h, const char* name, const void* host_data, int src_dtype,
+                      int64_t numel);
+/* deterministic synthetic tensor (fishmi/synth.py formula), generated on the device */
+int fm_llm_synth_tensor(fm_llm* h, const char* name, int64_t numel, uint64_t seed, float center,
+                        int log2_half);
+int fm_llm_finalize(fm_llm* h);
+/* resets slot's caches and runs the prompt; writes the first emitted column (C+1). */
+int fm_llm_prefill(fm_llm* h, int slot, const int32_t* tokens, int T, const fm_sampling* sp,
+                   int32_t* first_col);
+/* one frame for n slots (each continues from its own position); cols: n x (C+1) */
+int fm_llm_decode(fm_llm* h, const int32_t* slots, int n, int32_t* cols);
+/* full generate() for one slot: out (C+1) x max_new row-major; *n_out frames produced
+   (stops after emitting <|im_end|> unless mask_im_end). */
+int fm_llm_generate(fm_llm* h, int slot, const int32_t* prompt, int T, int max_new,
+                    const fm_sampling* sp, int32_t* out, int* n_out);
+/* teacher forcing for parity: run S positions of x ((C+1) x S) from pos0 on slot (pos0 == 0
+   resets the slot), return the last position's slow logits (V, with the semantic bias NOT
+   applied), the fast hidden (fast_dim), and -- when next_col != NULL -- the fast logits
+   ((C-1) x codebook_size) obtained by feeding next_col's codebook tokens. */
+int fm_llm_teacher_step(fm_llm* h, int slot, const int32_t* x, int S, int pos0,
+                        const int32_t* next_col, float* slow_logits, float* hidden,
+                        float* fast_logits);
+/* decode-step accounting for the roofline: algorithmic HBM bytes of one frame at batch n
+   (weights read once per frame + KV + embeddings) at cached length `pos`. */
+int64_t fm_llm_frame_bytes(fm_llm* h, int n, int pos);
+/* per-kernel-class timing (HIP events on the compute stream) */
+int fm_llm_profile(fm_llm* h, int enable);
+int fm_llm_profile_read(fm_llm* h, const char* kernel_class, double* total_ms, int64_t* launches,
+                        int64_t* bytes);
+int fm_llm_use_graph(fm_llm* h, int enable);
+int fm_llm_close(fm_llm* h);
+
+/* ---- codec (modded DAC decode side, modded_dac_vq.yaml shapes) --------------------- */
+typedef struct fm_codec_config {
+    int latent, decoder_dim, n_codebooks, codebook_size, semantic_codebook_size, codebook_dim;
+    int t_layers, t_heads, t_head_dim, t_inter, window;
+    float rope_base, norm_eps;
+} fm_codec_config;
+
+typedef struct fm_codec fm_codec;
+
+int fm_codec_open(const fm_codec_config* cfg, int device, int precision, int max_frames,
+                  fm_codec** out);
+int fm_codec_set_tensor(fm_codec* h, const char* name, const void* host_data, int src_dtype,
+                        int64_t numel);
+int fm_codec_synth_tensor(fm_codec* h, const char* name, int64_t numel, uint64_t seed,
+                          float center, int log2_half);
+int fm_codec_finalize(fm_codec* h);
+/* codes: (n_codebooks+1) x T row-major (clamped like rvq.py:354-359, input not mutated);
+   pcm: 2048*T floats in [-1, 1]. */
+int fm_codec_decode(fm_codec* h, const int32_t* codes, int T, float* pcm);
+int fm_codec_profile_read(fm_codec* h, double* total_ms, int64_t* launches, double* flops);
+int fm_codec_close(fm_codec* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FISHMI_H */

@@ -1,0 +1,192 @@
+"""GPU parity of the Dual-AR decode path (libfishmi, called through the C ABI) against the
+reference goldens and the CPU oracle.  Run on the MI355X box: pytest -m gpu."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+IM_END = 4
+
+
+def _cfg(name):
+    from fishmi.config import DualARConfig
+
+    cfg = DualARConfig.from_pretrained(os.path.join(GOLDEN, name))
+    cfg.im_end_id = IM_END
+    return cfg
+
+
+def _model(name, tag, golden, max_slots=1):
+    from fishmi.checkpoint import load_llm_weights
+    from fishmi.llm import DualARModel
+
+    g = golden(f"{name}_{tag}.npz")
+    cfg = _cfg(name)
+    prec = "bf16" if tag == "bf16" else "fp32"
+    m = DualARModel(cfg, 0, prec, max_slots)
+    if name == "llm_a":
+        m.load_weights(load_llm_weights(os.path.join(GOLDEN, name)))
+    else:
+        m.synth(int(g["synth_seed"]), int(g["log2_half"]))
+    m.finalize()
+    return m, g, cfg
+
+
+@pytest.mark.parametrize("name", ["llm_a", "llm_b"])
+def test_fp32_greedy_tokens_exact(name, golden):
+    """fp32 validation mode of the same kernels: free-running greedy == reference tokens."""
+    m, g, _ = _model(name, "fp32", golden)
+    T = g["prompt"].shape[1]
+    ref = g["seq"][:, T:]
+    out = m.generate(g["prompt"], ref.shape[1], top_k=1)
+    np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("name", ["llm_a", "llm_b"])
+def test_fp32_teacher_forced_logits(name, golden):
+    m, g, cfg = _model(name, "fp32", golden)
+    T = g["prompt"].shape[1]
+    seq = g["seq"]
+    x, pos = g["prompt"], 0
+    for i in range(seq.shape[1] - T):
+        col = seq[:, T + i]
+        lg, hid, fl = m.teacher_step(x, pos, next_col=col)
+        ref = g["slow_logits"][i]
+        fin = np.isfinite(ref)
+        assert np.array_equal(np.isfinite(lg), fin)
+        np.testing.assert_allclose(lg[fin], ref[fin], atol=1e-4, rtol=0)
+        np.testing.assert_allclose(hid, g["hidden"][i], atol=1e-4, rtol=0)
+        np.testing.assert_allclose(fl, g["fast_logits"][i], atol=1e-4, rtol=0)
+        pos = T + i
+        x = col.reshape(-1, 1)
+
+
+def _margin(v):
+    s = np.sort(v[np.isfinite(v)])[::-1]
+    return s[0] - s[1]
+
+
+@pytest.mark.parametrize("name", ["llm_a", "llm_b"])
+def test_bf16_teacher_forced_top1(name, golden):
+    """bf16 production mode: logits within bf16 noise of the reference's; top-1 agrees wherever
+    the reference's top-1/top-2 margin exceeds that noise."""
+    m, g, cfg = _model(name, "bf16", golden)
+    T = g["prompt"].shape[1]
+    seq = g["seq"]
+    x, pos = g["prompt"], 0
+    checked = agree = 0
+    for i in range(seq.shape[1] - T):
+        col = seq[:, T + i]
+        lg, hid, fl = m.teacher_step(x, pos, next_col=col)
+        ref = g["slow_logits"][i]
+        fin = np.isfinite(ref)
+        assert np.abs(lg[fin] - ref[fin]).max() <= 0.08 * max(1.0, np.abs(ref[fin]).max())
+        if _margin(ref) > 0.07:
+            checked += 1
+            agree += int(np.argmax(lg) == np.argmax(ref))
+        for c in range(cfg.num_codebooks - 1):
+            rf = g["fast_logits"][i, c]
+            assert np.abs(fl[c] - rf).max() <= 0.08 * max(1.0, np.abs(rf).max())
+            if _margin(rf) > 0.07:
+                checked += 1
+                agree += int(np.argmax(fl[c]) == np.argmax(rf))
+        pos = T + i
+        x = col.reshape(-1, 1)
+    assert checked > 20 and agree == checked
+
+
+def test_graph_matches_eager(golden):
+    m, g, _ = _model("llm_a", "bf16", golden)
+    T = g["prompt"].shape[1]
+    m.use_graph(False)
+    a = m.generate(g["prompt"], 20, top_k=30, seed=7)
+    m.use_graph(True)
+    b = m.generate(g["prompt"], 20, top_k=30, seed=7)
+    np.testing.assert_array_equal(a, b)
+
+
+def test_sampling_matches_oracle_fp32(golden):
+    """top_k=30 / top_p / temperature / RAS with the shared counter-based RNG: the GPU stream
+    equals the CPU restatement's (fp32 mode, so logits agree to ~1e-6)."""
+    import oracle as O
+
+    m, g, cfg = _model("llm_a", "fp32", golden)
+    o = O.OracleLLM(cfg, False)
+    from fishmi.checkpoint import load_llm_weights
+
+    o.load(load_llm_weights(os.path.join(GOLDEN, "llm_a")))
+    for seed in (1, 2, 3):
+        ref = o.generate(g["prompt"], 24, temperature=0.7, top_p=0.9, top_k=30, seed=seed)
+        out = m.generate(g["prompt"], 24, temperature=0.7, top_p=0.9, top_k=30, seed=seed)
+        np.testing.assert_array_equal(out, ref)
+
+
+def test_batched_slots_match_single(golden):
+    """Config-3 style batching: n slots decoded together give each slot's batch-1 stream."""
+    from fishmi.llm import DualARModel
+
+    m, g, cfg = _model("llm_b", "fp32", golden, max_slots=4)
+    rng = np.random.default_rng(0)
+    prompts = []
+    for s in range(4):
+        p = g["prompt"].copy()
+        p[0, 1:5] = rng.integers(16, cfg.semantic_begin_id, 4)
+        prompts.append(p)
+    n_new = 12
+    single = [m.generate(p, n_new, top_k=1, slot=s, mask_im_end=True) for s, p in enumerate(prompts)]
+    sp = DualARModel.sampling(top_k=1, mask_im_end=True)
+    cols = [[m.prefill(s, p, sp)] for s, p in enumerate(prompts)]
+    for _ in range(n_new - 1):
+        out = m.decode([0, 1, 2, 3])
+        for s in range(4):
+            cols[s].append(out[s])
+    for s in range(4):
+        np.testing.assert_array_equal(np.stack(cols[s], axis=1), single[s])
+
+
+def test_wide_real_widths_vs_reference(golden):
+    """S2-Pro widths (d=2560, 32/8x128 heads, I=9728, V=155776, C=10, cb=4096) at reduced depth,
+    bf16: teacher-forced logits/top-1 vs the reference goldens."""
+    from fishmi.llm import DualARModel
+
+    g = golden("llm_wide_bf16.npz")
+    cfg = _cfg("llm_wide")
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 1)
+    T = g["prompt"].shape[1]
+    seq, rows = g["seq"], g["slow_rows"]
+    x, pos = g["prompt"], 0
+    for i in range(seq.shape[1] - T):
+        col = seq[:, T + i]
+        lg, hid, fl = m.teacher_step(x, pos, next_col=col)
+        ref = g["slow_logits"][i]
+        assert np.abs(lg[rows] - ref).max() < 0.05 * max(1.0, np.abs(ref).max())
+        if _margin(ref) > 0.07:
+            assert rows[np.argmax(lg[rows])] == rows[np.argmax(ref)]
+        for c in range(cfg.num_codebooks - 1):
+            rf = g["fast_logits"][i, c]
+            assert np.abs(fl[c] - rf).max() < 0.05 * max(1.0, np.abs(rf).max())
+        pos = T + i
+        x = col.reshape(-1, 1)
+
+
+def test_im_end_stops_and_masking(golden):
+    """generate() stops after emitting <|im_end|> (inference.py:233); mask_im_end forbids it."""
+    m, g, cfg = _model("llm_a", "fp32", golden)
+    out = m.generate(g["prompt"], 40, top_k=30, seed=11, mask_im_end=True)
+    assert out.shape[1] == 40 and not (out[0] == IM_END).any()
+    assert ((out[0] >= cfg.semantic_begin_id) & (out[0] <= cfg.semantic_end_id)).all()
+    assert (out[1] == out[0] - cfg.semantic_begin_id).all()
+
+
+def test_profile_counters(golden):
+    m, g, cfg = _model("llm_a", "bf16", golden)
+    m.profile(True)
+    m.generate(g["prompt"], 4, top_k=1)
+    ms, n, b = m.profile_read("linear")
+    assert n > 0 and ms > 0 and b > 0
+    m.profile(False)
+    assert m.frame_bytes(1, 30) > 0
