@@ -1,0 +1,470 @@
+// fm_attn.hip -- decode attention with the qk-norm / RoPE / KV-cache write fused in, and the
+// radix-select sampler.
+//
+//   attn_decode_kernel  slow model, one row per stream: grid (R, nkv, splits of 64 positions).
+//                       The block of the split holding `pos` normalises+ropes k and v of the new
+//                       position (llama.py:894-910), writes them to the cache (llama.py:205-214)
+//                       and uses them from LDS; every block ropes its GQA group's q heads.  K/V
+//                       tiles are staged once per block in LDS (padded rows) and shared by the
+//                       group's q heads (no repeat_interleave, llama.py:912-913).  Output: split
+//                       partials (m, l, o) combined by attn_combine_kernel (fm_llm_kernels.hip).
+//   fast_attn_fused     fast model (llama.py:947-975) at codebook position cpos: same fusion,
+//                       every rounding of the matmul-softmax-matmul reproduced.
+//   sample_radix_kernel top-k via 4-pass radix select on order-preserving keys + rank-by-count
+//                       ordering (value desc, token id asc: the order of a stable sort), then
+//                       top-p / temperature / multinomial with the shared counter RNG
+//                       (inference.py:43-93) and RAS (inference.py:117-144).
+#include "fm_kernels.h"
+
+// normalise (optional) + rope one head held as pairs by a wave (lane p owns pair p, p+64)
+template <typename T>
+__device__ __forceinline__ void head_prep(const T* src, int hd, bool norm, const T* nw, float eps,
+                                          const float* tab, bool do_rope, float (&x0)[2],
+                                          float (&x1)[2], int& np, int lane) {
+    const int half = hd >> 1;
+    np = 0;
+    for (int p = lane; p < half; p += 64, ++np) {
+        x0[np] = ld(src, 2 * p);
+        x1[np] = ld(src, 2 * p + 1);
+    }
+    if (norm) {
+        float ss = 0.f;
+        for (int i = 0; i < np; ++i) ss += x0[i] * x0[i] + x1[i] * x1[i];
+        ss = wave_sum(ss);
+        const float rs = 1.0f / sqrtf(ss / (float)hd + eps);
+        for (int i = 0; i < np; ++i) {
+            const int p = lane + 64 * i;
+            x0[i] = rnd<T>((x0[i] * rs) * ld(nw, 2 * p));
+            x1[i] = rnd<T>((x1[i] * rs) * ld(nw, 2 * p + 1));
+        }
+    }
+    if (do_rope) {
+        for (int i = 0; i < np; ++i) {
+            const int p = lane + 64 * i;
+            const float c = tab[2 * p], s = tab[2 * p + 1];
+            const float y0 = x0[i] * c - x1[i] * s;
+            const float y1 = x1[i] * c + x0[i] * s;
+            x0[i] = rnd<T>(y0);
+            x1[i] = rnd<T>(y1);
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecArgs<T> a) {
+    constexpr int TILE = 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+    const int pos = a.row_pos[r];
+    const int j0 = sp * TILE;
+    if (j0 > pos) return;
+    const int nj = min(TILE, pos + 1 - j0);
+    const bool owner = (pos - j0) < TILE;  // this split holds the new position
+    const int slot = a.row_slot[r];
+    const int hd = a.hd, g = a.nh / a.nkv, ks = hd + 8;
+    T* Ks = reinterpret_cast<T*>(smem);
+    T* Vs = Ks + (size_t)TILE * ks;
+    float* qs = reinterpret_cast<float*>(Vs + (size_t)TILE * hd);  // [4][hd]
+    float* ps = qs + 4 * hd;                                        // [4][TILE]
+    const size_t base = (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
+    T* kc = a.kc + base;
+    T* vc = a.vc + base;
+    const T* raw = a.qkv + (size_t)r * a.ldqkv;
+    const float* tab = a.rope + (size_t)pos * hd;
+
+    // new k / v (owner block): waves 0 and 1
+    if (owner && wave < 2) {
+        float x0[2], x1[2];
+        int np;
+        const int hk = wave == 0 ? a.nh + kvh : a.nh + a.nkv + kvh;
+        head_prep<T>(raw + (size_t)hk * hd, hd, wave == 0 && a.qk_norm, a.kn, a.eps, tab, wave == 0,
+                     x0, x1, np, lane);
+        T* dst = (wave == 0 ? kc : vc) + (size_t)pos * hd;
+        T* tile = wave == 0 ? Ks + (size_t)(pos - j0) * ks : Vs + (size_t)(pos - j0) * hd;
+        for (int i = 0; i < np; ++i) {
+            const int p = lane + 64 * i;
+            st(dst, 2 * p, x0[i]);
+            st(dst, 2 * p + 1, x1[i]);
+            st(tile, 2 * p, x0[i]);
+            st(tile, 2 * p + 1, x1[i]);
+        }
+    }
+    // cached rows [j0, j0+nj) except the new one: 16-byte chunks
+    {
+        const int cpr = hd * (int)sizeof(T) / 16;  // chunks per row
+        const int nrows = owner ? nj - 1 : nj;
+        for (int idx = threadIdx.x; idx < nrows * cpr * 2; idx += 256) {
+            const int which = idx / (nrows * cpr);
+            const int rem = idx - which * nrows * cpr;
+            const int j = rem / cpr, c = rem - j * cpr;
+            const T* src = (which == 0 ? kc : vc) + (size_t)(j0 + j) * hd;
+            T* dst = which == 0 ? Ks + (size_t)j * ks : Vs + (size_t)j * hd;
+            *reinterpret_cast<u32x4_t*>(reinterpret_cast<char*>(dst) + 16 * c) =
+                *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const char*>(src) + 16 * c);
+        }
+    }
+    const float scale = a.scale;
+    for (int hb = 0; hb < g; hb += 4) {
+        const int ql = hb + wave;  // q head within the group
+        if (ql < g) {
+            float x0[2], x1[2];
+            int np;
+            const int h = kvh * g + ql;
+            head_prep<T>(raw + (size_t)h * hd, hd, a.qk_norm, a.qn, a.eps, tab, true, x0, x1, np, lane);
+            for (int i = 0; i < np; ++i) {
+                const int p = lane + 64 * i;
+                qs[wave * hd + 2 * p] = x0[i];
+                qs[wave * hd + 2 * p + 1] = x1[i];
+            }
+        }
+        __syncthreads();
+        if (ql < g) {
+            // scores: lane j of wave `wave`
+            float sc = -INFINITY;
+            if (lane < nj) {
+                const T* kr = Ks + (size_t)lane * ks;
+                float dot = 0.f;
+                for (int e = 0; e < hd; e += 8) {
+                    float kv[8];
+                    load8(kr + e, kv);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) dot += qs[wave * hd + e + u] * kv[u];
+                }
+                sc = dot * scale;
+            }
+            const float m = wave_max(sc);
+            const float p = lane < nj ? expf(sc - m) : 0.f;
+            const float l = wave_sum(p);
+            ps[wave * TILE + lane] = p;
+            __builtin_amdgcn_wave_barrier();
+            const int h = kvh * g + ql;
+            float* out = a.part + (((size_t)r * a.nh + h) * a.maxsplit + sp) * (hd + 2);
+            for (int e = lane; e < hd; e += 64) {
+                float o = 0.f;
+                for (int j = 0; j < nj; ++j) o += ps[wave * TILE + j] * ld(Vs + (size_t)j * hd, e);
+                out[2 + e] = o;
+            }
+            if (lane == 0) {
+                out[0] = m;
+                out[1] = l;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// fast model attention at codebook position cpos, fused with qk-norm/rope/cache write.
+// grid (R, nkv), block 256 (wave per q head of the GQA group).
+template <typename T>
+__global__ __launch_bounds__(256) void fast_attn_fused_kernel(FastFusedArgs<T> a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = blockIdx.x, kvh = blockIdx.y;
+    const int slot = a.row_slot[r];
+    const int hd = a.hd, g = a.nh / a.nkv, C = a.S, cpos = a.cpos;
+    float* Kt = reinterpret_cast<float*>(smem);  // [C][hd]
+    float* Vt = Kt + (size_t)C * hd;
+    float* qs = Vt + (size_t)C * hd;  // [4][hd]
+    float* ps = qs + 4 * hd;          // [4][64]
+    const size_t base = (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * C * hd;
+    T* kc = a.kc + base;
+    T* vc = a.vc + base;
+    const T* raw = a.qkv + (size_t)r * a.ldqkv;
+    const float* tab = a.rope + (size_t)cpos * hd;
+    if (wave < 2) {
+        float x0[2], x1[2];
+        int np;
+        const int hk = wave == 0 ? a.nh + kvh : a.nh + a.nkv + kvh;
+        head_prep<T>(raw + (size_t)hk * hd, hd, wave == 0 && a.qk_norm, a.kn, a.eps, tab, wave == 0, x0,
+                     x1, np, lane);
+        T* dst = (wave == 0 ? kc : vc) + (size_t)cpos * hd;
+        float* tile = (wave == 0 ? Kt : Vt) + (size_t)cpos * hd;
+        for (int i = 0; i < np; ++i) {
+            const int p = lane + 64 * i;
+            st(dst, 2 * p, x0[i]);
+            st(dst, 2 * p + 1, x1[i]);
+            tile[2 * p] = x0[i];
+            tile[2 * p + 1] = x1[i];
+        }
+    }
+    for (int idx = threadIdx.x; idx < cpos * hd; idx += 256) {
+        Kt[idx] = ld(kc, idx);
+        Vt[idx] = ld(vc, idx);
+    }
+    for (int hb = 0; hb < g; hb += 4) {
+        const int ql = hb + wave;
+        if (ql < g) {
+            float x0[2], x1[2];
+            int np;
+            head_prep<T>(raw + (size_t)(kvh * g + ql) * hd, hd, a.qk_norm, a.qn, a.eps, tab, true, x0,
+                         x1, np, lane);
+            for (int i = 0; i < np; ++i) {
+                const int p = lane + 64 * i;
+                qs[wave * hd + 2 * p] = x0[i];
+                qs[wave * hd + 2 * p + 1] = x1[i];
+            }
+        }
+        __syncthreads();
+        if (ql < g) {
+            float sc = -INFINITY;
+            if (lane <= cpos) {
+                float dot = 0.f;
+                for (int e = 0; e < hd; ++e) dot += qs[wave * hd + e] * Kt[(size_t)lane * hd + e];
+                sc = rnd<T>(rnd<T>(dot) * a.scale);
+            }
+            const float mx = wave_max(sc);
+            const float ex = lane <= cpos ? expf(sc - mx) : 0.f;
+            const float den = wave_sum(ex);
+            ps[wave * 64 + lane] = rnd<T>(ex / den);
+            __builtin_amdgcn_wave_barrier();
+            const int h = kvh * g + ql;
+            for (int e = lane; e < hd; e += 64) {
+                float o = 0.f;
+                for (int j = 0; j <= cpos; ++j) o += ps[wave * 64 + j] * Vt[(size_t)j * hd + e];
+                st(a.out, (size_t)r * a.nh * hd + (size_t)h * hd + e, o);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// =========================================================================================
+// sampler: radix-select top-K
+// =========================================================================================
+__device__ __forceinline__ uint32_t fkey(float v) {
+    const uint32_t u = __float_as_uint(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ bool cbetter(float v, int id, float bv, int bid) {
+    return v > bv || (v == bv && id < bid);
+}
+
+template <typename T>
+__device__ int sample_top(const float* cv, const int* cid, int K, float M, float den, float temperature,
+                          float top_p, int top_k, uint64_t seed, uint64_t step, uint32_t draw, int lane) {
+    const float v = lane < K ? cv[lane] : -INFINITY;
+    const int id = lane < K ? cid[lane] : 0x7fffffff;
+    const float p = (v == -INFINITY) ? 0.f : rnd<T>(expf(v - M) / den);
+    float cum = 0.f, mycum = 0.f;
+    for (int k = 0; k < K; ++k) {
+        cum += __shfl(p, k, 64);
+        if (lane == k) mycum = rnd<T>(cum);
+    }
+    const float t = rnd<T>(temperature), tp = rnd<T>(top_p);
+    const bool keep = lane < K && v != -INFINITY && (lane == 0 || (!(mycum > tp) && lane < top_k));
+    const float tt = fmaxf(t, 1e-5f);
+    const float lt = keep ? rnd<T>(v / tt) : -INFINITY;
+    const float m2 = wave_max(lt);
+    const float e = keep ? expf(lt - m2) : 0.f;
+    const float d2 = wave_sum(e);
+    const float prob = rnd<T>(e / d2);
+    float score = -1.f;
+    int bid = 0x7fffffff;
+    if (keep) {
+        const float u = rng_uniform_bf16(seed, step, draw, (uint32_t)id);
+        const float qv = rnd<T>(-logf(u));
+        score = rnd<T>(prob / qv);
+        bid = id;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float os = __shfl_xor(score, o, 64);
+        const int oid = __shfl_xor(bid, o, 64);
+        if (cbetter(os, oid, score, bid)) {
+            score = os;
+            bid = oid;
+        }
+    }
+    return bid;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void sample_radix_kernel(SampleArgs a) {
+    extern __shared__ float vals[];  // [Nl]
+    __shared__ float scratch[16];
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh_prefix, sh_rem, sh_nstrict, sh_ntie;
+    __shared__ float cv[64];
+    __shared__ int cid[64];
+    __shared__ float sv[64];
+    __shared__ int sid[64];
+    __shared__ int tid_[256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = blockIdx.x;
+    const int slot = a.row_slot[r];
+    const SlotParams sp = a.sp[slot];
+    const float* lg = a.logits + (size_t)r * a.ldl;
+    const int Nl = a.Nl;
+    for (int i = threadIdx.x; i < Nl; i += 256) {
+        float v = lg[i];
+        if (a.slow && sp.mask_im_end && i == Nl - 1) v = -INFINITY;
+        vals[i] = v;
+    }
+    __syncthreads();
+    auto tok_of = [&](int i) { return a.slow ? (i < Nl - 1 ? a.sb + i : a.im_end) : i; };
+    float mloc = -INFINITY;
+    for (int i = threadIdx.x; i < Nl; i += 256) mloc = fmaxf(mloc, vals[i]);
+    const float M = block_max(mloc, scratch);
+    float sloc = 0.f;
+    for (int i = threadIdx.x; i < Nl; i += 256) sloc += (vals[i] == -INFINITY) ? 0.f : expf(vals[i] - M);
+    const float den = block_sum(sloc, scratch);
+    int K = sp.top_k < 1 ? 1 : (sp.top_k > 64 ? 64 : sp.top_k);
+    if (K > Nl) K = Nl;
+
+    // ---- radix select: key of the K-th largest element ------------------------------------
+    uint32_t prefix = 0, mask = 0, rem = (uint32_t)K;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        hist[threadIdx.x] = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < Nl; i += 256) {
+            const uint32_t k = fkey(vals[i]);
+            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (wave == 0) {
+            uint32_t c[4];
+            uint32_t s = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c[q] = hist[255 - 4 * lane - q];
+                s += c[q];
+            }
+            uint32_t incl = s;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += t;
+            }
+            const uint64_t hit = __ballot(incl >= rem);
+            const int L = hit ? __ffsll((long long)hit) - 1 : 63;
+            if (lane == L) {
+                uint32_t run = incl - s;
+                int bin = 255 - 4 * lane - 3;
+                uint32_t nrem = rem - run;
+                for (int q = 0; q < 4; ++q) {
+                    if (run + c[q] >= rem) {
+                        bin = 255 - 4 * lane - q;
+                        nrem = rem - run;
+                        break;
+                    }
+                    run += c[q];
+                }
+                sh_prefix = prefix | ((uint32_t)bin << shift);
+                sh_rem = nrem;
+            }
+        }
+        __syncthreads();
+        prefix = sh_prefix;
+        rem = sh_rem;
+        mask |= 255u << shift;
+    }
+    const uint32_t thr = prefix;  // key of the K-th element; take `rem` of the ties
+    // ---- gather strict (> thr) and tie (== thr) candidates ----------------------------------
+    if (threadIdx.x == 0) {
+        sh_nstrict = 0;
+        sh_ntie = 0;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < Nl; i += 256) {
+        const uint32_t k = fkey(vals[i]);
+        if (k > thr) {
+            const uint32_t at = atomicAdd(&sh_nstrict, 1u);
+            if (at < 64) {
+                sv[at] = vals[i];
+                sid[at] = tok_of(i);
+            }
+        } else if (k == thr) {
+            const uint32_t at = atomicAdd(&sh_ntie, 1u);
+            if (at < 256) tid_[at] = tok_of(i);
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int ns = (int)sh_nstrict;  // == K - rem
+        const int nt = (int)sh_ntie;
+        // strict: rank by counting -> sorted (value desc, id asc)
+        if (lane < ns) {
+            int rk = 0;
+            for (int j = 0; j < ns; ++j) rk += cbetter(sv[j], sid[j], sv[lane], sid[lane]);
+            cv[rk] = sv[lane];
+            cid[rk] = sid[lane];
+        }
+        // ties: the `rem` smallest token ids
+        float tv = 0.f;
+        {
+            uint32_t u = thr & 0x80000000u ? (thr & 0x7fffffffu) : ~thr;
+            tv = __uint_as_float(u);
+        }
+        if (nt <= 256) {
+            for (int t = lane; t < nt; t += 64) {
+                int rk = 0;
+                for (int j = 0; j < nt; ++j) rk += tid_[j] < tid_[t];
+                if (rk < (int)rem) {
+                    cv[ns + rk] = tv;
+                    cid[ns + rk] = tid_[t];
+                }
+            }
+        } else if (lane == 0) {  // massive ties (degenerate logits): exact sequential scan by id
+            int taken = 0;
+            int last = -1;
+            while (taken < (int)rem) {
+                int best = 0x7fffffff;
+                for (int i = 0; i < Nl; ++i) {
+                    const int id = tok_of(i);
+                    if (fkey(vals[i]) == thr && id > last && id < best) best = id;
+                }
+                cv[ns + taken] = tv;
+                cid[ns + taken] = best;
+                last = best;
+                ++taken;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t step = (uint64_t)sp.step;
+        int32_t* col = a.cols + (size_t)r * a.ldc;
+        if (a.slow) {
+            int tok = sample_top<T>(cv, cid, K, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed, step,
+                                    0, lane);
+            const int hi = sample_top<T>(cv, cid, K, M, den, 1.0f, 0.9f, sp.top_k, sp.seed, step, 1, lane);
+            if (a.ras_enable) {
+                const int32_t* prev = a.ras + (size_t)slot * a.ras_stride;
+                bool inwin = false;
+                for (int j = 0; j < 10; ++j) inwin |= prev[j] == tok;
+                if (inwin && tok >= a.sb && tok <= a.se) tok = hi;
+            }
+            if (lane == 0) {
+                col[0] = tok;
+                int c = tok - a.sb;
+                c = c < 0 ? 0 : (c > a.cb - 1 ? a.cb - 1 : c);
+                col[1] = c;
+            }
+        } else {
+            const int code = sample_top<T>(cv, cid, K, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed,
+                                           step, (uint32_t)a.draw, lane);
+            if (lane == 0) col[a.col_idx] = code;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+template <typename T> void launch_attn_decode(hipStream_t s, const AttnDecArgs<T>& a, int R) {
+    dim3 g1(R, a.nkv, a.maxsplit);
+    const size_t lds = (size_t)64 * (a.hd + 8) * sizeof(T) + (size_t)64 * a.hd * sizeof(T) +
+                       (size_t)4 * a.hd * 4 + 4 * 64 * 4;
+    attn_decode_kernel<T><<<g1, 256, lds, s>>>(a);
+}
+template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFusedArgs<T>& a, int R) {
+    dim3 g(R, a.nkv);
+    const size_t lds = (size_t)2 * a.S * a.hd * 4 + (size_t)4 * a.hd * 4 + 4 * 64 * 4;
+    fast_attn_fused_kernel<T><<<g, 256, lds, s>>>(a);
+}
+template <typename T> void launch_sample_radix(hipStream_t s, const SampleArgs& a, int R) {
+    sample_radix_kernel<T><<<R, 256, sizeof(float) * a.Nl, s>>>(a);
+}
+template void launch_attn_decode<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
+template void launch_attn_decode<float>(hipStream_t, const AttnDecArgs<float>&, int);
+template void launch_fast_attn_fused<bf16_t>(hipStream_t, const FastFusedArgs<bf16_t>&, int);
+template void launch_fast_attn_fused<float>(hipStream_t, const FastFusedArgs<float>&, int);
+template void launch_sample_radix<bf16_t>(hipStream_t, const SampleArgs&, int);
+template void launch_sample_radix<float>(hipStream_t, const SampleArgs&, int);

@@ -5,6 +5,12 @@
 
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_F32 = 3 };
 
+// Packed weight layout used by every GEMM here: a [N][K] nn.Linear weight is stored as
+// [ceil(N/16)][K/32] blocks of 512 elements, each block holding one MFMA 16x32 A-fragment in
+// lane order (bf16: lane l's 8 elements at l*8; fp32: elements 0-3 at l*4, 4-7 at 256+l*4), so
+// every wave-load instruction reads 1 KB of contiguous memory.
+template <typename T> void launch_pack(hipStream_t s, const T* src, int N, int K, T* dst);
+
 template <typename T> struct LinearArgs {
     const T* W;      // [N(padded to 16)][K] row-major (nn.Linear layout)
     const T* W2;     // second weight for EPI_SWIGLU (w3), same shape
@@ -101,3 +107,77 @@ void launch_synth(hipStream_t s, T* dst, int64_t n, uint64_t seed, uint32_t tid,
                   int log2_half);
 template <typename T>
 void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* dst);
+
+// ---- decode weight-streaming path (fm_gemv.hip), R <= 8 rows --------------------------------
+enum { PRO_PLAIN = 0, PRO_NORM = 1, PRO_RESNORM = 2 };
+enum { EPI_SLAB = 4 };
+
+template <typename T> struct GemvArgs {
+    const T* W;
+    const T* W2;             // EPI_SWIGLU: w3
+    const T* bias;
+    const T* X;              // [R][ldx] (or a table gathered by xidx)
+    int ldx;
+    const int32_t* xidx;     // optional row gather: X row = xidx[r*xidx_ld + xidx_col]
+    int xidx_ld, xidx_col;
+    const int32_t* residx;   // optional row gather for res (same layout as xidx)
+    const T* res;            // PRO_RESNORM residual [R][ldr]
+    int ldr;
+    const float* slab;       // PRO_RESNORM: producer partials [nslab][R][slab_ld]
+    int slab_ld, nslab;
+    const T* nw;             // norm weight [K]
+    float eps;
+    int R, N, K;
+    T* Y;                    // EPI_STORE / EPI_SWIGLU [R][ldy]
+    int ldy;                 // also the slab row stride for EPI_SLAB / EPI_F32
+    float* Yf;               // EPI_F32 [R][ldy] | EPI_SLAB [KSB][R][ldy]
+    T* res_out;              // PRO_RESNORM: block (0,0) stores x = res + sum(slabs) here
+    int ldro;
+    T* xn_out;               // optional: block (0,0) stores X' (normalised row) here
+    int ldxo;
+};
+inline size_t gemv_lds_bytes(int R, int Kb, size_t esz) {
+    return (size_t)R * (Kb + 8) * esz + 16 * sizeof(float) + 2 * 8 * 64 * 16;
+}
+template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb);
+
+// ---- fused decode attention / sampler (fm_attn.hip) ------------------------------------------
+template <typename T> struct AttnDecArgs {
+    const T* qkv;        // raw projections [R][ldqkv] (q heads, k heads, v heads)
+    int ldqkv;
+    const int* row_slot;
+    const int* row_pos;
+    int nh, nkv, hd, qk_norm;
+    float eps;
+    const T* qn;
+    const T* kn;
+    const float* rope;   // [S][hd/2][2]
+    T* kc;
+    T* vc;
+    size_t slot_stride, layer_off;
+    int S, maxsplit;
+    float scale;
+    float* part;         // [R][nh][maxsplit][hd+2]
+};
+template <typename T> struct FastFusedArgs {
+    const T* qkv;
+    int ldqkv;
+    const int* row_slot;
+    int nh, nkv, hd, qk_norm;
+    float eps;
+    const T* qn;
+    const T* kn;
+    const float* rope;   // [C][hd/2][2]
+    T* kc;
+    T* vc;
+    size_t slot_stride, layer_off;
+    int S, cpos;         // S = num_codebooks (fast cache length)
+    float scale;
+    T* out;              // [R][nh*hd]
+};
+template <typename T> void launch_attn_decode(hipStream_t s, const AttnDecArgs<T>& a, int R);
+template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFusedArgs<T>& a, int R);
+template <typename T> void launch_sample_radix(hipStream_t s, const SampleArgs& a, int R);
+template <typename T>
+void launch_attn_combine(hipStream_t s, const float* part, const int* row_pos, int R, int nh, int hd,
+                         int split, int maxsplit, T* out);

@@ -25,6 +25,18 @@ extern "C" int fm_device_count(void) {
 
 static constexpr int PREFILL_CHUNK = 256;
 static constexpr int ATTN_SPLIT = 64;
+static constexpr int GEMV_MAX_ROWS = 8;  // frames with <= 8 streams take the fused GEMV path
+static constexpr int KSB_MAX = 8;
+
+// split-K factor across blocks for a GEMV with N output rows: >= ~512 blocks when possible,
+// K/(32*ksb) integral, LDS staging within budget.
+static int pick_ksb(int N, int K, int R, size_t esz) {
+    const int nb = (N + 15) / 16;
+    int ksb = 1;
+    while (ksb < KSB_MAX && nb * ksb < 512 && K % (32 * ksb * 2) == 0) ksb *= 2;
+    while (gemv_lds_bytes(R, K / ksb, esz) > 96 * 1024 && ksb < KSB_MAX && K % (32 * ksb * 2) == 0) ksb *= 2;
+    return ksb;
+}
 
 struct LayerW {
     void *wqkv = nullptr, *bqkv = nullptr, *wo = nullptr, *bo = nullptr, *qn = nullptr, *kn = nullptr;
@@ -58,6 +70,7 @@ struct fm_llm {
          *act = nullptr;
     void *xl = nullptr, *xnl = nullptr, *fx = nullptr, *fh = nullptr, *fxn = nullptr;
     float *part = nullptr, *logits = nullptr, *flogits = nullptr;
+    float *slabA = nullptr, *slabB = nullptr;  // split-K partials of wo / w2 (small-batch path)
     // rows / slots
     int *frame_slot = nullptr, *frame_pos = nullptr, *prow_slot = nullptr, *prow_pos = nullptr;
     int32_t *tok_in = nullptr, *cols = nullptr, *ptok = nullptr, *ras = nullptr;
@@ -211,6 +224,245 @@ template <typename T> struct Run {
                EPI_RESID, "linear");
     }
 
+    // ---------------- small-batch (<= 8 streams) fused path --------------------------------
+    GemvArgs<T> ga() {
+        GemvArgs<T> a{};
+        a.eps = m->c.norm_eps;
+        return a;
+    }
+    void gemv(GemvArgs<T> a, int pro, int epi, int ksb, const char* cls) {
+        const int64_t wbytes = (int64_t)a.N * a.K * E * (epi == EPI_SWIGLU ? 2 : 1);
+        const int64_t bytes = wbytes + (int64_t)a.R * a.K * E;
+        const double flops = 2.0 * a.R * a.N * a.K * (epi == EPI_SWIGLU ? 2 : 1);
+        m->prof.run(s, cls, bytes, flops, [&] { launch_gemv<T>(s, a, pro, epi, ksb); });
+    }
+    struct KsbPlan {
+        int wo, w2;
+    };
+    KsbPlan plan(const StackDims& d, int n) {
+        return KsbPlan{pick_ksb(d.dim, d.nq(), n, E), pick_ksb(d.dim, d.inter, n, E)};
+    }
+    // one pre-norm block; x_in: layer input (plain rows, or embedding table + xidx gather) when
+    // first, otherwise the residual is pending as (res=hb, slabs=slabB).
+    void block_small(const StackDims& d, const LayerW& L, int n, bool first, const void* x_in, int ldx_in,
+                     const int32_t* xidx, int xcol, void* xb, void* hb, bool is_fast, int cpos, int layer,
+                     const KsbPlan& kp, int ksb_prev) {
+        const int C1 = m->C1;
+        // QKV (+ residual of the previous block + attention_norm)
+        {
+            GemvArgs<T> a = ga();
+            a.W = (const T*)L.wqkv;
+            a.bias = (const T*)L.bqkv;
+            a.nw = (const T*)L.an;
+            a.R = n;
+            a.N = d.nqkv();
+            a.K = d.dim;
+            a.Y = (T*)m->qkv;
+            a.ldy = d.nqkv();
+            if (first) {
+                a.X = (const T*)x_in;
+                a.ldx = ldx_in;
+                a.xidx = xidx;
+                a.xidx_ld = C1;
+                a.xidx_col = xcol;
+                gemv(a, PRO_NORM, EPI_STORE, 1, "linear");
+            } else {
+                a.res = (const T*)hb;
+                a.ldr = d.dim;
+                a.slab = m->slabB;
+                a.slab_ld = d.dim;
+                a.nslab = ksb_prev;
+                a.res_out = (T*)xb;
+                a.ldro = d.dim;
+                gemv(a, PRO_RESNORM, EPI_STORE, 1, "linear");
+            }
+        }
+        const float scale = 1.0f / sqrtf((float)d.hd);
+        if (!is_fast) {
+            AttnDecArgs<T> aa{(const T*)m->qkv, d.nqkv(), m->frame_slot, m->frame_pos, d.nh, d.nkv, d.hd,
+                              d.qk_norm, m->c.norm_eps, (const T*)L.qn, (const T*)L.kn, m->rope, (T*)m->kc,
+                              (T*)m->vc, m->slot_stride, (size_t)layer * m->layer_stride, m->S,
+                              m->maxsplit, scale, m->part};
+            m->prof.run(s, "attn", 0, 0, [&] {
+                launch_attn_decode<T>(s, aa, n);
+                launch_attn_combine<T>(s, m->part, m->frame_pos, n, d.nh, d.hd, ATTN_SPLIT, m->maxsplit,
+                                       (T*)m->att);
+            });
+        } else {
+            FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), m->frame_slot, d.nh, d.nkv, d.hd, d.qk_norm,
+                                m->c.norm_eps, (const T*)L.qn, (const T*)L.kn, m->frope, (T*)m->fkc,
+                                (T*)m->fvc, m->fslot_stride, (size_t)layer * m->flayer_stride, m->C, cpos,
+                                scale, (T*)m->att};
+            m->prof.run(s, "attn", 0, 0, [&] { launch_fast_attn_fused<T>(s, fa, n); });
+        }
+        // wo -> split-K partials (slabA)
+        {
+            GemvArgs<T> a = ga();
+            a.W = (const T*)L.wo;
+            a.bias = (const T*)L.bo;
+            a.X = (const T*)m->att;
+            a.ldx = d.nq();
+            a.R = n;
+            a.N = d.dim;
+            a.K = d.nq();
+            a.Yf = m->slabA;
+            a.ldy = d.dim;
+            gemv(a, PRO_PLAIN, EPI_SLAB, kp.wo, "linear");
+        }
+        // W1/W3 (+ h = x + wo, ffn_norm) -> SwiGLU act
+        {
+            GemvArgs<T> a = ga();
+            a.W = (const T*)L.w1;
+            a.W2 = (const T*)L.w3;
+            a.nw = (const T*)L.fn;
+            a.R = n;
+            a.N = d.inter;
+            a.K = d.dim;
+            if (first) {
+                a.res = (const T*)x_in;
+                a.ldr = ldx_in;
+                a.residx = xidx;
+                a.xidx_ld = C1;
+                a.xidx_col = xcol;
+            } else {
+                a.res = (const T*)xb;
+                a.ldr = d.dim;
+            }
+            a.slab = m->slabA;
+            a.slab_ld = d.dim;
+            a.nslab = kp.wo;
+            a.res_out = (T*)hb;
+            a.ldro = d.dim;
+            a.Y = (T*)m->act;
+            a.ldy = d.inter;
+            gemv(a, PRO_RESNORM, EPI_SWIGLU, 1, "linear");
+        }
+        // W2 -> split-K partials (slabB); the next consumer adds them to h
+        {
+            GemvArgs<T> a = ga();
+            a.W = (const T*)L.w2;
+            a.X = (const T*)m->act;
+            a.ldx = d.inter;
+            a.R = n;
+            a.N = d.dim;
+            a.K = d.inter;
+            a.Yf = m->slabB;
+            a.ldy = d.dim;
+            gemv(a, PRO_PLAIN, EPI_SLAB, kp.w2, "linear");
+        }
+    }
+
+    void slow_small(int n) {
+        const KsbPlan kp = plan(m->sd, n);
+        for (int l = 0; l < m->sd.n_layer; ++l)
+            block_small(m->sd, m->slow[l], n, l == 0, m->x, m->c.dim, nullptr, 0, m->x, m->h, false, 0, l,
+                        kp, kp.w2);
+    }
+
+    // final norm (+ pending residual) -> constrained head logits and the fast-model hidden
+    const void* head_small(const void* xlast, bool pending, int n, int ksb_prev) {
+        const fm_model_config& c = m->c;
+        GemvArgs<T> a = ga();
+        a.W = (const T*)m->head_c;
+        a.nw = (const T*)m->norm;
+        a.R = n;
+        a.N = m->Nhead;
+        a.K = c.dim;
+        a.Yf = m->logits;
+        a.ldy = m->Nhead;
+        a.xn_out = (T*)m->xnl;
+        a.ldxo = c.dim;
+        if (pending) {
+            a.res = (const T*)m->h;
+            a.ldr = c.dim;
+            a.slab = m->slabB;
+            a.slab_ld = c.dim;
+            a.nslab = ksb_prev;
+            a.res_out = (T*)m->x;
+            a.ldro = c.dim;
+            gemv(a, PRO_RESNORM, EPI_F32, 1, "linear");
+        } else {
+            a.X = (const T*)xlast;
+            a.ldx = c.dim;
+            gemv(a, PRO_NORM, EPI_F32, 1, "linear");
+        }
+        const void* hid = c.norm_fastlayer_input ? m->xnl : (pending ? m->x : xlast);
+        if (m->fproj_w) {
+            GemvArgs<T> p = ga();
+            p.W = (const T*)m->fproj_w;
+            p.bias = (const T*)m->fproj_b;
+            p.X = (const T*)hid;
+            p.ldx = c.dim;
+            p.R = n;
+            p.N = c.fast_dim;
+            p.K = c.dim;
+            p.Y = (T*)m->xl;
+            p.ldy = c.fast_dim;
+            gemv(p, PRO_PLAIN, EPI_STORE, 1, "linear");
+            return m->xl;
+        }
+        return hid;
+    }
+
+    void fast_small(int n, int cc, bool with_head, const void* hidden) {
+        const fm_model_config& c = m->c;
+        const KsbPlan kp = plan(m->fdm, n);
+        for (int l = 0; l < m->fdm.n_layer; ++l) {
+            const bool first = l == 0;
+            const void* xin = cc == 0 ? hidden : m->femb;
+            const int32_t* xidx = cc == 0 ? nullptr : m->cols;
+            block_small(m->fdm, m->fast[l], n, first, xin, c.fast_dim, xidx, cc, m->fx, m->fh, true, cc, l, kp,
+                        kp.w2);
+        }
+        if (with_head) {
+            GemvArgs<T> a = ga();
+            a.W = (const T*)m->fout;
+            a.nw = (const T*)m->fnorm;
+            a.R = n;
+            a.N = m->cb;
+            a.K = c.fast_dim;
+            a.Yf = m->flogits;
+            a.ldy = m->cb;
+            a.res = (const T*)m->fh;
+            a.ldr = c.fast_dim;
+            a.slab = m->slabB;
+            a.slab_ld = c.fast_dim;
+            a.nslab = kp.w2;
+            a.res_out = (T*)m->fx;
+            a.ldro = c.fast_dim;
+            gemv(a, PRO_RESNORM, EPI_F32, 1, "linear");
+        }
+    }
+
+    void frame_tail_small(int n, bool ras_enable, bool sample, const void* hidden) {
+        if (sample) {
+            SampleArgs a = sargs(true, ras_enable, 0);
+            m->prof.run(s, "sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
+        }
+        fast_small(n, 0, false, hidden);  // position 0 fills the fast KV cache; logits discarded
+        for (int cc = 1; cc < m->C; ++cc) {
+            fast_small(n, cc, true, hidden);
+            if (sample) {
+                SampleArgs a = sargs(false, 0, cc);
+                m->prof.run(s, "sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
+            }
+        }
+    }
+
+    void decode_frame_small(int n) {
+        m->prof.run(s, "other", 0, 0, [&] {
+            launch_embed<T>(s, m->tok_in, n, (const T*)m->emb, (const T*)m->cbemb, m->c.dim, m->C, m->cb,
+                            m->c.semantic_begin_id, m->c.semantic_end_id, m->c.scale_codebook_embeddings,
+                            (T*)m->x, m->frame_slot);
+        });
+        slow_small(n);
+        const KsbPlan kp = plan(m->sd, n);
+        const void* hid = head_small(nullptr, true, n, kp.w2);
+        frame_tail_small(n, true, true, hid);
+        launch_finish(s, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10, m->C1,
+                      1, m->sp);
+    }
+
     void slow_layers(int R, const int* rslot, const int* rpos) {
         for (int l = 0; l < m->sd.n_layer; ++l)
             block(m->sd, m->slow[l], R, rslot, rpos, -1, false, m->kc, m->vc, m->slot_stride,
@@ -276,7 +528,7 @@ template <typename T> struct Run {
     void frame_tail(int n, bool ras_enable, bool sample) {
         if (sample) {
             SampleArgs a = sargs(true, ras_enable, 0);
-            m->prof.run(s, "sample", 0, 0, [&] { launch_sample<T>(s, a, n); });
+            m->prof.run(s, "sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
         }
         fast_pass(n, 0, false);  // position 0: fills the fast KV cache, logits discarded
         for (int cc = 1; cc < m->C; ++cc) {
@@ -286,12 +538,16 @@ template <typename T> struct Run {
             fast_pass(n, cc, true);
             if (sample) {
                 SampleArgs a = sargs(false, 0, cc);
-                m->prof.run(s, "sample", 0, 0, [&] { launch_sample<T>(s, a, n); });
+                m->prof.run(s, "sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
             }
         }
     }
 
     void decode_frame(int n) {
+        if (n <= GEMV_MAX_ROWS) {
+            decode_frame_small(n);
+            return;
+        }
         m->prof.run(s, "other", 0, 0, [&] {
             launch_embed<T>(s, m->tok_in, n, (const T*)m->emb, (const T*)m->cbemb, m->c.dim, m->C, m->cb,
                             m->c.semantic_begin_id, m->c.semantic_end_id, m->c.scale_codebook_embeddings,
@@ -343,10 +599,41 @@ static void* Wopt(fm_llm* m, const std::string& n) {
     return (it != m->w.end() && it->second.set) ? it->second.p : nullptr;
 }
 
+static bool is_linear_weight(const std::string& n) {
+    auto ends = [&](const char* suf) {
+        const size_t L = strlen(suf);
+        return n.size() >= L && n.compare(n.size() - L, L, suf) == 0;
+    };
+    return ends("attention.wqkv.weight") || ends("attention.wo.weight") || ends("feed_forward.w1.weight") ||
+           ends("feed_forward.w2.weight") || ends("feed_forward.w3.weight") || n == "fast_output.weight" ||
+           n == "fast_project_in.weight";
+}
+
+// row-major [rows][cols] device tensor -> packed fragment layout (fm_kernels.h)
+static void* pack_dev(fm_llm* m, const void* src, int rows, int cols) {
+    const size_t n = (size_t)(rows + 15) / 16 * 16 * cols;
+    void* dst = nullptr;
+    HIPCHK(hipMalloc(&dst, n * m->esz));
+    if (m->prec == FM_PREC_BF16)
+        launch_pack<bf16_t>(m->stream, (const bf16_t*)src, rows, cols, (bf16_t*)dst);
+    else
+        launch_pack<float>(m->stream, (const float*)src, rows, cols, (float*)dst);
+    HIPCHK(hipGetLastError());
+    return dst;
+}
+
 static void finalize(fm_llm* m) {
     if (m->finalized) return;
     const fm_model_config& c = m->c;
     for (auto& kv : m->w) FMCHECK(kv.second.set, "tensor not set: " + kv.first);
+    for (auto& kv : m->w) {
+        if (!is_linear_weight(kv.first)) continue;
+        DTensor& t = kv.second;
+        void* pk = pack_dev(m, t.p, (int)t.rows, (int)t.cols);
+        HIPCHK(hipStreamSynchronize(m->stream));
+        HIPCHK(hipFree(t.p));
+        t.p = pk;
+    }
     auto stack = [&](const std::string& pre, const StackDims& d, std::vector<LayerW>& out) {
         out.resize(d.n_layer);
         for (int i = 0; i < d.n_layer; ++i) {
@@ -382,12 +669,14 @@ static void finalize(fm_llm* m) {
     m->Nhead = m->nsem + 1;
     FMCHECK(m->Nhead <= 8192, "constrained head wider than 8192 rows is not supported");
     const size_t rowb = (size_t)c.dim * m->esz;
-    m->head_c = m->dalloc((size_t)(m->Nhead + 15) / 16 * 16 * rowb);
-    HIPCHK(hipMemcpyAsync(m->head_c, (const char*)outw + (size_t)c.semantic_begin_id * rowb,
+    void* head_rm = m->dalloc((size_t)(m->Nhead + 15) / 16 * 16 * rowb);
+    HIPCHK(hipMemcpyAsync(head_rm, (const char*)outw + (size_t)c.semantic_begin_id * rowb,
                           (size_t)m->nsem * rowb, hipMemcpyDeviceToDevice, m->stream));
-    HIPCHK(hipMemcpyAsync((char*)m->head_c + (size_t)m->nsem * rowb,
+    HIPCHK(hipMemcpyAsync((char*)head_rm + (size_t)m->nsem * rowb,
                           (const char*)outw + (size_t)c.im_end_id * rowb, rowb, hipMemcpyDeviceToDevice,
                           m->stream));
+    m->head_c = pack_dev(m, head_rm, m->Nhead, c.dim);
+    m->allocs.push_back(m->head_c);
     // caches [slot][layer][kv][S][hd]
     const StackDims& d = m->sd;
     m->layer_stride = (size_t)d.nkv * m->S * d.hd;
@@ -426,6 +715,8 @@ static void finalize(fm_llm* m) {
     m->fxn = m->dalloc((size_t)n * dmax * E);
     m->maxsplit = FM_CEIL(m->S, ATTN_SPLIT);
     m->part = (float*)m->dalloc((size_t)R * d.nh * m->maxsplit * (d.hd + 2) * 4, false);
+    m->slabA = (float*)m->dalloc((size_t)KSB_MAX * std::min(n, GEMV_MAX_ROWS) * dmax * 4);
+    m->slabB = (float*)m->dalloc((size_t)KSB_MAX * std::min(n, GEMV_MAX_ROWS) * dmax * 4);
     m->logits = (float*)m->dalloc((size_t)n * m->Nhead * 4);
     m->flogits = (float*)m->dalloc((size_t)n * m->cb * 4);
     m->frame_slot = (int*)m->dalloc(n * 4);
@@ -556,6 +847,8 @@ int fm_llm_open(const fm_model_config* cfg, int device, int precision, int max_s
         m->C1 = c.num_codebooks + 1;
         m->cb = c.codebook_size;
         HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+        const char* g = getenv("FISHMI_GRAPH");  // FISHMI_GRAPH=0: eager launches (profilers)
+        m->use_graph = !(g && g[0] == '0');
         build_inventory(m.get());
         *out = m.release();
     });
@@ -616,8 +909,8 @@ static void do_prefill(fm_llm* m, int slot, const int32_t* tokens, int T, const 
     HIPCHK(hipMemcpyAsync(m->frame_slot, &one, 4, hipMemcpyHostToDevice, m->stream));
     with_prec(m, [&](auto& r) {
         const void* last = r.prefill_slow(slot, tokens, T, 0);
-        r.head_and_hidden(last, 1);
-        r.frame_tail(1, false, true);
+        const void* hid = r.head_small(last, false, 1, 1);
+        r.frame_tail_small(1, false, true, hid);
     });
     int pos = T - 1;  // finish() advances it to T: the first decode frame runs at position T
     HIPCHK(hipMemcpyAsync(m->frame_pos, &pos, 4, hipMemcpyHostToDevice, m->stream));
@@ -731,11 +1024,11 @@ int fm_llm_teacher_step(fm_llm* m, int slot, const int32_t* x, int S, int pos0, 
         std::vector<float> lg(m->Nhead);
         with_prec(m, [&](auto& r) {
             const void* last = r.prefill_slow(slot, x, S, pos0);
-            r.head_and_hidden(last, 1);
+            const void* hid = r.head_small(last, false, 1, 1);
             HIPCHK(hipMemcpyAsync(lg.data(), m->logits, (size_t)m->Nhead * 4, hipMemcpyDeviceToHost, m->stream));
             if (hidden) {
                 std::vector<uint8_t> hb((size_t)c.fast_dim * m->esz);
-                HIPCHK(hipMemcpyAsync(hb.data(), m->fx, hb.size(), hipMemcpyDeviceToHost, m->stream));
+                HIPCHK(hipMemcpyAsync(hb.data(), hid, hb.size(), hipMemcpyDeviceToHost, m->stream));
                 HIPCHK(hipStreamSynchronize(m->stream));
                 for (int i = 0; i < c.fast_dim; ++i) {
                     if (m->esz == 2) {
@@ -748,12 +1041,9 @@ int fm_llm_teacher_step(fm_llm* m, int slot, const int32_t* x, int S, int pos0, 
             }
             if (next_col) {
                 HIPCHK(hipMemcpyAsync(m->cols, next_col, (size_t)m->C1 * 4, hipMemcpyHostToDevice, m->stream));
-                r.fast_pass(1, 0, false);
+                r.fast_small(1, 0, false, hid);
                 for (int cc = 1; cc < m->C; ++cc) {
-                    using TT = typename std::remove_reference_t<decltype(r)>::type_t;
-                    launch_gather_rows<TT>(m->stream, m->cols, m->C1, cc, (const TT*)m->femb, c.fast_dim, 1,
-                                           (TT*)m->fx);
-                    r.fast_pass(1, cc, true);
+                    r.fast_small(1, cc, true, hid);
                     if (fast_logits)
                         HIPCHK(hipMemcpyAsync(fast_logits + (size_t)(cc - 1) * m->cb, m->flogits, (size_t)m->cb * 4,
                                               hipMemcpyDeviceToHost, m->stream));

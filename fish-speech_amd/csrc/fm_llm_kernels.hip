@@ -80,11 +80,41 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const T* __restrict__ x, i
 // =========================================================================================
 // linear: Y[col][n] = epi( sum_k X[col][k] * W[n][k] )
 // =========================================================================================
+template <typename T>
+__global__ void pack_kernel(const T* __restrict__ src, int N, int K, T* __restrict__ dst) {
+    const int S = K >> 5;
+    const int64_t nblk = (int64_t)((N + 15) / 16) * S;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nblk * 64; q += stride) {
+        const int64_t blk = q >> 6;
+        const int l = (int)(q & 63);
+        const int t = (int)(blk / S), sidx = (int)(blk - (int64_t)t * S);
+        const int row = 16 * t + (l & 15);
+        const int k0 = 32 * sidx + 8 * (l >> 4);
+        T* d = dst + blk * 512;
+        for (int j = 0; j < 8; ++j) {
+            const T v = row < N ? src[(size_t)row * K + k0 + j] : (T)0;
+            if constexpr (is_bf16<T>::value) d[l * 8 + j] = v;
+            else d[j < 4 ? l * 4 + j : 256 + l * 4 + (j - 4)] = v;
+        }
+    }
+}
+template <typename T> void launch_pack(hipStream_t s, const T* src, int N, int K, T* dst) {
+    const int64_t n = (int64_t)((N + 15) / 16) * (K / 32) * 64;
+    const int blocks = (int)std::min<int64_t>(FM_CEIL(n, 256), 16384);
+    pack_kernel<T><<<blocks, 256, 0, s>>>(src, N, K, dst);
+}
+template void launch_pack<bf16_t>(hipStream_t, const bf16_t*, int, int, bf16_t*);
+template void launch_pack<float>(hipStream_t, const float*, int, int, float*);
+
 template <typename T> struct Mfma;
 template <> struct Mfma<bf16_t> {
     typedef u32x4_t frag;  // 8 bf16 along k
     static __device__ __forceinline__ frag load(const bf16_t* p) {
         return *reinterpret_cast<const u32x4_t*>(p);
+    }
+    static __device__ __forceinline__ frag load_packed(const bf16_t* blk, int lane) {
+        return *reinterpret_cast<const u32x4_t*>(blk + lane * 8);
     }
     static __device__ __forceinline__ f32x4_t mma(frag a, frag b, f32x4_t c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
@@ -99,6 +129,12 @@ template <> struct Mfma<float> {
         frag f;
         f.lo = *reinterpret_cast<const f32x4_t*>(p);
         f.hi = *reinterpret_cast<const f32x4_t*>(p + 4);
+        return f;
+    }
+    static __device__ __forceinline__ frag load_packed(const float* blk, int lane) {
+        frag f;
+        f.lo = *reinterpret_cast<const f32x4_t*>(blk + lane * 4);
+        f.hi = *reinterpret_cast<const f32x4_t*>(blk + 256 + lane * 4);
         return f;
     }
     // lane l holds k = 8*(l>>4) + j of a 32-wide k block; MFMA j covers {8g + j}: exact f32
@@ -124,8 +160,9 @@ __global__ __launch_bounds__(512) void linear_kernel(LinearArgs<T> a) {
     const int r = lane & 15, g = lane >> 4;
     const int nsteps = a.K >> 5;
     const int s0 = (wave * nsteps) >> 3, s1 = ((wave + 1) * nsteps) >> 3;
-    const T* wp = a.W + (size_t)(n0 + r) * a.K + 8 * g;
-    const T* wp2 = (EPI == EPI_SWIGLU) ? a.W2 + (size_t)(n0 + r) * a.K + 8 * g : nullptr;
+    // packed weights: block (tile, step) = 512 elements
+    const T* wp = a.W + (size_t)blockIdx.x * nsteps * 512;
+    const T* wp2 = (EPI == EPI_SWIGLU) ? a.W2 + (size_t)blockIdx.x * nsteps * 512 : nullptr;
 
     for (int c0 = 0; c0 < a.R; c0 += 16 * NCG) {
         f32x4_t acc[NACC][NCG];
@@ -143,8 +180,8 @@ __global__ __launch_bounds__(512) void linear_kernel(LinearArgs<T> a) {
             typename M::frag fa[NACC][U], fb[NCG][U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                fa[0][u] = M::load(wp + (size_t)(s + u) * 32);
-                if constexpr (NACC == 2) fa[1][u] = M::load(wp2 + (size_t)(s + u) * 32);
+                fa[0][u] = M::load_packed(wp + (size_t)(s + u) * 512, lane);
+                if constexpr (NACC == 2) fa[1][u] = M::load_packed(wp2 + (size_t)(s + u) * 512, lane);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -158,9 +195,9 @@ __global__ __launch_bounds__(512) void linear_kernel(LinearArgs<T> a) {
                     for (int q = 0; q < NACC; ++q) acc[q][c] = M::mma(fa[q][u], fb[c][u], acc[q][c]);
         }
         for (; s < s1; ++s) {
-            typename M::frag fa0 = M::load(wp + (size_t)s * 32);
+            typename M::frag fa0 = M::load_packed(wp + (size_t)s * 512, lane);
             typename M::frag fa1;
-            if constexpr (NACC == 2) fa1 = M::load(wp2 + (size_t)s * 32);
+            if constexpr (NACC == 2) fa1 = M::load_packed(wp2 + (size_t)s * 512, lane);
 #pragma unroll
             for (int c = 0; c < NCG; ++c) {
                 typename M::frag fb = M::load(xp[c] + (size_t)s * 32);
@@ -641,6 +678,11 @@ template <typename T> void launch_attn(hipStream_t s, const AttnArgs<T>& a, int 
     dim3 g2(R, a.nh);
     attn_combine_kernel<T><<<g2, 64, 0, s>>>(a.part, a.row_pos, a.nh, a.hd, a.split, a.maxsplit, out);
 }
+template <typename T>
+void launch_attn_combine(hipStream_t s, const float* part, const int* row_pos, int R, int nh, int hd,
+                         int split, int maxsplit, T* out) {
+    attn_combine_kernel<T><<<dim3(R, nh), 64, 0, s>>>(part, row_pos, nh, hd, split, maxsplit, out);
+}
 template <typename T> void launch_fast_attn(hipStream_t s, const FastAttnArgs<T>& a, int R) {
     dim3 g(R, a.nh);
     fast_attn_kernel<T><<<g, 64, 0, s>>>(a);
@@ -678,6 +720,8 @@ void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* 
     template void launch_qk_rope_cache<T>(hipStream_t, const QkArgs<T>&, int);                   \
     template void launch_attn<T>(hipStream_t, const AttnArgs<T>&, int, int, T*);                 \
     template void launch_fast_attn<T>(hipStream_t, const FastAttnArgs<T>&, int);                 \
+    template void launch_attn_combine<T>(hipStream_t, const float*, const int*, int, int, int, int, \
+                                         int, T*);                                               \
     template void launch_sample<T>(hipStream_t, const SampleArgs&, int);                         \
     template void launch_synth<T>(hipStream_t, T*, int64_t, uint64_t, uint32_t, float, int);    \
     template void launch_convert<T>(hipStream_t, const void*, int, int64_t, T*);
