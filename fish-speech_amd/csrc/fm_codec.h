@@ -1,0 +1,58 @@
+// fm_codec.h -- kernel argument blocks of the modded-DAC decode path (fm_codec_kernels.hip).
+#pragma once
+#include "fm_kernels.h"
+
+// epilogue flags of conv_gemm_kernel (combined bitwise)
+enum {
+    CE_BIAS = 1,      // + bias[co]
+    CE_GELU = 2,      // exact-erf GELU (nn.GELU, rvq.py:165)
+    CE_RES = 4,       // y = res + gamma[co] * y (LayerScale / ConvNeXt gamma) or res + y
+    CE_GAMMA = 8,     // with CE_RES: scale by gamma before the add
+    CE_STORE = 16,    // store y to out
+    CE_SNAKE = 32,    // store snake(y, alpha2) to out2 (the next stage's input)
+    CE_TANH = 64,     // y = tanh(y) (decoder output, modded_dac.py:795)
+    CE_F32OUT = 128,  // out is fp32 (final waveform)
+};
+
+// out[t_out][co] (time-major, ld = ldo) with t_out = tq * stride + phase, tq in [0, Lq):
+//   y = sum_{tap, ci} Wp[phase][co][tap*Ci + ci] * x[tq - shift[tap]][ci]   (x time-major, ldx)
+// Wp packed per phase (fm_kernels.h layout), rows = Co, cols = ntaps*Ci.
+template <typename T> struct ConvArgs {
+    const T* x;
+    int ldx, Ci, Lq, Lx;       // input rows available: [0, Lx); rows < 0 are causal zeros
+    const T* w;                // packed, phase-major
+    size_t wphase;             // elements per phase
+    int Co, ntaps, stride, nphase;
+    int shift[8];              // per tap
+    const T* bias;
+    const T* gamma;
+    const T* res;              // residual [t_out][co], ldr
+    int ldr;
+    const T* alpha2;           // snake alpha for out2
+    void* out;
+    int ldo;
+    T* out2;
+    int ldo2;
+    int flags;
+};
+
+struct RvqPtrs {
+    const float* cb[16];  // codebooks [size][cd]
+    const float* w[16];   // folded out_proj [D][cd]
+    const float* b[16];   // out_proj bias [D]
+};
+
+template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a);
+template <typename T> void launch_silu_mul(hipStream_t s, const T* g, T* y, size_t n);
+template <typename T>
+void launch_rvq_decode(hipStream_t s, const int32_t* codes, int Tn, int nq1, int sem, int cbs, int cd,
+                       const RvqPtrs& p, int D, T* z);
+template <typename T>
+void launch_dwconv_ln(hipStream_t s, const T* x, int L, int D, const T* dw, const T* db, const T* lw,
+                      const T* lb, T* y);
+template <typename T> void launch_rope_qk(hipStream_t s, T* qkv, int Tn, int H, int hd, const float* tab);
+template <typename T>
+void launch_window_attn(hipStream_t s, const T* qkv, int Tn, int H, int hd, int window, T* out);
+void launch_wn_fold(hipStream_t s, const float* g, const float* v, int rows, int per, float* w);
+template <typename T>
+void launch_conv_weight(hipStream_t s, const float* w, int kind, int Ci, int Co, int k, int st_, T* out);

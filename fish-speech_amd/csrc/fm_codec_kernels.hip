@@ -1,0 +1,359 @@
+// fm_codec_kernels.hip -- gfx950 kernels of the modded-DAC decode path (DAC.from_indices,
+// modded_dac.py:925-927).  All activations are time-major [t][channel] so that every causal
+// conv, transposed conv and linear layer is one implicit GEMM with channels on the MFMA k axis:
+//
+//   conv_gemm_kernel   out[t*stride+phase][co] = sum_{tap,ci} W[phase][co][tap,ci] x[t-shift][ci]
+//                      CausalConvNet (modded_dac.py:521-552): stride 1, taps j, shift (k-1-j)*dil
+//                      CausalTransConvNet (modded_dac.py:563-580, rvq.py:100-117): one GEMM per
+//                      output phase, taps {0: x[t], 1: x[t-1]} (kernel 2s) or {0} (kernel s)
+//                      nn.Linear: one tap.  Epilogues: bias, GELU, LayerScale/residual, SiLU-mul
+//                      (SwiGLU), tanh, and Snake1d of the NEXT stage (descript Snake1d:
+//                      x + (a+1e-9)^-1 sin^2(a x)) written to a second buffer.
+//   rvq_decode_kernel  rvq.py:352-366 + descript ResidualVectorQuantize.from_codes
+//   dwconv_ln_kernel   ConvNeXt depthwise causal k7 + LayerNorm (rvq.py:176-178)
+//   rope_qk_kernel / window_attn_kernel   WindowLimitedTransformer (modded_dac.py:349-439)
+#include "fm_codec.h"
+
+template <typename T> struct CF;
+template <> struct CF<bf16_t> {
+    typedef u32x4_t f;
+    static __device__ __forceinline__ f wload(const bf16_t* blk, int lane) {
+        return *reinterpret_cast<const u32x4_t*>(blk + lane * 8);
+    }
+    static __device__ __forceinline__ f xload(const bf16_t* p, bool valid) {
+        u32x4_t v = *reinterpret_cast<const u32x4_t*>(p);
+        const uint32_t m = valid ? 0xffffffffu : 0u;
+        return (u32x4_t){v[0] & m, v[1] & m, v[2] & m, v[3] & m};
+    }
+    static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                       __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+    }
+};
+template <> struct CF<float> {
+    struct f {
+        f32x4_t lo, hi;
+    };
+    static __device__ __forceinline__ f wload(const float* blk, int lane) {
+        f v;
+        v.lo = *reinterpret_cast<const f32x4_t*>(blk + lane * 4);
+        v.hi = *reinterpret_cast<const f32x4_t*>(blk + 256 + lane * 4);
+        return v;
+    }
+    static __device__ __forceinline__ f xload(const float* p, bool valid) {
+        f v;
+        v.lo = *reinterpret_cast<const f32x4_t*>(p);
+        v.hi = *reinterpret_cast<const f32x4_t*>(p + 4);
+        if (!valid) {
+            v.lo = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+            v.hi = v.lo;
+        }
+        return v;
+    }
+    static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[j], b.lo[j], c, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[j], b.hi[j], c, 0, 0, 0);
+        return c;
+    }
+};
+
+__device__ __forceinline__ float snake_f(float y, float al) {
+    const float s = sinf(al * y);
+    return y + (1.0f / (al + 1e-9f)) * (s * s);
+}
+
+// block = 4 waves, block tile 64 time x 64 channels, wave tile 32 x 32 (2x2 MFMA 16x16x32)
+template <typename T>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
+    using F = CF<T>;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tq0 = blockIdx.x * 64 + (wave & 1) * 32;
+    const int co0 = blockIdx.y * 64 + (wave >> 1) * 32;
+    const int phase = blockIdx.z;
+    if (co0 >= a.Co) return;
+    const int r = lane & 15, g = lane >> 4;
+    const int Kt = a.ntaps * a.Ci, S = (Kt + 31) >> 5;  // weights zero-padded to 32-multiples
+    const T* wb = a.w + (size_t)phase * a.wphase;
+    const bool c1 = co0 + 16 < a.Co;
+    const int ct0 = co0 >> 4;
+    f32x4_t acc[2][2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[c][u] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int tq[2] = {tq0 + r, tq0 + 16 + r};
+#pragma unroll 4
+    for (int s = 0; s < S; ++s) {
+        // this lane's 8-element chunk lies inside one tap (Ci % 8 == 0)
+        const int kl = s * 32 + 8 * g;
+        int tap = kl / a.Ci;
+        const bool kin = tap < a.ntaps;
+        tap = kin ? tap : a.ntaps - 1;
+        const int ci0 = kin ? kl - tap * a.Ci : 0;
+        const int sh = a.shift[tap];
+        typename F::f fa0 = F::wload(wb + ((size_t)ct0 * S + s) * 512, lane);
+        typename F::f fa1 = F::wload(wb + ((size_t)(c1 ? ct0 + 1 : ct0) * S + s) * 512, lane);
+        typename F::f fb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int row = tq[u] - sh;
+            const bool valid = kin && row >= 0 && row < a.Lx;
+            const int rc = row < 0 ? 0 : (row >= a.Lx ? a.Lx - 1 : row);
+            fb[u] = F::xload(a.x + (size_t)rc * a.ldx + ci0, valid);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            acc[0][u] = F::mma(fa0, fb[u], acc[0][u]);
+            acc[1][u] = F::mma(fa1, fb[u], acc[1][u]);
+        }
+    }
+    const int fl = a.flags;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (c == 1 && !c1) break;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int t = tq0 + 16 * u + (lane & 15);
+            if (t >= a.Lq) continue;
+            const int tout = t * a.stride + phase;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int co = co0 + 16 * c + 4 * (lane >> 4) + i;
+                if (co >= a.Co) continue;
+                float y = acc[c][u][i];
+                if (fl & CE_BIAS) y += ld(a.bias, co);
+                y = rnd<T>(y);
+                if (fl & CE_GELU) y = rnd<T>(0.5f * y * (1.0f + erff(y * 0.70710678118654752f)));
+                if (fl & CE_RES) {
+                    const float rv = ld(a.res, (size_t)tout * a.ldr + co);
+                    if (fl & CE_GAMMA) y = rnd<T>(rv + rnd<T>(ld(a.gamma, co) * y));
+                    else y = rnd<T>(rv + y);
+                }
+                if (fl & CE_TANH) y = tanhf(y);
+                if (fl & CE_STORE) {
+                    if (fl & CE_F32OUT) reinterpret_cast<float*>(a.out)[(size_t)tout * a.ldo + co] = y;
+                    else st(reinterpret_cast<T*>(a.out), (size_t)tout * a.ldo + co, y);
+                }
+                if (fl & CE_SNAKE) st(a.out2, (size_t)tout * a.ldo2 + co, snake_f(y, ld(a.alpha2, co)));
+            }
+        }
+    }
+}
+
+// SwiGLU helper epilogue: out = silu(round(g)) * y   (modded_dac.py:316-317) -- done by a tiny
+// elementwise kernel after the w3 GEMM to keep conv_gemm_kernel's epilogue set small.
+template <typename T>
+__global__ void silu_mul_kernel(const T* __restrict__ g, T* __restrict__ y, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const float a = ld(g, i);
+        st(y, i, rnd<T>(a / (1.0f + expf(-a))) * ld(y, i));
+    }
+}
+
+// z[t][c] = (semantic out_proj(cb[code])) + (sum of residual out_proj(cb_q[code_q]))
+template <typename T>
+__global__ __launch_bounds__(256) void rvq_decode_kernel(const int32_t* __restrict__ codes, int Tn, int nq1,
+                                                         int sem_size, int cb_size, int cd, RvqPtrs p,
+                                                         int D, T* __restrict__ z) {
+    const int t = blockIdx.x;
+    for (int c = threadIdx.x; c < D; c += blockDim.x) {
+        float zs = 0.f, zr = 0.f;
+        for (int q = 0; q < nq1; ++q) {
+            int code = codes[(size_t)q * Tn + t];
+            const int mx = (q == 0 ? sem_size : cb_size) - 1;
+            code = code > mx ? mx : code;  // rvq.py:354-359 clamps the max only
+            const float* e = p.cb[q] + (size_t)code * cd;
+            const float* w = p.w[q] + (size_t)c * cd;
+            float acc = 0.f;
+            for (int j = 0; j < cd; ++j) acc += w[j] * e[j];
+            acc += p.b[q][c];
+            if (q == 0) zs += acc;
+            else zr += acc;
+        }
+        st(z, (size_t)t * D + c, zs + zr);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dwconv_ln_kernel(const T* __restrict__ x, int L, int D,
+                                                        const T* __restrict__ dw, const T* __restrict__ db,
+                                                        const T* __restrict__ lw, const T* __restrict__ lb,
+                                                        T* __restrict__ y) {
+    __shared__ float scratch[16];
+    const int t = blockIdx.x;
+    float v[8];
+    int n = 0;
+    float s = 0.f;
+    for (int c = threadIdx.x; c < D; c += 256, ++n) {
+        float acc = ld(db, c);
+        for (int j = 0; j < 7; ++j) {
+            const int src = t - 6 + j;
+            if (src >= 0) acc += ld(dw, (size_t)c * 7 + j) * ld(x, (size_t)src * D + c);
+        }
+        v[n] = rnd<T>(acc);
+        s += v[n];
+    }
+    const float mu = block_sum(s, scratch) / (float)D;
+    float q = 0.f;
+    for (int i = 0; i < n; ++i) q += (v[i] - mu) * (v[i] - mu);
+    const float var = block_sum(q, scratch) / (float)D;
+    const float rs = 1.0f / sqrtf(var + 1e-6f);
+    n = 0;
+    for (int c = threadIdx.x; c < D; c += 256, ++n)
+        st(y, (size_t)t * D + c, (v[n] - mu) * rs * ld(lw, c) + ld(lb, c));
+}
+
+template <typename T>
+__global__ void rope_qk_kernel(T* __restrict__ qkv, int Tn, int H, int hd, const float* __restrict__ tab) {
+    const int t = blockIdx.x;
+    const int half = hd >> 1;
+    for (int idx = threadIdx.x; idx < 2 * H * half; idx += blockDim.x) {
+        const int head = idx / half, p = idx - head * half;
+        T* v = qkv + (size_t)t * 3 * H * hd + (size_t)head * hd;
+        const float x0 = ld(v, 2 * p), x1 = ld(v, 2 * p + 1);
+        const float c = tab[((size_t)t * half + p) * 2], s = tab[((size_t)t * half + p) * 2 + 1];
+        const float y0 = x0 * c - x1 * s;
+        const float y1 = x1 * c + x0 * s;
+        st(v, 2 * p, y0);
+        st(v, 2 * p + 1, y1);
+    }
+}
+
+// grid (T, H), one wave; window <= 128, hd <= 64
+template <typename T>
+__global__ __launch_bounds__(64) void window_attn_kernel(const T* __restrict__ qkv, int Tn, int H, int hd,
+                                                         int window, T* __restrict__ out) {
+    __shared__ float qs[64];
+    __shared__ float ps[128];
+    const int lane = threadIdx.x;
+    const int t = blockIdx.x, h = blockIdx.y;
+    const size_t ld3 = (size_t)3 * H * hd;
+    const T* q = qkv + (size_t)t * ld3 + (size_t)h * hd;
+    if (lane < hd) qs[lane] = ld(q, lane);
+    __syncthreads();
+    int j0 = t - window + 1;
+    if (j0 < 0) j0 = 0;
+    const int nj = t - j0 + 1;
+    const float scale = 1.0f / sqrtf((float)hd);
+    float sc[2] = {-INFINITY, -INFINITY};
+    for (int i = 0; i < 2; ++i) {
+        const int jj = lane + 64 * i;
+        if (jj < nj) {
+            const T* k = qkv + (size_t)(j0 + jj) * ld3 + (size_t)(H + h) * hd;
+            float dot = 0.f;
+            for (int e = 0; e < hd; e += 8) {
+                float kv[8];
+                load8(k + e, kv);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) dot += qs[e + u] * kv[u];
+            }
+            sc[i] = dot * scale;
+        }
+    }
+    const float m = wave_max(fmaxf(sc[0], sc[1]));
+    const float p0 = lane < nj ? expf(sc[0] - m) : 0.f;
+    const float p1 = lane + 64 < nj ? expf(sc[1] - m) : 0.f;
+    const float l = wave_sum(p0 + p1);
+    ps[lane] = p0;
+    ps[lane + 64] = p1;
+    __syncthreads();
+    if (lane < hd) {
+        float o = 0.f;
+        for (int jj = 0; jj < nj; ++jj)
+            o += ps[jj] * ld(qkv + (size_t)(j0 + jj) * ld3 + (size_t)(2 * H + h) * hd, lane);
+        st(out, (size_t)t * H * hd + (size_t)h * hd + lane, o / l);
+    }
+}
+
+// weight norm (torch _weight_norm, dim=0): w = v * (g / ||v||) per leading index
+__global__ __launch_bounds__(256) void wn_fold_kernel(const float* __restrict__ g, const float* __restrict__ v,
+                                                      int per, float* __restrict__ w) {
+    __shared__ float scratch[16];
+    const int row = blockIdx.x;
+    const float* vr = v + (size_t)row * per;
+    float ss = 0.f;
+    for (int i = threadIdx.x; i < per; i += 256) ss += vr[i] * vr[i];
+    ss = block_sum(ss, scratch);
+    const float f = g[row] / sqrtf(ss);
+    for (int i = threadIdx.x; i < per; i += 256) w[(size_t)row * per + i] = vr[i] * f;
+}
+
+// fp32 conv weights -> row-major [phase][co][tap*Ci + ci] in T.
+// kind 0: Conv1d [Co][Ci][k], tap j (shift (k-1-j)*dil set by the host)
+// kind 1: ConvTranspose1d [Ci][Co][2s]: phase p, tap0 = W[.][.][p] (x[t]), tap1 = W[.][.][p+s] (x[t-1])
+// kind 2: ConvTranspose1d [Ci][Co][s]: phase p, one tap W[.][.][p]
+// kind 3: Linear [Co][Ci]
+template <typename T>
+__global__ void conv_weight_kernel(const float* __restrict__ w, int kind, int Ci, int Co, int k, int s,
+                                   T* __restrict__ out) {
+    const int ntaps = kind == 0 ? k : (kind == 1 ? 2 : 1);
+    const int nph = kind == 0 || kind == 3 ? 1 : s;
+    const int64_t Kt = (int64_t)ntaps * Ci;
+    const int64_t Kp = (Kt + 31) / 32 * 32;  // zero-padded row length
+    const int64_t n = (int64_t)nph * Co * Kp;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t ph = i / (Co * Kp);
+        const int64_t rem = i - ph * Co * Kp;
+        const int co = (int)(rem / Kp);
+        const int kk = (int)(rem - (int64_t)co * Kp);
+        if (kk >= Kt) {
+            st(out, i, 0.f);
+            continue;
+        }
+        const int tap = kk / Ci, ci = kk - tap * Ci;
+        float v;
+        if (kind == 0) v = w[((size_t)co * Ci + ci) * k + tap];
+        else if (kind == 1) v = w[((size_t)ci * Co + co) * (2 * s) + ph + tap * s];
+        else if (kind == 2) v = w[((size_t)ci * Co + co) * s + ph];
+        else v = w[(size_t)co * Ci + ci];
+        st(out, i, v);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a) {
+    dim3 g(FM_CEIL(a.Lq, 64), FM_CEIL(a.Co, 64), a.nphase);
+    conv_gemm_kernel<T><<<g, 256, 0, s>>>(a);
+}
+template <typename T> void launch_silu_mul(hipStream_t s, const T* g, T* y, size_t n) {
+    silu_mul_kernel<T><<<(int)std::min<size_t>(FM_CEIL(n, 256), 16384), 256, 0, s>>>(g, y, n);
+}
+template <typename T>
+void launch_rvq_decode(hipStream_t s, const int32_t* codes, int Tn, int nq1, int sem, int cbs, int cd,
+                       const RvqPtrs& p, int D, T* z) {
+    rvq_decode_kernel<T><<<Tn, 256, 0, s>>>(codes, Tn, nq1, sem, cbs, cd, p, D, z);
+}
+template <typename T>
+void launch_dwconv_ln(hipStream_t s, const T* x, int L, int D, const T* dw, const T* db, const T* lw,
+                      const T* lb, T* y) {
+    dwconv_ln_kernel<T><<<L, 256, 0, s>>>(x, L, D, dw, db, lw, lb, y);
+}
+template <typename T> void launch_rope_qk(hipStream_t s, T* qkv, int Tn, int H, int hd, const float* tab) {
+    rope_qk_kernel<T><<<Tn, 256, 0, s>>>(qkv, Tn, H, hd, tab);
+}
+template <typename T>
+void launch_window_attn(hipStream_t s, const T* qkv, int Tn, int H, int hd, int window, T* out) {
+    window_attn_kernel<T><<<dim3(Tn, H), 64, 0, s>>>(qkv, Tn, H, hd, window, out);
+}
+void launch_wn_fold(hipStream_t s, const float* g, const float* v, int rows, int per, float* w) {
+    wn_fold_kernel<<<rows, 256, 0, s>>>(g, v, per, w);
+}
+template <typename T>
+void launch_conv_weight(hipStream_t s, const float* w, int kind, int Ci, int Co, int k, int st_, T* out) {
+    conv_weight_kernel<T><<<4096, 256, 0, s>>>(w, kind, Ci, Co, k, st_, out);
+}
+
+#define CINST(T)                                                                                     \
+    template void launch_conv_gemm<T>(hipStream_t, const ConvArgs<T>&);                              \
+    template void launch_silu_mul<T>(hipStream_t, const T*, T*, size_t);                             \
+    template void launch_rvq_decode<T>(hipStream_t, const int32_t*, int, int, int, int, int,         \
+                                       const RvqPtrs&, int, T*);                                     \
+    template void launch_dwconv_ln<T>(hipStream_t, const T*, int, int, const T*, const T*, const T*, \
+                                      const T*, T*);                                                 \
+    template void launch_rope_qk<T>(hipStream_t, T*, int, int, int, const float*);                   \
+    template void launch_window_attn<T>(hipStream_t, const T*, int, int, int, int, T*);              \
+    template void launch_conv_weight<T>(hipStream_t, const float*, int, int, int, int, int, T*);
+CINST(bf16_t)
+CINST(float)

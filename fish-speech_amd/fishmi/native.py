@@ -24,7 +24,8 @@ ABI_SYMBOLS = [
     "fm_llm_finalize", "fm_llm_prefill", "fm_llm_decode", "fm_llm_generate", "fm_llm_teacher_step",
     "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_use_graph",
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
-    "fm_codec_finalize", "fm_codec_decode", "fm_codec_profile_read", "fm_codec_close",
+    "fm_codec_finalize", "fm_codec_decode", "fm_codec_profile_read", "fm_codec_debug_read",
+    "fm_codec_close",
 ]
 
 
@@ -77,6 +78,7 @@ def lib():
                                             ctypes.POINTER(ctypes.c_int64),
                                             ctypes.POINTER(ctypes.c_double)]
         L.fm_codec_close.argtypes = [vp]
+        L.fm_codec_debug_read.argtypes = [vp, i32, i32, pf32]
     _lib = L
     return L
 

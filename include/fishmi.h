@@ -136,6 +136,10 @@ int fm_codec_finalize(fm_codec* h);
    pcm: 2048*T floats in [-1, 1]. */
 int fm_codec_decode(fm_codec* h, const int32_t* codes, int T, float* pcm);
 int fm_codec_profile_read(fm_codec* h, double* total_ms, int64_t* launches, double* flops);
+/* test hook: intermediate of the last decode as fp32, time-major (1 transformer out [T][latent],
+   2 first upsample [2T][latent], 3 decoder input [4T][latent]); other stages' buffers are
+   reused in place and are not readable. */
+int fm_codec_debug_read(fm_codec* h, int stage, int T, float* out);
 int fm_codec_close(fm_codec* h);
 
 #ifdef __cplusplus

@@ -333,7 +333,7 @@ def cmd_ops():
 # --------------------------------------------------------------------------------------
 # Codec (modded DAC decode)
 # --------------------------------------------------------------------------------------
-CODEC_TINY = dict(encoder_dim=8, latent=128, decoder_dim=64, n_codebooks=9, codebook_size=32,
+CODEC_TINY = dict(encoder_dim=8, latent=128, decoder_dim=256, n_codebooks=9, codebook_size=32,
                   semantic_codebook_size=64, codebook_dim=8, t_layers=2, t_heads=2,
                   t_head_dim=64, t_inter=384, window=16)
 CODEC_FULL = dict(encoder_dim=64, latent=1024, decoder_dim=1536, n_codebooks=9,
