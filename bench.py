@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json's headline metric on the MI355X-native path.
+
+Metric: synthesised audio-seconds per wall-second (aggregate over all GPUs) + p50 first-sample
+latency, S2-Pro 4B.  One "step" = one utterance per GPU of BASELINE config 2:
+a 64-token prompt, 216 decode frames (10.03 s of 44.1 kHz audio at 21.533 frames/s) with
+<|im_end|> masked so the length is fixed, and the codec decode of the [1, 10, 216] codes.
+The first 8 frames are vocoded as soon as they exist (the codec is causal end to end, so that
+chunk is exactly the prefix of the final waveform); the time from request to that PCM is the
+first-sample latency.  N>1: one process per GPU (torch.distributed.run), rank 0 scatters the
+request descriptors and gathers the int16 PCM over RCCL (fishmi/dp.py), weak scaling.
+
+Weights are seeded synthetic bf16 at the S2-Pro shapes (there is no checkpoint on the box).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fish-speech_amd"))
+
+METRIC = "audio-sec/wall-sec (RTF) + p50 first-sample latency, S2-Pro 4B @1/2/4/8 GPU"
+FRAME_RATE = 44100.0 / 2048.0          # codec frames per audio second (modded_dac.py:833,861)
+HBM_PEAK_GBPS = 8000.0                 # MI355X HBM3E (MI355X_MICROARCH.md §HBM)
+BF16_DENSE_TFLOPS = 2500.0             # MI355X dense bf16 MFMA peak (no sparsity)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--frames", type=int, default=216)
+    ap.add_argument("--prompt-len", type=int, default=64)
+    ap.add_argument("--first-chunk", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=4, help="oracle decode frames sampled")
+    ap.add_argument("--cpu-codec-frames", type=int, default=4, help="oracle codec frames sampled")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def make_prompt(cfg, T, seed):
+    """Template + text token ids: ids from [16, semantic_begin)."""
+    rng = np.random.default_rng(seed + 10**6)  # warmup steps use negative step ids
+    p = np.zeros((cfg.num_codebooks + 1, T), np.int32)
+    p[0] = rng.integers(16, cfg.semantic_begin_id, T)
+    return p
+
+
+def utterance(llm, codec, prompt, sp, frames, first_chunk):
+    """Request -> PCM for one stream.  Returns (pcm, timings in seconds)."""
+    t0 = time.perf_counter()
+    col0 = llm.prefill(0, prompt, sp)
+    t1 = time.perf_counter()
+    f0 = min(first_chunk, frames)
+    head = llm.decode_frames([0], f0 - 1)[:, 0, :]
+    cols = np.concatenate([col0[None], head], axis=0)          # (f0, C+1)
+    codec.decode_codes(np.ascontiguousarray(cols[:, 1:].T))      # first audio chunk
+    t2 = time.perf_counter()
+    rest = llm.decode_frames([0], frames - f0)[:, 0, :]
+    t3 = time.perf_counter()
+    codes = np.ascontiguousarray(np.concatenate([cols, rest], axis=0)[:, 1:].T)  # (C, frames)
+    pcm = codec.decode_codes(codes)
+    t4 = time.perf_counter()
+    return pcm, dict(first=t2 - t0, prefill=t1 - t0, head=t2 - t1, decode=t3 - t2, codec=t4 - t3,
+                     total=t4 - t0)
+
+
+def cpu_baseline(cfg, ccfg, prompt, frames, n_frames, n_codec, seed):
+    """The C oracle (oracle/, a restatement of the reference's CPU path) at full S2-Pro shapes on
+    the host cores: prompt pass + n_frames decode frames and a codec decode of n_codec frames,
+    extrapolated to the bench utterance (prefill + frames decode frames + codec of frames)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    llm = O.OracleLLM(cfg, True)
+    llm.synth(seed, 5)
+    out = llm.generate(prompt, 1 + n_frames, temperature=0.8, top_p=0.8, top_k=30, seed=seed)
+    t_pre, t_fr = O.OracleLLM.last_generate_timing()
+    n_fr = max(out.shape[1] - 1, 1)
+    del llm
+    codec = O.OracleCodec(ccfg)
+    codec.synth(seed)
+    codes = np.ascontiguousarray(out[1:, :1].repeat(n_codec, axis=1))
+    t0 = time.perf_counter()
+    codec.decode(codes)
+    t_codec = time.perf_counter() - t0
+    del codec
+    per_frame, per_codec = t_fr / n_fr, t_codec / n_codec
+    est = t_pre + (frames - 1) * per_frame + frames * per_codec
+    return {"value": round(frames / FRAME_RATE / est, 5), "unit": "audio-sec/wall-sec",
+            "cores": O.threads(), "kind": "port",
+            "sample": (f"C oracle at full S2-Pro shapes, bf16-rounded arithmetic: {prompt.shape[1]}-token "
+                       f"prompt pass {t_pre:.2f}s, {n_fr} decode frames {per_frame:.3f}s/frame, codec "
+                       f"{n_codec} frames {per_codec:.3f}s/frame; extrapolated to prefill + {frames} "
+                       f"frames + codec of {frames} frames = {est:.1f}s")}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from fishmi import dp
+    from fishmi.codec import FishMICodec
+    from fishmi.config import S2_PRO_CONFIG, S2_PRO_IM_END_ID, CodecConfig, DualARConfig
+    from fishmi.llm import DualARModel
+
+    cfg = DualARConfig._from_fish_qwen3_omni(S2_PRO_CONFIG)
+    cfg.im_end_id = S2_PRO_IM_END_ID
+    cfg.max_seq_len = max(1024, args.prompt_len + args.frames + 8)
+    ccfg = CodecConfig()
+    llm = DualARModel.synthetic(cfg, seed=args.seed, log2_half=5, device=local, precision="bf16",
+                                max_slots=1)
+    codec = FishMICodec.synthetic(ccfg, args.seed + 1, local, "bf16", max_frames=args.frames)
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    def one_step(step):
+        # rank 0 owns the request list; each rank gets one utterance (weak scaling)
+        if dist is not None:
+            prompts = [make_prompt(cfg, args.prompt_len, 1000 * step + r) for r in range(world)] \
+                if rank == 0 else None
+            prompt = dp.scatter_prompts(prompts, cfg.num_codebooks + 1)
+        else:
+            prompt = make_prompt(cfg, args.prompt_len, 1000 * step)
+        sp = DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30, seed=7919 * step + rank,
+                                  mask_im_end=True)
+        pcm, tm = utterance(llm, codec, prompt, sp, args.frames, args.first_chunk)
+        if dist is not None:
+            dp.gather_pcm(dp.pcm_to_int16(pcm))
+        return tm
+
+    for w in range(args.warmup):
+        one_step(-1 - w)
+    sync()
+    t0 = time.perf_counter()
+    tms = [one_step(k) for k in range(args.steps)]
+    sync()
+    elapsed = time.perf_counter() - t0
+    firsts = np.array([t["first"] for t in tms], np.float64)
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+        f = torch.tensor(firsts, device="cuda")
+        fl = [torch.zeros_like(f) for _ in range(world)]
+        dist.all_gather(fl, f)
+        firsts = torch.cat(fl).cpu().numpy()
+
+    # ---- roofline of the dominant kernel: the decode GEMV ("linear" class).  One decode frame's
+    # GEMV launches (exact args, weights and shapes of the timed frames) are recorded and
+    # replayed back to back as a graph between two HIP events on the compute stream. ----
+    pos = args.prompt_len + args.frames // 2
+    llm.prefill(0, make_prompt(cfg, args.prompt_len, 99), DualARModel.sampling(mask_im_end=True))
+    llm.decode_frames([0], args.frames // 2)
+    avg_us, lin_n, lin_bytes = llm.kernel_bench("linear", reps=20)
+    per_launch = lin_bytes / lin_n
+    achieved = per_launch / (avg_us * 1e-6) / 1e9
+    # per-class split of an eager frame (event-bracketed launches: diagnostic only)
+    llm.profile(True)
+    llm.decode_frames([0], 8)
+    cls_ms = {c: llm.profile_read(c)[0] / 8 for c in ("linear", "attn", "rope", "norm", "sample", "other")}
+    llm.profile(False)
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_gemv_r01.json")
+    if os.path.exists(pmc):
+        with open(pmc) as fh:
+            traffic = json.load(fh).get("hbm_bytes_per_launch")
+
+    # frame-level: algorithmic frame bytes / graph-replayed frame time inside the timed region
+    dec_s = np.mean([t["decode"] for t in tms]) / (args.frames - args.first_chunk)
+    frame_bytes = llm.frame_bytes(1, pos)
+    ms0, n0, fl0 = codec.profile()
+    codec.decode_codes(np.zeros((ccfg.n_codebooks + 1, args.frames), np.int32))
+    ms1, n1, fl1 = codec.profile()
+    codec_tflops = (fl1 - fl0) / ((ms1 - ms0) * 1e-3) / 1e12
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del llm, codec
+        cpu = cpu_baseline(cfg, ccfg, make_prompt(cfg, args.prompt_len, 0), args.frames,
+                           args.cpu_frames, args.cpu_codec_frames, args.seed)
+
+    if rank == 0:
+        audio_s = world * args.steps * args.frames / FRAME_RATE
+        out = {
+            "metric": METRIC,
+            "value": round(audio_s / elapsed, 4),
+            "unit": "audio-sec/wall-sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic: seeded random bf16 weights at S2-Pro 4B shapes, random prompt ids, "
+                    "<|im_end|> masked (fixed length)",
+            "config": {"workload": f"BASELINE config 2 per GPU: one utterance = {args.prompt_len}-token "
+                                   f"prompt + {args.frames} Dual-AR frames (top_k 30, top_p 0.8, temp 0.8) "
+                                   f"+ codec decode [1,10,{args.frames}] -> {args.frames * 2048} samples",
+                       "global_batch": world, "frames": args.frames, "prompt_len": args.prompt_len,
+                       "first_chunk_frames": args.first_chunk, "parallelism": f"dp{world}"},
+            "p50_first_sample_ms": round(float(np.median(firsts)) * 1e3, 2),
+            "per_stream_rtf": round(args.frames / FRAME_RATE / np.mean([t["total"] for t in tms]), 4),
+            "breakdown_ms": {k: round(float(np.mean([t[k] for t in tms])) * 1e3, 2)
+                             for k in ("prefill", "head", "decode", "codec", "total")},
+            "roofline": {"kernel": "gemv_kernel (decode linear layers, fused norm/residual prologues)",
+                         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic, "bytes_per_launch": int(per_launch),
+                         "avg_launch_us": round(avg_us, 3), "launches_per_frame": int(lin_n),
+                         "method": "one frame's GEMV launches replayed x20 as a graph, HIP events on "
+                                   "the compute stream"},
+            "frame_roofline": {"bytes_per_frame": int(frame_bytes), "ms_per_frame": round(dec_s * 1e3, 4),
+                               "achieved": round(frame_bytes / dec_s / 1e9, 1), "unit": "GB/s",
+                               "frac": round(frame_bytes / dec_s / 1e9 / HBM_PEAK_GBPS, 4),
+                               "eager_event_class_ms_per_frame": {k: round(v, 4) for k, v in cls_ms.items()}},
+            "codec_roofline": {"bound": "mfma", "achieved": round(codec_tflops, 2),
+                               "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                               "frac": round(codec_tflops / BF16_DENSE_TFLOPS, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

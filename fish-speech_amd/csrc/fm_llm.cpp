@@ -76,6 +76,8 @@ struct fm_llm {
     int32_t *tok_in = nullptr, *cols = nullptr, *ptok = nullptr, *ras = nullptr;
     SlotParams* sp = nullptr;
     int32_t* h_cols = nullptr;  // pinned [2][max_slots][C1]
+    int32_t* h_hist = nullptr;  // pinned, grown on demand: [frames][n][C1] of fm_llm_decode_frames
+    size_t h_hist_n = 0;
     std::vector<int> host_pos, host_step;
     std::vector<int> uploaded_slots;
     // graphs
@@ -91,6 +93,7 @@ struct fm_llm {
             if (kv.second.p) (void)hipFree(kv.second.p);
         for (void* p : allocs) (void)hipFree(p);
         if (h_cols) (void)hipHostFree(h_cols);
+        if (h_hist) (void)hipHostFree(h_hist);
         if (stream) (void)hipStreamDestroy(stream);
     }
     void* dalloc(size_t bytes, bool zero = true) {
@@ -187,7 +190,10 @@ template <typename T> struct Run {
         const int64_t wbytes = (int64_t)N * K * E * (epi == EPI_SWIGLU ? 2 : 1);
         const int64_t bytes = wbytes + (int64_t)R * K * E + (int64_t)R * N * (epi == EPI_F32 ? 4 : E);
         const double flops = 2.0 * R * N * K * (epi == EPI_SWIGLU ? 2 : 1);
-        m->prof.run(s, cls, bytes, flops, [&] { launch_linear<T>(s, a, epi); });
+        hipStream_t st = s;
+        auto go = [st, a, epi] { launch_linear<T>(st, a, epi); };
+        m->prof.record(cls, bytes, go);
+        m->prof.run(s, cls, bytes, flops, go);
     }
 
     // TransformerBlock.forward (llama.py:838-843) on R rows; x is updated in place.
@@ -234,7 +240,10 @@ template <typename T> struct Run {
         const int64_t wbytes = (int64_t)a.N * a.K * E * (epi == EPI_SWIGLU ? 2 : 1);
         const int64_t bytes = wbytes + (int64_t)a.R * a.K * E;
         const double flops = 2.0 * a.R * a.N * a.K * (epi == EPI_SWIGLU ? 2 : 1);
-        m->prof.run(s, cls, bytes, flops, [&] { launch_gemv<T>(s, a, pro, epi, ksb); });
+        hipStream_t st = s;
+        auto go = [st, a, pro, epi, ksb] { launch_gemv<T>(st, a, pro, epi, ksb); };
+        m->prof.record(cls, bytes, go);
+        m->prof.run(s, cls, bytes, flops, go);
     }
     struct KsbPlan {
         int wo, w2;
@@ -957,6 +966,41 @@ int fm_llm_decode(fm_llm* m, const int32_t* slots, int n, int32_t* cols) {
     });
 }
 
+int fm_llm_decode_frames(fm_llm* m, const int32_t* slots, int n, int nframes, int32_t* cols) {
+    return fm_guard([&] {
+        FMCHECK(m && slots && cols && n >= 1 && n <= m->max_slots && nframes >= 0, "bad arguments");
+        FMCHECK(m->finalized, "call fm_llm_prefill first");
+        HIPCHK(hipSetDevice(m->device));
+        for (int i = 0; i < n; ++i) {
+            FMCHECK(slots[i] >= 0 && slots[i] < m->max_slots, "bad slot");
+            for (int j = 0; j < i; ++j) FMCHECK(slots[j] != slots[i], "duplicate slot");
+            FMCHECK(m->host_pos[slots[i]] + nframes <= m->c.max_seq_len, "slot would pass max_seq_len");
+        }
+        if (nframes == 0) return;
+        const size_t per = (size_t)n * m->C1;
+        if (m->h_hist_n < per * nframes) {
+            if (m->h_hist) HIPCHK(hipHostFree(m->h_hist));
+            m->h_hist = nullptr;
+            m->h_hist_n = 0;
+            HIPCHK(hipHostMalloc((void**)&m->h_hist, per * nframes * 4, hipHostMallocDefault));
+            m->h_hist_n = per * nframes;
+        }
+        upload_frame_rows(m, slots, n);
+        // every frame is queued back to back; the columns stream to pinned memory behind them
+        for (int k = 0; k < nframes; ++k) {
+            launch_frame(m, n);
+            HIPCHK(hipMemcpyAsync(m->h_hist + per * k, m->cols, per * 4, hipMemcpyDeviceToHost, m->stream));
+        }
+        HIPCHK(hipStreamSynchronize(m->stream));
+        m->prof.collect();
+        for (int i = 0; i < n; ++i) {
+            m->host_pos[slots[i]] += nframes;
+            m->host_step[slots[i]] += nframes;
+        }
+        memcpy(cols, m->h_hist, per * nframes * 4);
+    });
+}
+
 int fm_llm_generate(fm_llm* m, int slot, const int32_t* prompt, int T, int max_new, const fm_sampling* sp,
                     int32_t* out, int* n_out) {
     return fm_guard([&] {
@@ -1096,6 +1140,59 @@ int fm_llm_profile_read(fm_llm* m, const char* cls, double* ms, int64_t* launche
         if (ms) *ms = a.ms;
         if (launches) *launches = a.n;
         if (bytes) *bytes = a.bytes;
+    });
+}
+
+int fm_llm_kernel_bench(fm_llm* m, const char* cls, int reps, double* avg_us, int64_t* launches,
+                        int64_t* bytes) {
+    return fm_guard([&] {
+        FMCHECK(m && cls && reps >= 1, "bad arguments");
+        FMCHECK(m->finalized && !m->uploaded_slots.empty(), "decode a frame first");
+        HIPCHK(hipSetDevice(m->device));
+        const int n = (int)m->uploaded_slots.size();
+        const bool was_on = m->prof.on;
+        // record the class's launches of one eager frame (the frame itself runs normally)
+        m->prof.on = false;
+        m->prof.rec.clear();
+        m->prof.rec_bytes.clear();
+        m->prof.rec_cls = cls;
+        with_prec(m, [&](auto& r) { r.decode_frame(n); });
+        m->prof.rec_cls.clear();
+        m->prof.on = was_on;
+        HIPCHK(hipStreamSynchronize(m->stream));
+        for (int s : m->uploaded_slots) {  // that frame advanced the slots on the device
+            m->host_pos[s]++;
+            m->host_step[s]++;
+        }
+        std::vector<std::function<void()>> rec;
+        rec.swap(m->prof.rec);
+        FMCHECK(!rec.empty(), std::string("no launches of class ") + cls + " in a decode frame");
+        int64_t b = 0;
+        for (int64_t x : m->prof.rec_bytes) b += x;
+        // replay them back to back as one graph, timed by two events on the compute stream
+        hipGraph_t g;
+        HIPCHK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
+        for (auto& f : rec) f();
+        HIPCHK(hipStreamEndCapture(m->stream, &g));
+        hipGraphExec_t ge;
+        HIPCHK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        HIPCHK(hipGraphDestroy(g));
+        hipEvent_t ea, eb;
+        HIPCHK(hipEventCreate(&ea));
+        HIPCHK(hipEventCreate(&eb));
+        HIPCHK(hipGraphLaunch(ge, m->stream));
+        HIPCHK(hipEventRecord(ea, m->stream));
+        for (int i = 0; i < reps; ++i) HIPCHK(hipGraphLaunch(ge, m->stream));
+        HIPCHK(hipEventRecord(eb, m->stream));
+        HIPCHK(hipEventSynchronize(eb));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, ea, eb));
+        (void)hipEventDestroy(ea);
+        (void)hipEventDestroy(eb);
+        (void)hipGraphExecDestroy(ge);
+        if (avg_us) *avg_us = (double)ms * 1e3 / ((double)reps * rec.size());
+        if (launches) *launches = (int64_t)rec.size();
+        if (bytes) *bytes = b;
     });
 }
 

@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -105,6 +106,16 @@ struct Profiler {
         double flops = 0;
     };
     std::map<std::string, Acc> acc;
+    // launch recording for kernel-class replay timing (fm_llm_kernel_bench)
+    std::string rec_cls;
+    std::vector<std::function<void()>> rec;
+    std::vector<int64_t> rec_bytes;
+    template <typename F> void record(const char* cls, int64_t bytes, const F& f) {
+        if (!rec_cls.empty() && rec_cls == cls) {
+            rec.emplace_back(f);
+            rec_bytes.push_back(bytes);
+        }
+    }
     hipEvent_t get() {
         if (pool.empty()) {
             hipEvent_t e;

@@ -140,6 +140,14 @@ class DualARModel:
         native.check(native.lib().fm_llm_decode(self.h, native.i32p(s), s.size, native.i32p(out)))
         return out
 
+    def decode_frames(self, slots, nframes: int) -> np.ndarray:
+        """decode_n_tokens without the per-frame host sync: (nframes, n, C+1) columns."""
+        s = np.ascontiguousarray(slots, dtype=np.int32)
+        out = np.zeros((nframes, s.size, self.C1), np.int32)
+        native.check(native.lib().fm_llm_decode_frames(self.h, native.i32p(s), s.size, nframes,
+                                                       native.i32p(out)))
+        return out
+
     def generate(self, prompt: np.ndarray, max_new_tokens: int, temperature=0.7, top_p=0.9,
                  top_k=30, seed=0, slot=0, mask_im_end=False) -> np.ndarray:
         """inference.generate: returns the emitted columns (C+1, n) (seq[:, T:])."""
@@ -178,6 +186,14 @@ class DualARModel:
         native.check(native.lib().fm_llm_profile_read(self.h, cls.encode(), ctypes.byref(ms),
                                                       ctypes.byref(n), ctypes.byref(b)))
         return ms.value, n.value, b.value
+
+    def kernel_bench(self, kernel_class: str = "linear", reps: int = 20):
+        """(avg us per launch, launches per frame, algorithmic bytes per frame) of one decode
+        frame's launches of kernel_class, replayed back to back (fm_llm_kernel_bench)."""
+        us, n, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+        native.check(native.lib().fm_llm_kernel_bench(self.h, kernel_class.encode(), reps, ctypes.byref(us),
+                                                      ctypes.byref(n), ctypes.byref(b)))
+        return us.value, n.value, b.value
 
     def use_graph(self, enable: bool):
         native.check(native.lib().fm_llm_use_graph(self.h, int(enable)))

@@ -21,8 +21,8 @@ _lib = None
 # every symbol include/fishmi.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = [
     "fm_device_count", "fm_last_error", "fm_llm_open", "fm_llm_set_tensor", "fm_llm_synth_tensor",
-    "fm_llm_finalize", "fm_llm_prefill", "fm_llm_decode", "fm_llm_generate", "fm_llm_teacher_step",
-    "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_use_graph",
+    "fm_llm_finalize", "fm_llm_prefill", "fm_llm_decode", "fm_llm_decode_frames", "fm_llm_generate", "fm_llm_teacher_step",
+    "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph",
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
     "fm_codec_finalize", "fm_codec_decode", "fm_codec_profile_read", "fm_codec_debug_read",
     "fm_codec_close",
@@ -58,6 +58,7 @@ def lib():
     L.fm_llm_finalize.argtypes = [vp]
     L.fm_llm_prefill.argtypes = [vp, i32, pi32, i32, ctypes.POINTER(SamplingC), pi32]
     L.fm_llm_decode.argtypes = [vp, pi32, i32, pi32]
+    L.fm_llm_decode_frames.argtypes = [vp, pi32, i32, i32, pi32]
     L.fm_llm_generate.argtypes = [vp, i32, pi32, i32, i32, ctypes.POINTER(SamplingC), pi32,
                                   ctypes.POINTER(ctypes.c_int)]
     L.fm_llm_teacher_step.argtypes = [vp, i32, pi32, i32, i32, pi32, pf32, pf32, pf32]
@@ -65,6 +66,8 @@ def lib():
     L.fm_llm_frame_bytes.restype = i64
     L.fm_llm_profile.argtypes = [vp, i32]
     L.fm_llm_profile_read.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    L.fm_llm_kernel_bench.argtypes = [vp, ctypes.c_char_p, i32, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.fm_llm_use_graph.argtypes = [vp, i32]
     L.fm_llm_close.argtypes = [vp]

@@ -13,6 +13,7 @@
  *                                       arange(T))             (inference.py:322-335)
  *   fm_llm_decode                    <- decode_one_token_ar per frame, batched over slots
  *                                                              (inference.py:96-181, 209-234)
+ *   fm_llm_decode_frames             <- decode_n_tokens        (inference.py:184-238)
  *   fm_llm_generate                  <- generate()             (inference.py:241-359)
  *   fm_llm_teacher_step              <- forward_generate + forward_generate_fast with given
  *                                       tokens (teacher forcing; parity tests)
@@ -95,6 +96,10 @@ int fm_llm_prefill(fm_llm* h, int slot, const int32_t* tokens, int T, const fm_s
                    int32_t* first_col);
 /* one frame for n slots (each continues from its own position); cols: n x (C+1) */
 int fm_llm_decode(fm_llm* h, const int32_t* slots, int n, int32_t* cols);
+/* nframes frames for the n slots, queued back to back with no host round trip per frame
+   (im_end does not stop it: callers drop columns after a slot's <|im_end|>, as the batched
+   engine does); cols: nframes x n x (C+1). */
+int fm_llm_decode_frames(fm_llm* h, const int32_t* slots, int n, int nframes, int32_t* cols);
 /* full generate() for one slot: out (C+1) x max_new row-major; *n_out frames produced
    (stops after emitting <|im_end|> unless mask_im_end). */
 int fm_llm_generate(fm_llm* h, int slot, const int32_t* prompt, int T, int max_new,
@@ -113,6 +118,13 @@ int64_t fm_llm_frame_bytes(fm_llm* h, int n, int pos);
 int fm_llm_profile(fm_llm* h, int enable);
 int fm_llm_profile_read(fm_llm* h, const char* kernel_class, double* total_ms, int64_t* launches,
                         int64_t* bytes);
+/* roofline hook: runs one decode frame for the last decoded slot set (advancing them one frame)
+   while recording the launches of kernel_class ("linear" = the decode GEMVs), then replays
+   exactly those launches back to back `reps` times as one graph between two HIP events on the
+   compute stream: average duration per launch, launches and algorithmic bytes per frame.
+   The replays clobber activation scratch only (KV caches and slot state are untouched). */
+int fm_llm_kernel_bench(fm_llm* h, const char* kernel_class, int reps, double* avg_us,
+                        int64_t* launches, int64_t* bytes);
 int fm_llm_use_graph(fm_llm* h, int enable);
 int fm_llm_close(fm_llm* h);
 

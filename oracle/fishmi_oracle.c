@@ -233,6 +233,7 @@ int orc_llm_synth_tensor(orc_llm* m, const char* name, int64_t n, uint64_t seed,
                          int log2_half) {
     tensor_t* t = store_put(&m->st, name, n);
     synth_fill(t->f, n, seed, name, center, log2_half);
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) t->f[i] = bf16r(t->f[i]); /* synthetic weights are bf16 */
     m->ready = 0;
     return 0;
@@ -247,6 +248,7 @@ static tensor_t* need(orc_llm* m, const char* name, int64_t n, int* bad) {
     }
     if (m->bf16 && !t->b) {
         t->b = (uint16_t*)malloc(sizeof(uint16_t) * t->n);
+#pragma omp parallel for schedule(static)
         for (int64_t i = 0; i < t->n; ++i) t->b[i] = f2bf(t->f[i]);
     }
     return t;
@@ -661,6 +663,14 @@ static int one_frame(orc_llm* m, const orc_sampling* sp, uint64_t step, const in
     return 0;
 }
 
+/* wall time of the last orc_llm_generate: prompt pass + first frame, and the decode frames
+   after it (bench.py's cpu_baseline leg reads these to avoid timing the prefill twice). */
+static double g_gen_prefill_s, g_gen_frames_s;
+void orc_llm_gen_timing(double* prefill_s, double* frames_s) {
+    if (prefill_s) *prefill_s = g_gen_prefill_s;
+    if (frames_s) *frames_s = g_gen_frames_s;
+}
+
 /* generate (inference.py:241-359): prompt (C+1) x T row-major -> out (C+1) x n_new
    row-major (stride max_new), returns n produced (stops after emitting im_end). */
 int orc_llm_generate(orc_llm* m, const int32_t* prompt, int T, int max_new, const orc_sampling* sp,
@@ -673,8 +683,11 @@ int orc_llm_generate(orc_llm* m, const int32_t* prompt, int T, int max_new, cons
     if (max_new <= 0 || T + max_new > c->max_seq_len) max_new = c->max_seq_len - T;
     (void)S;
     int32_t col[64];
+    const double t0 = omp_get_wtime();
     if (orc_llm_forward(m, prompt, T, 0, m->lg, NULL)) return -1;
     if (one_frame(m, sp, 0, NULL, col)) return -1;
+    const double t1 = omp_get_wtime();
+    g_gen_prefill_s = t1 - t0;
     for (int r = 0; r <= C; ++r) out[r * max_new + 0] = col[r];
     int n = 1;
     int* prev = (int*)calloc((size_t)(C + 1) * 10, sizeof(int));
@@ -691,6 +704,7 @@ int orc_llm_generate(orc_llm* m, const int32_t* prompt, int T, int max_new, cons
         n++;
         if (col[0] == c->im_end_id) break;
     }
+    g_gen_frames_s = omp_get_wtime() - t1;
     free(prev);
     return n;
 }

@@ -134,6 +134,13 @@ class OracleLLM:
         n = _check(lib().orc_llm_generate(self.h, _i32p(p), T, max_new, ctypes.byref(sp), _i32p(out)))
         return out[:, :n]
 
+    @staticmethod
+    def last_generate_timing():
+        """(prompt pass + first frame seconds, remaining frames seconds) of the last generate."""
+        a, b = ctypes.c_double(), ctypes.c_double()
+        lib().orc_llm_gen_timing(ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
 
 def logits_to_probs(logits, temperature, top_p, top_k, bf16=True):
     lg = np.ascontiguousarray(logits, np.float32)

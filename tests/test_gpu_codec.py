@@ -84,11 +84,12 @@ def test_intermediate_latents_match_oracle(golden):
     T = codes.shape[1]
     o = O.OracleCodec(cfg)
     o.synth(int(g["synth_seed"]))
-    wave_o, lat = o.decode(codes, want_latent=True)
     post = np.zeros((cfg.latent, T), np.float32)
     rvq = np.zeros_like(post)
     O.lib().orc_codec_debug_taps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    O.lib().orc_codec_debug_taps(rvq.ctypes.data, post.ctypes.data)
+    O.lib().orc_codec_debug_taps(rvq.ctypes.data, post.ctypes.data)  # filled by the next decode
+    wave_o, lat = o.decode(codes, want_latent=True)
+    O.lib().orc_codec_debug_taps(None, None)
     wave = m.decode_codes(codes)
     for stage, ref in ((1, post.T), (3, lat.T)):
         x = m.debug_read(stage, T)

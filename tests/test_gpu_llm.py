@@ -190,3 +190,36 @@ def test_profile_counters(golden):
     assert n > 0 and ms > 0 and b > 0
     m.profile(False)
     assert m.frame_bytes(1, 30) > 0
+    # replay hook used by bench.py's roofline: does not disturb the stream of the slot
+    sp = m.sampling(top_k=1, mask_im_end=True)
+    m.prefill(0, g["prompt"], sp)
+    a = m.decode_frames([0], 3)
+    us, n, b = m.kernel_bench("linear", reps=3)
+    assert us > 0 and n > 0 and b > 0
+    rest = m.decode_frames([0], 3)
+    ref = m.generate(g["prompt"], 8, top_k=1, mask_im_end=True)
+    np.testing.assert_array_equal(a[:, 0].T, ref[:, 1:4])
+    np.testing.assert_array_equal(rest[:, 0].T, ref[:, 5:8])  # frame 4 ran inside the hook
+
+
+def test_decode_frames_matches_generate(golden):
+    """decode_n_tokens without host sync: prefill + decode_frames over 3 slots (2 slots sampled,
+    one greedy) reproduces each slot's own generate() stream."""
+    from fishmi.llm import DualARModel
+
+    m, g, cfg = _model("llm_b", "bf16", golden, max_slots=3)
+    rng = np.random.default_rng(5)
+    prompts, sps = [], []
+    for s in range(3):
+        p = g["prompt"].copy()
+        p[0, 1:5] = rng.integers(16, cfg.semantic_begin_id, 4)
+        prompts.append(p)
+        sps.append(dict(top_k=1 if s == 2 else 30, seed=100 + s, mask_im_end=True))
+    n_new = 17
+    single = [m.generate(p, n_new, slot=s, **sps[s]) for s, p in enumerate(prompts)]
+    firsts = [m.prefill(s, p, DualARModel.sampling(**sps[s])) for s, p in enumerate(prompts)]
+    fr = m.decode_frames([0, 1, 2], n_new - 1)
+    assert fr.shape == (n_new - 1, 3, cfg.num_codebooks + 1)
+    for s in range(3):
+        got = np.concatenate([firsts[s][:, None], fr[:, s, :].T], axis=1)
+        np.testing.assert_array_equal(got, single[s])
