@@ -154,6 +154,406 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecArgs<T> a) {
     }
 }
 
+
+// Slow-model decode attention for the small-batch path.  grid (R, nkv, maxs), 512 threads.
+// One block normally covers ALL of a row's cached positions for one kv head (up to `cap` rows,
+// sized by the host to the LDS budget: 256 at hd 128 bf16), so the common case writes the bf16
+// output directly.  Longer contexts split into ceil(npos / cap) blocks whose (m, l, o) partials
+// are combined by the last-arriving block (agent-scope release/acquire ticket,
+// cdna_hip_programming.md §6 Guideline 16).  Round trips: (slot, pos, raw q/k/v, norm weights)
+// then (K/V rows, rope row), all loads issued together; the split owning `pos` normalises/ropes
+// the new k and writes k/v to the cache (llama.py:894-914).
+template <typename T>
+__global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+    const int hd = a.hd, g = a.nh / a.nkv, ks = hd + 8, cap = a.cap;
+    const int half = hd >> 1;
+    const T* raw = a.qkv + (size_t)r * a.ldqkv;
+    // ---- round trip 1: everything that does not depend on pos
+    const int slot = a.row_slot[r];
+    const int pos = a.row_pos[r];
+    float q0[2][2], q1[2][2];  // this wave's q heads (wave, wave + 8), pairs lane, lane + 64
+    for (int i = 0; i < 2; ++i) {
+        const int hh = wave + 8 * i;
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            const bool ok = hh < g && p < half;
+            const T* src = raw + (size_t)(kvh * g + (ok ? hh : 0)) * hd;
+            q0[i][u] = ok ? ld(src, 2 * p) : 0.f;
+            q1[i][u] = ok ? ld(src, 2 * p + 1) : 0.f;
+        }
+    }
+    const int kvw = wave >= 6;  // waves 6 / 7: new k / v
+    float k0[2] = {0.f, 0.f}, k1[2] = {0.f, 0.f};
+    if (kvw) {
+        const T* src = raw + (size_t)(wave == 6 ? a.nh + kvh : a.nh + a.nkv + kvh) * hd;
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            if (p < half) {
+                k0[u] = ld(src, 2 * p);
+                k1[u] = ld(src, 2 * p + 1);
+            }
+        }
+    }
+    const int npos = pos + 1;
+    const int nsp = (npos + cap - 1) / cap;
+    const int chunk = ((npos + nsp - 1) / nsp + 15) & ~15;
+    const int j0 = sp * chunk;
+    if (sp >= nsp) return;
+    const int nj = min(chunk, npos - j0);
+    const bool owner = j0 + nj == npos;
+    T* Ks = reinterpret_cast<T*>(smem);                  // [cap][hd+8]
+    T* Vs = Ks + (size_t)cap * ks;                       // [cap][hd]
+    float* qs = reinterpret_cast<float*>(Vs + (size_t)cap * hd);  // [g][hd]
+    float* ps = qs + (size_t)g * hd;                     // [g][cap]
+    int* flag = reinterpret_cast<int*>(ps + (size_t)g * cap);
+    const size_t base = (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
+    T* kc = a.kc + base;
+    T* vc = a.vc + base;
+    const float* tab = a.rope + (size_t)pos * hd;
+    // ---- round trip 2: the block's cached K/V rows (up to 16 x 16 B per thread in flight)
+    {
+        const int cpr = hd * (int)sizeof(T) / 16;
+        const int total = nj * cpr * 2;
+        for (int b0 = 0; b0 < total; b0 += 512 * 16) {
+            u32x4_t v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int idx = b0 + threadIdx.x + 512 * u;
+                if (idx < total) {
+                    const int which = idx >= nj * cpr;
+                    const int rem = idx - which * nj * cpr;
+                    const int j = rem / cpr, c = rem - j * cpr;
+                    const T* src = (which ? vc : kc) + (size_t)(j0 + j) * hd;
+                    v[u] = *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const char*>(src) + 16 * c);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int idx = b0 + threadIdx.x + 512 * u;
+                if (idx < total) {
+                    const int which = idx >= nj * cpr;
+                    const int rem = idx - which * nj * cpr;
+                    const int j = rem / cpr, c = rem - j * cpr;
+                    if (j0 + j == pos) continue;  // the new row comes from waves 6 / 7
+                    T* dst = which ? Vs + (size_t)j * hd : Ks + (size_t)j * ks;
+                    *reinterpret_cast<u32x4_t*>(reinterpret_cast<char*>(dst) + 16 * c) = v[u];
+                }
+            }
+        }
+    }
+    // q heads: qk-norm (fp32 incl. weight, one rounding) + RoPE (bf16 table, rounded)
+    for (int i = 0; i < 2; ++i) {
+        const int hh = wave + 8 * i;
+        if (hh >= g) break;
+        if (a.qk_norm) {
+            float ss = 0.f;
+            for (int u = 0; u < 2; ++u) ss += q0[i][u] * q0[i][u] + q1[i][u] * q1[i][u];
+            ss = wave_sum(ss);
+            const float rs = 1.0f / sqrtf(ss / (float)hd + a.eps);
+            for (int u = 0; u < 2; ++u) {
+                const int p = lane + 64 * u;
+                if (p < half) {
+                    q0[i][u] = rnd<T>((q0[i][u] * rs) * ld(a.qn, 2 * p));
+                    q1[i][u] = rnd<T>((q1[i][u] * rs) * ld(a.qn, 2 * p + 1));
+                }
+            }
+        }
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            if (p < half) {
+                const float c = tab[2 * p], sn = tab[2 * p + 1];
+                qs[hh * hd + 2 * p] = rnd<T>(q0[i][u] * c - q1[i][u] * sn);
+                qs[hh * hd + 2 * p + 1] = rnd<T>(q1[i][u] * c + q0[i][u] * sn);
+            }
+        }
+    }
+    if (kvw && owner) {
+        const bool isk = wave == 6;
+        if (isk && a.qk_norm) {
+            float ss = 0.f;
+            for (int u = 0; u < 2; ++u) ss += k0[u] * k0[u] + k1[u] * k1[u];
+            ss = wave_sum(ss);
+            const float rs = 1.0f / sqrtf(ss / (float)hd + a.eps);
+            for (int u = 0; u < 2; ++u) {
+                const int p = lane + 64 * u;
+                if (p < half) {
+                    k0[u] = rnd<T>((k0[u] * rs) * ld(a.kn, 2 * p));
+                    k1[u] = rnd<T>((k1[u] * rs) * ld(a.kn, 2 * p + 1));
+                }
+            }
+        }
+        T* dst = (isk ? kc : vc) + (size_t)pos * hd;
+        T* tile = isk ? Ks + (size_t)(pos - j0) * ks : Vs + (size_t)(pos - j0) * hd;
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            if (p >= half) break;
+            float y0 = k0[u], y1 = k1[u];
+            if (isk) {
+                const float c = tab[2 * p], sn = tab[2 * p + 1];
+                y0 = rnd<T>(k0[u] * c - k1[u] * sn);
+                y1 = rnd<T>(k1[u] * c + k0[u] * sn);
+            }
+            st(dst, 2 * p, y0);
+            st(dst, 2 * p + 1, y1);
+            st(tile, 2 * p, y0);
+            st(tile, 2 * p + 1, y1);
+        }
+    }
+    __syncthreads();
+    // ---- scores: item (head, row); a wave's 64 items share one head
+    const int rp = (nj + 63) & ~63;
+    const float scale = a.scale;
+    for (int idx = threadIdx.x; idx < g * rp; idx += 512) {
+        const int hh = idx / rp, j = idx - hh * rp;
+        if (j < nj) {
+            const T* kr = Ks + (size_t)j * ks;
+            const float* qv = qs + hh * hd;
+            float dot = 0.f;
+            for (int e = 0; e < hd; e += 8) {
+                float kv[8];
+                load8(kr + e, kv);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) dot += qv[e + u] * kv[u];
+            }
+            ps[hh * cap + j] = dot * scale;
+        }
+    }
+    __syncthreads();
+    // ---- softmax per head (wave per head): p = exp(s - m), l = sum p
+    float mh[2], lh[2];
+    for (int i = 0; i < 2; ++i) {
+        const int hh = wave + 8 * i;
+        mh[i] = -INFINITY;
+        lh[i] = 0.f;
+        if (hh >= g) continue;
+        float* pr = ps + hh * cap;
+        float mx = -INFINITY;
+        for (int j = lane; j < nj; j += 64) mx = fmaxf(mx, pr[j]);
+        mx = wave_max(mx);
+        float sum = 0.f;
+        for (int j = lane; j < nj; j += 64) {
+            const float p = expf(pr[j] - mx);
+            pr[j] = p;
+            sum += p;
+        }
+        mh[i] = mx;
+        lh[i] = wave_sum(sum);
+    }
+    if (lane == 0)
+        for (int i = 0; i < 2; ++i)
+            if (wave + 8 * i < g) {
+                reinterpret_cast<float*>(flag + 4)[2 * (wave + 8 * i)] = mh[i];
+                reinterpret_cast<float*>(flag + 4)[2 * (wave + 8 * i) + 1] = lh[i];
+            }
+    __syncthreads();
+    // ---- PV: item (head, dim pair); two threads per item split the rows (even / odd)
+    const int hp = hd >> 1;
+    const float* ml = reinterpret_cast<const float*>(flag + 4);
+    const bool single = nsp == 1;
+    float* part = a.part + (((size_t)r * a.nh + (size_t)kvh * g) * a.maxsplit + sp) * (hd + 2);
+    for (int idx = threadIdx.x; idx < g * hp * 2; idx += 512) {
+        const int it = idx >> 1, par = idx & 1;
+        const int hh = it / hp, e2 = 2 * (it - hh * hp);
+        const float* pr = ps + hh * cap;
+        float o0 = 0.f, o1 = 0.f;
+        for (int j = par; j < nj; j += 2) {
+            const float p = pr[j];
+            o0 += p * ld(Vs + (size_t)j * hd, e2);
+            o1 += p * ld(Vs + (size_t)j * hd, e2 + 1);
+        }
+        o0 += __shfl_xor(o0, 1);
+        o1 += __shfl_xor(o1, 1);
+        if (par == 0) {
+            if (single) {
+                const float il = 1.0f / ml[2 * hh + 1];
+                T* out = a.out + (size_t)r * a.nh * hd + (size_t)(kvh * g + hh) * hd;
+                st(out, e2, o0 * il);
+                st(out, e2 + 1, o1 * il);
+            } else {
+                float* pp = part + (size_t)hh * a.maxsplit * (hd + 2);
+                pp[2 + e2] = o0;
+                pp[3 + e2] = o1;
+                if (e2 == 0) {
+                    pp[0] = ml[2 * hh];
+                    pp[1] = ml[2 * hh + 1];
+                }
+            }
+        }
+    }
+    if (single) return;
+    // ---- split combine by the last-arriving block of (row, kv head)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(a.cnt + (size_t)r * a.nkv + kvh, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = t == nsp - 1;
+        if (t == nsp - 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(a.cnt + (size_t)r * a.nkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    const float* p0 = a.part + (((size_t)r * a.nh + (size_t)kvh * g) * a.maxsplit) * (hd + 2);
+    for (int idx = threadIdx.x; idx < g * hd; idx += 512) {
+        const int hh = idx / hd, e = idx - hh * hd;
+        const float* pp = p0 + (size_t)hh * a.maxsplit * (hd + 2);
+        float M = -INFINITY;
+        for (int q = 0; q < nsp; ++q) M = fmaxf(M, pp[(size_t)q * (hd + 2)]);
+        float L = 0.f, O = 0.f;
+        for (int q = 0; q < nsp; ++q) {
+            const float w = expf(pp[(size_t)q * (hd + 2)] - M);
+            L += w * pp[(size_t)q * (hd + 2) + 1];
+            O += w * pp[(size_t)q * (hd + 2) + 2 + e];
+        }
+        st(a.out + (size_t)r * a.nh * hd + (size_t)(kvh * g + hh) * hd, e, O / L);
+    }
+}
+
+// Fast-model attention at codebook position cpos (llama.py:947-975, every rounding of the
+// reference's matmul-softmax-matmul kept): grid (R, nh), ONE wave per q head, no LDS, no
+// barrier.  Lane l owns dimension pairs l, l+64 (RoPE pairs).  Each wave recomputes the new k
+// (qk-norm + RoPE, cheap) so waves never wait on each other; the first q head of each kv group
+// writes k/v of cpos to the fast cache.  Two round trips: (slot, raw q/k/v, norm weights, rope
+// row) then (the cpos cached rows).
+template <typename T>
+__global__ __launch_bounds__(64) void fast_attn2_kernel(FastFusedArgs<T> a) {
+    const int lane = threadIdx.x;
+    const int r = blockIdx.x, h = blockIdx.y;
+    const int hd = a.hd, g = a.nh / a.nkv, kvh = h / g, cpos = a.cpos, half = hd >> 1;
+    const T* raw = a.qkv + (size_t)r * a.ldqkv;
+    const float* tab = a.rope + (size_t)cpos * hd;
+    const int slot = a.row_slot[r];
+    float q0[2], q1[2], k0[2], k1[2], v0[2], v1[2], qw0[2], qw1[2], kw0[2], kw1[2], c_[2], s_[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int p = lane + 64 * u;
+        const bool ok = p < half;
+        const int pp = ok ? p : 0;
+        q0[u] = ld(raw + (size_t)h * hd, 2 * pp);
+        q1[u] = ld(raw + (size_t)h * hd, 2 * pp + 1);
+        k0[u] = ld(raw + (size_t)(a.nh + kvh) * hd, 2 * pp);
+        k1[u] = ld(raw + (size_t)(a.nh + kvh) * hd, 2 * pp + 1);
+        v0[u] = ld(raw + (size_t)(a.nh + a.nkv + kvh) * hd, 2 * pp);
+        v1[u] = ld(raw + (size_t)(a.nh + a.nkv + kvh) * hd, 2 * pp + 1);
+        qw0[u] = a.qk_norm ? ld(a.qn, 2 * pp) : 1.f;
+        qw1[u] = a.qk_norm ? ld(a.qn, 2 * pp + 1) : 1.f;
+        kw0[u] = a.qk_norm ? ld(a.kn, 2 * pp) : 1.f;
+        kw1[u] = a.qk_norm ? ld(a.kn, 2 * pp + 1) : 1.f;
+        c_[u] = tab[2 * pp];
+        s_[u] = tab[2 * pp + 1];
+        if (!ok) q0[u] = q1[u] = k0[u] = k1[u] = v0[u] = v1[u] = 0.f;
+    }
+    const size_t base = (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
+    T* kc = a.kc + base;
+    T* vc = a.vc + base;
+    // cached rows j < cpos (<= C - 1 <= 63 rows): the lane's two pairs of each
+    constexpr int MAXJ = 16;
+    float K0[MAXJ][2], K1[MAXJ][2], V0[MAXJ][2], V1[MAXJ][2];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        if (j < cpos) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int p = lane + 64 * u;
+                const int pp = p < half ? p : 0;
+                K0[j][u] = ld(kc + (size_t)j * hd, 2 * pp);
+                K1[j][u] = ld(kc + (size_t)j * hd, 2 * pp + 1);
+                V0[j][u] = ld(vc + (size_t)j * hd, 2 * pp);
+                V1[j][u] = ld(vc + (size_t)j * hd, 2 * pp + 1);
+                if (p >= half) K0[j][u] = K1[j][u] = V0[j][u] = V1[j][u] = 0.f;
+            }
+        }
+    }
+    // qk-norm (fp32 incl. weight, one rounding) + RoPE (bf16 table, rounded)
+    auto prep = [&](float (&x0)[2], float (&x1)[2], const float (&w0)[2], const float (&w1)[2], bool norm) {
+        if (norm) {
+            float ss = 0.f;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) ss += x0[u] * x0[u] + x1[u] * x1[u];
+            ss = wave_sum(ss);
+            const float rs = 1.0f / sqrtf(ss / (float)hd + a.eps);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                x0[u] = rnd<T>((x0[u] * rs) * w0[u]);
+                x1[u] = rnd<T>((x1[u] * rs) * w1[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const float y0 = rnd<T>(x0[u] * c_[u] - x1[u] * s_[u]);
+            const float y1 = rnd<T>(x1[u] * c_[u] + x0[u] * s_[u]);
+            x0[u] = y0;
+            x1[u] = y1;
+        }
+    };
+    prep(q0, q1, qw0, qw1, a.qk_norm);
+    prep(k0, k1, kw0, kw1, a.qk_norm);
+    if (h == kvh * g) {  // first q head of the group stores the new k / v
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            if (p < half) {
+                st(kc + (size_t)cpos * hd, 2 * p, k0[u]);
+                st(kc + (size_t)cpos * hd, 2 * p + 1, k1[u]);
+                st(vc + (size_t)cpos * hd, 2 * p, v0[u]);
+                st(vc + (size_t)cpos * hd, 2 * p + 1, v1[u]);
+            }
+        }
+    }
+    // scores round(round(q.k) * scale), softmax, probabilities rounded (fast SDPA path)
+    float sc[MAXJ + 1];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j <= MAXJ; ++j) {
+        if (j > cpos) break;
+        float d = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const float a0 = j < cpos ? K0[j < MAXJ ? j : 0][u] : k0[u];
+            const float a1 = j < cpos ? K1[j < MAXJ ? j : 0][u] : k1[u];
+            d += q0[u] * a0 + q1[u] * a1;
+        }
+        d = wave_sum(d);
+        sc[j] = rnd<T>(rnd<T>(d) * a.scale);
+        mx = fmaxf(mx, sc[j]);
+    }
+    float den = 0.f;
+#pragma unroll
+    for (int j = 0; j <= MAXJ; ++j) {
+        if (j > cpos) break;
+        sc[j] = expf(sc[j] - mx);
+        den += sc[j];
+    }
+    float o0[2] = {0.f, 0.f}, o1[2] = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j <= MAXJ; ++j) {
+        if (j > cpos) break;
+        const float p = rnd<T>(sc[j] / den);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            o0[u] += p * (j < cpos ? V0[j < MAXJ ? j : 0][u] : v0[u]);
+            o1[u] += p * (j < cpos ? V1[j < MAXJ ? j : 0][u] : v1[u]);
+        }
+    }
+    T* out = a.out + (size_t)r * a.nh * hd + (size_t)h * hd;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int p = lane + 64 * u;
+        if (p < half) {
+            st(out, 2 * p, o0[u]);
+            st(out, 2 * p + 1, o1[u]);
+        }
+    }
+}
+
 // fast model attention at codebook position cpos, fused with qk-norm/rope/cache write.
 // grid (R, nkv), block 256 (wave per q head of the GQA group).
 template <typename T>
@@ -433,6 +833,8 @@ __global__ __launch_bounds__(256) void sample_radix_kernel(SampleArgs a) {
                 for (int j = 0; j < 10; ++j) inwin |= prev[j] == tok;
                 if (inwin && tok >= a.sb && tok <= a.se) tok = hi;
             }
+            // never emit an out-of-range id (NaN logits leave no valid candidate): end the stream
+            if (!((tok >= a.sb && tok <= a.se) || tok == a.im_end)) tok = a.im_end;
             if (lane == 0) {
                 col[0] = tok;
                 int c = tok - a.sb;
@@ -442,7 +844,7 @@ __global__ __launch_bounds__(256) void sample_radix_kernel(SampleArgs a) {
         } else {
             const int code = sample_top<T>(cv, cid, K, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed,
                                            step, (uint32_t)a.draw, lane);
-            if (lane == 0) col[a.col_idx] = code;
+            if (lane == 0) col[a.col_idx] = (code >= 0 && code < a.cb) ? code : 0;
         }
     }
 }
@@ -454,6 +856,19 @@ template <typename T> void launch_attn_decode(hipStream_t s, const AttnDecArgs<T
                        (size_t)4 * a.hd * 4 + 4 * 64 * 4;
     attn_decode_kernel<T><<<g1, 256, lds, s>>>(a);
 }
+template <typename T> void launch_attn_decode2(hipStream_t s, const AttnDecArgs<T>& a, int R) {
+    dim3 g1(R, a.nkv, a.maxsplit);
+    static bool attr = false;  // > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_decode2_kernel<T>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    attn_decode2_kernel<T><<<g1, 512, attn2_lds_bytes(a.hd, a.nh / a.nkv, a.cap, sizeof(T)), s>>>(a);
+}
+template <typename T> void launch_fast_attn2(hipStream_t s, const FastFusedArgs<T>& a, int R) {
+    fast_attn2_kernel<T><<<dim3(R, a.nh), 64, 0, s>>>(a);
+}
 template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFusedArgs<T>& a, int R) {
     dim3 g(R, a.nkv);
     const size_t lds = (size_t)2 * a.S * a.hd * 4 + (size_t)4 * a.hd * 4 + 4 * 64 * 4;
@@ -464,6 +879,10 @@ template <typename T> void launch_sample_radix(hipStream_t s, const SampleArgs& 
 }
 template void launch_attn_decode<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
 template void launch_attn_decode<float>(hipStream_t, const AttnDecArgs<float>&, int);
+template void launch_attn_decode2<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
+template void launch_attn_decode2<float>(hipStream_t, const AttnDecArgs<float>&, int);
+template void launch_fast_attn2<bf16_t>(hipStream_t, const FastFusedArgs<bf16_t>&, int);
+template void launch_fast_attn2<float>(hipStream_t, const FastFusedArgs<float>&, int);
 template void launch_fast_attn_fused<bf16_t>(hipStream_t, const FastFusedArgs<bf16_t>&, int);
 template void launch_fast_attn_fused<float>(hipStream_t, const FastFusedArgs<float>&, int);
 template void launch_sample_radix<bf16_t>(hipStream_t, const SampleArgs&, int);

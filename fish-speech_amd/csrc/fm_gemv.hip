@@ -3,25 +3,29 @@
 // Y[r][n] = sum_k X'[r][k] W[n][k] with the producer/consumer seams of a pre-norm block fused:
 //   prologue  PRO_PLAIN   X' = X
 //             PRO_NORM    X' = rmsnorm(X)                       (llama.py:989-1000)
-//             PRO_RESNORM x  = round(res + round(sum_s slab_s))  (the previous linear's split-K
-//                         X' = rmsnorm(x)                        partials + residual add,
-//                                                                 llama.py:841-842); block 0
-//                                                                 stores x (and X') for later
+//             PRO_PRENORM X' = rmsnorm(X) where X is an already finalised residual row and the
+//                         statistic comes from the producer's per-tile sums of squares
 //   epilogue  EPI_STORE (T, +bias) | EPI_SWIGLU (round(silu(round(w1 x)))*round(w3 x))
-//             | EPI_F32 (logits) | EPI_SLAB (fp32 split-K partial, consumed by the next prologue)
+//             | EPI_F32 (logits) | EPI_SLAB (fp32 split-K partial)
+//             | EPI_SLABFIN (split-K partial; the tile's last-arriving block finalises
+//               x = round(res + round(sum partials)) (llama.py:841-842) and its sum of squares)
 //
 // Geometry: block = 8 waves, 16 weight rows (one 16x16x32 MFMA row tile; the R<=8 streams are
-// MFMA columns), grid = (N/16, KSB).  Wave w takes the block's 32-wide k-steps w, w+8, ...,
-// so the 8 waves read 512 contiguous bytes of each row per sweep.  A ring of U register
-// fragments keeps U weight loads in flight per wave (prefetch distance U, non-temporal loads:
-// each weight byte is read exactly once per frame).  X' is staged once per block in LDS.
+// MFMA columns), grid = (N/16, KSB).  Weights are pre-packed in MFMA-fragment order
+// (fm_kernels.h), so a fragment is 1 KiB of contiguous HBM; wave w owns a contiguous run of the
+// block's k-steps and streams them through a ring of U register fragments (predicated tail).
+// A decode GEMV gives each wave only 4-16 fragments, so latency rules: the prologue's loads go
+// out first (one round trip: x slice, norm weight, tile sums of squares), then the weight ring,
+// then the LDS staging, which therefore overlaps the weight flight.
 #include "fm_kernels.h"
 
 template <typename T> struct GFrag;
 template <> struct GFrag<bf16_t> {
     typedef u32x4_t f;
-    static __device__ __forceinline__ f load_w(const bf16_t* blk, int lane) {
-        return *reinterpret_cast<const u32x4_t*>(blk + lane * 8);
+    template <bool NT> static __device__ __forceinline__ f load_w(const bf16_t* blk, int lane) {
+        const u32x4_t* p = reinterpret_cast<const u32x4_t*>(blk + lane * 8);
+        if constexpr (NT) return __builtin_nontemporal_load(p);
+        else return *p;
     }
     static __device__ __forceinline__ f load_lds(const bf16_t* p) { return *reinterpret_cast<const u32x4_t*>(p); }
     static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
@@ -33,7 +37,7 @@ template <> struct GFrag<float> {
     struct f {
         f32x4_t lo, hi;
     };
-    static __device__ __forceinline__ f load_w(const float* blk, int lane) {
+    template <bool NT> static __device__ __forceinline__ f load_w(const float* blk, int lane) {
         f v;
         v.lo = *reinterpret_cast<const f32x4_t*>(blk + lane * 4);
         v.hi = *reinterpret_cast<const f32x4_t*>(blk + 256 + lane * 4);
@@ -56,22 +60,41 @@ template <> struct GFrag<float> {
 
 __device__ __forceinline__ float silu_g(float a) { return a / (1.0f + expf(-a)); }
 
-// x value of the prologue at (row r, k) before normalisation
-template <typename T, int PRO>
-__device__ __forceinline__ float pro_x(const GemvArgs<T>& a, const T* xr, const T* resr, int r, int k) {
-    if constexpr (PRO == PRO_RESNORM) {
-        float s = 0.f;
-        for (int q = 0; q < a.nslab; ++q) s += a.slab[((size_t)q * a.R + r) * a.slab_ld + k];
-        return rnd<T>(ld(resr, k) + rnd<T>(s));
+// 8 consecutive elements of T as raw 16-byte vectors (bf16: one, fp32: two)
+template <typename T> struct C8 {
+    u32x4_t v[sizeof(T) / 2];
+};
+template <typename T> __device__ __forceinline__ C8<T> load_c8(const T* p) {
+    C8<T> c;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 2); ++i) c.v[i] = reinterpret_cast<const u32x4_t*>(p)[i];
+    return c;
+}
+template <typename T> __device__ __forceinline__ void c8_to_f(const C8<T>& c, float (&o)[8]) {
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            o[2 * i] = __uint_as_float(c.v[0][i] << 16);
+            o[2 * i + 1] = __uint_as_float(c.v[0][i] & 0xffff0000u);
+        }
     } else {
-        return ld(xr, k);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            o[i] = __uint_as_float(c.v[0][i]);
+            o[4 + i] = __uint_as_float(c.v[1][i]);
+        }
     }
 }
 
-template <typename T, int PRO, int EPI, int U>
-__global__ __launch_bounds__(512) void gemv_kernel(GemvArgs<T> a) {
+constexpr int GEMV_RMAX = 8;  // rows (streams) of the small-batch path
+constexpr int GEMV_PRE = 8;   // (row, chunk) items of X preloaded per thread before the weight ring
+
+// WPB waves per block share one 16-row tile, each streaming a contiguous run of its k-steps.
+template <typename T, int PRO, int EPI, bool NT, int U, int WPB>
+__global__ __launch_bounds__(WPB * 64) void gemv_kernel(GemvArgs<T> a) {
     using G = GFrag<T>;
     constexpr int NACC = (EPI == EPI_SWIGLU) ? 2 : 1;
+    constexpr int NTH = WPB * 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n0 = blockIdx.x * 16;
@@ -81,44 +104,51 @@ __global__ __launch_bounds__(512) void gemv_kernel(GemvArgs<T> a) {
     const int R = a.R;
     const int xstride = Kb + 8;  // +16 B per row: conflict-free ds_read_b128 across rows
     T* xs = reinterpret_cast<T*>(smem);
-    float* rstd = reinterpret_cast<float*>(smem + (size_t)R * xstride * sizeof(T));
-    f32x4_t* red = reinterpret_cast<f32x4_t*>(rstd + 16);
+    int* flag = reinterpret_cast<int*>(smem + (size_t)R * xstride * sizeof(T));
+    float* red = reinterpret_cast<float*>(flag + 16);  // [NACC][WPB waves][16 rows][R] partials
+    float* fin = red + 2 * 8 * 16 * R;                // [R][16] EPI_SLABFIN, ksb == 1
+    float* rsl = fin + 16 * R;                        // [8 waves][GEMV_RMAX] PRO_PRENORM 1/rms
 
-    // ---------------- prologue: stage X'[r][kbeg .. kbeg+Kb) in LDS ---------------------------
-    // 16-byte chunks of 8 elements; every thread issues its loads at once (one round trip).
-    if constexpr (PRO == PRO_NORM || PRO == PRO_RESNORM) {
+    const unsigned long long ts0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    const int r = lane & 15, g = lane >> 4;
+    const int S = a.K >> 5, Sb = Kb >> 5, sb0 = ks * Sb;
+    const int wa = (wave * Sb) / WPB, wb = ((wave + 1) * Sb) / WPB, nmy = wb - wa;
+    typename G::f fa[U], fb[NACC == 2 ? U : 1];
+    // Fragment i of the run into ring slot u.  Branch-free on purpose: a load under a branch makes
+    // the compiler drain vmcnt(0) before every MFMA (no pipelining at all), so tail slots re-load
+    // the run's last fragment (a cache hit) instead of being predicated off.
+    const int ilast = nmy > 0 ? nmy - 1 : 0;
+    const size_t run0 = ((size_t)blockIdx.x * S + sb0 + (nmy > 0 ? wa : 0)) * 512;
+    const T* wrun = a.W + run0;
+    const T* wrun2 = (EPI == EPI_SWIGLU) ? a.W2 + run0 : nullptr;
+    auto issue = [&](int i, int u) {
+        const size_t off = (size_t)(i < ilast ? i : ilast) * 512;
+        fa[u] = G::template load_w<NT>(wrun + off, lane);
+        if constexpr (NACC == 2) fb[u] = G::template load_w<NT>(wrun2 + off, lane);
+    };
+
+    // ---------------- prologue: X'[r][kbeg .. kbeg+Kb) -> LDS ----------------------------------
+    // Round trip first: this thread's x chunks (and norm weight / tile sums of squares) are loaded
+    // BEFORE the weight ring is issued, so the in-order vmcnt waits of the staging below do not
+    // queue behind weight bytes.
+    if constexpr (PRO == PRO_NORM) {
+        // full-row statistic from the row itself (first layer: embeddings / gathered rows); the
+        // weight ring starts after it (its block reductions would otherwise wait on weights)
         __shared__ float red_s[16];
         const int nch = a.K >> 3;
         const bool writer = (blockIdx.x == 0 && ks == 0);
-        for (int r = 0; r < R; ++r) {
-            const int xi = a.xidx ? a.xidx[(size_t)r * a.xidx_ld + a.xidx_col] : r;
+        for (int rr = 0; rr < R; ++rr) {
+            const int xi = a.xidx ? a.xidx[(size_t)rr * a.xidx_ld + a.xidx_col] : rr;
             const T* xr = a.X + (size_t)xi * a.ldx;
-            const int ri = a.residx ? a.residx[(size_t)r * a.xidx_ld + a.xidx_col] : r;
-            const T* resr = a.res ? a.res + (size_t)ri * a.ldr : nullptr;
-            float xv[2][8];
+            float xv[4][8], wv[4][8];
             float ss = 0.f;
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int c = threadIdx.x + 512 * j;
+            for (int j = 0; j < 4; ++j) {
+                const int c = threadIdx.x + NTH * j;
                 if (c < nch) {
-                    if constexpr (PRO == PRO_RESNORM) {
-                        float rv[8], sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-                        load8(resr + 8 * c, rv);
-                        for (int q = 0; q < a.nslab; ++q) {
-                            const float* sp = a.slab + ((size_t)q * R + r) * a.slab_ld + 8 * c;
-                            const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(sp);
-                            const f32x4_t s1 = *reinterpret_cast<const f32x4_t*>(sp + 4);
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                sv[u] += s0[u];
-                                sv[4 + u] += s1[u];
-                            }
-                        }
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) xv[j][u] = rnd<T>(rv[u] + rnd<T>(sv[u]));
-                    } else {
-                        load8(xr + 8 * c, xv[j]);
-                    }
+                    const int k = 8 * c;
+                    if ((k >= kbeg && k < kbeg + Kb) || writer) load8(a.nw + k, wv[j]);
+                    load8(xr + k, xv[j]);
 #pragma unroll
                     for (int u = 0; u < 8; ++u) ss += xv[j][u] * xv[j][u];
                 }
@@ -126,92 +156,179 @@ __global__ __launch_bounds__(512) void gemv_kernel(GemvArgs<T> a) {
             ss = block_sum(ss, red_s);
             const float rs = 1.0f / sqrtf(ss / (float)a.K + a.eps);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int c = threadIdx.x + 512 * j;
+            for (int j = 0; j < 4; ++j) {
+                const int c = threadIdx.x + NTH * j;
                 if (c >= nch) continue;
                 const int k = 8 * c;
                 const bool mine = k >= kbeg && k < kbeg + Kb;
                 if (!mine && !writer) continue;
-                float wv[8];
-                load8(a.nw + k, wv);
                 float xn[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) xn[u] = rnd<T>(rnd<T>(xv[j][u] * rs) * wv[u]);
+                for (int u = 0; u < 8; ++u) xn[u] = rnd<T>(rnd<T>(xv[j][u] * rs) * wv[j][u]);
                 if (mine) {
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) st(xs, (size_t)r * xstride + (k - kbeg) + u, xn[u]);
+                    for (int u = 0; u < 8; ++u) st(xs, (size_t)rr * xstride + (k - kbeg) + u, xn[u]);
                 }
-                if (writer) {
+                if (writer && a.xn_out) {
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        if constexpr (PRO == PRO_RESNORM) st(a.res_out, (size_t)r * a.ldro + k + u, xv[j][u]);
-                        if (a.xn_out) st(a.xn_out, (size_t)r * a.ldxo + k + u, xn[u]);
-                    }
+                    for (int u = 0; u < 8; ++u) st(a.xn_out, (size_t)rr * a.ldxo + k + u, xn[u]);
                 }
             }
             __syncthreads();
         }
+#pragma unroll
+        for (int u = 0; u < U; ++u) issue(u, u);
     } else {
-        const int nchs = Kb >> 3;
-        constexpr int VB = 16 / sizeof(T);  // elements per 16 B
-        for (int idx = threadIdx.x; idx < R * nchs * (8 / VB); idx += 512) {
-            const int r = idx / (nchs * (8 / VB)), c = idx - r * (nchs * (8 / VB));
-            *reinterpret_cast<u32x4_t*>(xs + (size_t)r * xstride + VB * c) =
-                *reinterpret_cast<const u32x4_t*>(a.X + (size_t)r * a.ldx + kbeg + VB * c);
-        }
-    }
-    __syncthreads();
-
-    // ---------------- main loop: ring of U weight-fragment loads per wave ------------------------
-    // packed weights (fm_kernels.h): the (tile, step) fragment is 512 contiguous elements; wave w
-    // streams a contiguous run of the block's steps.
-    const int r = lane & 15, g = lane >> 4;
-    const int S = a.K >> 5, Sb = Kb >> 5, sb0 = ks * Sb;
-    const int wa = (wave * Sb) >> 3, wb = ((wave + 1) * Sb) >> 3, nmy = wb - wa;
-    const T* wp = a.W + ((size_t)blockIdx.x * S + sb0 + wa) * 512;
-    const T* wp2 = (EPI == EPI_SWIGLU) ? a.W2 + ((size_t)blockIdx.x * S + sb0 + wa) * 512 : nullptr;
-    const T* xp = xs + (size_t)(r < R ? r : R - 1) * xstride + (size_t)wa * 32 + 8 * g;
-    f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    if (nmy > 0) {
-        typename G::f fa[U], fb[U];
-        auto boff = [&](int i) { return (size_t)(i < nmy ? i : nmy - 1) * 512; };  // clamped tail
+        // PRO_PLAIN / PRO_PRENORM: (row, 8-element chunk) items of the slice, up to GEMV_PRE per
+        // thread preloaded ahead of the weight ring (the rest, large R x Kb only, after it)
+        const int nch = Kb >> 3, nitem = R * nch;
+        C8<T> xc[GEMV_PRE], wc[PRO == PRO_PRENORM ? GEMV_PRE : 1];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            fa[u] = G::load_w(wp + boff(u), lane);
-            if constexpr (NACC == 2) fb[u] = G::load_w(wp2 + boff(u), lane);
+        for (int q = 0; q < GEMV_PRE; ++q) {
+            const int it = threadIdx.x + NTH * q;
+            if (it < nitem) {
+                const int rr = it / nch, cc = it - rr * nch;
+                xc[q] = load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc);
+                if constexpr (PRO == PRO_PRENORM) wc[q] = load_c8(a.nw + kbeg + 8 * cc);
+            }
         }
-        for (int i = 0; i < nmy; i += U) {
+        float ssl[GEMV_RMAX];
+        if constexpr (PRO == PRO_PRENORM) {
+            // K <= 4096 -> <= 4 tile sums per lane and row; unconditional (clamped) loads so all
+            // of them are in flight together (a load under a branch costs a full vmcnt drain)
+            const int nt = a.K >> 4;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (i + u < nmy) {
-                    const typename G::f xb = G::load_lds(xp + (size_t)(i + u) * 32);
-                    acc0 = G::mma(fa[u], xb, acc0);
-                    if constexpr (NACC == 2) acc1 = G::mma(fb[u], xb, acc1);
+            for (int rr = 0; rr < GEMV_RMAX; ++rr) {
+                ssl[rr] = 0.f;
+                if (rr < R) {
+                    float v[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int t = lane + 64 * j;
+                        v[j] = a.ss_in[(size_t)(t < nt ? t : nt - 1) * R + rr];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) ssl[rr] += (lane + 64 * j < nt) ? v[j] : 0.f;
                 }
-                fa[u] = G::load_w(wp + boff(i + u + U), lane);
-                if constexpr (NACC == 2) fb[u] = G::load_w(wp2 + boff(i + u + U), lane);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) issue(u, u);
+        if constexpr (PRO == PRO_PRENORM) {
+            // per-row 1/rms in this wave's LDS slot (a register array indexed by the runtime row
+            // would be spilled to scratch: one more memory round trip per read)
+            float* rsw = rsl + wave * GEMV_RMAX;
+#pragma unroll
+            for (int rr = 0; rr < GEMV_RMAX; ++rr) {
+                const float v = rr < R ? 1.0f / sqrtf(wave_sum(ssl[rr]) / (float)a.K + a.eps) : 0.f;
+                if (lane == 0) rsw[rr] = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const bool writer = blockIdx.x == 0 && ks == 0 && a.xn_out;
+            auto put = [&](int rr, int cc, const C8<T>& xq, const C8<T>& wq) {
+                float xv[8], wv[8];
+                c8_to_f(xq, xv);
+                c8_to_f(wq, wv);
+                const float rs = rsw[rr];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float xn = rnd<T>(rnd<T>(xv[u] * rs) * wv[u]);
+                    st(xs, (size_t)rr * xstride + 8 * cc + u, xn);
+                    if (writer) st(a.xn_out, (size_t)rr * a.ldxo + kbeg + 8 * cc + u, xn);
+                }
+            };
+#pragma unroll
+            for (int q = 0; q < GEMV_PRE; ++q) {
+                const int it = threadIdx.x + NTH * q;
+                if (it < nitem) put(it / nch, it - (it / nch) * nch, xc[q], wc[q]);
+            }
+            for (int it = threadIdx.x + NTH * GEMV_PRE; it < nitem; it += NTH) {
+                const int rr = it / nch, cc = it - rr * nch;
+                put(rr, cc, load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc), load_c8(a.nw + kbeg + 8 * cc));
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < GEMV_PRE; ++q) {
+                const int it = threadIdx.x + NTH * q;
+                if (it < nitem) {
+                    const int rr = it / nch, cc = it - rr * nch;
+                    *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) = xc[q];
+                }
+            }
+            for (int it = threadIdx.x + NTH * GEMV_PRE; it < nitem; it += NTH) {  // large R x Kb
+                const int rr = it / nch, cc = it - rr * nch;
+                *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) =
+                    load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc);
             }
         }
     }
-    red[(0 * 8 + wave) * 64 + lane] = acc0;
-    if constexpr (NACC == 2) red[(1 * 8 + wave) * 64 + lane] = acc1;
     __syncthreads();
 
-    // ---------------- epilogue: 16 rows x R cols; C/D map row = 4*(lane>>4)+i, col = lane&15 ---
-    for (int o = threadIdx.x; o < 256; o += 512) {
-        const int i = o >> 6, ln = o & 63;
-        const int n = n0 + 4 * (ln >> 4) + i;
-        const int col = ln & 15;
-        if (col >= R || n >= a.N) continue;
+    const unsigned long long ts1 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    // ---------------- main loop: ring of U fragments per wave ------------------------------------
+    const T* xp = xs + (size_t)(r < R ? r : R - 1) * xstride + (size_t)wa * 32 + 8 * g;
+    f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < nmy; i += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (i + u < nmy) {
+                const typename G::f xb = G::load_lds(xp + (size_t)(i + u) * 32);
+                acc0 = G::mma(fa[u], xb, acc0);
+                if constexpr (NACC == 2) acc1 = G::mma(fb[u], xb, acc1);
+            }
+            issue(i + u + U, u);
+        }
+    }
+    // cross-wave reduction: only the R live columns of the 16x16 accumulator tile go to LDS
+    if ((lane & 15) < R) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = 4 * (lane >> 4) + i, col = lane & 15;
+            red[((0 * WPB + wave) * 16 + row) * R + col] = acc0[i];
+            if constexpr (NACC == 2) red[((1 * WPB + wave) * 16 + row) * R + col] = acc1[i];
+        }
+    }
+    const unsigned long long ts2 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    __syncthreads();
+    // developer timestamps: one record per block {tag, t0 start, t1 staged, t2 streamed, t3 end}
+    auto stamp = [&]() {
+        if (a.dbg && threadIdx.x == 0) {
+            const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long slot = atomicAdd(a.dbg, 1ull);
+            if (slot < (1ull << 20)) {
+                unsigned long long* q = a.dbg + 8 + slot * 8;
+                q[0] = ((unsigned long long)a.N << 32) | ((unsigned long long)blockIdx.y << 16) | blockIdx.x;
+                q[1] = ts0;
+                q[2] = ts1;
+                q[3] = ts2;
+                q[4] = t3;
+                q[5] = q[6] = q[7] = 0;
+            }
+        }
+    };
+
+    // ---------------- epilogue: 16 rows x R cols -----------------------------------------------
+    for (int o = threadIdx.x; o < 16 * R; o += NTH) {
+        const int row = o / R, col = o - row * R;
+        const int n = n0 + row;
+        if (n >= a.N) continue;
         float v0 = 0.f, v1 = 0.f;
 #pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            v0 += red[(0 * 8 + w) * 64 + ln][i];
-            if constexpr (NACC == 2) v1 += red[(1 * 8 + w) * 64 + ln][i];
+        for (int w = 0; w < WPB; ++w) {
+            v0 += red[((0 * WPB + w) * 16 + row) * R + col];
+            if constexpr (NACC == 2) v1 += red[((1 * WPB + w) * 16 + row) * R + col];
         }
         if constexpr (EPI == EPI_SLAB) {
             if (a.bias && ks == 0) v0 += ld(a.bias, n);
             a.Yf[((size_t)ks * R + col) * a.ldy + n] = v0;
+        } else if constexpr (EPI == EPI_SLABFIN) {
+            if (a.bias && ks == 0) v0 += ld(a.bias, n);
+            if (gridDim.y == 1) {  // whole K in this block: finalise from LDS below
+                fin[col * 16 + (n - n0)] = v0;
+            } else {  // write-through (sc1) partial: visible to the tile's reducer without a fence
+                __hip_atomic_store(a.Yf + ((size_t)ks * R + col) * a.ldy + n, v0, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
         } else {
             if (a.bias) v0 += ld(a.bias, n);
             const size_t yi = (size_t)col * a.ldy + n;
@@ -225,6 +342,79 @@ __global__ __launch_bounds__(512) void gemv_kernel(GemvArgs<T> a) {
             }
         }
     }
+    if constexpr (EPI == EPI_SLABFIN) {
+        // The last-arriving K-slice block of this 16-column tile finalises the residual stream:
+        // x = round(res + round(sum_q partial_q)) (llama.py:841-842) and the tile's sum of x^2 for
+        // the consumer's RMSNorm.  Hand-off in its write-through form (cdna_hip_programming.md §5,
+        // split-K recipe): sc1 partial stores drained by every wave, a relaxed agent ticket, sc1
+        // loads in the reducer -- no release / acquire fence.  ksb == 1: straight from LDS.
+        const int ksb = gridDim.y;
+        if (ksb > 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (ksb > 1) {
+            if (threadIdx.x == 0) {
+                const int t = __hip_atomic_fetch_add(a.tickets + blockIdx.x, 1, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                const int last = t == ksb - 1;
+                if (last) __hip_atomic_store(a.tickets + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                flag[0] = last;
+            }
+            __syncthreads();
+            if (!flag[0]) {
+                stamp();
+                return;
+            }
+        }
+        const int t = threadIdx.x;
+        if (t < 16 * R) {
+            const int col = t >> 4, n = n0 + (t & 15);
+            float y = 0.f;
+            if (ksb == 1)
+                y = fin[t];
+            else
+                for (int q = 0; q < ksb; ++q)
+                    y += __hip_atomic_load(a.Yf + ((size_t)q * R + col) * a.ldy + n, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            const int ri = a.residx ? a.residx[(size_t)col * a.xidx_ld + a.xidx_col] : col;
+            const float x = rnd<T>(ld(a.res + (size_t)ri * a.ldr, n) + rnd<T>(y));
+            st(a.res_out, (size_t)col * a.ldro + n, x);
+            float sq = x * x;
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) sq += __shfl_xor(sq, m);
+            if ((t & 15) == 0) a.ss_out[(size_t)blockIdx.x * R + col] = sq;
+        }
+    }
+    stamp();
+}
+
+template <typename T, int PRO, int EPI, bool NT, int U, int WPB>
+static void gemv_launch(hipStream_t s, const GemvArgs<T>& a0, dim3 grid, size_t lds) {
+    GemvArgs<T> a = a0;
+    a.dbg = fm_tuning().dbg;
+    static bool big = false;  // > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
+    if (lds > 64 * 1024 && !big) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<T, PRO, EPI, NT, U, WPB>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        big = true;
+    }
+    gemv_kernel<T, PRO, EPI, NT, U, WPB><<<grid, WPB * 64, lds, s>>>(a);
+}
+
+template <typename T, int PRO, int EPI, bool NT, int U>
+static void gemv_go_w(hipStream_t s, const GemvArgs<T>& a, dim3 grid, size_t lds) {
+    if (fm_tuning().gemv_wpb == 8)
+        gemv_launch<T, PRO, EPI, NT, U, 8>(s, a, grid, lds);
+    else
+        gemv_launch<T, PRO, EPI, NT, U, 4>(s, a, grid, lds);
+}
+
+template <typename T, int PRO, int EPI, bool NT>
+static void gemv_go_u(hipStream_t s, const GemvArgs<T>& a, dim3 grid, size_t lds) {
+    switch (fm_tuning().gemv_u) {
+        case 8: gemv_go_w<T, PRO, EPI, NT, 8>(s, a, grid, lds); break;
+        case 2: gemv_go_w<T, PRO, EPI, NT, 2>(s, a, grid, lds); break;
+        default: gemv_go_w<T, PRO, EPI, NT, 4>(s, a, grid, lds); break;
+    }
 }
 
 template <typename T, int PRO, int EPI>
@@ -232,7 +422,10 @@ static void gemv_go(hipStream_t s, const GemvArgs<T>& a, int ksb) {
     dim3 grid(FM_CEIL(a.N, 16), ksb);
     const int Kb = a.K / ksb;
     const size_t lds = gemv_lds_bytes(a.R, Kb, sizeof(T));
-    gemv_kernel<T, PRO, EPI, 4><<<grid, 512, lds, s>>>(a);
+    if (fm_tuning().gemv_nt)
+        gemv_go_u<T, PRO, EPI, true>(s, a, grid, lds);
+    else
+        gemv_go_u<T, PRO, EPI, false>(s, a, grid, lds);
 }
 
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb) {
@@ -241,12 +434,366 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
         gemv_go<T, P, E>(s, a, ksb);                       \
         return;                                            \
     }
-    GO(PRO_PLAIN, EPI_STORE) GO(PRO_PLAIN, EPI_SLAB) GO(PRO_PLAIN, EPI_F32) GO(PRO_PLAIN, EPI_SWIGLU)
-    GO(PRO_NORM, EPI_STORE) GO(PRO_NORM, EPI_SWIGLU) GO(PRO_NORM, EPI_F32) GO(PRO_NORM, EPI_SLAB)
-    GO(PRO_RESNORM, EPI_STORE) GO(PRO_RESNORM, EPI_SWIGLU) GO(PRO_RESNORM, EPI_F32)
-    GO(PRO_RESNORM, EPI_SLAB)
+    GO(PRO_PLAIN, EPI_STORE) GO(PRO_PLAIN, EPI_SLABFIN) GO(PRO_PLAIN, EPI_F32) GO(PRO_PLAIN, EPI_SLAB)
+    GO(PRO_NORM, EPI_STORE) GO(PRO_NORM, EPI_SWIGLU) GO(PRO_NORM, EPI_F32)
+    GO(PRO_PRENORM, EPI_STORE) GO(PRO_PRENORM, EPI_SWIGLU) GO(PRO_PRENORM, EPI_F32)
 #undef GO
 }
 
 template void launch_gemv<bf16_t>(hipStream_t, const GemvArgs<bf16_t>&, int, int, int);
 template void launch_gemv<float>(hipStream_t, const GemvArgs<float>&, int, int, int);
+
+// =============================================================================================
+// Stream-K decode GEMV.  grid = (CUs x bpc) persistent blocks of 8 waves.  The fragment space of
+// the packed weight ([tile][k-step] x 1 KiB, one contiguous HBM stream) is cut into equal
+// contiguous runs, one per wave: u in [gw*U/W, (gw+1)*U/W).  Every block stages the whole
+// X' (all K) once; a wave keeps one accumulator per tile it touches (at most two when a run is
+// shorter than a tile), writes each as a write-through (sc1) partial after its run, drains,
+// and takes a ticket on the tile; the tile's last contributor combines the partials in
+// contributor order (deterministic) and applies the epilogue.  No cross-block barrier, no
+// fence (cdna_hip_programming.md §5 split-K recipe, write-through form).
+// =============================================================================================
+__host__ __device__ inline int sk_first_wave(long long x, int Wact, long long Utot) {
+    return (int)(((x + 1) * Wact - 1) / Utot);  // max gw with floor(gw * Utot / Wact) <= x
+}
+
+template <typename T, int PRO, int EPI, bool NT, int U>
+__global__ __launch_bounds__(512) void gemv_sk_kernel(GemvArgs<T> a) {
+    using G = GFrag<T>;
+    constexpr int WPB = 8, NTH = 512;
+    constexpr int NACC = (EPI == EPI_SWIGLU) ? 2 : 1;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int R = a.R, K = a.K, S = K >> 5;
+    const int ntile = (a.N + 15) >> 4;
+    const int xstride = K + 8;
+    T* xs = reinterpret_cast<T*>(smem);
+    float* ssq = reinterpret_cast<float*>(smem + (size_t)R * xstride * sizeof(T));  // [WPB][16*R]
+    float* rsl = ssq + WPB * 16 * GEMV_RMAX;                                        // [WPB][GEMV_RMAX]
+    const unsigned long long ts0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long tsa = 0, tsb = 0, tsc = 0;
+
+    const long long Utot = (long long)ntile * S;
+    const int Wact = (int)(Utot < (long long)gridDim.x * WPB ? Utot : (long long)gridDim.x * WPB);
+    const int gw = blockIdx.x * WPB + wave;
+    const bool active = gw < Wact;
+    const int u0 = active ? (int)((long long)gw * Utot / Wact) : 0;
+    const int u1 = active ? (int)((long long)(gw + 1) * Utot / Wact) : 0;
+    const int ulast = u1 > u0 ? u1 - 1 : 0;
+    const int r = lane & 15, g = lane >> 4;
+    typename G::f fa[U], fb[NACC == 2 ? U : 1];
+    auto issue = [&](int i, int u) {  // branch-free ring (see gemv_kernel)
+        const int uj = u0 + i < ulast ? u0 + i : ulast;
+        fa[u] = G::template load_w<NT>(a.W + (size_t)uj * 512, lane);
+        if constexpr (NACC == 2) fb[u] = G::template load_w<NT>(a.W2 + (size_t)uj * 512, lane);
+    };
+
+    // ---------------- prologue: X'[r][0 .. K) -> LDS, once per block -------------------------------
+    if constexpr (PRO == PRO_NORM) {
+        __shared__ float red_s[16];
+        const int nch = K >> 3;
+        const bool writer = blockIdx.x == 0;
+        for (int rr = 0; rr < R; ++rr) {
+            const int xi = a.xidx ? a.xidx[(size_t)rr * a.xidx_ld + a.xidx_col] : rr;
+            const T* xr = a.X + (size_t)xi * a.ldx;
+            float xv[4][8], wv[4][8];
+            float ss = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = threadIdx.x + NTH * j;
+                if (c < nch) {
+                    load8(a.nw + 8 * c, wv[j]);
+                    load8(xr + 8 * c, xv[j]);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) ss += xv[j][u] * xv[j][u];
+                }
+            }
+            ss = block_sum(ss, red_s);
+            const float rs = 1.0f / sqrtf(ss / (float)K + a.eps);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = threadIdx.x + NTH * j;
+                if (c >= nch) continue;
+                float xn[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xn[u] = rnd<T>(rnd<T>(xv[j][u] * rs) * wv[j][u]);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    st(xs, (size_t)rr * xstride + 8 * c + u, xn[u]);
+                    if (writer && a.xn_out) st(a.xn_out, (size_t)rr * a.ldxo + 8 * c + u, xn[u]);
+                }
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) issue(u, u);
+    } else {
+        const int nch = K >> 3, nitem = R * nch;
+        C8<T> xc[GEMV_PRE], wc[PRO == PRO_PRENORM ? GEMV_PRE : 1];
+#pragma unroll
+        for (int q = 0; q < GEMV_PRE; ++q) {
+            const int it = threadIdx.x + NTH * q;
+            if (it < nitem) {
+                const int rr = it / nch, cc = it - rr * nch;
+                xc[q] = load_c8(a.X + (size_t)rr * a.ldx + 8 * cc);
+                if constexpr (PRO == PRO_PRENORM) {
+                    if (!(a.pro_exp & 2)) wc[q] = load_c8(a.nw + 8 * cc);
+                    else wc[q] = xc[q];
+                }
+            }
+        }
+        float ssl[GEMV_RMAX];
+        if constexpr (PRO == PRO_PRENORM) {
+            const int nt = K >> 4;  // K <= 4096 (host)
+#pragma unroll
+            for (int rr = 0; rr < GEMV_RMAX; ++rr) {
+                ssl[rr] = 0.f;
+                if (rr < R && (a.pro_exp & 1)) ssl[rr] = (float)K / 64.0f;  // EXPERIMENT: no loads, rs ~ 1
+                if (rr < R && !(a.pro_exp & 1)) {
+                    float v[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int t = lane + 64 * j;
+                        v[j] = a.ss_in[(size_t)(t < nt ? t : nt - 1) * R + rr];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) ssl[rr] += (lane + 64 * j < nt) ? v[j] : 0.f;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) issue(u, u);
+        tsa = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+        if (PRO == PRO_PRENORM && (a.pro_exp & 4)) {  // EXPERIMENT: stage raw x (no normalise)
+#pragma unroll
+            for (int q = 0; q < GEMV_PRE; ++q) {
+                const int it = threadIdx.x + NTH * q;
+                if (it < nitem) {
+                    const int rr = it / nch, cc = it - rr * nch;
+                    *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) = xc[q];
+                }
+            }
+        } else if constexpr (PRO == PRO_PRENORM) {
+            // per-row 1/rms in this wave's LDS slot (a register array indexed by the runtime row
+            // would be spilled to scratch: one more memory round trip per read)
+            float* rsw = rsl + wave * GEMV_RMAX;
+#pragma unroll
+            for (int rr = 0; rr < GEMV_RMAX; ++rr) {
+                const float v = rr < R ? 1.0f / sqrtf(wave_sum(ssl[rr]) / (float)K + a.eps) : 0.f;
+                if (lane == 0) rsw[rr] = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            tsb = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+            const bool writer = blockIdx.x == 0 && a.xn_out;
+            auto put = [&](int rr, int cc, const C8<T>& xq, const C8<T>& wq) {
+                float xv[8], wv[8];
+                c8_to_f(xq, xv);
+                c8_to_f(wq, wv);
+                const float rs = rsw[rr];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float xn = rnd<T>(rnd<T>(xv[u] * rs) * wv[u]);
+                    st(xs, (size_t)rr * xstride + 8 * cc + u, xn);
+                    if (writer) st(a.xn_out, (size_t)rr * a.ldxo + 8 * cc + u, xn);
+                }
+            };
+#pragma unroll
+            for (int q = 0; q < GEMV_PRE; ++q) {
+                const int it = threadIdx.x + NTH * q;
+                if (it < nitem) put(it / nch, it - (it / nch) * nch, xc[q], wc[q]);
+            }
+            for (int it = threadIdx.x + NTH * GEMV_PRE; it < nitem; it += NTH) {
+                const int rr = it / nch, cc = it - rr * nch;
+                put(rr, cc, load_c8(a.X + (size_t)rr * a.ldx + 8 * cc), load_c8(a.nw + 8 * cc));
+            }
+            tsc = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+        } else {
+#pragma unroll
+            for (int q = 0; q < GEMV_PRE; ++q) {
+                const int it = threadIdx.x + NTH * q;
+                if (it < nitem) {
+                    const int rr = it / nch, cc = it - rr * nch;
+                    *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) = xc[q];
+                }
+            }
+            for (int it = threadIdx.x + NTH * GEMV_PRE; it < nitem; it += NTH) {
+                const int rr = it / nch, cc = it - rr * nch;
+                *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) =
+                    load_c8(a.X + (size_t)rr * a.ldx + 8 * cc);
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned long long ts1 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+
+    // ---------------- tile finisher: partial -> ticket -> (last) combine + epilogue ------------
+    auto finish = [&](int t, const f32x4_t& c0, const f32x4_t& c1) {
+        const int fw = sk_first_wave((long long)t * S, Wact, Utot);
+        const int lw = sk_first_wave((long long)(t + 1) * S - 1, Wact, Utot);
+        const int nc = lw - fw + 1, ci = gw - fw;
+        float* pt = a.part + (size_t)t * a.maxc * NACC * 16 * R;
+        if ((lane & 15) < R) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = 4 * (lane >> 4) + i, col = lane & 15;
+                __hip_atomic_store(pt + ((size_t)ci * NACC * 16 + row) * R + col, c0[i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                if constexpr (NACC == 2)
+                    __hip_atomic_store(pt + ((size_t)ci * NACC * 16 + 16 + row) * R + col, c1[i], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int tk = 0;
+        if (lane == 0) tk = __hip_atomic_fetch_add(a.tickets + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tk = __shfl(tk, 0);
+        if (tk != nc - 1) return;
+        if (lane == 0) __hip_atomic_store(a.tickets + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float* sq = ssq + wave * 16 * GEMV_RMAX;
+        for (int o = lane; o < 16 * R; o += 64) {
+            const int row = o / R, col = o - row * R;
+            const int n = t * 16 + row;
+            float v0 = 0.f, v1 = 0.f;
+            for (int q = 0; q < nc; ++q) {
+                v0 += __hip_atomic_load(pt + ((size_t)q * NACC * 16 + row) * R + col, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+                if constexpr (NACC == 2)
+                    v1 += __hip_atomic_load(pt + ((size_t)q * NACC * 16 + 16 + row) * R + col, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (n >= a.N) {
+                if constexpr (EPI == EPI_SLABFIN) sq[row * R + col] = 0.f;
+                continue;
+            }
+            if (a.bias) v0 += ld(a.bias, n);
+            const size_t yi = (size_t)col * a.ldy + n;
+            if constexpr (EPI == EPI_STORE) {
+                st(a.Y, yi, v0);
+            } else if constexpr (EPI == EPI_SWIGLU) {
+                st(a.Y, yi, rnd<T>(silu_g(rnd<T>(v0))) * rnd<T>(v1));
+            } else if constexpr (EPI == EPI_F32) {
+                a.Yf[yi] = rnd<T>(v0);
+            } else {  // EPI_SLABFIN: x = round(res + round(y)), and the tile's sums of squares
+                const int ri = a.residx ? a.residx[(size_t)col * a.xidx_ld + a.xidx_col] : col;
+                const float x = rnd<T>(ld(a.res + (size_t)ri * a.ldr, n) + rnd<T>(v0));
+                st(a.res_out, (size_t)col * a.ldro + n, x);
+                sq[row * R + col] = x * x;
+            }
+        }
+        if constexpr (EPI == EPI_SLABFIN) {
+            __builtin_amdgcn_wave_barrier();
+            if (lane < R) {
+                float s2 = 0.f;
+                for (int row = 0; row < 16; ++row) s2 += sq[row * R + lane];
+                a.ss_out[(size_t)t * R + lane] = s2;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    };
+
+    // ---------------- main loop: this wave's contiguous run, ring of U fragments ----------------
+    if (active) {
+        int tcur = u0 / S, tend = (tcur + 1) * S;
+        int tprev = -1;
+        f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, p0 = acc0, p1 = acc0;
+        const T* xrow = xs + (size_t)(r < R ? r : R - 1) * xstride + 8 * g;
+        const int n = u1 - u0;
+        for (int i = 0; i < n; i += U) {
+#pragma unroll
+            for (int uu = 0; uu < U; ++uu) {
+                const int uj = u0 + i + uu;
+                if (uj < u1) {
+                    if (uj == tend) {  // tile switch: park the finished accumulator
+                        if (tprev >= 0) finish(tprev, p0, p1);  // a third tile: only when a run exceeds a tile
+                        tprev = tcur;
+                        p0 = acc0;
+                        p1 = acc1;
+                        acc0 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+                        acc1 = acc0;
+                        ++tcur;
+                        tend += S;
+                    }
+                    const typename G::f xb = G::load_lds(xrow + (size_t)(uj - tcur * S) * 32);
+                    acc0 = G::mma(fa[uu], xb, acc0);
+                    if constexpr (NACC == 2) acc1 = G::mma(fb[uu], xb, acc1);
+                }
+                issue(i + uu + U, uu);
+            }
+        }
+        if (tprev >= 0) finish(tprev, p0, p1);
+        finish(tcur, acc0, acc1);
+    }
+    if (a.dbg && lane == 0 && active) {
+        const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long slot = atomicAdd(a.dbg, 1ull);
+        if (slot < (1ull << 20)) {
+            unsigned long long* q = a.dbg + 8 + slot * 8;
+            q[0] = ((unsigned long long)a.N << 32) | ((unsigned long long)wave << 16) | blockIdx.x;
+            q[1] = ts0;
+            q[2] = ts1;
+            q[3] = t3;
+            q[4] = t3;
+            q[5] = tsa;
+            q[6] = tsb;
+            q[7] = tsc;
+        }
+    }
+}
+
+template <typename T, int PRO, int EPI, bool NT, int U>
+static void gemv_sk_go(hipStream_t s, const GemvArgs<T>& a0, int nblk, size_t lds) {
+    GemvArgs<T> a = a0;
+    a.dbg = fm_tuning().dbg;
+    a.pro_exp = fm_tuning().pro_exp;
+    static bool big = false;
+    if (lds > 64 * 1024 && !big) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_sk_kernel<T, PRO, EPI, NT, U>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        big = true;
+    }
+    gemv_sk_kernel<T, PRO, EPI, NT, U><<<nblk, 512, lds, s>>>(a);
+}
+
+static int sk_num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    }
+    return n;
+}
+
+template <typename T> bool launch_gemv_sk(hipStream_t s, const GemvArgs<T>& a0, int pro, int epi) {
+    const FmTuning& tu = fm_tuning();
+    if (!tu.gemv_sk || a0.R > GEMV_RMAX || !a0.part || !a0.tickets) return false;
+    if (pro == PRO_PRENORM && a0.K > 4096) return false;
+    if (pro == PRO_NORM && a0.K > 4 * 512 * 8) return false;
+    const size_t lds = (size_t)a0.R * (a0.K + 8) * sizeof(T) + (size_t)8 * 17 * GEMV_RMAX * sizeof(float);
+    if (lds > 150 * 1024) return false;
+    const int nacc = epi == EPI_SWIGLU ? 2 : 1;
+    const int ntile = (a0.N + 15) / 16, S = a0.K / 32;
+    const int nblk = sk_num_cus() * tu.gemv_sk_bpc;
+    const long long Utot = (long long)ntile * S;
+    const int Wact = (int)std::min<long long>(Utot, (long long)nblk * 8);
+    // contributors per tile <= ceil(S * Wact / Utot) + 1
+    const int maxc = (int)(((long long)S * Wact + Utot - 1) / Utot) + 1;
+    if ((long long)ntile * maxc * nacc * 16 * a0.R > a0.part_cap) return false;
+    GemvArgs<T> a = a0;
+    a.maxc = maxc;
+    const int U = tu.gemv_u == 8 ? 8 : 4;
+#define SKGO(P, E)                                                                       \
+    if (pro == P && epi == E) {                                                         \
+        if (U == 8) gemv_sk_go<T, P, E, true, 8>(s, a, nblk, lds);                       \
+        else gemv_sk_go<T, P, E, true, 4>(s, a, nblk, lds);                              \
+        return true;                                                                     \
+    }
+    SKGO(PRO_PLAIN, EPI_STORE) SKGO(PRO_PLAIN, EPI_SLABFIN) SKGO(PRO_PLAIN, EPI_F32)
+    SKGO(PRO_NORM, EPI_STORE) SKGO(PRO_NORM, EPI_SWIGLU) SKGO(PRO_NORM, EPI_F32)
+    SKGO(PRO_PRENORM, EPI_STORE) SKGO(PRO_PRENORM, EPI_SWIGLU) SKGO(PRO_PRENORM, EPI_F32)
+#undef SKGO
+    return false;
+}
+
+template bool launch_gemv_sk<bf16_t>(hipStream_t, const GemvArgs<bf16_t>&, int, int);
+template bool launch_gemv_sk<float>(hipStream_t, const GemvArgs<float>&, int, int);

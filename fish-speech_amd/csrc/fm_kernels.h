@@ -109,8 +109,8 @@ template <typename T>
 void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* dst);
 
 // ---- decode weight-streaming path (fm_gemv.hip), R <= 8 rows --------------------------------
-enum { PRO_PLAIN = 0, PRO_NORM = 1, PRO_RESNORM = 2 };
-enum { EPI_SLAB = 4 };
+enum { PRO_PLAIN = 0, PRO_NORM = 1, PRO_PRENORM = 3 };
+enum { EPI_SLAB = 4, EPI_SLABFIN = 5 };
 
 template <typename T> struct GemvArgs {
     const T* W;
@@ -121,25 +121,47 @@ template <typename T> struct GemvArgs {
     const int32_t* xidx;     // optional row gather: X row = xidx[r*xidx_ld + xidx_col]
     int xidx_ld, xidx_col;
     const int32_t* residx;   // optional row gather for res (same layout as xidx)
-    const T* res;            // PRO_RESNORM residual [R][ldr]
+    const T* res;            // EPI_SLABFIN residual [R][ldr]
     int ldr;
-    const float* slab;       // PRO_RESNORM: producer partials [nslab][R][slab_ld]
-    int slab_ld, nslab;
+    const float* ss_in;      // PRO_PRENORM: per-16-column-tile sums of squares of X [K/16][R]
     const T* nw;             // norm weight [K]
     float eps;
     int R, N, K;
     T* Y;                    // EPI_STORE / EPI_SWIGLU [R][ldy]
     int ldy;                 // also the slab row stride for EPI_SLAB / EPI_F32
-    float* Yf;               // EPI_F32 [R][ldy] | EPI_SLAB [KSB][R][ldy]
-    T* res_out;              // PRO_RESNORM: block (0,0) stores x = res + sum(slabs) here
+    float* Yf;               // EPI_F32 [R][ldy] | EPI_SLAB(FIN) partials [KSB][R][ldy]
+    T* res_out;              // EPI_SLABFIN: x = round(res + round(sum of partials)) [R][ldro]
     int ldro;
-    T* xn_out;               // optional: block (0,0) stores X' (normalised row) here
+    float* ss_out;           // EPI_SLABFIN: per-tile sums of squares of x [N/16][R]
+    int* tickets;            // EPI_SLABFIN: per-tile arrival counters (zero between launches)
+    T* xn_out;               // optional (ksb == 1): block (0,0) stores X' (normalised row) here
     int ldxo;
+    unsigned long long* dbg; // developer timestamps (fm_tune "debug_ts"); null in production
+    float* part;             // stream-K: per-(tile, contributor) partial tiles (sc1), capacity part_cap
+    long long part_cap;      //   floats
+    int maxc;                // stream-K: contributor slots per tile (set by the launcher)
+    int pro_exp;             // EXPERIMENT knob (see FmTuning)
 };
+// developer knobs for the decode GEMV (fm_tune): weight load policy and split-K policy
+struct FmTuning {
+    int gemv_nt = 1;         // 1: non-temporal weight loads (each weight byte is read once a frame)
+    int gemv_u = 8;          // weight fragments in flight per wave (2, 4 or 8)
+    int gemv_wpb = 4;        // waves per block (4 or 8) sharing one 16-row tile
+    int gemv_sk = 0;         // 1: stream-K decode GEMV (one persistent block per CU), 0: tiled
+    int gemv_sk_bpc = 1;     // stream-K blocks per CU
+    int pro_exp = 0;         // EXPERIMENT: 1 skip tile-sum loads, 2 skip norm-weight loads, 3 both
+    int ksb_blocks = 512;    // split K until the grid has at least this many blocks
+    int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
+    unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
+};
+FmTuning& fm_tuning();
 inline size_t gemv_lds_bytes(int R, int Kb, size_t esz) {
-    return (size_t)R * (Kb + 8) * esz + 16 * sizeof(float) + 2 * 8 * 64 * 16;
+    return (size_t)R * (Kb + 8) * esz + 16 * sizeof(float) + (2 * 8 * 16 + 16) * (size_t)R * sizeof(float) +
+           8 * 8 * sizeof(float);
 }
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb);
+// stream-K decode GEMV; returns false (nothing launched) when the shape is not eligible
+template <typename T> bool launch_gemv_sk(hipStream_t s, const GemvArgs<T>& a, int pro, int epi);
 
 // ---- fused decode attention / sampler (fm_attn.hip) ------------------------------------------
 template <typename T> struct AttnDecArgs {
@@ -158,6 +180,10 @@ template <typename T> struct AttnDecArgs {
     int S, maxsplit;
     float scale;
     float* part;         // [R][nh][maxsplit][hd+2]
+    // attn_decode2 only
+    int cap;             // rows per block
+    int* cnt;            // [R][nkv] arrival tickets (zeroed at allocation, reset by the last block)
+    T* out;              // [R][nh*hd]
 };
 template <typename T> struct FastFusedArgs {
     const T* qkv;
@@ -176,7 +202,24 @@ template <typename T> struct FastFusedArgs {
     T* out;              // [R][nh*hd]
 };
 template <typename T> void launch_attn_decode(hipStream_t s, const AttnDecArgs<T>& a, int R);
+// decode attention for the small-batch path (see fm_attn.hip): a.cap rows per block, a.maxsplit =
+// ceil(S / cap) blocks per (row, kv head), output straight to a.out (bf16 / T)
+template <typename T> void launch_attn_decode2(hipStream_t s, const AttnDecArgs<T>& a, int R);
+inline size_t attn2_lds_bytes(int hd, int g, int cap, size_t esz) {
+    return (size_t)cap * (hd + 8) * esz + (size_t)cap * hd * esz + (size_t)g * hd * 4 + (size_t)g * cap * 4 +
+           16 + 8 * (size_t)g * 4;
+}
+// rows per attn_decode2 block within ~150 KB of LDS (multiple of 16, <= 256)
+inline int attn2_cap(int hd, int g, size_t esz) {
+    long budget = 150L * 1024 - 16 - 8L * g * 4 - (long)g * hd * 4;
+    long per = (long)(2 * hd + 8) * (long)esz + 4L * g;
+    long c = budget / per;
+    c = c > 256 ? 256 : c;
+    return (int)(c & ~15L);
+}
 template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFusedArgs<T>& a, int R);
+// fast-model attention, one wave per q head (cpos < 16 cached rows, hd <= 256)
+template <typename T> void launch_fast_attn2(hipStream_t s, const FastFusedArgs<T>& a, int R);
 template <typename T> void launch_sample_radix(hipStream_t s, const SampleArgs& a, int R);
 template <typename T>
 void launch_attn_combine(hipStream_t s, const float* part, const int* row_pos, int R, int nh, int hd,

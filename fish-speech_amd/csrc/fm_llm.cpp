@@ -30,11 +30,34 @@ static constexpr int KSB_MAX = 8;
 
 // split-K factor across blocks for a GEMV with N output rows: >= ~512 blocks when possible,
 // K/(32*ksb) integral, LDS staging within budget.
+FmTuning& fm_tuning() {
+    static FmTuning t;
+    return t;
+}
+
 static int pick_ksb(int N, int K, int R, size_t esz) {
     const int nb = (N + 15) / 16;
+    const FmTuning& tu = fm_tuning();
     int ksb = 1;
-    while (ksb < KSB_MAX && nb * ksb < 512 && K % (32 * ksb * 2) == 0) ksb *= 2;
+    while (ksb < KSB_MAX && nb * ksb < tu.ksb_blocks && K % (32 * ksb * 2) == 0) ksb *= 2;
+    if (tu.ksb_balance) {
+        // among the admissible split factors pick the one whose grid wastes the least of its
+        // last round of 256 CUs (ties: the smaller split)
+        double best = 1e9;
+        int bk = ksb;
+        for (int k = 1; k <= KSB_MAX && K % (32 * k) == 0; k *= 2) {
+            const int b = nb * k;
+            if (b < 256) continue;
+            const double rounds = (double)((b + 255) / 256), waste = rounds * 256.0 / b;
+            if (waste < best - 1e-3) {
+                best = waste;
+                bk = k;
+            }
+        }
+        ksb = bk;
+    }
     while (gemv_lds_bytes(R, K / ksb, esz) > 96 * 1024 && ksb < KSB_MAX && K % (32 * ksb * 2) == 0) ksb *= 2;
+    while (K / ksb > 4096 && K % (32 * ksb * 2) == 0) ksb *= 2;  // one 8-element chunk per thread
     return ksb;
 }
 
@@ -70,6 +93,11 @@ struct fm_llm {
          *act = nullptr;
     void *xl = nullptr, *xnl = nullptr, *fx = nullptr, *fh = nullptr, *fxn = nullptr;
     float *part = nullptr, *logits = nullptr, *flogits = nullptr;
+    int* attn_cnt = nullptr;
+    float *ssX = nullptr, *ssH = nullptr;  // per-16-column tile sums of squares of the residual rows
+    int* tickets = nullptr;               // EPI_SLABFIN / stream-K arrival counters (zero between launches)
+    float* skpart = nullptr;              // stream-K partial tiles
+    long long skpart_cap = 0;  // [Rmax][nkv] arrival tickets of attn_decode2 (kept zero between launches)
     float *slabA = nullptr, *slabB = nullptr;  // split-K partials of wo / w2 (small-batch path)
     // rows / slots
     int *frame_slot = nullptr, *frame_pos = nullptr, *prow_slot = nullptr, *prow_pos = nullptr;
@@ -241,23 +269,36 @@ template <typename T> struct Run {
         const int64_t bytes = wbytes + (int64_t)a.R * a.K * E;
         const double flops = 2.0 * a.R * a.N * a.K * (epi == EPI_SWIGLU ? 2 : 1);
         hipStream_t st = s;
-        auto go = [st, a, pro, epi, ksb] { launch_gemv<T>(st, a, pro, epi, ksb); };
+        a.part = m->skpart;
+        a.part_cap = m->skpart_cap;
+        if (!a.tickets) a.tickets = m->tickets;
+        auto go = [st, a, pro, epi, ksb] {
+            if (!launch_gemv_sk<T>(st, a, pro, epi)) launch_gemv<T>(st, a, pro, epi, ksb);
+        };
         m->prof.record(cls, bytes, go);
         m->prof.run(s, cls, bytes, flops, go);
     }
     struct KsbPlan {
         int wo, w2;
     };
+    // wo / w2 finalise the residual rows (EPI_SLABFIN): whole K per block (local finalise, no
+    // cross-block hand-off) whenever the x slice fits the LDS budget, else split K
     KsbPlan plan(const StackDims& d, int n) {
-        return KsbPlan{pick_ksb(d.dim, d.nq(), n, E), pick_ksb(d.dim, d.inter, n, E)};
+        auto fin_ksb = [&](int N, int K) {
+            if (gemv_lds_bytes(n, K, E) <= 120 * 1024) return 1;
+            return pick_ksb(N, K, n, E);
+        };
+        return KsbPlan{fin_ksb(d.dim, d.nq()), fin_ksb(d.dim, d.inter)};
     }
-    // one pre-norm block; x_in: layer input (plain rows, or embedding table + xidx gather) when
-    // first, otherwise the residual is pending as (res=hb, slabs=slabB).
+    // one pre-norm block (TransformerBlock.forward, llama.py:838-843) on n rows.  Residual rows
+    // are always finalised by the producing GEMV (EPI_SLABFIN: x / h in bf16 plus per-tile sums of
+    // squares ssX / ssH), so every RMSNorm consumer is PRO_PRENORM.  x_in: the first layer's input
+    // (plain rows, or an embedding table + xidx gather), whose norm is computed in place.
     void block_small(const StackDims& d, const LayerW& L, int n, bool first, const void* x_in, int ldx_in,
                      const int32_t* xidx, int xcol, void* xb, void* hb, bool is_fast, int cpos, int layer,
-                     const KsbPlan& kp, int ksb_prev) {
+                     const KsbPlan& kp) {
         const int C1 = m->C1;
-        // QKV (+ residual of the previous block + attention_norm)
+        // QKV (+ attention_norm)
         {
             GemvArgs<T> a = ga();
             a.W = (const T*)L.wqkv;
@@ -276,14 +317,10 @@ template <typename T> struct Run {
                 a.xidx_col = xcol;
                 gemv(a, PRO_NORM, EPI_STORE, 1, "linear");
             } else {
-                a.res = (const T*)hb;
-                a.ldr = d.dim;
-                a.slab = m->slabB;
-                a.slab_ld = d.dim;
-                a.nslab = ksb_prev;
-                a.res_out = (T*)xb;
-                a.ldro = d.dim;
-                gemv(a, PRO_RESNORM, EPI_STORE, 1, "linear");
+                a.X = (const T*)xb;
+                a.ldx = d.dim;
+                a.ss_in = m->ssX;
+                gemv(a, PRO_PRENORM, EPI_STORE, 1, "linear");
             }
         }
         const float scale = 1.0f / sqrtf((float)d.hd);
@@ -292,19 +329,24 @@ template <typename T> struct Run {
                               d.qk_norm, m->c.norm_eps, (const T*)L.qn, (const T*)L.kn, m->rope, (T*)m->kc,
                               (T*)m->vc, m->slot_stride, (size_t)layer * m->layer_stride, m->S,
                               m->maxsplit, scale, m->part};
-            m->prof.run(s, "attn", 0, 0, [&] {
-                launch_attn_decode<T>(s, aa, n);
-                launch_attn_combine<T>(s, m->part, m->frame_pos, n, d.nh, d.hd, ATTN_SPLIT, m->maxsplit,
-                                       (T*)m->att);
-            });
+            aa.cap = attn2_cap(d.hd, d.nh / d.nkv, E);
+            aa.maxsplit = FM_CEIL(m->S, aa.cap);
+            aa.cnt = m->attn_cnt;
+            aa.out = (T*)m->att;
+            m->prof.run(s, "attn", 0, 0, [&] { launch_attn_decode2<T>(s, aa, n); });
         } else {
             FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), m->frame_slot, d.nh, d.nkv, d.hd, d.qk_norm,
                                 m->c.norm_eps, (const T*)L.qn, (const T*)L.kn, m->frope, (T*)m->fkc,
                                 (T*)m->fvc, m->fslot_stride, (size_t)layer * m->flayer_stride, m->C, cpos,
                                 scale, (T*)m->att};
-            m->prof.run(s, "attn", 0, 0, [&] { launch_fast_attn_fused<T>(s, fa, n); });
+            m->prof.run(s, "attn", 0, 0, [&] {
+                if (cpos < 16 && d.hd <= 256)
+                    launch_fast_attn2<T>(s, fa, n);
+                else
+                    launch_fast_attn_fused<T>(s, fa, n);
+            });
         }
-        // wo -> split-K partials (slabA)
+        // wo, split-K; the last block of each tile finalises h = x + wo(att) and its sums of squares
         {
             GemvArgs<T> a = ga();
             a.W = (const T*)L.wo;
@@ -316,17 +358,6 @@ template <typename T> struct Run {
             a.K = d.nq();
             a.Yf = m->slabA;
             a.ldy = d.dim;
-            gemv(a, PRO_PLAIN, EPI_SLAB, kp.wo, "linear");
-        }
-        // W1/W3 (+ h = x + wo, ffn_norm) -> SwiGLU act
-        {
-            GemvArgs<T> a = ga();
-            a.W = (const T*)L.w1;
-            a.W2 = (const T*)L.w3;
-            a.nw = (const T*)L.fn;
-            a.R = n;
-            a.N = d.inter;
-            a.K = d.dim;
             if (first) {
                 a.res = (const T*)x_in;
                 a.ldr = ldx_in;
@@ -337,16 +368,29 @@ template <typename T> struct Run {
                 a.res = (const T*)xb;
                 a.ldr = d.dim;
             }
-            a.slab = m->slabA;
-            a.slab_ld = d.dim;
-            a.nslab = kp.wo;
             a.res_out = (T*)hb;
             a.ldro = d.dim;
+            a.ss_out = m->ssH;
+            a.tickets = m->tickets;
+            gemv(a, PRO_PLAIN, EPI_SLABFIN, kp.wo, "linear");
+        }
+        // W1/W3 (+ ffn_norm) -> SwiGLU act
+        {
+            GemvArgs<T> a = ga();
+            a.W = (const T*)L.w1;
+            a.W2 = (const T*)L.w3;
+            a.nw = (const T*)L.fn;
+            a.R = n;
+            a.N = d.inter;
+            a.K = d.dim;
+            a.X = (const T*)hb;
+            a.ldx = d.dim;
+            a.ss_in = m->ssH;
             a.Y = (T*)m->act;
             a.ldy = d.inter;
-            gemv(a, PRO_RESNORM, EPI_SWIGLU, 1, "linear");
+            gemv(a, PRO_PRENORM, EPI_SWIGLU, 1, "linear");
         }
-        // W2 -> split-K partials (slabB); the next consumer adds them to h
+        // W2, split-K; finalises the block output x = h + w2(act) into xb and its sums of squares
         {
             GemvArgs<T> a = ga();
             a.W = (const T*)L.w2;
@@ -357,7 +401,13 @@ template <typename T> struct Run {
             a.K = d.inter;
             a.Yf = m->slabB;
             a.ldy = d.dim;
-            gemv(a, PRO_PLAIN, EPI_SLAB, kp.w2, "linear");
+            a.res = (const T*)hb;
+            a.ldr = d.dim;
+            a.res_out = (T*)xb;
+            a.ldro = d.dim;
+            a.ss_out = m->ssX;
+            a.tickets = m->tickets;
+            gemv(a, PRO_PLAIN, EPI_SLABFIN, kp.w2, "linear");
         }
     }
 
@@ -365,7 +415,7 @@ template <typename T> struct Run {
         const KsbPlan kp = plan(m->sd, n);
         for (int l = 0; l < m->sd.n_layer; ++l)
             block_small(m->sd, m->slow[l], n, l == 0, m->x, m->c.dim, nullptr, 0, m->x, m->h, false, 0, l,
-                        kp, kp.w2);
+                        kp);
     }
 
     // final norm (+ pending residual) -> constrained head logits and the fast-model hidden
@@ -381,15 +431,11 @@ template <typename T> struct Run {
         a.ldy = m->Nhead;
         a.xn_out = (T*)m->xnl;
         a.ldxo = c.dim;
-        if (pending) {
-            a.res = (const T*)m->h;
-            a.ldr = c.dim;
-            a.slab = m->slabB;
-            a.slab_ld = c.dim;
-            a.nslab = ksb_prev;
-            a.res_out = (T*)m->x;
-            a.ldro = c.dim;
-            gemv(a, PRO_RESNORM, EPI_F32, 1, "linear");
+        if (pending) {  // the last slow layer's W2 finalised x (m->x) and its sums of squares
+            a.X = (const T*)m->x;
+            a.ldx = c.dim;
+            a.ss_in = m->ssX;
+            gemv(a, PRO_PRENORM, EPI_F32, 1, "linear");
         } else {
             a.X = (const T*)xlast;
             a.ldx = c.dim;
@@ -420,8 +466,7 @@ template <typename T> struct Run {
             const bool first = l == 0;
             const void* xin = cc == 0 ? hidden : m->femb;
             const int32_t* xidx = cc == 0 ? nullptr : m->cols;
-            block_small(m->fdm, m->fast[l], n, first, xin, c.fast_dim, xidx, cc, m->fx, m->fh, true, cc, l, kp,
-                        kp.w2);
+            block_small(m->fdm, m->fast[l], n, first, xin, c.fast_dim, xidx, cc, m->fx, m->fh, true, cc, l, kp);
         }
         if (with_head) {
             GemvArgs<T> a = ga();
@@ -432,14 +477,10 @@ template <typename T> struct Run {
             a.K = c.fast_dim;
             a.Yf = m->flogits;
             a.ldy = m->cb;
-            a.res = (const T*)m->fh;
-            a.ldr = c.fast_dim;
-            a.slab = m->slabB;
-            a.slab_ld = c.fast_dim;
-            a.nslab = kp.w2;
-            a.res_out = (T*)m->fx;
-            a.ldro = c.fast_dim;
-            gemv(a, PRO_RESNORM, EPI_F32, 1, "linear");
+            a.X = (const T*)m->fx;
+            a.ldx = c.fast_dim;
+            a.ss_in = m->ssX;
+            gemv(a, PRO_PRENORM, EPI_F32, 1, "linear");
         }
     }
 
@@ -723,7 +764,18 @@ static void finalize(fm_llm* m) {
     m->fh = m->dalloc((size_t)n * dmax * E);
     m->fxn = m->dalloc((size_t)n * dmax * E);
     m->maxsplit = FM_CEIL(m->S, ATTN_SPLIT);
-    m->part = (float*)m->dalloc((size_t)R * d.nh * m->maxsplit * (d.hd + 2) * 4, false);
+    m->part = (float*)m->dalloc((size_t)R * d.nh * std::max(m->maxsplit, FM_CEIL(m->S, 16)) * (d.hd + 2) * 4, false);
+    m->attn_cnt = (int*)m->dalloc((size_t)R * d.nkv * sizeof(int), false);
+    m->ssX = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
+    m->ssH = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
+    {
+        // arrival counters: one per 16-row tile of the largest decode GEMV (the slow head / W13)
+        const int maxn = std::max({m->Nhead, c.intermediate_size, c.fast_intermediate_size, qkvmax, dmax, m->cb});
+        m->tickets = (int*)m->dalloc((size_t)(maxn / 16 + 16) * sizeof(int));
+        m->skpart_cap = 8ll << 20;  // 32 MiB of partial tiles
+        m->skpart = (float*)m->dalloc((size_t)m->skpart_cap * sizeof(float), false);
+    }
+    HIPCHK(hipMemset(m->attn_cnt, 0, (size_t)R * d.nkv * sizeof(int)));
     m->slabA = (float*)m->dalloc((size_t)KSB_MAX * std::min(n, GEMV_MAX_ROWS) * dmax * 4);
     m->slabB = (float*)m->dalloc((size_t)KSB_MAX * std::min(n, GEMV_MAX_ROWS) * dmax * 4);
     m->logits = (float*)m->dalloc((size_t)n * m->Nhead * 4);
@@ -1143,6 +1195,59 @@ int fm_llm_profile_read(fm_llm* m, const char* cls, double* ms, int64_t* launche
     });
 }
 
+int fm_tune(const char* key, int value) {
+    return fm_guard([&] {
+        FMCHECK(key, "null key");
+        FmTuning& t = fm_tuning();
+        const std::string k = key;
+        if (k == "gemv_nt") {
+            t.gemv_nt = value != 0;
+        } else if (k == "gemv_u") {
+            FMCHECK(value == 2 || value == 4 || value == 8, "gemv_u must be 2, 4 or 8");
+            t.gemv_u = value;
+        } else if (k == "pro_exp") {
+            t.pro_exp = value;
+        } else if (k == "gemv_sk") {
+            t.gemv_sk = value != 0;
+        } else if (k == "gemv_sk_bpc") {
+            FMCHECK(value >= 1 && value <= 4, "gemv_sk_bpc must be in [1, 4]");
+            t.gemv_sk_bpc = value;
+        } else if (k == "gemv_wpb") {
+            FMCHECK(value == 4 || value == 8, "gemv_wpb must be 4 or 8");
+            t.gemv_wpb = value;
+        } else if (k == "ksb_blocks") {
+            FMCHECK(value >= 1, "ksb_blocks must be >= 1");
+            t.ksb_blocks = value;
+        } else if (k == "ksb_balance") {
+            t.ksb_balance = value != 0;
+        } else if (k == "debug_ts") {  // (re)arm the per-block timestamp buffer; 0 frees it
+            if (t.dbg) HIPCHK(hipFree(t.dbg));
+            t.dbg = nullptr;
+            if (value) {
+                HIPCHK(hipMalloc(&t.dbg, (8 + 8 * (1 << 20)) * sizeof(unsigned long long)));
+                HIPCHK(hipMemset(t.dbg, 0, 8 * sizeof(unsigned long long)));
+            }
+        } else {
+            FMCHECK(false, "unknown tuning key: " + k);
+        }
+    });
+}
+
+int fm_debug_ts_read(unsigned long long* out, int64_t max_records, int64_t* n_records) {
+    return fm_guard([&] {
+        FMCHECK(out && n_records, "null argument");
+        const FmTuning& t = fm_tuning();
+        FMCHECK(t.dbg, "debug_ts is not armed");
+        HIPCHK(hipDeviceSynchronize());
+        unsigned long long n = 0;
+        HIPCHK(hipMemcpy(&n, t.dbg, sizeof n, hipMemcpyDeviceToHost));
+        n = std::min<unsigned long long>(n, 1ull << 20);
+        n = std::min<unsigned long long>(n, (unsigned long long)max_records);
+        HIPCHK(hipMemcpy(out, t.dbg + 8, n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        *n_records = (int64_t)n;
+    });
+}
+
 int fm_llm_kernel_bench(fm_llm* m, const char* cls, int reps, double* avg_us, int64_t* launches,
                         int64_t* bytes) {
     return fm_guard([&] {
@@ -1200,6 +1305,9 @@ int fm_llm_use_graph(fm_llm* m, int enable) {
     return fm_guard([&] {
         FMCHECK(m, "null handle");
         m->use_graph = enable != 0;
+        // captured frames are dropped so that the next ones pick up any fm_tune change
+        for (auto& g : m->graphs) (void)hipGraphExecDestroy(g.second);
+        m->graphs.clear();
     });
 }
 

@@ -25,22 +25,37 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
                                                     int cb, int sb, int se, int scale,
                                                     T* __restrict__ x,
                                                     const int* __restrict__ row_slot) {
+    // grid (R, ceil(d / 2048)): a thread owns 8 consecutive features; all C + 1 row reads of a
+    // thread are in flight together
     const int r = blockIdx.x;
     if (r >= R) return;
     // prefill: tokens per row; decode: the slot's last emitted column (row_slot != null)
     const int32_t* t = tok + (size_t)(row_slot ? row_slot[r] : r) * (C + 1);
-    const int t0 = t[0];
+    const int i = 8 * (blockIdx.y * 256 + threadIdx.x);
+    if (i >= d) return;
+    int t0 = t[0];
+    t0 = t0 < 0 ? 0 : t0;  // defence in depth: decode tokens come from the sampler (ids <= se)
+    if (row_slot) t0 = t0 > se ? se : t0;
     const bool sem = t0 >= sb && t0 <= se;
-    const float inv = sqrtf((float)(C + 1));
-    for (int i = threadIdx.x; i < d; i += blockDim.x) {
-        float v = 0.f;
-        if (sem) {
-            for (int q = 0; q < C; ++q) v += ld(cbemb, (size_t)(t[1 + q] + q * cb) * d + i);
-            v = rnd<T>(v);
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (sem) {
+        for (int q = 0; q < C; ++q) {
+            float c8[8];
+            int cq = t[1 + q];
+            cq = cq < 0 ? 0 : (cq >= cb ? cb - 1 : cq);
+            load8(cbemb + (size_t)(cq + q * cb) * d + i, c8);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] += c8[u];
         }
-        float e = rnd<T>(ld(emb, (size_t)t0 * d + i) + v);
+    }
+    float e8[8];
+    load8(emb + (size_t)t0 * d + i, e8);
+    const float inv = sqrtf((float)(C + 1));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        float e = rnd<T>(e8[u] + (sem ? rnd<T>(v[u]) : 0.f));
         if (scale && sem) e = rnd<T>(e / inv);
-        st(x, (size_t)r * d + i, e);
+        st(x, (size_t)r * d + i + u, e);
     }
 }
 
@@ -637,7 +652,7 @@ __global__ void convert_kernel(const void* __restrict__ src, int src_bf16, int64
 template <typename T>
 void launch_embed(hipStream_t s, const int32_t* tok, int R, const T* emb, const T* cbemb, int d,
                   int C, int cb, int sb, int se, int scale, T* x, const int* row_slot) {
-    embed_kernel<T><<<R, 256, 0, s>>>(tok, R, emb, cbemb, d, C, cb, sb, se, scale, x, row_slot);
+    embed_kernel<T><<<dim3(R, FM_CEIL(d, 2048)), 256, 0, s>>>(tok, R, emb, cbemb, d, C, cb, sb, se, scale, x, row_slot);
 }
 template <typename T>
 void launch_gather_rows(hipStream_t s, const int32_t* codes, int ldc, int col, const T* table,

@@ -22,7 +22,7 @@ _lib = None
 ABI_SYMBOLS = [
     "fm_device_count", "fm_last_error", "fm_llm_open", "fm_llm_set_tensor", "fm_llm_synth_tensor",
     "fm_llm_finalize", "fm_llm_prefill", "fm_llm_decode", "fm_llm_decode_frames", "fm_llm_generate", "fm_llm_teacher_step",
-    "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph",
+    "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph", "fm_tune", "fm_debug_ts_read",
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
     "fm_codec_finalize", "fm_codec_decode", "fm_codec_profile_read", "fm_codec_debug_read",
     "fm_codec_close",
@@ -70,6 +70,8 @@ def lib():
     L.fm_llm_kernel_bench.argtypes = [vp, ctypes.c_char_p, i32, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.fm_llm_use_graph.argtypes = [vp, i32]
+    L.fm_tune.argtypes = [ctypes.c_char_p, i32]
+    L.fm_debug_ts_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), i64, ctypes.POINTER(ctypes.c_int64)]
     L.fm_llm_close.argtypes = [vp]
     if hasattr(L, "fm_codec_open"):
         L.fm_codec_open.argtypes = [vp, i32, i32, i32, ctypes.POINTER(vp)]
@@ -102,3 +104,17 @@ def i32p(a: np.ndarray):
 
 def f32p(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def tune(key: str, value: int):
+    """Process-wide developer knob of the decode GEMV (see fm_tune in include/fishmi.h)."""
+    check(lib().fm_tune(key.encode(), int(value)))
+
+
+def debug_ts_read(max_records: int = 1 << 20) -> np.ndarray:
+    """Per-block GEMV phase timestamps (developer hook, see fm_debug_ts_read): (n, 8) uint64."""
+    out = np.zeros((max_records, 8), np.uint64)
+    n = ctypes.c_int64(0)
+    check(lib().fm_debug_ts_read(out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), max_records,
+                                 ctypes.byref(n)))
+    return out[: n.value]

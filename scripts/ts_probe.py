@@ -1,0 +1,74 @@
+"""Per-block phase timing of the decode GEMVs at S2-Pro shapes (fm_tune "debug_ts").
+For each GEMV shape: kernel span, dispatch spread, and per-block prologue / stream / epilogue
+times (us).  Usage: python scripts/ts_probe.py [frames]"""
+import os
+import sys
+from collections import defaultdict
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fish-speech_amd"))
+from fishmi import native  # noqa: E402
+from fishmi.config import S2_PRO_CONFIG, S2_PRO_IM_END_ID, DualARConfig  # noqa: E402
+from fishmi.llm import DualARModel  # noqa: E402
+
+frames = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+for kv in sys.argv[2:]:
+    k, v = kv.split("=")
+    native.tune(k, int(v))
+cfg = DualARConfig._from_fish_qwen3_omni(S2_PRO_CONFIG)
+cfg.im_end_id = S2_PRO_IM_END_ID
+cfg.max_seq_len = 1024
+m = DualARModel.synthetic(cfg, seed=0, log2_half=5, device=0, precision="bf16", max_slots=1)
+p = np.zeros((cfg.num_codebooks + 1, 64), np.int32)
+p[0] = np.random.default_rng(1).integers(16, cfg.semantic_begin_id, 64)
+m.prefill(0, p, DualARModel.sampling(mask_im_end=True))
+m.decode_frames([0], 8)
+native.tune("debug_ts", 1)
+m.use_graph(False)
+m.decode_frames([0], frames)
+rec = native.debug_ts_read().astype(np.int64)
+native.tune("debug_ts", 0)
+rec = rec[np.argsort(rec[:, 1])]
+if os.environ.get("TS_SK"):
+    for tag in sorted(set((rec[:, 0] >> 32).tolist())):
+        a = rec[(rec[:, 0] >> 32) == tag].astype(np.float64)
+        a = a[a[:, 5] > 0]
+        if len(a):
+            d = lambda i, j: np.mean(a[:, j] - a[:, i]) / 100.0
+            print(f"sk N={tag}: issue {d(1, 5):.2f}  rms {d(5, 6):.2f}  stage {d(6, 7):.2f}  barrier {d(7, 2):.2f}  stream {d(2, 3):.2f} us")
+launches = []
+cur = None
+for r in rec:
+    tag = int(r[0]) >> 32
+    if cur is None or tag != cur["tag"] or r[1] > cur["end"]:
+        cur = {"tag": tag, "rows": [], "end": 0}
+        launches.append(cur)
+    cur["rows"].append(r)
+    cur["end"] = max(cur["end"], int(r[4]))
+by = defaultdict(list)
+for L in launches:
+    a = np.array(L["rows"])
+    t0, t1, t2, t3 = (a[:, i] for i in (1, 2, 3, 4))
+    by[L["tag"]].append(((t3.max() - t0.min()), (t0.max() - t0.min()), np.mean(t1 - t0), np.mean(t2 - t1),
+                         np.mean(t3 - t2), len(a), np.mean(t3 - t0)))
+print(f"{'N':>7s} {'launch':>6s} {'blocks':>6s} {'span':>7s} {'disp':>6s} {'pro':>6s} {'stream':>6s} {'epi':>6s} {'blk':>6s}  (us)")
+for tag, v in sorted(by.items(), key=lambda kv: -sum(x[0] for x in kv[1])):
+    a = np.array(v, dtype=np.float64) / 100.0  # 100 MHz ticks -> us
+    print(f"{tag:7d} {len(v):6d} {v[0][5]:6d} {a[:, 0].mean():7.2f} {a[:, 1].mean():6.2f} {a[:, 2].mean():6.2f} "
+          f"{a[:, 3].mean():6.2f} {a[:, 4].mean():6.2f} {a[:, 6].mean():6.2f}")
+if os.environ.get("TS_DETAIL"):
+    tag = int(os.environ["TS_DETAIL"])
+    L = [x for x in launches if x["tag"] == tag][3]
+    a = np.array(L["rows"])
+    t0 = (a[:, 1] - a[:, 1].min()) / 100.0
+    t3 = (a[:, 4] - a[:, 1].min()) / 100.0
+    order = np.argsort(t0)
+    print("start-time percentiles (us):", np.percentile(t0, [0, 10, 25, 40, 50, 60, 75, 90, 100]).round(2))
+    print("end-time percentiles (us):  ", np.percentile(t3, [0, 10, 25, 50, 75, 90, 100]).round(2))
+    bx = (a[:, 0] & 0xffff)[order]
+    print("first 40 started blocks:", bx[:40].tolist())
+    print("last 40 started blocks:", bx[-40:].tolist())
+    hist = np.histogram(t0, bins=20)
+    print("start histogram:", hist[0].tolist(), "edges", hist[1].round(1).tolist())

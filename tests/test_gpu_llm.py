@@ -223,3 +223,27 @@ def test_decode_frames_matches_generate(golden):
     for s in range(3):
         got = np.concatenate([firsts[s][:, None], fr[:, s, :].T], axis=1)
         np.testing.assert_array_equal(got, single[s])
+
+
+def test_long_context_split_attention_matches_oracle(golden):
+    """Contexts longer than one attention block's rows (256 here) take the split path of the
+    decode attention (per-split partials + last-arriver combine): greedy stream == oracle."""
+    import oracle as O
+    from fishmi.llm import DualARModel
+
+    cfg = _cfg("llm_b")
+    cfg.max_seq_len = 640
+    g = golden("llm_b_fp32.npz")
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "fp32", 1)
+    o = O.OracleLLM(cfg, False)
+    o.synth(int(g["synth_seed"]), int(g["log2_half"]))
+    rng = np.random.default_rng(3)
+    T = 300
+    p = np.zeros((cfg.num_codebooks + 1, T), np.int32)
+    p[0] = rng.integers(16, cfg.semantic_begin_id, T)
+    sem = rng.random(T) < 0.5  # semantic positions carry codebook tokens
+    p[0, sem] = rng.integers(cfg.semantic_begin_id, cfg.semantic_end_id + 1, int(sem.sum()))
+    p[1:, sem] = rng.integers(0, cfg.codebook_size, (cfg.num_codebooks, int(sem.sum())))
+    ref = o.generate(p, 12, top_k=1)
+    out = m.generate(p, 12, top_k=1)
+    np.testing.assert_array_equal(out, ref)
