@@ -1,0 +1,176 @@
+"""LLM worker seam: the drop-in for the reference's
+  * GenerateResponse / WrappedGenerateResponse / GenerateRequest  inference.py:447-451, 736-745
+  * generate_long                                                  inference.py:523-733
+  * launch_thread_safe_queue                                       inference.py:748-799
+backed by libfishmi (fishmi.llm.DualARModel).  Same request keys, same response stream
+(one "sample" per text batch with codes = y[1:, T:-1], then "next"), same error contract (an
+exception becomes status="error" carrying the exception; the worker keeps serving), one daemon
+worker thread owning the model, FIFO requests, `None` stops the worker.
+
+Differences, by design: codes are host int32 numpy arrays (C, N) rather than device tensors
+(the vocoder handle takes host codes); sampling uses the counter-based RNG of the HIP sampler,
+seeded by the request's `seed` (a fresh random seed when absent), since torch's global RNG
+stream is not reproducible across implementations anyway.
+"""
+from __future__ import annotations
+
+import copy
+import logging
+import os
+import queue
+import threading
+import time
+import traceback
+from dataclasses import dataclass
+from typing import Iterator, List, Literal, Optional, Union
+
+import numpy as np
+
+from . import prompt as P
+
+log = logging.getLogger("fishmi.engine")
+
+
+@dataclass
+class GenerateResponse:
+    action: Literal["sample", "next"]
+    codes: Optional[np.ndarray] = None
+    text: Optional[str] = None
+
+
+@dataclass
+class WrappedGenerateResponse:
+    status: Literal["success", "error"]
+    response: Optional[Union[GenerateResponse, Exception]] = None
+
+
+@dataclass
+class GenerateRequest:
+    request: dict
+    response_queue: queue.Queue
+
+
+def _codes(x) -> np.ndarray:
+    try:  # torch tensors from callers of the reference API
+        import torch
+
+        if isinstance(x, torch.Tensor):
+            return x.detach().cpu().numpy()
+    except ImportError:  # pragma: no cover
+        pass
+    return np.asarray(x)
+
+
+def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = None, device=None,
+                  decode_one_token=None, num_samples: int = 1, max_new_tokens: int = 0,
+                  top_p: float = 0.9, top_k: int = 30, repetition_penalty: float = 1.1,
+                  temperature: float = 1.0, compile: bool = False, iterative_prompt: bool = True,
+                  chunk_length: int = 512, prompt_text: Optional[Union[str, List[str]]] = None,
+                  prompt_tokens=None, seed: Optional[int] = None) -> Iterator[GenerateResponse]:
+    """inference.py:523-733 on the native model.  `device`, `decode_one_token`, `compile`,
+    `iterative_prompt` and `repetition_penalty` are accepted for signature compatibility; like
+    the reference, repetition_penalty is not applied (RAS is, inside the sampler)."""
+    if not (0 < top_p <= 1):
+        raise AssertionError("top_p must be in (0, 1]")
+    if not (0 < temperature < 2):
+        raise AssertionError("temperature must be in (0, 2)")
+    tok = tokenizer if tokenizer is not None else getattr(model, "tokenizer", None)
+    if tok is None:
+        raise ValueError("generate_long needs the checkpoint tokenizer (tokenizer.json)")
+    C = model.cfg.num_codebooks
+    if isinstance(prompt_tokens, (list, tuple)):
+        ptoks = [_codes(t) for t in prompt_tokens]
+    elif prompt_tokens is not None:
+        ptoks = [_codes(prompt_tokens)]
+    else:
+        ptoks = None
+    base = P.base_conversation(prompt_text, ptoks)
+    turns = P.split_text_by_speaker(text)
+    batches = P.group_turns_into_batches(turns, max_speakers=5, max_bytes=chunk_length) if turns else [text]
+    log.info("Split into %d turns, grouped into %d batches", len(turns), len(batches))
+    max_len = model.cfg.max_seq_len
+    rng = np.random.default_rng(seed)
+    for sample_idx in range(num_samples):
+        conv = copy.deepcopy(base)
+        t0 = time.perf_counter()
+        for batch_idx, batch_text in enumerate(batches):
+            conv.append(P.Message(role="user", parts=[P.TextPart(text=batch_text)]))
+            gen = copy.deepcopy(conv)
+            gen.append(P.Message(role="assistant", parts=[], modality="voice", add_im_end=False))
+            encoded, _, _ = gen.encode_for_inference(tok, num_codebooks=C)
+            if encoded.shape[1] > max_len - 2048:
+                raise ValueError(f"Prompt is too long: {encoded.shape[1]} > {max_len - 2048}")
+            s = int(rng.integers(0, 2**63 - 1)) if seed is None else seed + 1000003 * sample_idx + batch_idx
+            y = model.generate(encoded.astype(np.int32), max_new_tokens, temperature=temperature,
+                               top_p=top_p, top_k=top_k, seed=s)
+            codes = np.ascontiguousarray(y[1:, :-1])  # y[1:, prompt_length:-1] of the reference
+            if (codes < 0).any():
+                raise AssertionError(f"Negative code found: {codes}")
+            dt = time.perf_counter() - t0
+            log.info("Batch %d: generated %d frames in %.2fs", batch_idx, y.shape[1], dt)
+            conv.append(P.Message(role="assistant", parts=[P.VQPart(codes=codes)], modality="voice"))
+            yield GenerateResponse(action="sample", codes=codes, text=batch_text)
+        yield GenerateResponse(action="next")
+
+
+def _device_index(device) -> int:
+    if device is None:
+        return 0
+    if isinstance(device, int):
+        return device
+    if not isinstance(device, str):  # torch.device
+        idx = getattr(device, "index", None)
+        return int(idx) if isinstance(idx, int) else 0
+    return int(device.split(":")[1]) if ":" in device else 0
+
+
+def _precision(precision) -> str:
+    s = str(precision).lower()
+    if "float32" in s or s in ("fp32", "f32", "float"):
+        return "fp32"
+    return "bf16"  # torch.bfloat16 / torch.half / "bf16": the bf16 path
+
+
+def load_model(checkpoint_path: str, device=0, precision="bf16", max_slots: int = 1):
+    """init_model (inference.py:362-392): the native Dual-AR model with its tokenizer attached."""
+    from .llm import DualARModel
+
+    model = DualARModel.from_pretrained(checkpoint_path, device=_device_index(device),
+                                       precision=_precision(precision), max_slots=max_slots)
+    if model.tokenizer is None:
+        raise ValueError(f"{checkpoint_path} has no tokenizer.json")
+    return model
+
+
+def launch_thread_safe_queue(checkpoint_path, device, precision, compile: bool = False,
+                             model=None) -> "queue.Queue":
+    """inference.py:748-799: a daemon worker owning the model; returns its input queue once the
+    model is loaded.  `model` (optional) hands in an already-built DualARModel (tests)."""
+    input_queue: "queue.Queue" = queue.Queue()
+    ready = threading.Event()
+    failure: List[BaseException] = []
+
+    def worker():
+        try:
+            m = model if model is not None else load_model(checkpoint_path, device, precision)
+        except BaseException as e:  # surface load failures to the caller instead of hanging
+            failure.append(e)
+            ready.set()
+            return
+        ready.set()
+        while True:
+            item = input_queue.get()
+            if item is None:
+                break
+            try:
+                for chunk in generate_long(model=m, **item.request):
+                    item.response_queue.put(WrappedGenerateResponse(status="success", response=chunk))
+            except Exception as e:
+                log.error(traceback.format_exc())
+                item.response_queue.put(WrappedGenerateResponse(status="error", response=e))
+
+    threading.Thread(target=worker, daemon=True).start()
+    ready.wait()
+    if failure:
+        raise failure[0]
+    return input_queue

@@ -59,6 +59,7 @@ class DualARModel:
         native.check(L.fm_llm_open(ctypes.byref(self._c), device, prec, max_slots, ctypes.byref(h)))
         self.h = h
         self._finalized = False
+        self.tokenizer = None  # FishTokenizer when loaded from a checkpoint with tokenizer.json
 
     # ---- construction --------------------------------------------------------------
     @classmethod
@@ -67,6 +68,14 @@ class DualARModel:
         cfg = DualARConfig.from_pretrained(path)
         if max_length is not None:
             cfg.max_seq_len = max_length
+        tok = None
+        if (Path(path) / "tokenizer.json").exists():
+            # llama.py:499-509: the tokenizer's <|semantic:i|> range overrides the config's
+            from .prompt import FishTokenizer
+
+            tok = FishTokenizer(str(path))
+            if tok.semantic_end_id > 0:
+                cfg.semantic_begin_id, cfg.semantic_end_id = tok.semantic_begin_id, tok.semantic_end_id
         im = im_end_id if im_end_id is not None else resolve_im_end_id(path)
         if im is None:
             raise ValueError(f"cannot resolve <|im_end|> id: no tokenizer.json in {path}; pass im_end_id")
@@ -74,6 +83,7 @@ class DualARModel:
         m = cls(cfg, device, precision, max_slots)
         m.load_weights(load_llm_weights(path))
         m.finalize()
+        m.tokenizer = tok
         return m
 
     @classmethod

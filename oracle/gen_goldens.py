@@ -20,6 +20,10 @@ Reference call sites exercised (file:line in /root/reference):
   * DAC.from_indices -> DownsampleResidualVectorQuantize.decode
     -> WindowLimitedTransformer -> upsample -> Decoder          modded_dac.py:925-927, rvq.py:352-366
   * causal-prefix property of the codec (rvq.py:374-398 style)
+  * Conversation.encode_for_inference, split_text_by_speaker, group_turns_into_batches and the
+    generate_long conversation flow                             conversation.py:39-103,
+                                                                content_sequence.py:154-324,
+                                                                inference.py:454-707
 """
 from __future__ import annotations
 
@@ -468,9 +472,136 @@ def cmd_llm_wide():
           seq[:, 16:18].T.tolist())
 
 
+# --------------------------------------------------------------------------------------
+# Prompt side: the reference's own Conversation / ContentSequence
+# encode_for_inference and the speaker batching of generate_long (inference.py:454-651),
+# driven with a tiny local tokenizer (tests/golden/tok_tiny, written here) whose ids match the
+# llm_a fixture (semantic 200..327, <|im_end|> = 4).
+# --------------------------------------------------------------------------------------
+def write_tiny_tokenizer(path):
+    from tokenizers import AddedToken, Regex, Tokenizer, models, pre_tokenizers
+
+    specials = ["<|endoftext|>", "<|pad|>", "<|im_start|>", "<|phoneme_start|>", "<|im_end|>",
+                "<|phoneme_end|>", "<|text|>", "<|voice|>", "<|interleave|>", "<|audio_start|>",
+                "<|audio_end|>", "<|audio_pad|>"] + [f"<|speaker:{i}|>" for i in range(5)]
+    vocab = {t: i for i, t in enumerate(specials)}
+    for ch in [chr(c) for c in range(32, 127)] + ["\n"]:
+        vocab[ch] = len(vocab)
+    vocab["[UNK]"] = len(vocab)
+    while len(vocab) < 200:
+        vocab[f"<|reserved_{len(vocab)}|>"] = len(vocab)
+    sem = [f"<|semantic:{i}|>" for i in range(128)]
+    for t in sem:
+        vocab[t] = len(vocab)
+    while len(vocab) < 512:
+        vocab[f"<|reserved_{len(vocab)}|>"] = len(vocab)
+    tk = Tokenizer(models.WordLevel(vocab=vocab, unk_token="[UNK]"))
+    tk.pre_tokenizer = pre_tokenizers.Split(Regex("."), behavior="isolated")
+    tk.add_special_tokens([AddedToken(t, special=True, normalized=False) for t in specials + sem])
+    os.makedirs(path, exist_ok=True)
+    tk.save(os.path.join(path, "tokenizer.json"))
+    with open(os.path.join(path, "tokenizer_config.json"), "w") as f:
+        json.dump({"tokenizer_class": "PreTrainedTokenizerFast", "eos_token": "<|endoftext|>",
+                   "pad_token": "<|pad|>"}, f)
+
+
+def cmd_prompt():
+    import torch
+    from fish_speech.content_sequence import TextPart, VQPart
+    from fish_speech.conversation import Conversation, Message
+    from fish_speech.models.text2semantic.inference import group_turns_into_batches, split_text_by_speaker
+    from fish_speech.tokenizer import FishTokenizer
+    from copy import deepcopy
+
+    tdir = os.path.join(GOLD, "tok_tiny")
+    write_tiny_tokenizer(tdir)
+    tok = FishTokenizer(tdir)
+    C = 10
+    rng = np.random.default_rng(5)
+    texts = ["Hello there, how are you today?",
+             "<|speaker:0|>Hi! <|speaker:1|>Hey, long time. <|speaker:0|>Indeed, it has been a while "
+             "since we last met at the station. <|speaker:2|>Third voice here.",
+             "no speaker tags at all, just a sentence that is longer than the chunk length limit of "
+             "this test so that grouping has to split it into several batches? no, without tags it "
+             "stays one batch."]
+    out = {}
+    cases = []
+    for ti, text in enumerate(texts):
+        turns = split_text_by_speaker(text)
+        batches = group_turns_into_batches(turns, max_speakers=5, max_bytes=40) if turns else [text]
+        out[f"turns_{ti}"] = np.array(json.dumps(turns))
+        out[f"batches_{ti}"] = np.array(json.dumps(batches))
+        for use_prompt in (False, True):
+            # base conversation exactly as generate_long builds it (inference.py:558-600)
+            base = Conversation()
+            ptoks = None
+            if use_prompt:
+                ptext = ["reference one", "<|speaker:1|>second reference"]
+                ptoks = [torch.from_numpy(rng.integers(0, 128, (C, 6))), torch.from_numpy(rng.integers(0, 128, (C, 4)))]
+                tagged = [t if "<|speaker:" in t else f"<|speaker:{i}|>{t}" for i, t in enumerate(ptext)]
+                parts = [TextPart(text="convert the provided text to speech reference to the following:\n\nText:\n",
+                                  cal_loss=False),
+                         TextPart(text="\n".join(tagged), cal_loss=False),
+                         TextPart(text="\n\nSpeech:\n", cal_loss=False),
+                         VQPart(codes=torch.cat(ptoks, dim=1), cal_loss=False)]
+                out[f"ptoks_{ti}"] = np.concatenate([p.numpy() for p in ptoks], axis=1)
+            else:
+                parts = [TextPart(text="convert the provided text to speech", cal_loss=False)]
+            base.append(Message(role="system", parts=parts, cal_loss=False, add_im_start=True, add_im_end=True))
+            conv = deepcopy(base)
+            for bi, bt in enumerate(batches):
+                conv.append(Message(role="user", parts=[TextPart(text=bt, cal_loss=False)], cal_loss=False,
+                                    add_im_start=True, add_im_end=True))
+                gen = deepcopy(conv)
+                gen.append(Message(role="assistant", parts=[], cal_loss=False, modality="voice",
+                                   add_im_start=True, add_im_end=False))
+                enc, am, ap = gen.encode_for_inference(tok, num_codebooks=C)
+                key = f"enc_{ti}_{int(use_prompt)}_{bi}"
+                out[key] = enc.numpy().astype(np.int64)
+                # the "generated" codes appended back (inference.py:696-707), synthetic here
+                codes = torch.from_numpy(rng.integers(0, 128, (C, 3 + bi)))
+                out[f"gen_{ti}_{int(use_prompt)}_{bi}"] = codes.numpy()
+                conv.append(Message(role="assistant", parts=[VQPart(codes=codes.cpu(), cal_loss=False)],
+                                    cal_loss=False, modality="voice", add_im_start=True, add_im_end=True))
+                cases.append(key)
+    out["texts"] = np.array(json.dumps(texts))
+    out["cases"] = np.array(json.dumps(cases))
+    np.savez_compressed(os.path.join(GOLD, "prompt.npz"), **out)
+    print(f"prompt: {len(cases)} encoded conversations; e.g. {cases[:3]} shape {out[cases[0]].shape}")
+
+
+def cmd_engine():
+    """generate_long (inference.py:523-733) end to end, greedy fp32, on the llm_a weights with the
+    tiny tokenizer: reference prompt (speaker-tagged text + VQ codes), a multi-speaker text split
+    into batches, the conversation growing with each batch's codes."""
+    import copy as _copy
+
+    from fish_speech.models.text2semantic import inference
+    from fish_speech.tokenizer import FishTokenizer
+
+    cfg = _copy.deepcopy(LLM_A_CONFIG)
+    cfg["text_config"]["max_seq_len"] = 2560  # generate_long refuses prompts > max_len - 2048
+    model = build_llm(cfg, None, seed=11, log2_half=3).to(torch.float32)
+    model.tokenizer = FishTokenizer(os.path.join(GOLD, "tok_tiny"))
+    rng = np.random.default_rng(9)
+    ptoks = [torch.from_numpy(rng.integers(0, 128, (10, 5))), torch.from_numpy(rng.integers(0, 128, (10, 3)))]
+    text = "<|speaker:0|>Good morning. <|speaker:1|>Morning! Coffee? <|speaker:0|>Yes please, black."
+    outs = list(inference.generate_long(model=model, device="cpu", decode_one_token=inference.decode_one_token_ar,
+                                        text=text, max_new_tokens=7, top_p=0.9, top_k=1, temperature=0.7,
+                                        chunk_length=30, prompt_text=["ref a", "<|speaker:1|>ref b"],
+                                        prompt_tokens=ptoks))
+    res = {"text": np.array(text), "ptok0": ptoks[0].numpy(), "ptok1": ptoks[1].numpy(),
+           "actions": np.array(json.dumps([o.action for o in outs])),
+           "batch_texts": np.array(json.dumps([o.text for o in outs if o.action == "sample"]))}
+    for i, o in enumerate([o for o in outs if o.action == "sample"]):
+        res[f"codes_{i}"] = o.codes.numpy().astype(np.int32)
+    np.savez_compressed(os.path.join(GOLD, "engine.npz"), **res)
+    print("engine:", [o.action for o in outs], [res[k].shape for k in res if k.startswith("codes_")])
+
+
 if __name__ == "__main__":
     cmds = sys.argv[1:] or ["all"]
     if cmds == ["all"]:
-        cmds = ["ops", "llm", "codec", "codec_full", "llm_wide"]
+        cmds = ["ops", "llm", "codec", "codec_full", "llm_wide", "prompt", "engine"]
     for c in cmds:
         globals()[f"cmd_{c}"]()

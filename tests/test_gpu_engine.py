@@ -1,0 +1,96 @@
+"""B1 worker seam on the GPU: fishmi.engine.generate_long / launch_thread_safe_queue against the
+reference's own generate_long (tests/golden/engine.npz: greedy, fp32, llm_a weights, tiny
+tokenizer, reference prompt + three speaker batches).  Codes must be identical."""
+import json
+import os
+import queue
+import shutil
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _ckpt(tmp_path):
+    d = tmp_path / "ckpt"
+    shutil.copytree(os.path.join(GOLDEN, "llm_a"), d)
+    for f in ("tokenizer.json", "tokenizer_config.json"):
+        shutil.copy(os.path.join(GOLDEN, "tok_tiny", f), d / f)
+    return str(d)
+
+
+def _request(g, **kw):
+    r = dict(device="cuda", max_new_tokens=7, text=str(g["text"]), top_p=0.9, repetition_penalty=1.1,
+             temperature=0.7, compile=False, iterative_prompt=True, chunk_length=30,
+             prompt_tokens=[g["ptok0"], g["ptok1"]], prompt_text=["ref a", "<|speaker:1|>ref b"], top_k=1)
+    r.update(kw)
+    return r
+
+
+def _drain(q):
+    out = []
+    while True:
+        w = q.get(timeout=300)
+        out.append(w)
+        if w.status == "error" or w.response.action == "next":
+            return out
+
+
+def test_generate_long_matches_reference(golden, tmp_path):
+    from fishmi import engine
+
+    g = golden("engine.npz")
+    from fishmi.llm import DualARModel
+
+    # generate_long refuses prompts longer than max_seq_len - 2048 (inference.py:651-654), so the
+    # reference ran with max_length 2560 as well
+    m = DualARModel.from_pretrained(_ckpt(tmp_path), device=0, precision="fp32", max_length=2560)
+    assert m.tokenizer is not None and m.cfg.im_end_id == 4
+    req = _request(g)
+    outs = list(engine.generate_long(model=m, **req))
+    assert [o.action for o in outs] == json.loads(str(g["actions"]))
+    samples = [o for o in outs if o.action == "sample"]
+    assert [o.text for o in samples] == json.loads(str(g["batch_texts"]))
+    for i, o in enumerate(samples):
+        np.testing.assert_array_equal(o.codes, g[f"codes_{i}"])
+
+
+def test_worker_queue_contract(golden, tmp_path):
+    """launch_thread_safe_queue: FIFO requests, sample* + next per request, an exception becomes
+    status="error" and the worker keeps serving, None stops it (inference.py:748-799)."""
+    from fishmi import engine
+    from fishmi.llm import DualARModel
+
+    g = golden("engine.npz")
+    m = DualARModel.from_pretrained(_ckpt(tmp_path), device=0, precision="fp32", max_length=2560)
+    q = engine.launch_thread_safe_queue(None, "cuda:0", "float32", model=m)
+    rq = queue.Queue()
+    q.put(engine.GenerateRequest(request=_request(g, temperature=5.0), response_queue=rq))  # invalid
+    q.put(engine.GenerateRequest(request=_request(g), response_queue=rq))
+    bad = _drain(rq)
+    assert len(bad) == 1 and bad[0].status == "error" and isinstance(bad[0].response, AssertionError)
+    good = _drain(rq)
+    assert all(w.status == "success" for w in good)
+    codes = [w.response.codes for w in good if w.response.action == "sample"]
+    for i, c in enumerate(codes):
+        np.testing.assert_array_equal(c, g[f"codes_{i}"])
+    # sampled (top_k=30) requests are reproducible with the same seed
+    q.put(engine.GenerateRequest(request=_request(g, top_k=30, seed=5), response_queue=rq))
+    a = [w.response.codes for w in _drain(rq) if w.response.action == "sample"]
+    q.put(engine.GenerateRequest(request=_request(g, top_k=30, seed=5), response_queue=rq))
+    b = [w.response.codes for w in _drain(rq) if w.response.action == "sample"]
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    q.put(None)
+
+
+def test_load_model_from_checkpoint_dir(tmp_path):
+    """init_model path: config.json + safetensors shards + tokenizer.json in one directory."""
+    from fishmi import engine
+
+    m = engine.load_model(_ckpt(tmp_path), "cuda:0", "bfloat16")
+    assert m.tokenizer.semantic_begin_id == m.cfg.semantic_begin_id == 200
+    assert m.cfg.im_end_id == 4
