@@ -849,6 +849,288 @@ __global__ __launch_bounds__(256) void sample_radix_kernel(SampleArgs a) {
     }
 }
 
+// Two-stage top-K select (K <= 64) for the decode sampler: per-wave binary radix search for the
+// wave's K-th largest key (register-resident values, wave reductions only), block threshold =
+// max of the wave thresholds (every global top-K element is >= it, and each wave's elements
+// >= it are among that wave's candidates), candidates >= threshold through LDS, then an exact
+// select on <= 4*CAP candidates by wave 0.  Degenerate ties (more than CAP candidates in a wave)
+// take an exact full scan by wave 0.  Same output order as sample_radix_kernel: value desc,
+// token id asc, ties at the K-th value by smallest id.
+constexpr int SF_PER = 17;   // values per thread: Nl <= 256 * 17 = 4352 (4097 slow, 4096 fast)
+constexpr int SF_CAP = 64;   // candidates kept per wave
+
+// wave total and exclusive lane prefix of a small per-lane count (< 2^B) by bit-plane ballots:
+// B scalar popcounts instead of a cross-lane shuffle tree
+template <int B>
+__device__ __forceinline__ uint32_t sf_wave_count(uint32_t c, uint32_t* excl) {
+    uint32_t tot = 0, pre = 0;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const uint64_t m = __ballot((c >> b) & 1u);
+        tot += (uint32_t)__popcll(m) << b;
+        if (excl) pre += (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+    }
+    if (excl) *excl = pre;
+    return tot;
+}
+constexpr int sf_bits(int n) { return n < 2 ? 1 : 1 + sf_bits(n >> 1); }
+
+template <int N>
+__device__ __forceinline__ uint32_t sf_radix_kth(const uint32_t (&k)[N], uint32_t K, uint32_t kmax, uint32_t cap) {
+    // a threshold t with K <= #{key >= t} <= cap over the wave's N keys per lane (the exact K-th
+    // largest key when ties leave no such t).  Binary search on the key bits; each step counts
+    // per lane on the VALU and totals the wave by bit-plane ballots.  Bits that would lift t
+    // above the wave maximum `kmax` are skipped (count 0), and the search stops as soon as the
+    // count fits in `cap`.
+    uint32_t t = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t c = t | (1u << bit);
+        if (c > kmax) continue;
+        uint32_t cl = 0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) cl += k[i] >= c ? 1u : 0u;
+        const uint32_t cnt = sf_wave_count<sf_bits(N)>(cl, nullptr);
+        if (cnt >= K) {
+            t = c;
+            if (cnt <= cap) break;
+        }
+    }
+    return t;
+}
+
+// wave-wide bitonic sort of one (value, id) per lane into "better first" order (value desc,
+// id asc); padding lanes carry (-inf, INT_MAX)
+__device__ __forceinline__ void sf_bitonic(float& v, int& id, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const float ov = __shfl_xor(v, j, 64);
+            const int oi = __shfl_xor(id, j, 64);
+            const bool lower = (lane & j) == 0, dir = (lane & k) == 0;
+            const bool other_better = cbetter(ov, oi, v, id);
+            if ((lower == dir) == other_better) {
+                v = ov;
+                id = oi;
+            }
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void sample_fast_kernel(SampleArgs a) {
+    unsigned long long tsx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define SFTS(n) if (a.dbg) tsx[n] = __builtin_amdgcn_s_memrealtime();
+    SFTS(0)
+    extern __shared__ float vals[];  // [Nl] (fallback path only)
+    __shared__ float redm[4], reds[4];
+    __shared__ uint32_t wthr[4];
+    __shared__ uint32_t ncand[4];
+    __shared__ __align__(16) float2 cand[4 * SF_CAP];  // (value, token id bits)
+    __shared__ __align__(16) uint64_t ckey[4 * SF_CAP];  // (key << 32 | ~id): larger = better
+    __shared__ float cv[64];
+    __shared__ int cid[64];
+    __shared__ int overflow;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = blockIdx.x;
+    const int slot = a.row_slot[r];
+    const SlotParams sp = a.sp[slot];
+    const float* lg = a.logits + (size_t)r * a.ldl;
+    const int Nl = a.Nl;
+    auto tok_of = [&](int i) { return a.slow ? (i < Nl - 1 ? a.sb + i : a.im_end) : i; };
+    // this thread's values: indices threadIdx.x + 256 * i (coalesced loads, all in flight)
+    float v[SF_PER];
+    uint32_t key[SF_PER];
+#pragma unroll
+    for (int i = 0; i < SF_PER; ++i) {
+        const int idx = threadIdx.x + 256 * i;
+        float x = idx < Nl ? lg[idx < Nl ? idx : 0] : -INFINITY;
+        if (a.slow && sp.mask_im_end && idx == Nl - 1) x = -INFINITY;
+        v[i] = x;
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < SF_PER; ++i) {
+        mloc = fmaxf(mloc, v[i]);
+        key[i] = threadIdx.x + 256 * i < Nl ? fkey(v[i]) : 0u;  // padding never qualifies
+    }
+    SFTS(1)
+    mloc = wave_max(mloc);
+    if (lane == 0) redm[wave] = mloc;
+    if (threadIdx.x == 0) overflow = 0;
+    // per-wave K-th largest key (the wave holds 64 * SF_PER slots; padding is -inf -> key 0x007fffff)
+    int K = sp.top_k < 1 ? 1 : (sp.top_k > 64 ? 64 : sp.top_k);
+    if (K > Nl) K = Nl;
+    SFTS(2)
+    const uint32_t kth = sf_radix_kth<SF_PER>(key, (uint32_t)K, fkey(mloc), (uint32_t)SF_CAP);
+    SFTS(3)
+    if (lane == 0) wthr[wave] = kth;
+    __syncthreads();
+    const float M = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+    const uint32_t thrT = max(max(wthr[0], wthr[1]), max(wthr[2], wthr[3]));
+    float sloc = 0.f;
+#pragma unroll
+    for (int i = 0; i < SF_PER; ++i) sloc += (v[i] == -INFINITY) ? 0.f : expf(v[i] - M);
+    sloc = wave_sum(sloc);
+    if (lane == 0) reds[wave] = sloc;
+    // candidates >= thrT of this wave -> LDS (order: lane-major, stable)
+    uint32_t mine = 0;
+#pragma unroll
+    for (int i = 0; i < SF_PER; ++i) mine += (key[i] >= thrT && key[i] != 0u) ? 1u : 0u;
+    uint32_t excl;
+    const uint32_t tot = sf_wave_count<sf_bits(SF_PER)>(mine, &excl);
+    if (tot > (uint32_t)SF_CAP) {
+        if (lane == 0) overflow = 1;
+    } else {
+        uint32_t at = excl;
+#pragma unroll
+        for (int i = 0; i < SF_PER; ++i) {
+            if (key[i] >= thrT && key[i] != 0u) {
+                const int id = tok_of(threadIdx.x + 256 * i);
+                cand[wave * SF_CAP + at] = make_float2(v[i], __int_as_float(id));
+                ckey[wave * SF_CAP + at] = ((uint64_t)key[i] << 32) | (uint32_t)~(uint32_t)id;
+                ++at;
+            }
+        }
+        // pad the wave's list to a multiple of 8 with entries that never rank above anything
+        if (lane >= (int)tot && lane < (int)((tot + 7u) & ~7u))
+            ckey[wave * SF_CAP + lane] = 0ull;
+    }
+    if (lane == 0) ncand[wave] = tot;
+    __syncthreads();
+    SFTS(4)
+    const float den = reds[0] + reds[1] + reds[2] + reds[3];
+    if (overflow) {  // degenerate ties: park everything in LDS for the exact scan below
+#pragma unroll
+        for (int i = 0; i < SF_PER; ++i) {
+            const int idx = threadIdx.x + 256 * i;
+            if (idx < Nl) vals[idx] = v[i];
+        }
+    } else {
+        // exact ranks by counting: candidate j's rank is the number of candidates better than it
+        // (value desc, id asc -- a total order, ids are unique), so the K best land sorted in cv/cid
+        const int n0 = ncand[0], n1 = ncand[1], n2 = ncand[2], n3 = ncand[3];
+        const int j = threadIdx.x, nc = n0 + n1 + n2 + n3;
+        if (j < nc) {
+            const int w = j < n0 ? 0 : (j < n0 + n1 ? 1 : (j < n0 + n1 + n2 ? 2 : 3));
+            const int o = j - (w == 0 ? 0 : (w == 1 ? n0 : (w == 2 ? n0 + n1 : n0 + n1 + n2)));
+            const float2 me = cand[w * SF_CAP + o];
+            const int mid = __float_as_int(me.y);
+            int rank = 0;
+            const int nw[4] = {n0, n1, n2, n3};
+            const uint64_t mk = ckey[w * SF_CAP + o];
+#pragma unroll
+            for (int w2 = 0; w2 < 4; ++w2) {
+                const ulonglong2* cp = reinterpret_cast<const ulonglong2*>(ckey + w2 * SF_CAP);
+                const int nq = ((nw[w2] + 7) & ~7) >> 1;  // 16 bytes = two keys
+                for (int q = 0; q < nq; q += 4) {  // four independent 16-byte LDS reads per step
+                    const ulonglong2 c0 = cp[q], c1 = cp[q + 1], c2 = cp[q + 2], c3 = cp[q + 3];
+                    rank += (c0.x > mk) + (c0.y > mk) + (c1.x > mk) + (c1.y > mk) + (c2.x > mk) +
+                            (c2.y > mk) + (c3.x > mk) + (c3.y > mk);
+                }
+            }
+            if (rank < K) {
+                cv[rank] = me.x;
+                cid[rank] = mid;
+            }
+        }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    // ---- wave 0: sample over the K best (exact full scan first on overflow) ------------------
+    int ns = 0;        // strict (> K-th value) count
+    uint32_t thr = 0;  // key of the K-th element
+    uint32_t rem = 0;  // how many of the K-th value's ties to take
+    if (overflow) {
+        // exact full scan of vals[] by one wave (rare: massive ties)
+        thr = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t c = thr | (1u << bit);
+            uint32_t cnt = 0;
+            for (int i = lane; i < Nl; i += 64) cnt += fkey(vals[i]) >= c ? 1u : 0u;
+            cnt = (uint32_t)wave_sum((float)cnt);
+            if (cnt >= (uint32_t)K) thr = c;
+        }
+        uint32_t gt = 0;
+        for (int i = lane; i < Nl; i += 64) gt += fkey(vals[i]) > thr ? 1u : 0u;
+        ns = (int)wave_sum((float)gt);
+        rem = (uint32_t)(K - ns);
+        if (lane == 0) {  // strict ones (< 64 of them) by selection, then the smallest tie ids
+            int taken = 0;
+            float lastv = INFINITY;
+            int lasti = -1;
+            while (taken < ns) {
+                float bv = -INFINITY;
+                int bi = 0x7fffffff;
+                for (int i = 0; i < Nl; ++i) {
+                    const float x = vals[i];
+                    const int id = tok_of(i);
+                    if (fkey(x) > thr && cbetter(lastv, lasti, x, id) && cbetter(x, id, bv, bi)) {
+                        bv = x;
+                        bi = id;
+                    }
+                }
+                cv[taken] = bv;
+                cid[taken] = bi;
+                lastv = bv;
+                lasti = bi;
+                ++taken;
+            }
+            int last = -1;
+            for (uint32_t t2 = 0; t2 < rem; ++t2) {
+                int best = 0x7fffffff;
+                float bv = 0.f;
+                for (int i = 0; i < Nl; ++i) {
+                    const int id = tok_of(i);
+                    if (fkey(vals[i]) == thr && id > last && id < best) {
+                        best = id;
+                        bv = vals[i];
+                    }
+                }
+                cv[ns + t2] = bv;
+                cid[ns + t2] = best;
+                last = best;
+            }
+        }
+    }
+    (void)ns;
+    (void)rem;
+    __builtin_amdgcn_wave_barrier();
+    SFTS(5)
+    const uint64_t step = (uint64_t)sp.step;
+    int32_t* col = a.cols + (size_t)r * a.ldc;
+    if (a.dbg && lane == 0) {
+        tsx[6] = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long slot2 = atomicAdd(a.dbg, 1ull);
+        if (slot2 < (1ull << 20)) {
+            unsigned long long* q = a.dbg + 8 + slot2 * 8;
+            q[0] = (0xFFFFull << 32) | (unsigned)(ncand[0] + ncand[1] + ncand[2] + ncand[3]) | ((unsigned long long)overflow << 16);
+            for (int z = 0; z < 7; ++z) q[1 + z] = tsx[z];
+        }
+    }
+    if (a.slow) {
+        int tok = sample_top<T>(cv, cid, K, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed, step, 0, lane);
+        const int hi = sample_top<T>(cv, cid, K, M, den, 1.0f, 0.9f, sp.top_k, sp.seed, step, 1, lane);
+        if (a.ras_enable) {
+            const int32_t* prev = a.ras + (size_t)slot * a.ras_stride;
+            bool inwin = false;
+            for (int j = 0; j < 10; ++j) inwin |= prev[j] == tok;
+            if (inwin && tok >= a.sb && tok <= a.se) tok = hi;
+        }
+        if (!((tok >= a.sb && tok <= a.se) || tok == a.im_end)) tok = a.im_end;
+        if (lane == 0) {
+            col[0] = tok;
+            int c = tok - a.sb;
+            c = c < 0 ? 0 : (c > a.cb - 1 ? a.cb - 1 : c);
+            col[1] = c;
+        }
+    } else {
+        const int code = sample_top<T>(cv, cid, K, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed, step,
+                                       (uint32_t)a.draw, lane);
+        if (lane == 0) col[a.col_idx] = (code >= 0 && code < a.cb) ? code : 0;
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 template <typename T> void launch_attn_decode(hipStream_t s, const AttnDecArgs<T>& a, int R) {
     dim3 g1(R, a.nkv, a.maxsplit);
@@ -875,7 +1157,10 @@ template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFused
     fast_attn_fused_kernel<T><<<g, 256, lds, s>>>(a);
 }
 template <typename T> void launch_sample_radix(hipStream_t s, const SampleArgs& a, int R) {
-    sample_radix_kernel<T><<<R, 256, sizeof(float) * a.Nl, s>>>(a);
+    if (a.Nl <= 256 * SF_PER && fm_tuning().sampler_fast)
+        sample_fast_kernel<T><<<R, 256, sizeof(float) * a.Nl, s>>>(a);
+    else
+        sample_radix_kernel<T><<<R, 256, sizeof(float) * a.Nl, s>>>(a);
 }
 template void launch_attn_decode<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
 template void launch_attn_decode<float>(hipStream_t, const AttnDecArgs<float>&, int);

@@ -80,6 +80,7 @@ struct SampleArgs {
     const int32_t* ras;   // [slot][ras_stride]
     int ras_stride, ras_enable;
     int slow, sb, se, im_end, cb, draw, col_idx;
+    unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
     int32_t* cols;        // [R][ldc]
     int ldc;
 };
@@ -150,6 +151,7 @@ struct FmTuning {
     int gemv_sk = 0;         // 1: stream-K decode GEMV (one persistent block per CU), 0: tiled
     int gemv_sk_bpc = 1;     // stream-K blocks per CU
     int pro_exp = 0;         // EXPERIMENT: 1 skip tile-sum loads, 2 skip norm-weight loads, 3 both
+    int sampler_fast = 1;    // 1: two-stage register top-K sampler, 0: LDS radix-select sampler
     int ksb_blocks = 512;    // split K until the grid has at least this many blocks
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)

@@ -571,6 +571,7 @@ template <typename T> struct Run {
         a.col_idx = c + 1;
         a.cols = m->cols;
         a.ldc = m->C1;
+        a.dbg = fm_tuning().dbg;
         return a;
     }
 
@@ -1205,6 +1206,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "gemv_u") {
             FMCHECK(value == 2 || value == 4 || value == 8, "gemv_u must be 2, 4 or 8");
             t.gemv_u = value;
+        } else if (k == "sampler_fast") {
+            t.sampler_fast = value != 0;
         } else if (k == "pro_exp") {
             t.pro_exp = value;
         } else if (k == "gemv_sk") {

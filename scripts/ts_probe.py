@@ -31,6 +31,13 @@ m.decode_frames([0], frames)
 rec = native.debug_ts_read().astype(np.int64)
 native.tune("debug_ts", 0)
 rec = rec[np.argsort(rec[:, 1])]
+smp = rec[(rec[:, 0] >> 32) == 0xFFFF].astype(np.float64)
+if len(smp):
+    d = np.diff(smp[:, 1:8], axis=1).mean(axis=0) / 100.0
+    print("sampler phases (us): load", round(d[0], 2), "max", round(d[1], 2), "kth", round(d[2], 2),
+          "bar1+cand+bar2", round(d[3], 2), "rank", round(d[4], 2), "-", round(d[5], 2))
+    lo = (smp[:, 0].astype(np.int64) & 0xFFFF)
+    print("sampler candidates: mean", round(lo.mean(), 1), "max", lo.max(), "overflow", int(((smp[:, 0].astype(np.int64) >> 16) & 1).sum()))
 if os.environ.get("TS_SK"):
     for tag in sorted(set((rec[:, 0] >> 32).tolist())):
         a = rec[(rec[:, 0] >> 32) == tag].astype(np.float64)

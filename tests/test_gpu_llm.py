@@ -247,3 +247,21 @@ def test_long_context_split_attention_matches_oracle(golden):
     ref = o.generate(p, 12, top_k=1)
     out = m.generate(p, 12, top_k=1)
     np.testing.assert_array_equal(out, ref)
+
+
+def test_fast_sampler_equals_radix_sampler(golden):
+    """The two-stage register top-K sampler and the LDS radix-select sampler draw the same
+    streams (same candidates in the same order, same RNG draws), sampled and greedy."""
+    from fishmi import native
+
+    m, g, cfg = _model("llm_a", "bf16", golden)
+    outs = {}
+    for fast in (1, 0):
+        native.tune("sampler_fast", fast)
+        m.use_graph(False)
+        outs[fast] = [m.generate(g["prompt"], 24, top_k=k, seed=s, temperature=0.9, top_p=0.95)
+                      for k, s in ((30, 1), (64, 2), (1, 3), (5, 4))]
+    native.tune("sampler_fast", 1)
+    m.use_graph(True)
+    for a, b in zip(outs[1], outs[0]):
+        np.testing.assert_array_equal(a, b)
