@@ -15,6 +15,7 @@
 //                       top-p / temperature / multinomial with the shared counter RNG
 //                       (inference.py:43-93) and RAS (inference.py:117-144).
 #include "fm_kernels.h"
+#include "fm_attn_dev.h"
 
 // normalise (optional) + rope one head held as pairs by a wave (lane p owns pair p, p+64)
 template <typename T>
@@ -166,6 +167,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecArgs<T> a) {
 template <typename T>
 __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned long long tz[7] = {0, 0, 0, 0, 0, 0, 0};
+    DBG_TS(tz, 0)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
     const int hd = a.hd, g = a.nh / a.nkv, ks = hd + 8, cap = a.cap;
@@ -244,6 +247,7 @@ __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
             }
         }
     }
+    DBG_TS(tz, 1)
     // q heads: qk-norm (fp32 incl. weight, one rounding) + RoPE (bf16 table, rounded)
     for (int i = 0; i < 2; ++i) {
         const int hh = wave + 8 * i;
@@ -303,6 +307,7 @@ __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
         }
     }
     __syncthreads();
+    DBG_TS(tz, 2)
     // ---- scores: item (head, row); a wave's 64 items share one head
     const int rp = (nj + 63) & ~63;
     const float scale = a.scale;
@@ -322,6 +327,7 @@ __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
         }
     }
     __syncthreads();
+    DBG_TS(tz, 3)
     // ---- softmax per head (wave per head): p = exp(s - m), l = sum p
     float mh[2], lh[2];
     for (int i = 0; i < 2; ++i) {
@@ -349,6 +355,7 @@ __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
                 reinterpret_cast<float*>(flag + 4)[2 * (wave + 8 * i) + 1] = lh[i];
             }
     __syncthreads();
+    DBG_TS(tz, 4)
     // ---- PV: item (head, dim pair); two threads per item split the rows (even / odd)
     const int hp = hd >> 1;
     const float* ml = reinterpret_cast<const float*>(flag + 4);
@@ -382,6 +389,11 @@ __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
                 }
             }
         }
+    }
+    DBG_TS(tz, 5)
+    if (a.dbg && threadIdx.x == 0) {
+        tz[6] = __builtin_amdgcn_s_memrealtime();
+        dbg_record(a.dbg, 0xFFFD, (unsigned)(nsp << 16 | nj), tz);
     }
     if (single) return;
     // ---- split combine by the last-arriving block of (row, kv head)
@@ -417,140 +429,17 @@ __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
     }
 }
 
-// Fast-model attention at codebook position cpos (llama.py:947-975, every rounding of the
-// reference's matmul-softmax-matmul kept): grid (R, nh), ONE wave per q head, no LDS, no
-// barrier.  Lane l owns dimension pairs l, l+64 (RoPE pairs).  Each wave recomputes the new k
-// (qk-norm + RoPE, cheap) so waves never wait on each other; the first q head of each kv group
-// writes k/v of cpos to the fast cache.  Two round trips: (slot, raw q/k/v, norm weights, rope
-// row) then (the cpos cached rows).
+// Fast-model attention at codebook position cpos: grid (R, nh), one wave per q head (body in
+// fm_attn_dev.h, shared with the QKV GEMV's fused tail).  Two round trips: (slot, raw q/k/v,
+// norm weights, rope row) then (the cpos cached rows).
 template <typename T>
 __global__ __launch_bounds__(64) void fast_attn2_kernel(FastFusedArgs<T> a) {
-    const int lane = threadIdx.x;
-    const int r = blockIdx.x, h = blockIdx.y;
-    const int hd = a.hd, g = a.nh / a.nkv, kvh = h / g, cpos = a.cpos, half = hd >> 1;
-    const T* raw = a.qkv + (size_t)r * a.ldqkv;
-    const float* tab = a.rope + (size_t)cpos * hd;
-    const int slot = a.row_slot[r];
-    float q0[2], q1[2], k0[2], k1[2], v0[2], v1[2], qw0[2], qw1[2], kw0[2], kw1[2], c_[2], s_[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int p = lane + 64 * u;
-        const bool ok = p < half;
-        const int pp = ok ? p : 0;
-        q0[u] = ld(raw + (size_t)h * hd, 2 * pp);
-        q1[u] = ld(raw + (size_t)h * hd, 2 * pp + 1);
-        k0[u] = ld(raw + (size_t)(a.nh + kvh) * hd, 2 * pp);
-        k1[u] = ld(raw + (size_t)(a.nh + kvh) * hd, 2 * pp + 1);
-        v0[u] = ld(raw + (size_t)(a.nh + a.nkv + kvh) * hd, 2 * pp);
-        v1[u] = ld(raw + (size_t)(a.nh + a.nkv + kvh) * hd, 2 * pp + 1);
-        qw0[u] = a.qk_norm ? ld(a.qn, 2 * pp) : 1.f;
-        qw1[u] = a.qk_norm ? ld(a.qn, 2 * pp + 1) : 1.f;
-        kw0[u] = a.qk_norm ? ld(a.kn, 2 * pp) : 1.f;
-        kw1[u] = a.qk_norm ? ld(a.kn, 2 * pp + 1) : 1.f;
-        c_[u] = tab[2 * pp];
-        s_[u] = tab[2 * pp + 1];
-        if (!ok) q0[u] = q1[u] = k0[u] = k1[u] = v0[u] = v1[u] = 0.f;
-    }
-    const size_t base = (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
-    T* kc = a.kc + base;
-    T* vc = a.vc + base;
-    // cached rows j < cpos (<= C - 1 <= 63 rows): the lane's two pairs of each
-    constexpr int MAXJ = 16;
-    float K0[MAXJ][2], K1[MAXJ][2], V0[MAXJ][2], V1[MAXJ][2];
-#pragma unroll
-    for (int j = 0; j < MAXJ; ++j) {
-        if (j < cpos) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int p = lane + 64 * u;
-                const int pp = p < half ? p : 0;
-                K0[j][u] = ld(kc + (size_t)j * hd, 2 * pp);
-                K1[j][u] = ld(kc + (size_t)j * hd, 2 * pp + 1);
-                V0[j][u] = ld(vc + (size_t)j * hd, 2 * pp);
-                V1[j][u] = ld(vc + (size_t)j * hd, 2 * pp + 1);
-                if (p >= half) K0[j][u] = K1[j][u] = V0[j][u] = V1[j][u] = 0.f;
-            }
-        }
-    }
-    // qk-norm (fp32 incl. weight, one rounding) + RoPE (bf16 table, rounded)
-    auto prep = [&](float (&x0)[2], float (&x1)[2], const float (&w0)[2], const float (&w1)[2], bool norm) {
-        if (norm) {
-            float ss = 0.f;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) ss += x0[u] * x0[u] + x1[u] * x1[u];
-            ss = wave_sum(ss);
-            const float rs = 1.0f / sqrtf(ss / (float)hd + a.eps);
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                x0[u] = rnd<T>((x0[u] * rs) * w0[u]);
-                x1[u] = rnd<T>((x1[u] * rs) * w1[u]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const float y0 = rnd<T>(x0[u] * c_[u] - x1[u] * s_[u]);
-            const float y1 = rnd<T>(x1[u] * c_[u] + x0[u] * s_[u]);
-            x0[u] = y0;
-            x1[u] = y1;
-        }
-    };
-    prep(q0, q1, qw0, qw1, a.qk_norm);
-    prep(k0, k1, kw0, kw1, a.qk_norm);
-    if (h == kvh * g) {  // first q head of the group stores the new k / v
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int p = lane + 64 * u;
-            if (p < half) {
-                st(kc + (size_t)cpos * hd, 2 * p, k0[u]);
-                st(kc + (size_t)cpos * hd, 2 * p + 1, k1[u]);
-                st(vc + (size_t)cpos * hd, 2 * p, v0[u]);
-                st(vc + (size_t)cpos * hd, 2 * p + 1, v1[u]);
-            }
-        }
-    }
-    // scores round(round(q.k) * scale), softmax, probabilities rounded (fast SDPA path)
-    float sc[MAXJ + 1];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j <= MAXJ; ++j) {
-        if (j > cpos) break;
-        float d = 0.f;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const float a0 = j < cpos ? K0[j < MAXJ ? j : 0][u] : k0[u];
-            const float a1 = j < cpos ? K1[j < MAXJ ? j : 0][u] : k1[u];
-            d += q0[u] * a0 + q1[u] * a1;
-        }
-        d = wave_sum(d);
-        sc[j] = rnd<T>(rnd<T>(d) * a.scale);
-        mx = fmaxf(mx, sc[j]);
-    }
-    float den = 0.f;
-#pragma unroll
-    for (int j = 0; j <= MAXJ; ++j) {
-        if (j > cpos) break;
-        sc[j] = expf(sc[j] - mx);
-        den += sc[j];
-    }
-    float o0[2] = {0.f, 0.f}, o1[2] = {0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j <= MAXJ; ++j) {
-        if (j > cpos) break;
-        const float p = rnd<T>(sc[j] / den);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            o0[u] += p * (j < cpos ? V0[j < MAXJ ? j : 0][u] : v0[u]);
-            o1[u] += p * (j < cpos ? V1[j < MAXJ ? j : 0][u] : v1[u]);
-        }
-    }
-    T* out = a.out + (size_t)r * a.nh * hd + (size_t)h * hd;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int p = lane + 64 * u;
-        if (p < half) {
-            st(out, 2 * p, o0[u]);
-            st(out, 2 * p + 1, o1[u]);
-        }
+    unsigned long long tz[7] = {0, 0, 0, 0, 0, 0, 0};
+    DBG_TS(tz, 0)
+    fast_attn_head<T, false>(a, blockIdx.x, blockIdx.y, threadIdx.x, tz);
+    if (a.dbg && threadIdx.x == 0) {
+        tz[4] = __builtin_amdgcn_s_memrealtime();
+        dbg_record(a.dbg, 0xFFFE, (unsigned)a.cpos, tz);
     }
 }
 

@@ -1,0 +1,164 @@
+// Device-side fast-model attention for one (row, q head), shared by the standalone
+// fast_attn2_kernel (fm_attn.hip) and the fused tail of the QKV GEMV (fm_gemv.hip, EPI_QKVATT).
+//
+// Fast-model attention at codebook position cpos (llama.py:947-975), every rounding of the
+// reference's matmul-softmax-matmul kept: ONE wave per q head, no LDS, no barrier.  Lane l owns
+// dimension pairs l, l+64 (RoPE pairs).  Each wave recomputes the new k (qk-norm + RoPE, cheap) so
+// waves never wait on each other; the first q head of each kv group writes k/v of cpos to the fast
+// cache.  COH: read the raw q/k/v projections with agent-coherent (write-through-visible) loads --
+// the fused tail reads rows other workgroups of the same launch have just written.
+#pragma once
+#include "fm_common.h"
+#include "fm_kernels.h"
+
+constexpr int FAST_ATTN_MAXJ = 16;  // cached rows a wave keeps in registers (cpos < 16)
+
+// (p[0], p[1]) as floats; COH: one agent-scope relaxed load per 32-bit word (sc1, bypasses the
+// non-coherent per-XCD L2 lines another XCD may hold)
+template <typename T, bool COH>
+__device__ __forceinline__ void ld_pair(const T* p, float& x0, float& x1) {
+    if constexpr (sizeof(T) == 2) {
+        uint32_t w;
+        if constexpr (COH)
+            w = __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            w = *reinterpret_cast<const uint32_t*>(p);
+        x0 = __uint_as_float(w << 16);
+        x1 = __uint_as_float(w & 0xffff0000u);
+    } else {
+        if constexpr (COH) {
+            x0 = __hip_atomic_load(reinterpret_cast<const float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            x1 = __hip_atomic_load(reinterpret_cast<const float*>(p) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            x0 = ld(p, 0);
+            x1 = ld(p, 1);
+        }
+    }
+}
+
+template <typename T, bool COH>
+__device__ __forceinline__ void fast_attn_head(const FastFusedArgs<T>& a, int r, int h, int lane,
+                                               unsigned long long (&tz)[7]) {
+    const int hd = a.hd, g = a.nh / a.nkv, kvh = h / g, cpos = a.cpos, half = hd >> 1;
+    const T* raw = a.qkv + (size_t)r * a.ldqkv;
+    const float* tab = a.rope + (size_t)cpos * hd;
+    const int slot = a.row_slot[r];
+    float q0[2], q1[2], k0[2], k1[2], v0[2], v1[2], qw0[2], qw1[2], kw0[2], kw1[2], c_[2], s_[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int p = lane + 64 * u;
+        const bool ok = p < half;
+        const int pp = ok ? p : 0;
+        ld_pair<T, COH>(raw + (size_t)h * hd + 2 * pp, q0[u], q1[u]);
+        ld_pair<T, COH>(raw + (size_t)(a.nh + kvh) * hd + 2 * pp, k0[u], k1[u]);
+        ld_pair<T, COH>(raw + (size_t)(a.nh + a.nkv + kvh) * hd + 2 * pp, v0[u], v1[u]);
+        qw0[u] = a.qk_norm ? ld(a.qn, 2 * pp) : 1.f;
+        qw1[u] = a.qk_norm ? ld(a.qn, 2 * pp + 1) : 1.f;
+        kw0[u] = a.qk_norm ? ld(a.kn, 2 * pp) : 1.f;
+        kw1[u] = a.qk_norm ? ld(a.kn, 2 * pp + 1) : 1.f;
+        c_[u] = tab[2 * pp];
+        s_[u] = tab[2 * pp + 1];
+        if (!ok) q0[u] = q1[u] = k0[u] = k1[u] = v0[u] = v1[u] = 0.f;
+    }
+    const size_t base = (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
+    T* kc = a.kc + base;
+    T* vc = a.vc + base;
+    // cached rows j < cpos: the lane's two pairs of each
+    float K0[FAST_ATTN_MAXJ][2], K1[FAST_ATTN_MAXJ][2], V0[FAST_ATTN_MAXJ][2], V1[FAST_ATTN_MAXJ][2];
+#pragma unroll
+    for (int j = 0; j < FAST_ATTN_MAXJ; ++j) {
+        if (j < cpos) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int p = lane + 64 * u;
+                const int pp = p < half ? p : 0;
+                ld_pair<T, false>(kc + (size_t)j * hd + 2 * pp, K0[j][u], K1[j][u]);
+                ld_pair<T, false>(vc + (size_t)j * hd + 2 * pp, V0[j][u], V1[j][u]);
+                if (p >= half) K0[j][u] = K1[j][u] = V0[j][u] = V1[j][u] = 0.f;
+            }
+        }
+    }
+    if (a.dbg) tz[1] = __builtin_amdgcn_s_memrealtime();
+    // qk-norm (fp32 incl. weight, one rounding) + RoPE (bf16 table, rounded)
+    auto prep = [&](float (&x0)[2], float (&x1)[2], const float (&w0)[2], const float (&w1)[2], bool norm) {
+        if (norm) {
+            float ss = 0.f;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) ss += x0[u] * x0[u] + x1[u] * x1[u];
+            ss = wave_sum(ss);
+            const float rs = 1.0f / sqrtf(ss / (float)hd + a.eps);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                x0[u] = rnd<T>((x0[u] * rs) * w0[u]);
+                x1[u] = rnd<T>((x1[u] * rs) * w1[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const float y0 = rnd<T>(x0[u] * c_[u] - x1[u] * s_[u]);
+            const float y1 = rnd<T>(x1[u] * c_[u] + x0[u] * s_[u]);
+            x0[u] = y0;
+            x1[u] = y1;
+        }
+    };
+    prep(q0, q1, qw0, qw1, a.qk_norm);
+    prep(k0, k1, kw0, kw1, a.qk_norm);
+    if (a.dbg) tz[2] = __builtin_amdgcn_s_memrealtime();
+    if (h == kvh * g) {  // first q head of the group stores the new k / v
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            if (p < half) {
+                st(kc + (size_t)cpos * hd, 2 * p, k0[u]);
+                st(kc + (size_t)cpos * hd, 2 * p + 1, k1[u]);
+                st(vc + (size_t)cpos * hd, 2 * p, v0[u]);
+                st(vc + (size_t)cpos * hd, 2 * p + 1, v1[u]);
+            }
+        }
+    }
+    // scores round(round(q.k) * scale), softmax, probabilities rounded (fast SDPA path)
+    float sc[FAST_ATTN_MAXJ + 1];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j <= FAST_ATTN_MAXJ; ++j) {
+        if (j > cpos) break;
+        float d = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const float a0 = j < cpos ? K0[j < FAST_ATTN_MAXJ ? j : 0][u] : k0[u];
+            const float a1 = j < cpos ? K1[j < FAST_ATTN_MAXJ ? j : 0][u] : k1[u];
+            d += q0[u] * a0 + q1[u] * a1;
+        }
+        d = wave_sum(d);
+        sc[j] = rnd<T>(rnd<T>(d) * a.scale);
+        mx = fmaxf(mx, sc[j]);
+    }
+    if (a.dbg) tz[3] = __builtin_amdgcn_s_memrealtime();
+    float den = 0.f;
+#pragma unroll
+    for (int j = 0; j <= FAST_ATTN_MAXJ; ++j) {
+        if (j > cpos) break;
+        sc[j] = expf(sc[j] - mx);
+        den += sc[j];
+    }
+    float o0[2] = {0.f, 0.f}, o1[2] = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j <= FAST_ATTN_MAXJ; ++j) {
+        if (j > cpos) break;
+        const float p = rnd<T>(sc[j] / den);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            o0[u] += p * (j < cpos ? V0[j < FAST_ATTN_MAXJ ? j : 0][u] : v0[u]);
+            o1[u] += p * (j < cpos ? V1[j < FAST_ATTN_MAXJ ? j : 0][u] : v1[u]);
+        }
+    }
+    T* out = a.out + (size_t)r * a.nh * hd + (size_t)h * hd;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int p = lane + 64 * u;
+        if (p < half) {
+            st(out, 2 * p, o0[u]);
+            st(out, 2 * p + 1, o1[u]);
+        }
+    }
+}

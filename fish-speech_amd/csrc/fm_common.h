@@ -17,12 +17,9 @@ template <> struct is_bf16<bf16_t> { static constexpr bool value = true; };
 
 __device__ __forceinline__ float bf2f(bf16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 
-// round-to-nearest-even fp32 -> bf16 bits, NaN stays NaN
-__device__ __forceinline__ bf16_t f2bf(float x) {
-    uint32_t u = __float_as_uint(x);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40u);
-    return (bf16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-}
+// round-to-nearest-even fp32 -> bf16 bits, NaN stays NaN: gfx950's v_cvt_pk_bf16_f32 (one VALU
+// op, no NaN branch)
+__device__ __forceinline__ bf16_t f2bf(float x) { return __builtin_bit_cast(bf16_t, static_cast<__bf16>(x)); }
 __device__ __forceinline__ float bfround(float x) { return bf2f(f2bf(x)); }
 
 template <typename T> __device__ __forceinline__ float rnd(float x) {
@@ -55,6 +52,18 @@ template <typename T> __device__ __forceinline__ void load8(const T* p, float (&
         for (int j = 0; j < 4; ++j) { o[j] = a[j]; o[4 + j] = b[j]; }
     }
 }
+
+// developer phase timestamps: one 8-word record {tag << 32 | aux, t0..t6} per call
+__device__ __forceinline__ void dbg_record(unsigned long long* dbg, unsigned tag, unsigned aux,
+                                           const unsigned long long (&t)[7]) {
+    const unsigned long long slot = atomicAdd(dbg, 1ull);
+    if (slot < (1ull << 20)) {
+        unsigned long long* q = dbg + 8 + slot * 8;
+        q[0] = ((unsigned long long)tag << 32) | aux;
+        for (int z = 0; z < 7; ++z) q[1 + z] = t[z];
+    }
+}
+#define DBG_TS(arr, n) if (a.dbg) arr[n] = __builtin_amdgcn_s_memrealtime();
 
 // ---- wave (64-lane) reductions ------------------------------------------------------------
 // DPP lane exchanges inside each 16-lane row (quad xor 1, quad xor 2, half-row mirror, row

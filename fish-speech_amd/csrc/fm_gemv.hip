@@ -18,6 +18,8 @@
 // out first (one round trip: x slice, norm weight, tile sums of squares), then the weight ring,
 // then the LDS staging, which therefore overlaps the weight flight.
 #include "fm_kernels.h"
+#include "fm_runtime.h"
+#include "fm_attn_dev.h"
 
 template <typename T> struct GFrag;
 template <> struct GFrag<bf16_t> {
@@ -91,7 +93,7 @@ constexpr int GEMV_PRE = 8;   // (row, chunk) items of X preloaded per thread be
 
 // WPB waves per block share one 16-row tile, each streaming a contiguous run of its k-steps.
 template <typename T, int PRO, int EPI, bool NT, int U, int WPB>
-__global__ __launch_bounds__(WPB * 64) void gemv_kernel(GemvArgs<T> a) {
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(3))) void gemv_kernel(GemvArgs<T> a) {
     using G = GFrag<T>;
     constexpr int NACC = (EPI == EPI_SWIGLU) ? 2 : 1;
     constexpr int NTH = WPB * 64;
@@ -110,6 +112,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(GemvArgs<T> a) {
     float* rsl = fin + 16 * R;                        // [8 waves][GEMV_RMAX] PRO_PRENORM 1/rms
 
     const unsigned long long ts0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long tsA = 0, tsB = 0;  // PRO_PRENORM: tile sums staged / X' written
     const int r = lane & 15, g = lane >> 4;
     const int S = a.K >> 5, Sb = Kb >> 5, sb0 = ks * Sb;
     const int wa = (wave * Sb) / WPB, wb = ((wave + 1) * Sb) / WPB, nmy = wb - wa;
@@ -192,35 +195,42 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(GemvArgs<T> a) {
                 if constexpr (PRO == PRO_PRENORM) wc[q] = load_c8(a.nw + kbeg + 8 * cc);
             }
         }
-        float ssl[GEMV_RMAX];
+        // PRO_PRENORM: the [K/16][R] tile sums of squares, flattened over the block's threads,
+        // GEMV_SSQ loads each, unconditional (clamped) and issued before the weight ring so their
+        // wait does not queue behind weight bytes (a load under a branch makes the compiler drain
+        // vmcnt(0) right there, before the ring is even issued)
+        constexpr int GEMV_SSQ = 2;
+        const int nss = (a.K >> 4) * R;
+        float ssv[PRO == PRO_PRENORM ? GEMV_SSQ : 1];
         if constexpr (PRO == PRO_PRENORM) {
-            // K <= 4096 -> <= 4 tile sums per lane and row; unconditional (clamped) loads so all
-            // of them are in flight together (a load under a branch costs a full vmcnt drain)
-            const int nt = a.K >> 4;
 #pragma unroll
-            for (int rr = 0; rr < GEMV_RMAX; ++rr) {
-                ssl[rr] = 0.f;
-                if (rr < R) {
-                    float v[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int t = lane + 64 * j;
-                        v[j] = a.ss_in[(size_t)(t < nt ? t : nt - 1) * R + rr];
-                    }
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) ssl[rr] += (lane + 64 * j < nt) ? v[j] : 0.f;
-                }
+            for (int q = 0; q < GEMV_SSQ; ++q) {
+                const int e = threadIdx.x + NTH * q;
+                ssv[q] = a.ss_in[e < nss ? e : nss - 1];
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) issue(u, u);
         if constexpr (PRO == PRO_PRENORM) {
-            // per-row 1/rms in this wave's LDS slot (a register array indexed by the runtime row
-            // would be spilled to scratch: one more memory round trip per read)
+            // stage the tile sums in `red` (free until the cross-wave reduction), then every wave
+            // reduces each row's sums itself: per-row 1/rms in the wave's LDS slot (a register
+            // array indexed by the runtime row would be spilled to scratch)
+#pragma unroll
+            for (int q = 0; q < GEMV_SSQ; ++q) {  // unconditional: the clamped tail re-stores the
+                const int e = threadIdx.x + NTH * q;  // last sum (same value), and no branch lets
+                red[e < nss ? e : nss - 1] = ssv[q];  // the compiler sink a load past the ring
+            }
+            for (int e = threadIdx.x + NTH * GEMV_SSQ; e < nss; e += NTH) red[e] = a.ss_in[e];  // R * K large
+            __syncthreads();
+            if (a.dbg) tsA = __builtin_amdgcn_s_memrealtime();
+            const int nt = a.K >> 4;
             float* rsw = rsl + wave * GEMV_RMAX;
 #pragma unroll
             for (int rr = 0; rr < GEMV_RMAX; ++rr) {
-                const float v = rr < R ? 1.0f / sqrtf(wave_sum(ssl[rr]) / (float)a.K + a.eps) : 0.f;
+                if (rr >= R) break;
+                float sl = 0.f;
+                for (int t = lane; t < nt; t += 64) sl += red[t * R + rr];
+                const float v = 1.0f / sqrtf(wave_sum(sl) / (float)a.K + a.eps);
                 if (lane == 0) rsw[rr] = v;
             }
             __builtin_amdgcn_wave_barrier();
@@ -230,12 +240,12 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(GemvArgs<T> a) {
                 c8_to_f(xq, xv);
                 c8_to_f(wq, wv);
                 const float rs = rsw[rr];
+                C8<T> o;
+                T* ov = reinterpret_cast<T*>(&o);
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const float xn = rnd<T>(rnd<T>(xv[u] * rs) * wv[u]);
-                    st(xs, (size_t)rr * xstride + 8 * cc + u, xn);
-                    if (writer) st(a.xn_out, (size_t)rr * a.ldxo + kbeg + 8 * cc + u, xn);
-                }
+                for (int u = 0; u < 8; ++u) st(ov, u, rnd<T>(xv[u] * rs) * wv[u]);
+                *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) = o;  // one 16/32-B store
+                if (writer) *reinterpret_cast<C8<T>*>(a.xn_out + (size_t)rr * a.ldxo + kbeg + 8 * cc) = o;
             };
 #pragma unroll
             for (int q = 0; q < GEMV_PRE; ++q) {
@@ -246,6 +256,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(GemvArgs<T> a) {
                 const int rr = it / nch, cc = it - rr * nch;
                 put(rr, cc, load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc), load_c8(a.nw + kbeg + 8 * cc));
             }
+            if (a.dbg) tsB = __builtin_amdgcn_s_memrealtime();
         } else {
 #pragma unroll
             for (int q = 0; q < GEMV_PRE; ++q) {
@@ -302,7 +313,9 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(GemvArgs<T> a) {
                 q[2] = ts1;
                 q[3] = ts2;
                 q[4] = t3;
-                q[5] = q[6] = q[7] = 0;
+                q[5] = tsA;
+                q[6] = tsB;
+                q[7] = 0;
             }
         }
     };
@@ -334,6 +347,16 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(GemvArgs<T> a) {
             const size_t yi = (size_t)col * a.ldy + n;
             if constexpr (EPI == EPI_STORE) {
                 st(a.Y, yi, v0);
+            } else if constexpr (EPI == EPI_QKVATT) {  // write-through: read back by another block
+                if constexpr (sizeof(T) == 2) {
+                    const float rv = rnd<T>(v0);
+                    __hip_atomic_store(reinterpret_cast<unsigned short*>(a.Y) + yi,
+                                       (unsigned short)(__float_as_uint(rv) >> 16), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    __hip_atomic_store(reinterpret_cast<float*>(a.Y) + yi, v0, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
             } else if constexpr (EPI == EPI_SWIGLU) {
                 const float ga = rnd<T>(v0), ub = rnd<T>(v1);
                 st(a.Y, yi, rnd<T>(silu_g(ga)) * ub);
@@ -341,6 +364,36 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(GemvArgs<T> a) {
                 a.Yf[yi] = rnd<T>(v0);
             }
         }
+    }
+    if constexpr (EPI == EPI_QKVATT) {
+        // Ticket on the tile's kv group (its q heads, k head and v head rows); the group's last
+        // block runs the group's fast-model attention, one wave per (row, q head).  Hand-off in the
+        // write-through form: sc1 stores drained by every wave, relaxed agent ticket, sc1 loads of
+        // the raw projections in fast_attn_head<T, true>.
+        const FastFusedArgs<T>& at = a.att;
+        const int hd = at.hd, g = at.nh / at.nkv, qr = at.nh * hd, kr = at.nkv * hd;
+        const int grp = n0 < qr ? n0 / (g * hd) : (n0 < qr + kr ? (n0 - qr) / hd : (n0 - qr - kr) / hd);
+        const int need = (g + 2) * hd / 16;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int t = __hip_atomic_fetch_add(a.att_tickets + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = t == need - 1;
+            if (last) __hip_atomic_store(a.att_tickets + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            flag[0] = last;
+        }
+        __syncthreads();
+        if (flag[0]) {
+            unsigned long long tz[7] = {0, 0, 0, 0, 0, 0, 0};
+            if (a.dbg) tz[0] = __builtin_amdgcn_s_memrealtime();
+            for (int it = wave; it < R * g; it += WPB) fast_attn_head<T, true>(at, it / g, grp * g + it % g, lane, tz);
+            if (a.dbg && lane == 0) {
+                tz[4] = __builtin_amdgcn_s_memrealtime();
+                dbg_record(a.dbg, 0xFFFC, (unsigned)at.cpos, tz);
+            }
+        }
+        stamp();
+        return;
     }
     if constexpr (EPI == EPI_SLABFIN) {
         // The last-arriving K-slice block of this 16-column tile finalises the residual stream:
@@ -429,6 +482,8 @@ static void gemv_go(hipStream_t s, const GemvArgs<T>& a, int ksb) {
 }
 
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb) {
+    // PRO_PRENORM stages the [K/16][R] tile sums in the 256 * R floats of the reduction buffer
+    FMCHECK(pro != PRO_PRENORM || (a.K <= 4096 && a.R <= GEMV_RMAX), "PRO_PRENORM needs K <= 4096, R <= 8");
 #define GO(P, E)                                           \
     if (pro == P && epi == E) {                            \
         gemv_go<T, P, E>(s, a, ksb);                       \
@@ -437,6 +492,7 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
     GO(PRO_PLAIN, EPI_STORE) GO(PRO_PLAIN, EPI_SLABFIN) GO(PRO_PLAIN, EPI_F32) GO(PRO_PLAIN, EPI_SLAB)
     GO(PRO_NORM, EPI_STORE) GO(PRO_NORM, EPI_SWIGLU) GO(PRO_NORM, EPI_F32)
     GO(PRO_PRENORM, EPI_STORE) GO(PRO_PRENORM, EPI_SWIGLU) GO(PRO_PRENORM, EPI_F32)
+    GO(PRO_NORM, EPI_QKVATT) GO(PRO_PRENORM, EPI_QKVATT)
 #undef GO
 }
 
@@ -669,6 +725,16 @@ __global__ __launch_bounds__(512) void gemv_sk_kernel(GemvArgs<T> a) {
             const size_t yi = (size_t)col * a.ldy + n;
             if constexpr (EPI == EPI_STORE) {
                 st(a.Y, yi, v0);
+            } else if constexpr (EPI == EPI_QKVATT) {  // write-through: read back by another block
+                if constexpr (sizeof(T) == 2) {
+                    const float rv = rnd<T>(v0);
+                    __hip_atomic_store(reinterpret_cast<unsigned short*>(a.Y) + yi,
+                                       (unsigned short)(__float_as_uint(rv) >> 16), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    __hip_atomic_store(reinterpret_cast<float*>(a.Y) + yi, v0, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
             } else if constexpr (EPI == EPI_SWIGLU) {
                 st(a.Y, yi, rnd<T>(silu_g(rnd<T>(v0))) * rnd<T>(v1));
             } else if constexpr (EPI == EPI_F32) {

@@ -111,8 +111,28 @@ void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* 
 
 // ---- decode weight-streaming path (fm_gemv.hip), R <= 8 rows --------------------------------
 enum { PRO_PLAIN = 0, PRO_NORM = 1, PRO_PRENORM = 3 };
-enum { EPI_SLAB = 4, EPI_SLABFIN = 5 };
+enum { EPI_SLAB = 4, EPI_SLABFIN = 5, EPI_QKVATT = 6 };
+// EPI_QKVATT (fast model, cpos < 16, whole K per block): the QKV GEMV stores its tile write-through,
+// takes a ticket on the tile's kv group, and the group's last-arriving block runs the fast-model
+// attention of that group's q heads (fm_attn_dev.h) -- no separate attention launch.
 
+template <typename T> struct FastFusedArgs {
+    const T* qkv;
+    int ldqkv;
+    const int* row_slot;
+    int nh, nkv, hd, qk_norm;
+    float eps;
+    const T* qn;
+    const T* kn;
+    const float* rope;   // [C][hd/2][2]
+    T* kc;
+    T* vc;
+    size_t slot_stride, layer_off;
+    int S, cpos;         // S = num_codebooks (fast cache length)
+    float scale;
+    T* out;              // [R][nh*hd]
+    unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
+};
 template <typename T> struct GemvArgs {
     const T* W;
     const T* W2;             // EPI_SWIGLU: w3
@@ -142,6 +162,8 @@ template <typename T> struct GemvArgs {
     long long part_cap;      //   floats
     int maxc;                // stream-K: contributor slots per tile (set by the launcher)
     int pro_exp;             // EXPERIMENT knob (see FmTuning)
+    FastFusedArgs<T> att;    // EPI_QKVATT: the attention the group's last block runs
+    int* att_tickets;        // EPI_QKVATT: per-kv-group arrival counters (zero between launches)
 };
 // developer knobs for the decode GEMV (fm_tune): weight load policy and split-K policy
 struct FmTuning {
@@ -152,6 +174,7 @@ struct FmTuning {
     int gemv_sk_bpc = 1;     // stream-K blocks per CU
     int pro_exp = 0;         // EXPERIMENT: 1 skip tile-sum loads, 2 skip norm-weight loads, 3 both
     int sampler_fast = 1;    // 1: two-stage register top-K sampler, 0: LDS radix-select sampler
+    int attn_fuse = 0;       // 1: fast-model attention fused into the QKV GEMV's tail (EPI_QKVATT)
     int ksb_blocks = 512;    // split K until the grid has at least this many blocks
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
@@ -186,22 +209,7 @@ template <typename T> struct AttnDecArgs {
     int cap;             // rows per block
     int* cnt;            // [R][nkv] arrival tickets (zeroed at allocation, reset by the last block)
     T* out;              // [R][nh*hd]
-};
-template <typename T> struct FastFusedArgs {
-    const T* qkv;
-    int ldqkv;
-    const int* row_slot;
-    int nh, nkv, hd, qk_norm;
-    float eps;
-    const T* qn;
-    const T* kn;
-    const float* rope;   // [C][hd/2][2]
-    T* kc;
-    T* vc;
-    size_t slot_stride, layer_off;
-    int S, cpos;         // S = num_codebooks (fast cache length)
-    float scale;
-    T* out;              // [R][nh*hd]
+    unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
 };
 template <typename T> void launch_attn_decode(hipStream_t s, const AttnDecArgs<T>& a, int R);
 // decode attention for the small-batch path (see fm_attn.hip): a.cap rows per block, a.maxsplit =

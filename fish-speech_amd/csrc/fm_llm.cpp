@@ -94,6 +94,7 @@ struct fm_llm {
     void *xl = nullptr, *xnl = nullptr, *fx = nullptr, *fh = nullptr, *fxn = nullptr;
     float *part = nullptr, *logits = nullptr, *flogits = nullptr;
     int* attn_cnt = nullptr;
+    int* att_tickets = nullptr;           // EPI_QKVATT per-kv-group arrival counters
     float *ssX = nullptr, *ssH = nullptr;  // per-16-column tile sums of squares of the residual rows
     int* tickets = nullptr;               // EPI_SLABFIN / stream-K arrival counters (zero between launches)
     float* skpart = nullptr;              // stream-K partial tiles
@@ -298,6 +299,15 @@ template <typename T> struct Run {
                      const int32_t* xidx, int xcol, void* xb, void* hb, bool is_fast, int cpos, int layer,
                      const KsbPlan& kp) {
         const int C1 = m->C1;
+        const float scale = 1.0f / sqrtf((float)d.hd);
+        FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), m->frame_slot, d.nh, d.nkv, d.hd, d.qk_norm,
+                            m->c.norm_eps, (const T*)L.qn, (const T*)L.kn, m->frope, (T*)m->fkc,
+                            (T*)m->fvc, m->fslot_stride, (size_t)layer * m->flayer_stride, m->C, cpos,
+                            scale, (T*)m->att};
+        fa.dbg = fm_tuning().dbg;
+        // fast model: attention runs in the QKV GEMV's tail (EPI_QKVATT) when it fits the tail
+        const bool fuse = is_fast && fm_tuning().attn_fuse && cpos < 16 && d.nkv <= 256 && d.hd <= 256 &&
+                          d.hd % 16 == 0 && d.nh % d.nkv == 0;
         // QKV (+ attention_norm)
         {
             GemvArgs<T> a = ga();
@@ -309,21 +319,25 @@ template <typename T> struct Run {
             a.K = d.dim;
             a.Y = (T*)m->qkv;
             a.ldy = d.nqkv();
+            const int epi = fuse ? EPI_QKVATT : EPI_STORE;
+            if (fuse) {
+                a.att = fa;
+                a.att_tickets = m->att_tickets;
+            }
             if (first) {
                 a.X = (const T*)x_in;
                 a.ldx = ldx_in;
                 a.xidx = xidx;
                 a.xidx_ld = C1;
                 a.xidx_col = xcol;
-                gemv(a, PRO_NORM, EPI_STORE, 1, "linear");
+                gemv(a, PRO_NORM, epi, 1, "linear");
             } else {
                 a.X = (const T*)xb;
                 a.ldx = d.dim;
                 a.ss_in = m->ssX;
-                gemv(a, PRO_PRENORM, EPI_STORE, 1, "linear");
+                gemv(a, PRO_PRENORM, epi, 1, "linear");
             }
         }
-        const float scale = 1.0f / sqrtf((float)d.hd);
         if (!is_fast) {
             AttnDecArgs<T> aa{(const T*)m->qkv, d.nqkv(), m->frame_slot, m->frame_pos, d.nh, d.nkv, d.hd,
                               d.qk_norm, m->c.norm_eps, (const T*)L.qn, (const T*)L.kn, m->rope, (T*)m->kc,
@@ -332,13 +346,10 @@ template <typename T> struct Run {
             aa.cap = attn2_cap(d.hd, d.nh / d.nkv, E);
             aa.maxsplit = FM_CEIL(m->S, aa.cap);
             aa.cnt = m->attn_cnt;
+            aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
             m->prof.run(s, "attn", 0, 0, [&] { launch_attn_decode2<T>(s, aa, n); });
-        } else {
-            FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), m->frame_slot, d.nh, d.nkv, d.hd, d.qk_norm,
-                                m->c.norm_eps, (const T*)L.qn, (const T*)L.kn, m->frope, (T*)m->fkc,
-                                (T*)m->fvc, m->fslot_stride, (size_t)layer * m->flayer_stride, m->C, cpos,
-                                scale, (T*)m->att};
+        } else if (!fuse) {
             m->prof.run(s, "attn", 0, 0, [&] {
                 if (cpos < 16 && d.hd <= 256)
                     launch_fast_attn2<T>(s, fa, n);
@@ -766,7 +777,8 @@ static void finalize(fm_llm* m) {
     m->fxn = m->dalloc((size_t)n * dmax * E);
     m->maxsplit = FM_CEIL(m->S, ATTN_SPLIT);
     m->part = (float*)m->dalloc((size_t)R * d.nh * std::max(m->maxsplit, FM_CEIL(m->S, 16)) * (d.hd + 2) * 4, false);
-    m->attn_cnt = (int*)m->dalloc((size_t)R * d.nkv * sizeof(int), false);
+    m->attn_cnt = (int*)m->dalloc((size_t)R * d.nkv * sizeof(int));  // tickets: zeroed
+    m->att_tickets = (int*)m->dalloc(256 * sizeof(int));
     m->ssX = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
     m->ssH = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
     {
@@ -1208,6 +1220,8 @@ int fm_tune(const char* key, int value) {
             t.gemv_u = value;
         } else if (k == "sampler_fast") {
             t.sampler_fast = value != 0;
+        } else if (k == "attn_fuse") {
+            t.attn_fuse = value != 0;
         } else if (k == "pro_exp") {
             t.pro_exp = value;
         } else if (k == "gemv_sk") {

@@ -11,8 +11,13 @@ sys.path.insert(0, os.path.join(ROOT, "fish-speech_amd"))
 from fishmi.config import S2_PRO_CONFIG, S2_PRO_IM_END_ID, DualARConfig  # noqa: E402
 from fishmi.llm import DualARModel  # noqa: E402
 
-frames = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-B = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+args = [x for x in sys.argv[1:] if "=" not in x]
+frames = int(args[0]) if len(args) > 0 else 64
+B = int(args[1]) if len(args) > 1 else 1
+from fishmi import native  # noqa: E402
+for kv in (x for x in sys.argv[1:] if "=" in x):  # developer knobs: key=value (fm_tune)
+    k, v = kv.split("=")
+    native.tune(k, int(v))
 cfg = DualARConfig._from_fish_qwen3_omni(S2_PRO_CONFIG)
 cfg.im_end_id = S2_PRO_IM_END_ID
 cfg.max_seq_len = 1024

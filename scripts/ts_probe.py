@@ -38,6 +38,16 @@ if len(smp):
           "bar1+cand+bar2", round(d[3], 2), "rank", round(d[4], 2), "-", round(d[5], 2))
     lo = (smp[:, 0].astype(np.int64) & 0xFFFF)
     print("sampler candidates: mean", round(lo.mean(), 1), "max", lo.max(), "overflow", int(((smp[:, 0].astype(np.int64) >> 16) & 1).sum()))
+for tag, name, labels in ((0xFFFE, "fast_attn2", ("load", "prep", "scores", "pv+store")),
+                          (0xFFFC, "qkv tail attn", ("load", "prep", "scores", "pv+store")),
+                          (0xFFFD, "attn_decode2", ("kv load", "q prep", "scores", "softmax", "pv", "rec"))):
+    a = rec[(rec[:, 0] >> 32) == tag].astype(np.float64)
+    if len(a):
+        nz = [i for i in range(1, 8) if a[:, i].max() > 0]
+        d = np.diff(a[:, nz], axis=1).mean(axis=0) / 100.0
+        aux = a[:, 0].astype(np.int64) & 0xFFFFFFFF
+        print(f"{name} phases (us):", " ".join(f"{l} {v:.2f}" for l, v in zip(labels, d)),
+              "| blocks", len(a), "aux mean", round(float(aux.mean()), 1))
 if os.environ.get("TS_SK"):
     for tag in sorted(set((rec[:, 0] >> 32).tolist())):
         a = rec[(rec[:, 0] >> 32) == tag].astype(np.float64)
@@ -49,6 +59,8 @@ launches = []
 cur = None
 for r in rec:
     tag = int(r[0]) >> 32
+    if tag >= 0xFFF0:
+        continue
     if cur is None or tag != cur["tag"] or r[1] > cur["end"]:
         cur = {"tag": tag, "rows": [], "end": 0}
         launches.append(cur)
@@ -65,6 +77,16 @@ for tag, v in sorted(by.items(), key=lambda kv: -sum(x[0] for x in kv[1])):
     a = np.array(v, dtype=np.float64) / 100.0  # 100 MHz ticks -> us
     print(f"{tag:7d} {len(v):6d} {v[0][5]:6d} {a[:, 0].mean():7.2f} {a[:, 1].mean():6.2f} {a[:, 2].mean():6.2f} "
           f"{a[:, 3].mean():6.2f} {a[:, 4].mean():6.2f} {a[:, 6].mean():6.2f}")
+for L in launches[:0]:
+    pass
+pre = defaultdict(list)
+for L in launches:
+    a = np.array(L["rows"]).astype(np.float64)
+    if a[:, 5].min() > 0:
+        pre[L["tag"]].append(np.mean(a[:, [5, 6, 2]] - a[:, [1, 5, 6]], axis=0) / 100.0)
+for tag, v in pre.items():
+    v = np.mean(v, axis=0)
+    print(f"PRENORM N={tag}: loads+ss staged {v[0]:.2f}  rms+X' {v[1]:.2f}  barrier {v[2]:.2f} us")
 if os.environ.get("TS_DETAIL"):
     tag = int(os.environ["TS_DETAIL"])
     L = [x for x in launches if x["tag"] == tag][3]
