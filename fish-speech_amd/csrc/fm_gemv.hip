@@ -90,10 +90,18 @@ template <typename T> __device__ __forceinline__ void c8_to_f(const C8<T>& c, fl
 
 constexpr int GEMV_RMAX = 8;  // rows (streams) of the small-batch path
 constexpr int GEMV_PRE = 8;   // (row, chunk) items of X preloaded per thread before the weight ring
+// occupancy target (waves per SIMD) of the tiled GEMV: the interleaved W1||W3 grid (1216 blocks of
+// 4 waves) is resident at 5; the others need 3 (enough for their grids)
+constexpr int gemv_wpe(int pro, int epi) { return pro == PRO_PRENORM && epi == EPI_SWIGLU8 ? 5 : 3; }
 
 // WPB waves per block share one 16-row tile, each streaming a contiguous run of its k-steps.
 template <typename T, int PRO, int EPI, bool NT, int U, int WPB>
-__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(3))) void gemv_kernel(GemvArgs<T> a) {
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(gemv_wpe(PRO, EPI))))
+void gemv_kernel(GemvArgs<T> a) {
+    // X items preloaded per thread ahead of the weight ring: PRO_PRENORM's operand is one dim-wide
+    // row per stream (2 items per thread at R = 1), and its register budget is what lets the
+    // 1216-block W1||W3 grid stay resident (5 waves per SIMD)
+    constexpr int PRE_N = PRO == PRO_PRENORM ? 3 : GEMV_PRE;
     using G = GFrag<T>;
     constexpr int NACC = (EPI == EPI_SWIGLU) ? 2 : 1;
     constexpr int NTH = WPB * 64;
@@ -182,12 +190,12 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(3))) v
 #pragma unroll
         for (int u = 0; u < U; ++u) issue(u, u);
     } else {
-        // PRO_PLAIN / PRO_PRENORM: (row, 8-element chunk) items of the slice, up to GEMV_PRE per
+        // PRO_PLAIN / PRO_PRENORM: (row, 8-element chunk) items of the slice, up to PRE_N per
         // thread preloaded ahead of the weight ring (the rest, large R x Kb only, after it)
         const int nch = Kb >> 3, nitem = R * nch;
-        C8<T> xc[GEMV_PRE], wc[PRO == PRO_PRENORM ? GEMV_PRE : 1];
+        C8<T> xc[PRE_N], wc[PRO == PRO_PRENORM ? PRE_N : 1];
 #pragma unroll
-        for (int q = 0; q < GEMV_PRE; ++q) {
+        for (int q = 0; q < PRE_N; ++q) {
             const int it = threadIdx.x + NTH * q;
             if (it < nitem) {
                 const int rr = it / nch, cc = it - rr * nch;
@@ -248,25 +256,25 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(3))) v
                 if (writer) *reinterpret_cast<C8<T>*>(a.xn_out + (size_t)rr * a.ldxo + kbeg + 8 * cc) = o;
             };
 #pragma unroll
-            for (int q = 0; q < GEMV_PRE; ++q) {
+            for (int q = 0; q < PRE_N; ++q) {
                 const int it = threadIdx.x + NTH * q;
                 if (it < nitem) put(it / nch, it - (it / nch) * nch, xc[q], wc[q]);
             }
-            for (int it = threadIdx.x + NTH * GEMV_PRE; it < nitem; it += NTH) {
+            for (int it = threadIdx.x + NTH * PRE_N; it < nitem; it += NTH) {
                 const int rr = it / nch, cc = it - rr * nch;
                 put(rr, cc, load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc), load_c8(a.nw + kbeg + 8 * cc));
             }
             if (a.dbg) tsB = __builtin_amdgcn_s_memrealtime();
         } else {
 #pragma unroll
-            for (int q = 0; q < GEMV_PRE; ++q) {
+            for (int q = 0; q < PRE_N; ++q) {
                 const int it = threadIdx.x + NTH * q;
                 if (it < nitem) {
                     const int rr = it / nch, cc = it - rr * nch;
                     *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) = xc[q];
                 }
             }
-            for (int it = threadIdx.x + NTH * GEMV_PRE; it < nitem; it += NTH) {  // large R x Kb
+            for (int it = threadIdx.x + NTH * PRE_N; it < nitem; it += NTH) {  // large R x Kb
                 const int rr = it / nch, cc = it - rr * nch;
                 *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) =
                     load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc);
@@ -321,6 +329,22 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(3))) v
     };
 
     // ---------------- epilogue: 16 rows x R cols -----------------------------------------------
+    if constexpr (EPI == EPI_SWIGLU8) {  // rows 0-7 gate, 8-15 up of the same 8 outputs
+        for (int o = threadIdx.x; o < 8 * R; o += NTH) {
+            const int row = o / R, col = o - row * R;
+            const int n = blockIdx.x * 8 + row;
+            if (n >= (a.N >> 1)) continue;
+            float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+            for (int w = 0; w < WPB; ++w) {
+                v0 += red[(w * 16 + row) * R + col];
+                v1 += red[(w * 16 + row + 8) * R + col];
+            }
+            st(a.Y, (size_t)col * a.ldy + n, rnd<T>(silu_g(rnd<T>(v0))) * rnd<T>(v1));
+        }
+        stamp();
+        return;
+    }
     for (int o = threadIdx.x; o < 16 * R; o += NTH) {
         const int row = o / R, col = o - row * R;
         const int n = n0 + row;
@@ -492,7 +516,7 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
     GO(PRO_PLAIN, EPI_STORE) GO(PRO_PLAIN, EPI_SLABFIN) GO(PRO_PLAIN, EPI_F32) GO(PRO_PLAIN, EPI_SLAB)
     GO(PRO_NORM, EPI_STORE) GO(PRO_NORM, EPI_SWIGLU) GO(PRO_NORM, EPI_F32)
     GO(PRO_PRENORM, EPI_STORE) GO(PRO_PRENORM, EPI_SWIGLU) GO(PRO_PRENORM, EPI_F32)
-    GO(PRO_NORM, EPI_QKVATT) GO(PRO_PRENORM, EPI_QKVATT)
+    GO(PRO_NORM, EPI_QKVATT) GO(PRO_PRENORM, EPI_QKVATT) GO(PRO_PRENORM, EPI_SWIGLU8)
 #undef GO
 }
 

@@ -9,6 +9,9 @@ enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_F32 = 3 };
 // [ceil(N/16)][K/32] blocks of 512 elements, each block holding one MFMA 16x32 A-fragment in
 // lane order (bf16: lane l's 8 elements at l*8; fp32: elements 0-3 at l*4, 4-7 at 256+l*4), so
 // every wave-load instruction reads 1 KB of contiguous memory.
+// act[r][j] = round(silu(t[r][16*(j/8) + j%8])) * t[r][16*(j/8) + 8 + j%8]: SwiGLU over the output of
+// the row-interleaved W1||W3 (batched path)
+template <typename T> void launch_swiglu_i8(hipStream_t s, const T* t, int ldt, T* act, int lda, int inter, int R);
 template <typename T> void launch_pack(hipStream_t s, const T* src, int N, int K, T* dst);
 
 template <typename T> struct LinearArgs {
@@ -111,7 +114,9 @@ void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* 
 
 // ---- decode weight-streaming path (fm_gemv.hip), R <= 8 rows --------------------------------
 enum { PRO_PLAIN = 0, PRO_NORM = 1, PRO_PRENORM = 3 };
-enum { EPI_SLAB = 4, EPI_SLABFIN = 5, EPI_QKVATT = 6 };
+enum { EPI_SLAB = 4, EPI_SLABFIN = 5, EPI_QKVATT = 6, EPI_SWIGLU8 = 7 };
+// EPI_SWIGLU8: W is the row-interleaved W1||W3 (each 16-row tile = 8 gate rows then the same 8 up
+// rows, see pack_w13 in fm_llm.cpp); a tile yields 8 SwiGLU outputs, N = 2 * intermediate.
 // EPI_QKVATT (fast model, cpos < 16, whole K per block): the QKV GEMV stores its tile write-through,
 // takes a ticket on the tile's kv group, and the group's last-arriving block runs the fast-model
 // attention of that group's q heads (fm_attn_dev.h) -- no separate attention launch.
@@ -174,6 +179,7 @@ struct FmTuning {
     int gemv_sk_bpc = 1;     // stream-K blocks per CU
     int pro_exp = 0;         // EXPERIMENT: 1 skip tile-sum loads, 2 skip norm-weight loads, 3 both
     int sampler_fast = 1;    // 1: two-stage register top-K sampler, 0: LDS radix-select sampler
+    int attn_cap = 32;       // slow decode attention rows per block cap (0: the LDS-budget maximum)
     int attn_fuse = 0;       // 1: fast-model attention fused into the QKV GEMV's tail (EPI_QKVATT)
     int ksb_blocks = 512;    // split K until the grid has at least this many blocks
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)

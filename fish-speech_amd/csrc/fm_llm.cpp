@@ -63,7 +63,7 @@ static int pick_ksb(int N, int K, int R, size_t esz) {
 
 struct LayerW {
     void *wqkv = nullptr, *bqkv = nullptr, *wo = nullptr, *bo = nullptr, *qn = nullptr, *kn = nullptr;
-    void *w1 = nullptr, *w3 = nullptr, *w2 = nullptr, *an = nullptr, *fn = nullptr;
+    void *w13 = nullptr, *w2 = nullptr, *an = nullptr, *fn = nullptr;  // w13: row-interleaved W1||W3
 };
 
 struct StackDims {
@@ -93,6 +93,7 @@ struct fm_llm {
          *act = nullptr;
     void *xl = nullptr, *xnl = nullptr, *fx = nullptr, *fh = nullptr, *fxn = nullptr;
     float *part = nullptr, *logits = nullptr, *flogits = nullptr;
+    void* act2 = nullptr;  // batched path: [R][2 * inter] output of the interleaved W1||W3
     int* attn_cnt = nullptr;
     int* att_tickets = nullptr;           // EPI_QKVATT per-kv-group arrival counters
     float *ssX = nullptr, *ssH = nullptr;  // per-16-column tile sums of squares of the residual rows
@@ -253,8 +254,11 @@ template <typename T> struct Run {
         m->prof.run(s, "norm", 0, 0, [&] {
             launch_rmsnorm<T>(s, (const T*)hb, d.dim, (const T*)L.fn, d.dim, eps, (T*)xnb, d.dim, R);
         });
-        linear(L.w1, L.w3, nullptr, xnb, d.dim, R, d.inter, d.dim, m->act, d.inter, nullptr, 0, nullptr,
-               EPI_SWIGLU, "linear");
+        linear(L.w13, nullptr, nullptr, xnb, d.dim, R, 2 * d.inter, d.dim, m->act2, 2 * d.inter, nullptr, 0,
+               nullptr, EPI_STORE, "linear");
+        m->prof.run(s, "other", 0, 0, [&] {
+            launch_swiglu_i8<T>(s, (const T*)m->act2, 2 * d.inter, (T*)m->act, d.inter, d.inter, R);
+        });
         linear(L.w2, nullptr, nullptr, m->act, d.inter, R, d.dim, d.inter, xb, d.dim, hb, d.dim, nullptr,
                EPI_RESID, "linear");
     }
@@ -344,6 +348,7 @@ template <typename T> struct Run {
                               (T*)m->vc, m->slot_stride, (size_t)layer * m->layer_stride, m->S,
                               m->maxsplit, scale, m->part};
             aa.cap = attn2_cap(d.hd, d.nh / d.nkv, E);
+            if (fm_tuning().attn_cap) aa.cap = std::min(aa.cap, fm_tuning().attn_cap);
             aa.maxsplit = FM_CEIL(m->S, aa.cap);
             aa.cnt = m->attn_cnt;
             aa.dbg = fm_tuning().dbg;
@@ -388,18 +393,17 @@ template <typename T> struct Run {
         // W1/W3 (+ ffn_norm) -> SwiGLU act
         {
             GemvArgs<T> a = ga();
-            a.W = (const T*)L.w1;
-            a.W2 = (const T*)L.w3;
+            a.W = (const T*)L.w13;
             a.nw = (const T*)L.fn;
             a.R = n;
-            a.N = d.inter;
+            a.N = 2 * d.inter;
             a.K = d.dim;
             a.X = (const T*)hb;
             a.ldx = d.dim;
             a.ss_in = m->ssH;
             a.Y = (T*)m->act;
             a.ldy = d.inter;
-            gemv(a, PRO_PRENORM, EPI_SWIGLU, 1, "linear");
+            gemv(a, PRO_PRENORM, EPI_SWIGLU8, 1, "linear");
         }
         // W2, split-K; finalises the block output x = h + w2(act) into xb and its sums of squares
         {
@@ -684,12 +688,44 @@ static void* pack_dev(fm_llm* m, const void* src, int rows, int cols) {
     return dst;
 }
 
+static bool is_ffn_w13(const std::string& n) {
+    auto ends = [&](const char* suf) {
+        const size_t L = strlen(suf);
+        return n.size() >= L && n.compare(n.size() - L, L, suf) == 0;
+    };
+    return ends("feed_forward.w1.weight") || ends("feed_forward.w3.weight");
+}
+
+// W1 [inter][dim] and W3 -> one packed [2*inter][dim] matrix whose 16-row tiles hold 8 rows of W1
+// then the same 8 rows of W3, so one GEMV tile (EPI_SWIGLU8) has both halves of 8 SwiGLU outputs and
+// the decode grid is 2*inter/16 single-matrix blocks.  The row-major W1/W3 are freed; their map
+// entries keep the shapes (the packed matrix hangs off the w1 entry).
+static void* pack_w13(fm_llm* m, const std::string& p, int inter, int dim) {
+    FMCHECK(inter % 8 == 0, "intermediate_size must be a multiple of 8");
+    DTensor& t1 = m->w.at(p + "feed_forward.w1.weight");
+    DTensor& t3 = m->w.at(p + "feed_forward.w3.weight");
+    const size_t E = m->esz, rb = (size_t)dim * E;
+    void* tmp = nullptr;
+    HIPCHK(hipMalloc(&tmp, 2 * (size_t)inter * rb));
+    HIPCHK(hipMemcpy2DAsync(tmp, 16 * rb, t1.p, 8 * rb, 8 * rb, inter / 8, hipMemcpyDeviceToDevice, m->stream));
+    HIPCHK(hipMemcpy2DAsync((char*)tmp + 8 * rb, 16 * rb, t3.p, 8 * rb, 8 * rb, inter / 8, hipMemcpyDeviceToDevice,
+                            m->stream));
+    void* pk = pack_dev(m, tmp, 2 * inter, dim);
+    HIPCHK(hipStreamSynchronize(m->stream));
+    HIPCHK(hipFree(tmp));
+    HIPCHK(hipFree(t1.p));
+    HIPCHK(hipFree(t3.p));
+    t1.p = pk;
+    t3.p = nullptr;
+    return pk;
+}
+
 static void finalize(fm_llm* m) {
     if (m->finalized) return;
     const fm_model_config& c = m->c;
     for (auto& kv : m->w) FMCHECK(kv.second.set, "tensor not set: " + kv.first);
     for (auto& kv : m->w) {
-        if (!is_linear_weight(kv.first)) continue;
+        if (!is_linear_weight(kv.first) || is_ffn_w13(kv.first)) continue;  // W1/W3: pack_w13 below
         DTensor& t = kv.second;
         void* pk = pack_dev(m, t.p, (int)t.rows, (int)t.cols);
         HIPCHK(hipStreamSynchronize(m->stream));
@@ -707,8 +743,7 @@ static void finalize(fm_llm* m) {
             L.bo = Wopt(m, p + "attention.wo.bias");
             L.qn = Wopt(m, p + "attention.q_norm.weight");
             L.kn = Wopt(m, p + "attention.k_norm.weight");
-            L.w1 = W(m, p + "feed_forward.w1.weight");
-            L.w3 = W(m, p + "feed_forward.w3.weight");
+            L.w13 = pack_w13(m, p, d.inter, d.dim);
             L.w2 = W(m, p + "feed_forward.w2.weight");
             L.an = W(m, p + "attention_norm.weight");
             L.fn = W(m, p + "ffn_norm.weight");
@@ -769,6 +804,7 @@ static void finalize(fm_llm* m) {
     m->q = m->dalloc((size_t)R * qmax * E);
     m->att = m->dalloc((size_t)R * qmax * E);
     m->act = m->dalloc((size_t)R * imax * E);
+    m->act2 = m->dalloc((size_t)R * 2 * imax * E);
     const int n = m->max_slots;
     m->xl = m->dalloc((size_t)n * dmax * E);
     m->xnl = m->dalloc((size_t)n * dmax * E);
@@ -1220,6 +1256,9 @@ int fm_tune(const char* key, int value) {
             t.gemv_u = value;
         } else if (k == "sampler_fast") {
             t.sampler_fast = value != 0;
+        } else if (k == "attn_cap") {
+            FMCHECK(value == 0 || (value >= 16 && value % 16 == 0), "attn_cap must be 0 or a multiple of 16");
+            t.attn_cap = value;
         } else if (k == "attn_fuse") {
             t.attn_fuse = value != 0;
         } else if (k == "pro_exp") {

@@ -120,6 +120,23 @@ template <typename T> void launch_pack(hipStream_t s, const T* src, int N, int K
     pack_kernel<T><<<blocks, 256, 0, s>>>(src, N, K, dst);
 }
 template void launch_pack<bf16_t>(hipStream_t, const bf16_t*, int, int, bf16_t*);
+
+template <typename T>
+__global__ void swiglu_i8_kernel(const T* __restrict__ t, int ldt, T* __restrict__ act, int lda, int inter, int R) {
+    const int64_t n = (int64_t)R * inter;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+        const int r = (int)(q / inter), j = (int)(q - (int64_t)r * inter);
+        const T* tr = t + (size_t)r * ldt + 16 * (j >> 3) + (j & 7);
+        const float g = ld(tr, 0), u = ld(tr, 8);
+        st(act + (size_t)r * lda, j, rnd<T>(g / (1.0f + expf(-g))) * u);
+    }
+}
+template <typename T> void launch_swiglu_i8(hipStream_t s, const T* t, int ldt, T* act, int lda, int inter, int R) {
+    const int64_t n = (int64_t)R * inter;
+    swiglu_i8_kernel<T><<<(int)std::min<int64_t>(FM_CEIL(n, 256), 16384), 256, 0, s>>>(t, ldt, act, lda, inter, R);
+}
+template void launch_swiglu_i8<bf16_t>(hipStream_t, const bf16_t*, int, bf16_t*, int, int, int);
+template void launch_swiglu_i8<float>(hipStream_t, const float*, int, float*, int, int, int);
 template void launch_pack<float>(hipStream_t, const float*, int, int, float*);
 
 template <typename T> struct Mfma;

@@ -132,14 +132,14 @@ int main() {
     CK(hipMalloc(&X, 16384 * 2));
     CK(hipMemset(X, 0x3c, 16384 * 2));
     CK(hipMalloc(&Y, 8 * 32768 * 4));
-    for (int nb : {10, 1, 2}) {
+    for (int nb : {10}) {
         g_nbuf = nb;
         for (auto& sh : shapes) {
-            run<4, true, false, 1, 4>(&"u4 nt run 1x4"[0], Ws, X, Y, sh, 1);
-            run<4, false, false, 1, 4>(&"u4 run 1x4"[0], Ws, X, Y, sh, 1);
-            run<8, false, false, 1, 4>(&"u8 run 1x4"[0], Ws, X, Y, sh, 1);
-            run<4, false, false, 1, 8>(&"u4 run 1x8"[0], Ws, X, Y, sh, 1);
-            run<4, false, false, 1, 4>(&"u4 run 1x4"[0], Ws, X, Y, sh, 2);
+            for (int ksb : {1, 2, 4, 8}) {
+                run<8, true, false, 1, 4>(&"u8 nt run 1x4"[0], Ws, X, Y, sh, ksb);
+                run<16, true, false, 1, 4>(&"u16 nt run 1x4"[0], Ws, X, Y, sh, ksb);
+                run<8, true, false, 1, 8>(&"u8 nt run 1x8"[0], Ws, X, Y, sh, ksb);
+            }
         }
     }
     return 0;
