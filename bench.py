@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=4, help="oracle decode frames sampled")
     ap.add_argument("--cpu-codec-frames", type=int, default=4, help="oracle codec frames sampled")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=32,
+                    help="throughput leg (BASELINE config 3): concurrent streams per GPU (0: skip)")
+    ap.add_argument("--batch-frames", type=int, default=256, help="throughput leg: frames decoded")
     return ap.parse_args()
 
 
@@ -57,22 +60,60 @@ def make_prompt(cfg, T, seed):
 
 
 def utterance(llm, codec, prompt, sp, frames, first_chunk):
-    """Request -> PCM for one stream.  Returns (pcm, timings in seconds)."""
+    """Request -> PCM for one stream.  Returns (pcm, timings in seconds).  The vocoder streams:
+    the first chunk is decoded as soon as its frames exist, the rest continues the same codec
+    stream (carried causal state, fm_codec_decode_chunk), so no frame is vocoded twice."""
     t0 = time.perf_counter()
     col0 = llm.prefill(0, prompt, sp)
     t1 = time.perf_counter()
     f0 = min(first_chunk, frames)
     head = llm.decode_frames([0], f0 - 1)[:, 0, :]
     cols = np.concatenate([col0[None], head], axis=0)          # (f0, C+1)
-    codec.decode_codes(np.ascontiguousarray(cols[:, 1:].T))      # first audio chunk
+    codec.stream_reset()
+    pcm0 = codec.decode_chunk(np.ascontiguousarray(cols[:, 1:].T))  # first audio chunk
     t2 = time.perf_counter()
     rest = llm.decode_frames([0], frames - f0)[:, 0, :]
     t3 = time.perf_counter()
-    codes = np.ascontiguousarray(np.concatenate([cols, rest], axis=0)[:, 1:].T)  # (C, frames)
-    pcm = codec.decode_codes(codes)
+    pcm = np.concatenate([pcm0, codec.decode_chunk(np.ascontiguousarray(rest[:, 1:].T))])
     t4 = time.perf_counter()
     return pcm, dict(first=t2 - t0, prefill=t1 - t0, head=t2 - t1, decode=t3 - t2, codec=t4 - t3,
                      total=t4 - t0)
+
+
+def throughput_leg(llm, cfg, batch, frames, sync, dist, world):
+    """BASELINE config 3 (config 4 at N GPUs): `batch` concurrent prompts per GPU with lengths
+    uniform in [16, 256] (seed 2), prefilled into their own KV slots, then decoded
+    together: one batched Dual-AR frame (slow pass + 10 fast passes + samplers of every stream)
+    per graph replay.  Returns aggregate audio-seconds per wall-second over all ranks."""
+    from fishmi.llm import DualARModel
+
+    rank = dist.get_rank() if dist is not None else 0
+    rng = np.random.default_rng(2 + 7919 * rank)
+    lens = rng.integers(16, 257, batch)
+    for s in range(batch):
+        llm.prefill(s, make_prompt(cfg, int(lens[s]), 5000 + 97 * rank + s),
+                    DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30, seed=31 * s + rank,
+                                         mask_im_end=True))
+    slots = list(range(batch))
+    llm.decode_frames(slots, 4)  # graph capture for n = batch
+    sync()
+    t0 = time.perf_counter()
+    llm.decode_frames(slots, frames)
+    sync()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        e = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        dt = float(e.item())
+    return {"workload": f"BASELINE config 3 per GPU: {batch} concurrent streams (prompt lengths "
+                        f"uniform 16-256, seed 2), {frames} batched Dual-AR frames each (top_k 30, "
+                        f"top_p 0.8, temp 0.8), hipGraph per frame; aggregate over {world} GPU(s)",
+            "batch_per_gpu": batch, "frames": frames,
+            "value": round(world * batch * frames / FRAME_RATE / dt, 2), "unit": "audio-sec/wall-sec",
+            "ms_per_frame": round(dt / frames * 1e3, 3),
+            "per_stream_rtf": round(frames / FRAME_RATE / dt, 3)}
 
 
 def cpu_baseline(cfg, ccfg, prompt, frames, n_frames, n_codec, seed):
@@ -125,10 +166,10 @@ def main():
 
     cfg = DualARConfig._from_fish_qwen3_omni(S2_PRO_CONFIG)
     cfg.im_end_id = S2_PRO_IM_END_ID
-    cfg.max_seq_len = max(1024, args.prompt_len + args.frames + 8)
+    cfg.max_seq_len = max(1024, args.prompt_len + args.frames + 8, 256 + args.batch_frames + 8)
     ccfg = CodecConfig()
     llm = DualARModel.synthetic(cfg, seed=args.seed, log2_half=5, device=local, precision="bf16",
-                                max_slots=1)
+                                max_slots=max(1, args.batch))
     codec = FishMICodec.synthetic(ccfg, args.seed + 1, local, "bf16", max_frames=args.frames)
 
     def sync():
@@ -197,6 +238,8 @@ def main():
     ms1, n1, fl1 = codec.profile()
     codec_tflops = (fl1 - fl0) / ((ms1 - ms0) * 1e-3) / 1e12
 
+    thr = throughput_leg(llm, cfg, args.batch, args.batch_frames, sync, dist, world) if args.batch > 0 else None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         del llm, codec
@@ -242,6 +285,7 @@ def main():
             "codec_roofline": {"bound": "mfma", "achieved": round(codec_tflops, 2),
                                "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                                "frac": round(codec_tflops / BF16_DENSE_TFLOPS, 4)},
+            "throughput": thr,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -162,3 +162,133 @@ __device__ __forceinline__ void fast_attn_head(const FastFusedArgs<T>& a, int r,
         }
     }
 }
+
+// The same fast-model attention for EIGHT q heads at once (one wave: 8 lanes per head, lane sub
+// owns RoPE pairs sub, sub+8, ...), every operand already staged in LDS by the Wo GEMV's PRO_FATT
+// prologue (fm_gemv.hip): raw = the row's q|k|v projections, kvs = cached rows [nkv][k|v][cpos][hd],
+// qn / kn = QK-norm weights, tab = the RoPE row at cpos.  Same roundings as fast_attn_head (the
+// fp32 reduction order of the dot products differs).  Heads hbase .. hbase+7 (< hend); head h's
+// output goes to out + (h - hbase) * hd.  store_kv: the first q head of each kv group writes the
+// new k / v of cpos to the fast cache (one block per launch).
+constexpr int FATT_MAXPP = 8;  // RoPE pairs per lane: hd <= 128
+template <typename T>
+__device__ __forceinline__ void fast_attn_heads8_lds(const FastFusedArgs<T>& a, int hbase, int hend, int lane,
+                                                     const T* raw, const T* kvs, const T* qn, const T* kn,
+                                                     const float* tab, T* out, bool store_kv, int slot) {
+    const int hd = a.hd, g = a.nh / a.nkv, cpos = a.cpos, PP = hd >> 4;
+    const int sub = lane & 7, h = hbase + (lane >> 3);
+    const bool live = h < hend;
+    const int hh = live ? h : hbase, kvh = hh / g;
+    float q0[FATT_MAXPP], q1[FATT_MAXPP], k0[FATT_MAXPP], k1[FATT_MAXPP], v0[FATT_MAXPP], v1[FATT_MAXPP];
+#pragma unroll
+    for (int i = 0; i < FATT_MAXPP; ++i) {
+        const int d = 2 * (sub + 8 * (i < PP ? i : 0));
+        q0[i] = ld(raw, (size_t)hh * hd + d);
+        q1[i] = ld(raw, (size_t)hh * hd + d + 1);
+        k0[i] = ld(raw, (size_t)(a.nh + kvh) * hd + d);
+        k1[i] = ld(raw, (size_t)(a.nh + kvh) * hd + d + 1);
+        v0[i] = ld(raw, (size_t)(a.nh + a.nkv + kvh) * hd + d);
+        v1[i] = ld(raw, (size_t)(a.nh + a.nkv + kvh) * hd + d + 1);
+        if (i >= PP) q0[i] = q1[i] = k0[i] = k1[i] = v0[i] = v1[i] = 0.f;
+    }
+    auto sum8 = [](float v) {
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        return v;
+    };
+    auto prep = [&](float (&x0)[FATT_MAXPP], float (&x1)[FATT_MAXPP], const T* w, bool norm) {
+        if (norm) {
+            float ss = 0.f;
+#pragma unroll
+            for (int i = 0; i < FATT_MAXPP; ++i) ss += x0[i] * x0[i] + x1[i] * x1[i];
+            ss = sum8(ss);
+            const float rs = 1.0f / sqrtf(ss / (float)hd + a.eps);
+#pragma unroll
+            for (int i = 0; i < FATT_MAXPP; ++i) {
+                const int d = 2 * (sub + 8 * (i < PP ? i : 0));
+                x0[i] = rnd<T>((x0[i] * rs) * ld(w, d));
+                x1[i] = rnd<T>((x1[i] * rs) * ld(w, d + 1));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < FATT_MAXPP; ++i) {
+            const int d = 2 * (sub + 8 * (i < PP ? i : 0));
+            const float c = tab[d], s = tab[d + 1];
+            const float y0 = rnd<T>(x0[i] * c - x1[i] * s);
+            const float y1 = rnd<T>(x1[i] * c + x0[i] * s);
+            x0[i] = y0;
+            x1[i] = y1;
+        }
+    };
+    prep(q0, q1, qn, a.qk_norm);
+    prep(k0, k1, kn, a.qk_norm);
+    if (store_kv && live && h == kvh * g) {
+        const size_t base = (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd + (size_t)cpos * hd;
+#pragma unroll
+        for (int i = 0; i < FATT_MAXPP; ++i) {
+            if (i < PP) {
+                const int d = 2 * (sub + 8 * i);
+                st(a.kc + base, d, k0[i]);
+                st(a.kc + base, d + 1, k1[i]);
+                st(a.vc + base, d, v0[i]);
+                st(a.vc + base, d + 1, v1[i]);
+            }
+        }
+    }
+    const T* K = kvs + (size_t)(2 * kvh) * cpos * hd;
+    const T* V = K + (size_t)cpos * hd;
+    float sc[FAST_ATTN_MAXJ + 1];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j <= FAST_ATTN_MAXJ; ++j) {
+        if (j > cpos) break;
+        float dd = 0.f;
+#pragma unroll
+        for (int i = 0; i < FATT_MAXPP; ++i) {
+            if (i < PP) {
+                const int d = 2 * (sub + 8 * i);
+                const float a0 = j < cpos ? ld(K, (size_t)j * hd + d) : k0[i];
+                const float a1 = j < cpos ? ld(K, (size_t)j * hd + d + 1) : k1[i];
+                dd += q0[i] * a0 + q1[i] * a1;
+            }
+        }
+        dd = sum8(dd);
+        sc[j] = rnd<T>(rnd<T>(dd) * a.scale);
+        mx = fmaxf(mx, sc[j]);
+    }
+    float den = 0.f;
+#pragma unroll
+    for (int j = 0; j <= FAST_ATTN_MAXJ; ++j) {
+        if (j > cpos) break;
+        sc[j] = expf(sc[j] - mx);
+        den += sc[j];
+    }
+    float o0[FATT_MAXPP], o1[FATT_MAXPP];
+#pragma unroll
+    for (int i = 0; i < FATT_MAXPP; ++i) o0[i] = o1[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j <= FAST_ATTN_MAXJ; ++j) {
+        if (j > cpos) break;
+        const float pj = rnd<T>(sc[j] / den);
+#pragma unroll
+        for (int i = 0; i < FATT_MAXPP; ++i) {
+            if (i < PP) {
+                const int d = 2 * (sub + 8 * i);
+                o0[i] += pj * (j < cpos ? ld(V, (size_t)j * hd + d) : v0[i]);
+                o1[i] += pj * (j < cpos ? ld(V, (size_t)j * hd + d + 1) : v1[i]);
+            }
+        }
+    }
+    if (live) {
+        T* o = out + (size_t)(h - hbase) * hd;
+#pragma unroll
+        for (int i = 0; i < FATT_MAXPP; ++i) {
+            if (i < PP) {
+                const int d = 2 * (sub + 8 * i);
+                st(o, d, o0[i]);
+                st(o, d + 1, o1[i]);
+            }
+        }
+    }
+}

@@ -35,6 +35,15 @@ struct DBlock {
     RU ru[3];
 };
 
+// Streamed decode (fm_codec_decode_chunk): the codec is causal end to end, so chunk k of a
+// stream is decoded exactly like the matching rows of the one-shot decode when every causal
+// reader sees the previous chunk's rows it would have read: each conv site's last (k-1)*dil input
+// rows, the ConvNeXt depthwise k7 inputs, each transformer layer's window-1 post-RoPE key/value
+// rows (and the RoPE position).  Those rows live in per-site state buffers, copied into a prefix
+// of the activation buffer before the reader runs and refreshed from it right after.
+static constexpr int CODEC_HALO = 128;           // prefix rows of the buffers read with context
+static constexpr int CODEC_STREAM_MAX = 1 << 15;  // RoPE positions of one stream (25 min of audio)
+
 struct fm_codec {
     fm_codec_config c{};
     int device = 0, prec = FM_PREC_BF16, max_frames = 0;
@@ -59,6 +68,12 @@ struct fm_codec {
     void *u0 = nullptr, *u1 = nullptr, *hh = nullptr, *gb = nullptr;
     void *xb = nullptr, *A = nullptr, *B = nullptr, *Cb = nullptr;
     float* wave = nullptr;
+    // stream state: carried rows per causal site (zeros at a stream start == causal padding)
+    void* st_kv[16] = {};                   // per transformer layer: window-1 qkv rows
+    void *st_dw[2] = {}, *st_c0 = nullptr, *st_cf = nullptr;
+    void *st_ct[4] = {}, *st_c7[4][3] = {};
+    std::vector<std::pair<void*, size_t>> st_all;
+    int spos = 0;                           // frames already streamed
     double last_ms = 0, flops = 0, total_ms = 0, total_flops = 0;
     int64_t launches = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -71,6 +86,14 @@ struct fm_codec {
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (stream) (void)hipStreamDestroy(stream);
+    }
+    void* dalloc_prefixed(size_t body, size_t prefix) {  // prefix bytes in front of the base
+        return (char*)dalloc(prefix + body) + prefix;
+    }
+    void* dstate(size_t bytes) {
+        void* p = dalloc(bytes);
+        st_all.emplace_back(p, bytes);
+        return p;
     }
     void* dalloc(size_t bytes) {
         void* p = nullptr;
@@ -286,7 +309,7 @@ static void finalize(fm_codec* m) {
     m->falpha = as_T(m, raw(m, "decoder.model.5.alpha"), cin);
     m->convf = prep_wn_conv(m, "decoder.model.6.", cin, 1, 7, 1);
     // rope table for the transformer (positions 0..Tmax-1, bf16-valued)
-    auto rt = rope_table_host(m->max_frames, c.t_head_dim, c.rope_base);
+    auto rt = rope_table_host(std::max(m->max_frames, CODEC_STREAM_MAX), c.t_head_dim, c.rope_base);
     m->rope = (float*)m->dalloc(rt.size() * 4);
     HIPCHK(hipMemcpy(m->rope, rt.data(), rt.size() * 4, hipMemcpyHostToDevice));
     // activations
@@ -294,12 +317,12 @@ static void finalize(fm_codec* m) {
     m->d_codes = (int32_t*)m->dalloc((size_t)(c.n_codebooks + 1) * Tm * 4);
     m->z = m->dalloc(Tm * D * E);
     m->xn = m->dalloc(Tm * D * E);
-    m->qkv = m->dalloc(Tm * 3 * HD * E);
+    m->qkv = m->dalloc_prefixed(Tm * 3 * HD * E, (size_t)CODEC_HALO * 3 * HD * E);
     m->att = m->dalloc(Tm * HD * E);
     m->g1 = m->dalloc(Tm * I * E);
     m->g3 = m->dalloc(Tm * I * E);
-    m->u0 = m->dalloc(Tm * 2 * D * E);
-    m->u1 = m->dalloc(Tm * 4 * D * E);
+    m->u0 = m->dalloc_prefixed(Tm * 2 * D * E, (size_t)CODEC_HALO * D * E);
+    m->u1 = m->dalloc_prefixed(Tm * 4 * D * E, (size_t)CODEC_HALO * D * E);
     m->hh = m->dalloc(Tm * 4 * D * E);
     m->gb = m->dalloc(Tm * 4 * 4 * D * E);
     size_t maxact = (size_t)4 * ch;
@@ -312,8 +335,22 @@ static void finalize(fm_codec* m) {
         }
     }
     m->xb = m->dalloc(Tm * maxact * E);
-    m->A = m->dalloc(Tm * maxact * E);
-    m->B = m->dalloc(Tm * maxact * E);
+    m->A = m->dalloc_prefixed(Tm * maxact * E, (size_t)CODEC_HALO * std::max(ch, D) * E);
+    m->B = m->dalloc_prefixed(Tm * maxact * E, (size_t)CODEC_HALO * std::max(ch, D) * E);
+    FMCHECK(c.t_layers <= 16 && c.window - 1 <= CODEC_HALO, "codec stream state: t_layers <= 16, window <= 129");
+    for (int l = 0; l < c.t_layers; ++l) m->st_kv[l] = m->dstate((size_t)(c.window - 1) * 3 * HD * E);
+    for (int u = 0; u < 2; ++u) m->st_dw[u] = m->dstate((size_t)6 * D * E);
+    m->st_c0 = m->dstate((size_t)6 * D * E);
+    {
+        int cc = ch;
+        const int dl[3] = {1, 3, 9};
+        for (int b = 0; b < 4; ++b) {
+            m->st_ct[b] = m->dstate((size_t)cc * E);
+            for (int r = 0; r < 3; ++r) m->st_c7[b][r] = m->dstate((size_t)6 * dl[r] * (cc / 2) * E);
+            cc /= 2;
+        }
+        m->st_cf = m->dstate((size_t)6 * cc * E);
+    }
     m->Cb = m->dalloc(Tm * maxact * E);
     m->wave = (float*)m->dalloc(Tm * 2048 * 4);
     HIPCHK(hipEventCreate(&m->e0));
@@ -329,7 +366,7 @@ template <typename T> struct CRun {
 
     void gemm(const PackedW& W, const void* x, int ldx, int Lq, int Lx, void* out, int ldo, int flags,
               const void* res = nullptr, int ldr = 0, const void* gamma = nullptr, const void* alpha2 = nullptr,
-              void* out2 = nullptr, int ldo2 = 0) {
+              void* out2 = nullptr, int ldo2 = 0, int lo = 0) {
         ConvArgs<T> a{};
         a.x = (const T*)x;
         a.ldx = ldx;
@@ -353,22 +390,39 @@ template <typename T> struct CRun {
         a.out2 = (T*)out2;
         a.ldo2 = ldo2;
         a.flags = flags | (W.bias ? CE_BIAS : 0) | (out2 ? CE_SNAKE : 0);
+        a.lo = lo;
         launch_conv_gemm<T>(s, a);
         m->flops += 2.0 * Lq * W.nphase * (double)W.Co * W.ntaps * W.Ci;
         m->launches++;
     }
 
-    void decode(int Tn) {
+    // streamed chunk: a causal reader's carried rows -> the prefix of its input buffer, and back
+    void site_in(bool on, const void* base, int width, int rows, void* st) {
+        if (!on || rows <= 0) return;
+        const size_t b = (size_t)rows * width * sizeof(T);
+        HIPCHK(hipMemcpyAsync((char*)base - b, st, b, hipMemcpyDeviceToDevice, s));
+    }
+    void site_out(bool on, const void* base, int width, int rows, int L, void* st) {
+        if (!on || rows <= 0) return;
+        const size_t b = (size_t)rows * width * sizeof(T);
+        HIPCHK(hipMemcpyAsync(st, (const char*)base + ((ptrdiff_t)L - rows) * width * (ptrdiff_t)sizeof(T), b,
+                              hipMemcpyDeviceToDevice, s));
+    }
+
+    void decode(int Tn, bool stream = false) {
         const fm_codec_config& c = m->c;
         const int D = c.latent, H = c.t_heads, hd = c.t_head_dim, I = c.t_inter;
+        const int W1 = c.window - 1, pos0 = stream ? m->spos : 0, npre = stream ? std::min(m->spos, W1) : 0;
         launch_rvq_decode<T>(s, m->d_codes, Tn, c.n_codebooks + 1, c.semantic_codebook_size, c.codebook_size,
                              c.codebook_dim, m->rvq, D, (T*)m->z);
         for (int l = 0; l < c.t_layers; ++l) {
             const TLayer& L = m->tl[l];
             launch_rmsnorm<T>(s, (const T*)m->z, D, (const T*)L.an, D, c.norm_eps, (T*)m->xn, D, Tn);
             gemm(L.wqkv, m->xn, D, Tn, Tn, m->qkv, 3 * H * hd, CE_STORE);
-            launch_rope_qk<T>(s, (T*)m->qkv, Tn, H, hd, m->rope);
-            launch_window_attn<T>(s, (const T*)m->qkv, Tn, H, hd, c.window, (T*)m->att);
+            launch_rope_qk<T>(s, (T*)m->qkv, Tn, H, hd, m->rope, pos0);
+            site_in(stream, m->qkv, 3 * H * hd, W1, m->st_kv[l]);
+            launch_window_attn<T>(s, (const T*)m->qkv, Tn, H, hd, c.window, (T*)m->att, npre);
+            site_out(stream, m->qkv, 3 * H * hd, W1, Tn, m->st_kv[l]);
             gemm(L.wo, m->att, H * hd, Tn, Tn, m->z, D, CE_STORE | CE_RES | CE_GAMMA, m->z, D, L.ag);
             launch_rmsnorm<T>(s, (const T*)m->z, D, (const T*)L.fn, D, c.norm_eps, (T*)m->xn, D, Tn);
             gemm(L.w1, m->xn, D, Tn, Tn, m->g1, I, CE_STORE);
@@ -385,15 +439,19 @@ template <typename T> struct CRun {
             void* uo = ubuf[u];
             gemm(m->up_ct[u], xin, D, L, L, uo, D, CE_STORE);
             L *= 2;
+            site_in(stream, uo, D, 6, m->st_dw[u]);
             launch_dwconv_ln<T>(s, (const T*)uo, L, D, (const T*)m->up_dw[u], (const T*)m->up_db[u],
-                                (const T*)m->up_lw[u], (const T*)m->up_lb[u], (T*)m->hh);
+                                (const T*)m->up_lw[u], (const T*)m->up_lb[u], (T*)m->hh, stream ? -6 : 0);
+            site_out(stream, uo, D, 6, L, m->st_dw[u]);
             gemm(m->up_pw1[u], m->hh, D, L, L, m->gb, 4 * D, CE_STORE | CE_GELU);
             gemm(m->up_pw2[u], m->gb, 4 * D, L, L, uo, D, CE_STORE | CE_RES | CE_GAMMA, uo, D, m->up_gm[u]);
             xin = uo;
         }
         // decoder
         const int ch = c.decoder_dim;
-        gemm(m->conv0, xin, D, L, L, nullptr, 0, 0, nullptr, 0, nullptr, m->blk[0].alpha, m->A, ch);
+        site_in(stream, xin, D, 6, m->st_c0);
+        gemm(m->conv0, xin, D, L, L, nullptr, 0, 0, nullptr, 0, nullptr, m->blk[0].alpha, m->A, ch, stream ? -6 : 0);
+        site_out(stream, xin, D, 6, L, m->st_c0);
         void* in = m->A;
         void* alt = m->B;
         int cin = ch;
@@ -401,11 +459,18 @@ template <typename T> struct CRun {
         for (int b = 0; b < 4; ++b) {
             const DBlock& Bk = m->blk[b];
             const int cout = cin / 2, st_ = rates[b];
-            gemm(Bk.ct, in, cin, L, L, m->xb, cout, CE_STORE, nullptr, 0, nullptr, Bk.ru[0].a0, alt, cout);
+            site_in(stream, in, cin, 1, m->st_ct[b]);
+            gemm(Bk.ct, in, cin, L, L, m->xb, cout, CE_STORE, nullptr, 0, nullptr, Bk.ru[0].a0, alt, cout,
+                 stream ? -1 : 0);
+            site_out(stream, in, cin, 1, L, m->st_ct[b]);
             L *= st_;
+            const int dl[3] = {1, 3, 9};
             for (int r = 0; r < 3; ++r) {
                 const RU& R = Bk.ru[r];
-                gemm(R.c7, alt, cout, L, L, nullptr, 0, 0, nullptr, 0, nullptr, R.a2, m->Cb, cout);
+                const int hr = 6 * dl[r];
+                site_in(stream, alt, cout, hr, m->st_c7[b][r]);
+                gemm(R.c7, alt, cout, L, L, nullptr, 0, 0, nullptr, 0, nullptr, R.a2, m->Cb, cout, stream ? -hr : 0);
+                site_out(stream, alt, cout, hr, L, m->st_c7[b][r]);
                 const void* an = r < 2 ? Bk.ru[r + 1].a0 : (b < 3 ? m->blk[b + 1].alpha : m->falpha);
                 gemm(R.c1, m->Cb, cout, L, L, m->xb, cout, (r < 2 ? CE_STORE : 0) | CE_RES, m->xb, cout, nullptr,
                      an, alt, cout);
@@ -413,7 +478,10 @@ template <typename T> struct CRun {
             std::swap(in, alt);
             cin = cout;
         }
-        gemm(m->convf, in, cin, L, L, m->wave, 1, CE_STORE | CE_TANH | CE_F32OUT);
+        site_in(stream, in, cin, 6, m->st_cf);
+        gemm(m->convf, in, cin, L, L, m->wave, 1, CE_STORE | CE_TANH | CE_F32OUT, nullptr, 0, nullptr, nullptr,
+             nullptr, 0, stream ? -6 : 0);
+        site_out(stream, in, cin, 6, L, m->st_cf);
     }
 };
 
@@ -486,8 +554,34 @@ int fm_codec_finalize(fm_codec* m) {
     });
 }
 
+static void codec_decode(fm_codec* m, const int32_t* codes, int T, float* pcm, bool stream);
+
 int fm_codec_decode(fm_codec* m, const int32_t* codes, int T, float* pcm) {
+    return fm_guard([&] { codec_decode(m, codes, T, pcm, false); });
+}
+
+int fm_codec_stream_reset(fm_codec* m) {
     return fm_guard([&] {
+        FMCHECK(m, "null handle");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        for (auto& pb : m->st_all) HIPCHK(hipMemsetAsync(pb.first, 0, pb.second, m->stream));
+        HIPCHK(hipStreamSynchronize(m->stream));
+        m->spos = 0;
+    });
+}
+
+int fm_codec_decode_chunk(fm_codec* m, const int32_t* codes, int T, float* pcm) {
+    return fm_guard([&] {
+        FMCHECK(m, "null handle");
+        FMCHECK(m->spos + (int64_t)T <= CODEC_STREAM_MAX, "stream longer than the RoPE table: reset it");
+        codec_decode(m, codes, T, pcm, true);
+        m->spos += T;
+    });
+}
+
+static void codec_decode(fm_codec* m, const int32_t* codes, int T, float* pcm, bool stream) {
+    {
         FMCHECK(m && codes && pcm, "null argument");
         FMCHECK(T >= 1 && T <= m->max_frames, "T must be in [1, max_frames]");
         HIPCHK(hipSetDevice(m->device));
@@ -499,10 +593,10 @@ int fm_codec_decode(fm_codec* m, const int32_t* codes, int T, float* pcm) {
         HIPCHK(hipEventRecord(m->e0, m->stream));
         if (m->prec == FM_PREC_BF16) {
             CRun<bf16_t> r(m);
-            r.decode(T);
+            r.decode(T, stream);
         } else {
             CRun<float> r(m);
-            r.decode(T);
+            r.decode(T, stream);
         }
         HIPCHK(hipEventRecord(m->e1, m->stream));
         HIPCHK(hipMemcpyAsync(pcm, m->wave, (size_t)T * 2048 * 4, hipMemcpyDeviceToHost, m->stream));
@@ -512,7 +606,7 @@ int fm_codec_decode(fm_codec* m, const int32_t* codes, int T, float* pcm) {
         m->last_ms = ms;
         m->total_ms += ms;
         m->total_flops += m->flops;
-    });
+    }
 }
 
 // test hook: copy an intermediate of the last decode as fp32 (time-major):

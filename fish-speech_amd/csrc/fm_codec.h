@@ -34,6 +34,8 @@ template <typename T> struct ConvArgs {
     T* out2;
     int ldo2;
     int flags;
+    int lo;                    // lowest input row read (<= 0): rows [lo, 0) are the carried causal
+                               // context of a streamed chunk (buffer prefix), 0 = causal zeros
 };
 
 struct RvqPtrs {
@@ -47,12 +49,16 @@ template <typename T> void launch_silu_mul(hipStream_t s, const T* g, T* y, size
 template <typename T>
 void launch_rvq_decode(hipStream_t s, const int32_t* codes, int Tn, int nq1, int sem, int cbs, int cd,
                        const RvqPtrs& p, int D, T* z);
+// lo <= 0: rows [lo, 0) of x are carried causal context (streamed chunk), else causal zeros
 template <typename T>
 void launch_dwconv_ln(hipStream_t s, const T* x, int L, int D, const T* dw, const T* db, const T* lw,
-                      const T* lb, T* y);
-template <typename T> void launch_rope_qk(hipStream_t s, T* qkv, int Tn, int H, int hd, const float* tab);
+                      const T* lb, T* y, int lo = 0);
+// pos0: absolute position of row 0 (streamed chunk)
 template <typename T>
-void launch_window_attn(hipStream_t s, const T* qkv, int Tn, int H, int hd, int window, T* out);
+void launch_rope_qk(hipStream_t s, T* qkv, int Tn, int H, int hd, const float* tab, int pos0 = 0);
+// npre: rows [-npre, 0) of qkv hold the carried (post-RoPE) keys / values of earlier frames
+template <typename T>
+void launch_window_attn(hipStream_t s, const T* qkv, int Tn, int H, int hd, int window, T* out, int npre = 0);
 void launch_wn_fold(hipStream_t s, const float* g, const float* v, int rows, int per, float* w);
 template <typename T>
 void launch_conv_weight(hipStream_t s, const float* w, int kind, int Ci, int Co, int k, int st_, T* out);

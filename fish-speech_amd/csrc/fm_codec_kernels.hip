@@ -99,9 +99,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int row = tq[u] - sh;
-            const bool valid = kin && row >= 0 && row < a.Lx;
-            const int rc = row < 0 ? 0 : (row >= a.Lx ? a.Lx - 1 : row);
-            fb[u] = F::xload(a.x + (size_t)rc * a.ldx + ci0, valid);
+            const bool valid = kin && row >= a.lo && row < a.Lx;
+            const int rc = row < a.lo ? a.lo : (row >= a.Lx ? a.Lx - 1 : row);
+            fb[u] = F::xload(a.x + (ptrdiff_t)rc * a.ldx + ci0, valid);
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -180,7 +180,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void dwconv_ln_kernel(const T* __restrict__ x, int L, int D,
                                                         const T* __restrict__ dw, const T* __restrict__ db,
                                                         const T* __restrict__ lw, const T* __restrict__ lb,
-                                                        T* __restrict__ y) {
+                                                        T* __restrict__ y, int lo) {
     __shared__ float scratch[16];
     const int t = blockIdx.x;
     float v[8];
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void dwconv_ln_kernel(const T* __restrict__ x,
         float acc = ld(db, c);
         for (int j = 0; j < 7; ++j) {
             const int src = t - 6 + j;
-            if (src >= 0) acc += ld(dw, (size_t)c * 7 + j) * ld(x, (size_t)src * D + c);
+            if (src >= lo) acc += ld(dw, (size_t)c * 7 + j) * ld(x + (ptrdiff_t)src * D, c);
         }
         v[n] = rnd<T>(acc);
         s += v[n];
@@ -206,14 +206,15 @@ __global__ __launch_bounds__(256) void dwconv_ln_kernel(const T* __restrict__ x,
 }
 
 template <typename T>
-__global__ void rope_qk_kernel(T* __restrict__ qkv, int Tn, int H, int hd, const float* __restrict__ tab) {
-    const int t = blockIdx.x;
+__global__ void rope_qk_kernel(T* __restrict__ qkv, int Tn, int H, int hd, const float* __restrict__ tab,
+                               int pos0) {
+    const int t = blockIdx.x, tp = t + pos0;
     const int half = hd >> 1;
     for (int idx = threadIdx.x; idx < 2 * H * half; idx += blockDim.x) {
         const int head = idx / half, p = idx - head * half;
         T* v = qkv + (size_t)t * 3 * H * hd + (size_t)head * hd;
         const float x0 = ld(v, 2 * p), x1 = ld(v, 2 * p + 1);
-        const float c = tab[((size_t)t * half + p) * 2], s = tab[((size_t)t * half + p) * 2 + 1];
+        const float c = tab[((size_t)tp * half + p) * 2], s = tab[((size_t)tp * half + p) * 2 + 1];
         const float y0 = x0 * c - x1 * s;
         const float y1 = x1 * c + x0 * s;
         st(v, 2 * p, y0);
@@ -224,7 +225,7 @@ __global__ void rope_qk_kernel(T* __restrict__ qkv, int Tn, int H, int hd, const
 // grid (T, H), one wave; window <= 128, hd <= 64
 template <typename T>
 __global__ __launch_bounds__(64) void window_attn_kernel(const T* __restrict__ qkv, int Tn, int H, int hd,
-                                                         int window, T* __restrict__ out) {
+                                                         int window, T* __restrict__ out, int npre) {
     __shared__ float qs[64];
     __shared__ float ps[128];
     const int lane = threadIdx.x;
@@ -233,15 +234,15 @@ __global__ __launch_bounds__(64) void window_attn_kernel(const T* __restrict__ q
     const T* q = qkv + (size_t)t * ld3 + (size_t)h * hd;
     if (lane < hd) qs[lane] = ld(q, lane);
     __syncthreads();
-    int j0 = t - window + 1;
-    if (j0 < 0) j0 = 0;
+    int j0 = t - window + 1;  // rows [-npre, 0): carried keys / values of the previous chunk
+    if (j0 < -npre) j0 = -npre;
     const int nj = t - j0 + 1;
     const float scale = 1.0f / sqrtf((float)hd);
     float sc[2] = {-INFINITY, -INFINITY};
     for (int i = 0; i < 2; ++i) {
         const int jj = lane + 64 * i;
         if (jj < nj) {
-            const T* k = qkv + (size_t)(j0 + jj) * ld3 + (size_t)(H + h) * hd;
+            const T* k = qkv + (ptrdiff_t)(j0 + jj) * (ptrdiff_t)ld3 + (size_t)(H + h) * hd;
             float dot = 0.f;
             for (int e = 0; e < hd; e += 8) {
                 float kv[8];
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(64) void window_attn_kernel(const T* __restrict__ q
     if (lane < hd) {
         float o = 0.f;
         for (int jj = 0; jj < nj; ++jj)
-            o += ps[jj] * ld(qkv + (size_t)(j0 + jj) * ld3 + (size_t)(2 * H + h) * hd, lane);
+            o += ps[jj] * ld(qkv + (ptrdiff_t)(j0 + jj) * (ptrdiff_t)ld3 + (size_t)(2 * H + h) * hd, lane);
         st(out, (size_t)t * H * hd + (size_t)h * hd + lane, o / l);
     }
 }
@@ -327,15 +328,16 @@ void launch_rvq_decode(hipStream_t s, const int32_t* codes, int Tn, int nq1, int
 }
 template <typename T>
 void launch_dwconv_ln(hipStream_t s, const T* x, int L, int D, const T* dw, const T* db, const T* lw,
-                      const T* lb, T* y) {
-    dwconv_ln_kernel<T><<<L, 256, 0, s>>>(x, L, D, dw, db, lw, lb, y);
-}
-template <typename T> void launch_rope_qk(hipStream_t s, T* qkv, int Tn, int H, int hd, const float* tab) {
-    rope_qk_kernel<T><<<Tn, 256, 0, s>>>(qkv, Tn, H, hd, tab);
+                      const T* lb, T* y, int lo) {
+    dwconv_ln_kernel<T><<<L, 256, 0, s>>>(x, L, D, dw, db, lw, lb, y, lo);
 }
 template <typename T>
-void launch_window_attn(hipStream_t s, const T* qkv, int Tn, int H, int hd, int window, T* out) {
-    window_attn_kernel<T><<<dim3(Tn, H), 64, 0, s>>>(qkv, Tn, H, hd, window, out);
+void launch_rope_qk(hipStream_t s, T* qkv, int Tn, int H, int hd, const float* tab, int pos0) {
+    rope_qk_kernel<T><<<Tn, 256, 0, s>>>(qkv, Tn, H, hd, tab, pos0);
+}
+template <typename T>
+void launch_window_attn(hipStream_t s, const T* qkv, int Tn, int H, int hd, int window, T* out, int npre) {
+    window_attn_kernel<T><<<dim3(Tn, H), 64, 0, s>>>(qkv, Tn, H, hd, window, out, npre);
 }
 void launch_wn_fold(hipStream_t s, const float* g, const float* v, int rows, int per, float* w) {
     wn_fold_kernel<<<rows, 256, 0, s>>>(g, v, per, w);
@@ -351,9 +353,9 @@ void launch_conv_weight(hipStream_t s, const float* w, int kind, int Ci, int Co,
     template void launch_rvq_decode<T>(hipStream_t, const int32_t*, int, int, int, int, int,         \
                                        const RvqPtrs&, int, T*);                                     \
     template void launch_dwconv_ln<T>(hipStream_t, const T*, int, int, const T*, const T*, const T*, \
-                                      const T*, T*);                                                 \
-    template void launch_rope_qk<T>(hipStream_t, T*, int, int, int, const float*);                   \
-    template void launch_window_attn<T>(hipStream_t, const T*, int, int, int, int, T*);              \
+                                      const T*, T*, int);                                            \
+    template void launch_rope_qk<T>(hipStream_t, T*, int, int, int, const float*, int);              \
+    template void launch_window_attn<T>(hipStream_t, const T*, int, int, int, int, T*, int);         \
     template void launch_conv_weight<T>(hipStream_t, const float*, int, int, int, int, int, T*);
 CINST(bf16_t)
 CINST(float)

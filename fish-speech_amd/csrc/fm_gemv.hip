@@ -92,7 +92,7 @@ constexpr int GEMV_RMAX = 8;  // rows (streams) of the small-batch path
 constexpr int GEMV_PRE = 8;   // (row, chunk) items of X preloaded per thread before the weight ring
 // occupancy target (waves per SIMD) of the tiled GEMV: the interleaved W1||W3 grid (1216 blocks of
 // 4 waves) is resident at 5; the others need 3 (enough for their grids)
-constexpr int gemv_wpe(int pro, int epi) { return pro == PRO_PRENORM && epi == EPI_SWIGLU8 ? 5 : 3; }
+constexpr int gemv_wpe(int pro, int epi) { return pro == PRO_PRENORM && epi == EPI_SWIGLU8 ? 5 : (pro == PRO_FATT ? 1 : 3); }
 
 // WPB waves per block share one 16-row tile, each streaming a contiguous run of its k-steps.
 template <typename T, int PRO, int EPI, bool NT, int U, int WPB>
@@ -189,6 +189,70 @@ void gemv_kernel(GemvArgs<T> a) {
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) issue(u, u);
+    } else if constexpr (PRO == PRO_FATT) {
+        // One row (host).  Round trip 1: slot, the raw q|k|v row, qk-norm weights, RoPE row; then
+        // the weight ring; round trip 2: the cpos cached K/V rows of every kv head (they need the
+        // slot).  Then wave-per-head attention from LDS straight into X' (fm_attn_dev.h).
+        const FastFusedArgs<T>& at = a.att;
+        const int hd = at.hd, cpos = at.cpos, nkv = at.nkv;
+        T* raw_s = reinterpret_cast<T*>(smem + a.fatt_off);  // raw row | qn | kn | tab: contiguous
+        T* qn_s = raw_s + at.ldqkv;
+        T* kn_s = qn_s + hd;
+        float* tab_s = reinterpret_cast<float*>(kn_s + hd);
+        T* kv_s = reinterpret_cast<T*>(tab_s + hd);
+        constexpr int CE = 16 / sizeof(T);  // elements per 16-B chunk
+        const int n_raw = at.ldqkv / CE, n_w = hd / CE, n_tab = hd * 4 / 16;
+        const int n1 = n_raw + 2 * n_w + n_tab;
+        auto src1 = [&](int i) -> const u32x4_t* {
+            if (i < n_raw) return reinterpret_cast<const u32x4_t*>(at.qkv) + i;
+            i -= n_raw;
+            if (i < n_w) return reinterpret_cast<const u32x4_t*>(at.qk_norm ? at.qn : at.qkv) + i;
+            i -= n_w;
+            if (i < n_w) return reinterpret_cast<const u32x4_t*>(at.qk_norm ? at.kn : at.qkv) + i;
+            return reinterpret_cast<const u32x4_t*>(at.rope + (size_t)cpos * hd) + (i - n_w);
+        };
+        auto dst1 = [&](int i) -> u32x4_t* { return reinterpret_cast<u32x4_t*>(raw_s) + i; };
+        constexpr int P1 = 4, P2 = 10;
+        u32x4_t c1[P1];
+        const int slot = at.row_slot[0];
+#pragma unroll
+        for (int q = 0; q < P1; ++q) {
+            const int i = threadIdx.x + NTH * q;
+            if (i < n1) c1[q] = *src1(i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) issue(u, u);
+        const int rc = hd / CE, n2 = nkv * 2 * cpos * rc;
+        const size_t cbase = (size_t)slot * at.slot_stride + at.layer_off;
+        auto src2 = [&](int i) -> const u32x4_t* {
+            const int row = i / rc, c = i - row * rc;
+            const int kvh = row / (2 * cpos), rem = row - kvh * 2 * cpos, which = rem / cpos, j = rem - which * cpos;
+            const T* base = (which ? at.vc : at.kc) + cbase + (size_t)kvh * at.S * hd + (size_t)j * hd;
+            return reinterpret_cast<const u32x4_t*>(base) + c;
+        };
+        u32x4_t c2[P2];
+#pragma unroll
+        for (int q = 0; q < P2; ++q) {
+            const int i = threadIdx.x + NTH * q;
+            if (i < n2) c2[q] = *src2(i);
+        }
+#pragma unroll
+        for (int q = 0; q < P1; ++q) {
+            const int i = threadIdx.x + NTH * q;
+            if (i < n1) *dst1(i) = c1[q];
+        }
+        for (int i = threadIdx.x + NTH * P1; i < n1; i += NTH) *dst1(i) = *src1(i);
+#pragma unroll
+        for (int q = 0; q < P2; ++q) {
+            const int i = threadIdx.x + NTH * q;
+            if (i < n2) reinterpret_cast<u32x4_t*>(kv_s)[i] = c2[q];
+        }
+        for (int i = threadIdx.x + NTH * P2; i < n2; i += NTH) reinterpret_cast<u32x4_t*>(kv_s)[i] = *src2(i);
+        __syncthreads();
+        const int h0 = kbeg / hd, h1 = (kbeg + Kb) / hd;
+        for (int hb = h0 + 8 * wave; hb < h1; hb += 8 * WPB)
+            fast_attn_heads8_lds<T>(at, hb, h1, lane, raw_s, kv_s, qn_s, kn_s, tab_s, xs + (size_t)(hb - h0) * hd,
+                                    blockIdx.x == 0, slot);
     } else {
         // PRO_PLAIN / PRO_PRENORM: (row, 8-element chunk) items of the slice, up to PRE_N per
         // thread preloaded ahead of the weight ring (the rest, large R x Kb only, after it)
@@ -498,16 +562,26 @@ template <typename T, int PRO, int EPI>
 static void gemv_go(hipStream_t s, const GemvArgs<T>& a, int ksb) {
     dim3 grid(FM_CEIL(a.N, 16), ksb);
     const int Kb = a.K / ksb;
-    const size_t lds = gemv_lds_bytes(a.R, Kb, sizeof(T));
+    size_t lds = gemv_lds_bytes(a.R, Kb, sizeof(T));
+    GemvArgs<T> b = a;
+    if constexpr (PRO == PRO_FATT) {
+        lds = (lds + 15) & ~(size_t)15;
+        b.fatt_off = (int)lds;
+        lds += fatt_lds_bytes(a.att.ldqkv, a.att.nkv, a.att.S, a.att.hd, sizeof(T));
+    }
     if (fm_tuning().gemv_nt)
-        gemv_go_u<T, PRO, EPI, true>(s, a, grid, lds);
+        gemv_go_u<T, PRO, EPI, true>(s, b, grid, lds);
     else
-        gemv_go_u<T, PRO, EPI, false>(s, a, grid, lds);
+        gemv_go_u<T, PRO, EPI, false>(s, b, grid, lds);
 }
 
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb) {
     // PRO_PRENORM stages the [K/16][R] tile sums in the 256 * R floats of the reduction buffer
     FMCHECK(pro != PRO_PRENORM || (a.K <= 4096 && a.R <= GEMV_RMAX), "PRO_PRENORM needs K <= 4096, R <= 8");
+    FMCHECK(pro != PRO_FATT || (a.R == 1 && a.att.cpos < FAST_ATTN_MAXJ && a.att.cpos < a.att.S &&
+                                (a.K / ksb) % a.att.hd == 0 && a.att.hd % 16 == 0 && a.att.hd <= 16 * FATT_MAXPP &&
+                                a.att.ldqkv % 8 == 0),
+            "PRO_FATT needs one row, cpos < 16, whole heads per K slice");
 #define GO(P, E)                                           \
     if (pro == P && epi == E) {                            \
         gemv_go<T, P, E>(s, a, ksb);                       \
@@ -517,6 +591,7 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
     GO(PRO_NORM, EPI_STORE) GO(PRO_NORM, EPI_SWIGLU) GO(PRO_NORM, EPI_F32)
     GO(PRO_PRENORM, EPI_STORE) GO(PRO_PRENORM, EPI_SWIGLU) GO(PRO_PRENORM, EPI_F32)
     GO(PRO_NORM, EPI_QKVATT) GO(PRO_PRENORM, EPI_QKVATT) GO(PRO_PRENORM, EPI_SWIGLU8)
+    GO(PRO_FATT, EPI_SLABFIN)
 #undef GO
 }
 

@@ -113,7 +113,10 @@ template <typename T>
 void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* dst);
 
 // ---- decode weight-streaming path (fm_gemv.hip), R <= 8 rows --------------------------------
-enum { PRO_PLAIN = 0, PRO_NORM = 1, PRO_PRENORM = 3 };
+enum { PRO_PLAIN = 0, PRO_NORM = 1, PRO_PRENORM = 3, PRO_FATT = 4 };
+// PRO_FATT (fast model, one row, cpos < 16): X' is the fast-model attention output, recomputed by
+// every block from the raw QKV row and the cached K/V rows staged in LDS (llama.py:947-975), so
+// the Wo GEMV needs no separate attention launch; blockIdx.x == 0 writes the new k / v of cpos.
 enum { EPI_SLAB = 4, EPI_SLABFIN = 5, EPI_QKVATT = 6, EPI_SWIGLU8 = 7 };
 // EPI_SWIGLU8: W is the row-interleaved W1||W3 (each 16-row tile = 8 gate rows then the same 8 up
 // rows, see pack_w13 in fm_llm.cpp); a tile yields 8 SwiGLU outputs, N = 2 * intermediate.
@@ -169,6 +172,7 @@ template <typename T> struct GemvArgs {
     int pro_exp;             // EXPERIMENT knob (see FmTuning)
     FastFusedArgs<T> att;    // EPI_QKVATT: the attention the group's last block runs
     int* att_tickets;        // EPI_QKVATT: per-kv-group arrival counters (zero between launches)
+    int fatt_off;            // PRO_FATT: byte offset of the attention staging area in LDS (launcher)
 };
 // developer knobs for the decode GEMV (fm_tune): weight load policy and split-K policy
 struct FmTuning {
@@ -181,11 +185,16 @@ struct FmTuning {
     int sampler_fast = 1;    // 1: two-stage register top-K sampler, 0: LDS radix-select sampler
     int attn_cap = 32;       // slow decode attention rows per block cap (0: the LDS-budget maximum)
     int attn_fuse = 0;       // 1: fast-model attention fused into the QKV GEMV's tail (EPI_QKVATT)
+    int attn_wo = 0;         // 1: fast-model attention recomputed in the Wo GEMV's prologue (PRO_FATT, R == 1; measured 0.37 ms/frame slower)
     int ksb_blocks = 512;    // split K until the grid has at least this many blocks
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
 };
 FmTuning& fm_tuning();
+// PRO_FATT staging: raw q|k|v row, cached K/V rows [nkv][2][S-1][hd], qk-norm weights, RoPE row
+inline size_t fatt_lds_bytes(int ldqkv, int nkv, int S, int hd, size_t esz) {
+    return ((size_t)ldqkv + (size_t)nkv * 2 * (S - 1) * hd + 2 * (size_t)hd) * esz + (size_t)hd * 4 + 64;
+}
 inline size_t gemv_lds_bytes(int R, int Kb, size_t esz) {
     return (size_t)R * (Kb + 8) * esz + 16 * sizeof(float) + (2 * 8 * 16 + 16) * (size_t)R * sizeof(float) +
            8 * 8 * sizeof(float);

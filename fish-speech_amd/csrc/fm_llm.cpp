@@ -312,6 +312,9 @@ template <typename T> struct Run {
         // fast model: attention runs in the QKV GEMV's tail (EPI_QKVATT) when it fits the tail
         const bool fuse = is_fast && fm_tuning().attn_fuse && cpos < 16 && d.nkv <= 256 && d.hd <= 256 &&
                           d.hd % 16 == 0 && d.nh % d.nkv == 0;
+        // ... or recomputed by every block of the Wo GEMV (PRO_FATT, one row): no attention launch
+        const bool att_wo = is_fast && !fuse && fm_tuning().attn_wo && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
+                            d.hd <= 128 && d.nh % d.nkv == 0 && (d.nq() / kp.wo) % d.hd == 0 && d.nqkv() % 8 == 0;
         // QKV (+ attention_norm)
         {
             GemvArgs<T> a = ga();
@@ -354,7 +357,7 @@ template <typename T> struct Run {
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
             m->prof.run(s, "attn", 0, 0, [&] { launch_attn_decode2<T>(s, aa, n); });
-        } else if (!fuse) {
+        } else if (!fuse && !att_wo) {
             m->prof.run(s, "attn", 0, 0, [&] {
                 if (cpos < 16 && d.hd <= 256)
                     launch_fast_attn2<T>(s, fa, n);
@@ -388,7 +391,12 @@ template <typename T> struct Run {
             a.ldro = d.dim;
             a.ss_out = m->ssH;
             a.tickets = m->tickets;
-            gemv(a, PRO_PLAIN, EPI_SLABFIN, kp.wo, "linear");
+            if (att_wo) {
+                a.att = fa;
+                gemv(a, PRO_FATT, EPI_SLABFIN, kp.wo, "linear");
+            } else {
+                gemv(a, PRO_PLAIN, EPI_SLABFIN, kp.wo, "linear");
+            }
         }
         // W1/W3 (+ ffn_norm) -> SwiGLU act
         {
@@ -1261,6 +1269,8 @@ int fm_tune(const char* key, int value) {
             t.attn_cap = value;
         } else if (k == "attn_fuse") {
             t.attn_fuse = value != 0;
+        } else if (k == "attn_wo") {
+            t.attn_wo = value != 0;
         } else if (k == "pro_exp") {
             t.pro_exp = value;
         } else if (k == "gemv_sk") {

@@ -78,6 +78,21 @@ class FishMICodec:
         native.check(native.lib().fm_codec_decode(self.h, native.i32p(cd), cd.shape[1], native.f32p(out)))
         return out
 
+    # ---- streamed decode (BASELINE config 5) -----------------------------------------------
+    def stream_reset(self):
+        """Start a new stream: the carried causal context is zeroed (== the causal padding)."""
+        native.check(native.lib().fm_codec_stream_reset(self.h))
+
+    def decode_chunk(self, codes: np.ndarray) -> np.ndarray:
+        """Next chunk of the stream: codes (C, T) int -> float32 PCM (2048*T,).  The chunks'
+        concatenated PCM equals decode_codes of the concatenated codes (causal decode with the
+        previous chunk's rows carried, fm_codec_decode_chunk)."""
+        cd = np.ascontiguousarray(codes, dtype=np.int32)
+        assert cd.ndim == 2 and cd.shape[0] == self.cfg.n_codebooks + 1
+        out = np.zeros(cd.shape[1] * self.frame_length, np.float32)
+        native.check(native.lib().fm_codec_decode_chunk(self.h, native.i32p(cd), cd.shape[1], native.f32p(out)))
+        return out
+
     def from_indices(self, indices) -> np.ndarray:
         idx = np.asarray(indices)
         if idx.ndim == 2:

@@ -24,8 +24,8 @@ ABI_SYMBOLS = [
     "fm_llm_finalize", "fm_llm_prefill", "fm_llm_decode", "fm_llm_decode_frames", "fm_llm_generate", "fm_llm_teacher_step",
     "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph", "fm_tune", "fm_debug_ts_read",
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
-    "fm_codec_finalize", "fm_codec_decode", "fm_codec_profile_read", "fm_codec_debug_read",
-    "fm_codec_close",
+    "fm_codec_finalize", "fm_codec_decode", "fm_codec_stream_reset", "fm_codec_decode_chunk",
+    "fm_codec_profile_read", "fm_codec_debug_read", "fm_codec_close",
 ]
 
 
@@ -79,6 +79,8 @@ def lib():
         L.fm_codec_synth_tensor.argtypes = [vp, ctypes.c_char_p, i64, u64, f32, i32]
         L.fm_codec_finalize.argtypes = [vp]
         L.fm_codec_decode.argtypes = [vp, pi32, i32, pf32]
+        L.fm_codec_stream_reset.argtypes = [vp]
+        L.fm_codec_decode_chunk.argtypes = [vp, pi32, i32, pf32]
         L.fm_codec_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_int64),
                                             ctypes.POINTER(ctypes.c_double)]

@@ -154,6 +154,15 @@ int fm_codec_finalize(fm_codec* h);
 /* codes: (n_codebooks+1) x T row-major (clamped like rvq.py:354-359, input not mutated);
    pcm: 2048*T floats in [-1, 1]. */
 int fm_codec_decode(fm_codec* h, const int32_t* codes, int T, float* pcm);
+/* Streamed decode (BASELINE config 5: long-form audio vocoded chunk by chunk while the LLM is
+   still generating; the reference decodes each generated segment on its own,
+   inference_engine/vq_manager.py:16-21).  The codec is causal end to end, so a stream of chunks
+   that carries each causal reader's previous rows (conv inputs, the transformer's window of
+   keys/values, the RoPE position) reproduces the one-shot fm_codec_decode of the concatenated
+   codes exactly.  One stream per handle: stream_reset starts it, each decode_chunk appends T
+   frames (T <= max_frames) and returns their 2048*T samples. */
+int fm_codec_stream_reset(fm_codec* h);
+int fm_codec_decode_chunk(fm_codec* h, const int32_t* codes, int T, float* pcm);
 int fm_codec_profile_read(fm_codec* h, double* total_ms, int64_t* launches, double* flops);
 /* test hook: intermediate of the last decode as fp32, time-major (1 transformer out [T][latent],
    2 first upsample [2T][latent], 3 decoder input [4T][latent]); other stages' buffers are

@@ -1,0 +1,54 @@
+"""GPU: streamed codec decode (BASELINE config 5's chunked vocoder) against the one-shot decode.
+
+The codec is causal end to end (causal convs, window-limited causal attention), so decoding a
+stream of chunks with each causal reader's previous rows carried (fm_codec_decode_chunk) must
+reproduce the one-shot decode of the concatenated codes.  Every output element is computed by the
+same kernels with the same operands in the same order, so the bound is bit-for-bit equality.
+"""
+import json
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _codec(golden, prec, max_frames):
+    from fishmi.codec import FishMICodec
+    from fishmi.config import CodecConfig
+
+    g = golden("codec_full.npz")
+    cfg = CodecConfig.from_spec(json.loads(str(g["spec"])))
+    return FishMICodec.synthetic(cfg, int(g["synth_seed"]), 0, prec, max_frames)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_streamed_chunks_equal_one_shot(prec, golden):
+    """300 frames (past the transformer's 128-frame window and every conv's receptive field)
+    decoded as ragged chunks give the one-shot waveform; a reset starts an independent stream."""
+    m = _codec(golden, prec, 320)
+    rng = np.random.default_rng(9)
+    C1, T = m.cfg.n_codebooks + 1, 300
+    codes = np.zeros((C1, T), np.int32)
+    codes[0] = rng.integers(0, m.cfg.semantic_codebook_size, T)
+    codes[1:] = rng.integers(0, m.cfg.codebook_size, (C1 - 1, T))
+    full = m.decode_codes(codes)
+    for sizes in ((1, 7, 22, 22, 100, 148), (22,) * 13 + (14,), (300,)):
+        m.stream_reset()
+        pcm, t = [], 0
+        for n in sizes:
+            pcm.append(m.decode_chunk(np.ascontiguousarray(codes[:, t:t + n])))
+            t += n
+        assert t == T
+        np.testing.assert_array_equal(np.concatenate(pcm), full)
+    m.close()
+
+
+def test_stream_rejects_oversized_chunk(golden):
+    from fishmi.native import FishMIError
+
+    m = _codec(golden, "bf16", 16)
+    m.stream_reset()
+    with pytest.raises(FishMIError):
+        m.decode_chunk(np.zeros((m.cfg.n_codebooks + 1, 17), np.int32))
+    m.close()

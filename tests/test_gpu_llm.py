@@ -265,3 +265,20 @@ def test_fast_sampler_equals_radix_sampler(golden):
     m.use_graph(True)
     for a, b in zip(outs[1], outs[0]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["llm_a", "llm_b"])
+def test_fast_attention_in_wo_prologue(name, golden):
+    """fm_tune attn_wo=1 (PRO_FATT): the fast model's attention recomputed by every block of the
+    Wo GEMV from LDS-staged operands gives the same fp32 greedy stream as the reference."""
+    from fishmi import native
+
+    native.tune("attn_wo", 1)
+    try:
+        m, g, _ = _model(name, "fp32", golden)
+        T = g["prompt"].shape[1]
+        ref = g["seq"][:, T:]
+        out = m.generate(g["prompt"], ref.shape[1], top_k=1)
+        np.testing.assert_array_equal(out, ref)
+    finally:
+        native.tune("attn_wo", 0)
