@@ -25,6 +25,10 @@ template <typename T> struct LinearArgs {
     const T* res;    // residual [R][ldr] (EPI_RESID)
     int ldr;
     float* Yf;       // fp32 output (EPI_F32)
+    // split-K (gridDim.y > 1, R <= 16 * NCG): fp32 tile partials [ksb][NACC][R][N] and one arrival
+    // counter per 16-row tile (zero between launches; the last-arriving block resets it)
+    float* part = nullptr;
+    int* tickets = nullptr;
 };
 
 template <typename T> struct QkArgs {
@@ -98,6 +102,8 @@ template <typename T>
 void launch_rmsnorm(hipStream_t s, const T* x, int ldx, const T* w, int d, float eps, T* y,
                     int ldy, int R);
 template <typename T> void launch_linear(hipStream_t s, const LinearArgs<T>& a, int epi);
+constexpr size_t LINEAR_PART_CAP = (size_t)8 << 20;     // floats of split-K partials (= fm_llm skpart)
+int linear_ksb(int N, int K, int R, int nacc, bool can_split);
 template <typename T> void launch_qk_rope_cache(hipStream_t s, const QkArgs<T>& a, int R);
 template <typename T>
 void launch_attn(hipStream_t s, const AttnArgs<T>& a, int R, int nsplit, T* out);
@@ -187,6 +193,15 @@ struct FmTuning {
     int attn_fuse = 0;       // 1: fast-model attention fused into the QKV GEMV's tail (EPI_QKVATT)
     int attn_wo = 0;         // 1: fast-model attention recomputed in the Wo GEMV's prologue (PRO_FATT, R == 1; measured 0.37 ms/frame slower)
     int ksb_blocks = 512;    // split K until the grid has at least this many blocks
+    int batched_fused_attn = 1;  // batched decode (one row per slot): fused QK-norm/RoPE/KV-write attention kernels
+    int attn_cap_batched = 128;  // rows per block of the batched decode attention (one row per slot)
+    int linear_u32 = 4;      // linear_kernel weight fragments in flight per wave at 16 < R <= 32 (4 or 8)
+    int linear_fill = 0;     // batched linear_kernel: split K until this many blocks (0: never; measured slower)
+    int bgemv = 0;           // 1: batched decode linears (8 < R <= 32) on bgemv_kernel (measured slower at B=32), 0: linear_kernel
+    int bgemv_u = 8;         // bgemv weight fragments in flight per wave (4 or 8)
+    int bgemv_tpb = 4;       // bgemv max 16-row tiles per block sharing one staged X slice (1, 2, 4)
+    int bgemv_lds_kb = 84;   // bgemv X-slice LDS budget (KiB) before splitting K
+    int bgemv_fill = 512;    // bgemv: split K until the grid has this many blocks
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
 };
@@ -200,6 +215,27 @@ inline size_t gemv_lds_bytes(int R, int Kb, size_t esz) {
            8 * 8 * sizeof(float);
 }
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb);
+
+// ---- batched decode weight streaming, 8 < R <= 32 rows (fm_bgemv.hip) ---------------------------
+template <typename T> struct BgemvArgs {
+    const T* W;      // packed MFMA-fragment layout [tiles][K/32][512]
+    const T* bias;   // [N] or null
+    const T* X;      // [R][ldx]
+    int ldx, R, N, K;
+    T* Y;            // EPI_STORE / EPI_RESID [R][ldy]
+    int ldy;
+    const T* res;    // EPI_RESID residual [R][ldr] (may alias Y)
+    int ldr;
+    float* Yf;       // EPI_F32 [R][ldy]
+    float* part;     // split-K partials [ksb][R][N] (<= LINEAR_PART_CAP floats)
+    int* tickets;    // one arrival counter per block column (zero between launches)
+    int tpb = 1;     // set by the launcher
+};
+struct BgemvPlan {
+    int tpb, ksb;
+};
+BgemvPlan bgemv_plan(int N, int K, int R, size_t esz);
+template <typename T> void launch_bgemv(hipStream_t s, const BgemvArgs<T>& a, int epi);
 // stream-K decode GEMV; returns false (nothing launched) when the shape is not eligible
 template <typename T> bool launch_gemv_sk(hipStream_t s, const GemvArgs<T>& a, int pro, int epi);
 

@@ -211,17 +211,31 @@ template <typename T> struct Run {
     fm_llm* m;
     hipStream_t s;
     int64_t E;  // element size
+    bool rows_distinct_slots = false;  // slow_layers rows are one per slot (batched decode frame)
     explicit Run(fm_llm* mm) : m(mm), s(mm->stream), E(sizeof(T)) {}
 
     void linear(const void* W, const void* W2, const void* bias, const void* X, int ldx, int R, int N,
                 int K, void* Y, int ldy, const void* res, int ldr, float* Yf, int epi, const char* cls) {
         LinearArgs<T> a{(const T*)W, (const T*)W2, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y,
                         ldy, (const T*)res, ldr, Yf};
+        if (R > GEMV_MAX_ROWS && R <= 64) {  // batched decode: split-K over the idle CUs
+            FMCHECK(m->skpart_cap >= (long long)LINEAR_PART_CAP, "split-K partial buffer too small");
+            a.part = m->skpart;
+            a.tickets = m->tickets;
+        }
+        const bool bg = fm_tuning().bgemv && R > GEMV_MAX_ROWS && R <= 32 && epi != EPI_SWIGLU && K % 32 == 0;
+        BgemvArgs<T> b{(const T*)W, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y, ldy, (const T*)res, ldr,
+                       Yf, m->skpart, m->tickets};
         const int64_t wbytes = (int64_t)N * K * E * (epi == EPI_SWIGLU ? 2 : 1);
         const int64_t bytes = wbytes + (int64_t)R * K * E + (int64_t)R * N * (epi == EPI_F32 ? 4 : E);
         const double flops = 2.0 * R * N * K * (epi == EPI_SWIGLU ? 2 : 1);
         hipStream_t st = s;
-        auto go = [st, a, epi] { launch_linear<T>(st, a, epi); };
+        auto go = [st, a, b, bg, epi] {
+            if (bg)
+                launch_bgemv<T>(st, b, epi);
+            else
+                launch_linear<T>(st, a, epi);
+        };
         m->prof.record(cls, bytes, go);
         m->prof.run(s, cls, bytes, flops, go);
     }
@@ -236,18 +250,41 @@ template <typename T> struct Run {
         });
         linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
                nullptr, EPI_STORE, "linear");
-        QkArgs<T> qa{(const T*)m->qkv, d.nqkv(), rslot, rpos, fixed_pos, d.nh, d.nkv, d.hd, d.qk_norm,
-                     eps, (const T*)L.qn, (const T*)L.kn, rope, (T*)m->q, (T*)kc, (T*)vc, sstride, loff, Sc};
-        m->prof.run(s, "rope", 0, 0, [&] { launch_qk_rope_cache<T>(s, qa, R); });
         const float scale = 1.0f / sqrtf((float)d.hd);
-        if (!is_fast) {
-            AttnArgs<T> aa{(const T*)m->q, rslot, rpos, (const T*)kc, (const T*)vc, sstride, loff, Sc,
-                           d.nh, d.nkv, d.hd, ATTN_SPLIT, m->maxsplit, scale, m->part};
-            m->prof.run(s, "attn", 0, 0, [&] { launch_attn<T>(s, aa, R, m->maxsplit, (T*)m->att); });
+        // One row per slot (batched decode frames, every fast pass): the fused decode attention
+        // kernels of the small-batch path do QK-norm, RoPE and the KV write themselves.  Prompt
+        // chunks (rows of one slot, causal among themselves) keep the separate write + attention.
+        const bool rows_are_slots = is_fast || rows_distinct_slots;
+        if (rows_are_slots && !is_fast && fm_tuning().batched_fused_attn) {
+            AttnDecArgs<T> aa{(const T*)m->qkv, d.nqkv(), rslot, rpos, d.nh, d.nkv, d.hd, d.qk_norm, eps,
+                              (const T*)L.qn, (const T*)L.kn, rope, (T*)kc, (T*)vc, sstride, loff, Sc,
+                              m->maxsplit, scale, m->part};
+            aa.cap = attn2_cap(d.hd, d.nh / d.nkv, E);
+            if (fm_tuning().attn_cap_batched) aa.cap = std::min(aa.cap, fm_tuning().attn_cap_batched);
+            aa.maxsplit = FM_CEIL(Sc, aa.cap);
+            aa.cnt = m->attn_cnt;
+            aa.dbg = fm_tuning().dbg;
+            aa.out = (T*)m->att;
+            m->prof.run(s, "attn", 0, 0, [&] { launch_attn_decode2<T>(s, aa, R); });
+        } else if (is_fast && fm_tuning().batched_fused_attn && fixed_pos >= 0 && fixed_pos < 16 && d.hd <= 256) {
+            FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), rslot, d.nh, d.nkv, d.hd, d.qk_norm, eps,
+                                (const T*)L.qn, (const T*)L.kn, rope, (T*)kc, (T*)vc, sstride, loff, Sc,
+                                fixed_pos, scale, (T*)m->att};
+            fa.dbg = fm_tuning().dbg;
+            m->prof.run(s, "attn", 0, 0, [&] { launch_fast_attn2<T>(s, fa, R); });
         } else {
-            FastAttnArgs<T> fa{(const T*)m->q, rslot, (const T*)kc, (const T*)vc, sstride, loff, Sc,
-                               d.nh, d.nkv, d.hd, fixed_pos, scale, (T*)m->att};
-            m->prof.run(s, "attn", 0, 0, [&] { launch_fast_attn<T>(s, fa, R); });
+            QkArgs<T> qa{(const T*)m->qkv, d.nqkv(), rslot, rpos, fixed_pos, d.nh, d.nkv, d.hd, d.qk_norm,
+                         eps, (const T*)L.qn, (const T*)L.kn, rope, (T*)m->q, (T*)kc, (T*)vc, sstride, loff, Sc};
+            m->prof.run(s, "rope", 0, 0, [&] { launch_qk_rope_cache<T>(s, qa, R); });
+            if (!is_fast) {
+                AttnArgs<T> aa{(const T*)m->q, rslot, rpos, (const T*)kc, (const T*)vc, sstride, loff, Sc,
+                               d.nh, d.nkv, d.hd, ATTN_SPLIT, m->maxsplit, scale, m->part};
+                m->prof.run(s, "attn", 0, 0, [&] { launch_attn<T>(s, aa, R, m->maxsplit, (T*)m->att); });
+            } else {
+                FastAttnArgs<T> fa{(const T*)m->q, rslot, (const T*)kc, (const T*)vc, sstride, loff, Sc,
+                                   d.nh, d.nkv, d.hd, fixed_pos, scale, (T*)m->att};
+                m->prof.run(s, "attn", 0, 0, [&] { launch_fast_attn<T>(s, fa, R); });
+            }
         }
         linear(L.wo, nullptr, L.bo, m->att, d.nq(), R, d.dim, d.nq(), hb, d.dim, xb, d.dim, nullptr,
                EPI_RESID, "linear");
@@ -627,7 +664,9 @@ template <typename T> struct Run {
                             m->c.semantic_begin_id, m->c.semantic_end_id, m->c.scale_codebook_embeddings,
                             (T*)m->x, m->frame_slot);
         });
+        rows_distinct_slots = true;
         slow_layers(n, m->frame_slot, m->frame_pos);
+        rows_distinct_slots = false;
         head_and_hidden(m->x, n);
         frame_tail(n, true, true);
         launch_finish(s, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10,
@@ -827,7 +866,7 @@ static void finalize(fm_llm* m) {
     m->ssH = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
     {
         // arrival counters: one per 16-row tile of the largest decode GEMV (the slow head / W13)
-        const int maxn = std::max({m->Nhead, c.intermediate_size, c.fast_intermediate_size, qkvmax, dmax, m->cb});
+        const int maxn = std::max({m->Nhead, 2 * c.intermediate_size, 2 * c.fast_intermediate_size, qkvmax, dmax, m->cb});  // W1||W3 is one 2*I-row linear on the batched path
         m->tickets = (int*)m->dalloc((size_t)(maxn / 16 + 16) * sizeof(int));
         m->skpart_cap = 8ll << 20;  // 32 MiB of partial tiles
         m->skpart = (float*)m->dalloc((size_t)m->skpart_cap * sizeof(float), false);
@@ -1284,6 +1323,31 @@ int fm_tune(const char* key, int value) {
         } else if (k == "ksb_blocks") {
             FMCHECK(value >= 1, "ksb_blocks must be >= 1");
             t.ksb_blocks = value;
+        } else if (k == "bgemv") {
+            t.bgemv = value != 0;
+        } else if (k == "bgemv_u") {
+            FMCHECK(value == 4 || value == 8, "bgemv_u must be 4 or 8");
+            t.bgemv_u = value;
+        } else if (k == "bgemv_tpb") {
+            FMCHECK(value == 1 || value == 2 || value == 4, "bgemv_tpb must be 1, 2 or 4");
+            t.bgemv_tpb = value;
+        } else if (k == "bgemv_lds_kb") {
+            FMCHECK(value >= 16 && value <= 140, "bgemv_lds_kb must be in [16, 140]");
+            t.bgemv_lds_kb = value;
+        } else if (k == "bgemv_fill") {
+            FMCHECK(value >= 1, "bgemv_fill must be >= 1");
+            t.bgemv_fill = value;
+        } else if (k == "attn_cap_batched") {
+            FMCHECK(value == 0 || (value >= 16 && value % 16 == 0), "attn_cap_batched must be 0 or a multiple of 16");
+            t.attn_cap_batched = value;
+        } else if (k == "linear_u32") {
+            FMCHECK(value == 4 || value == 8, "linear_u32 must be 4 or 8");
+            t.linear_u32 = value;
+        } else if (k == "batched_fused_attn") {
+            t.batched_fused_attn = value != 0;
+        } else if (k == "linear_fill") {
+            FMCHECK(value >= 0, "linear_fill must be >= 0");
+            t.linear_fill = value;
         } else if (k == "ksb_balance") {
             t.ksb_balance = value != 0;
         } else if (k == "debug_ts") {  // (re)arm the per-block timestamp buffer; 0 frees it

@@ -181,17 +181,40 @@ template <> struct Mfma<float> {
 
 __device__ __forceinline__ float silu_f(float a) { return a / (1.0f + expf(-a)); }
 
-template <typename T, int NCG, int EPI>
+template <typename T, int EPI>
+__device__ __forceinline__ void linear_epi(const LinearArgs<T>& a, int n, int col, float v0, float v1) {
+    const size_t yi = (size_t)col * a.ldy + n;
+    if (a.bias) v0 += ld(a.bias, n);
+    if constexpr (EPI == EPI_STORE) {
+        st(a.Y, yi, v0);
+    } else if constexpr (EPI == EPI_RESID) {
+        st(a.Y, yi, ld(a.res, (size_t)col * a.ldr + n) + rnd<T>(v0));
+    } else if constexpr (EPI == EPI_SWIGLU) {
+        const float ga = rnd<T>(v0), ub = rnd<T>(v1);
+        st(a.Y, yi, rnd<T>(silu_f(ga)) * ub);
+    } else {  // EPI_F32: logits as fp32 holding the T-rounded value
+        a.Yf[yi] = rnd<T>(v0);
+    }
+}
+
+// grid = (N/16 tiles, ksb K-slices).  ksb > 1 (host: R <= 16 * NCG): every block reduces its
+// waves in LDS, stores its fp32 tile partial write-through (sc1), drains, takes a relaxed agent
+// ticket; the tile's last-arriving block sums the ksb partials in slice order (deterministic)
+// with sc1 loads and runs the epilogue (cdna_hip_programming.md split-K recipe, the same hand-off
+// as gemv_kernel's EPI_SLABFIN).
+template <typename T, int NCG, int EPI, int U>
 __global__ __launch_bounds__(512) void linear_kernel(LinearArgs<T> a) {
     using M = Mfma<T>;
     constexpr int NACC = (EPI == EPI_SWIGLU) ? 2 : 1;
-    constexpr int U = (NCG == 1) ? 8 : 4;
     __shared__ f32x4_t red[8][NACC * NCG][64];
+    __shared__ int last_flag;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n0 = blockIdx.x * 16;
     const int r = lane & 15, g = lane >> 4;
     const int nsteps = a.K >> 5;
-    const int s0 = (wave * nsteps) >> 3, s1 = ((wave + 1) * nsteps) >> 3;
+    const int ksb = gridDim.y, ks = blockIdx.y;
+    const int b0 = (ks * nsteps) / ksb, b1 = ((ks + 1) * nsteps) / ksb;
+    const int s0 = b0 + ((wave * (b1 - b0)) >> 3), s1 = b0 + (((wave + 1) * (b1 - b0)) >> 3);
     // packed weights: block (tile, step) = 512 elements
     const T* wp = a.W + (size_t)blockIdx.x * nsteps * 512;
     const T* wp2 = (EPI == EPI_SWIGLU) ? a.W2 + (size_t)blockIdx.x * nsteps * 512 : nullptr;
@@ -242,7 +265,7 @@ __global__ __launch_bounds__(512) void linear_kernel(LinearArgs<T> a) {
 #pragma unroll
             for (int c = 0; c < NCG; ++c) red[wave][q * NCG + c][lane] = acc[q][c];
         __syncthreads();
-        // epilogue: 16 rows x (16*NCG) cols; C/D map: row = 4*(lane>>4)+i, col = lane&15
+        // 16 rows x (16*NCG) cols; C/D map: row = 4*(lane>>4)+i, col = lane&15
         for (int o = threadIdx.x; o < 256 * NCG; o += 512) {
             const int c = o >> 8, rem = o & 255, i = rem >> 6, ln = rem & 63;
             const int n = n0 + 4 * (ln >> 4) + i;
@@ -254,18 +277,39 @@ __global__ __launch_bounds__(512) void linear_kernel(LinearArgs<T> a) {
                 if constexpr (NACC == 2) v1 += red[w][NCG + c][ln][i];
             }
             if (n < a.N && col < a.R) {
-                const size_t yi = (size_t)col * a.ldy + n;
-                if (a.bias) v0 += ld(a.bias, n);
-                if constexpr (EPI == EPI_STORE) {
-                    st(a.Y, yi, v0);
-                } else if constexpr (EPI == EPI_RESID) {
-                    st(a.Y, yi, ld(a.res, (size_t)col * a.ldr + n) + rnd<T>(v0));
-                } else if constexpr (EPI == EPI_SWIGLU) {
-                    const float ga = rnd<T>(v0), ub = rnd<T>(v1);
-                    st(a.Y, yi, rnd<T>(silu_f(ga)) * ub);
-                } else {  // EPI_F32: logits as fp32 holding the T-rounded value
-                    a.Yf[yi] = rnd<T>(v0);
+                if (ksb == 1) {
+                    linear_epi<T, EPI>(a, n, col, v0, v1);
+                } else {
+                    float* pp = a.part + (((size_t)ks * NACC) * a.R + col) * a.N + n;
+                    __hip_atomic_store(pp, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if constexpr (NACC == 2)
+                        __hip_atomic_store(pp + (size_t)a.R * a.N, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
+            }
+        }
+        if (ksb > 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const int t = __hip_atomic_fetch_add(a.tickets + blockIdx.x, 1, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                const int last = t == ksb - 1;
+                if (last) __hip_atomic_store(a.tickets + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last_flag = last;
+            }
+            __syncthreads();
+            if (!last_flag) return;  // host guarantees a single column group (R <= 16 * NCG)
+            for (int o = threadIdx.x; o < 16 * a.R; o += 512) {
+                const int col = o >> 4, n = n0 + (o & 15);
+                if (n >= a.N) continue;
+                float v0 = 0.f, v1 = 0.f;
+                for (int q = 0; q < ksb; ++q) {
+                    const float* pp = a.part + (((size_t)q * NACC) * a.R + col) * a.N + n;
+                    v0 += __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if constexpr (NACC == 2)
+                        v1 += __hip_atomic_load(pp + (size_t)a.R * a.N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                linear_epi<T, EPI>(a, n, col, v0, v1);
             }
         }
         __syncthreads();
@@ -682,15 +726,33 @@ void launch_rmsnorm(hipStream_t s, const T* x, int ldx, const T* w, int d, float
     rmsnorm_kernel<T><<<R, 256, 0, s>>>(x, ldx, w, d, eps, y, ldy);
 }
 
+// K-slices for the batched decode path: enough blocks to cover the chip (>= tu.linear_fill), each
+// slice at least 8 k-steps (one per wave), one column group (R <= 64), partials within the
+// caller's buffer (LINEAR_PART_CAP floats)
+int linear_ksb(int N, int K, int R, int nacc, bool can_split) {
+    const FmTuning& tu = fm_tuning();
+    if (!can_split || R > 64 || tu.linear_fill <= 0) return 1;
+    const int tiles = FM_CEIL(N, 16), nsteps = K >> 5;
+    int ksb = 1;
+    while (ksb < 16 && tiles * ksb < tu.linear_fill && nsteps / (2 * ksb) >= 8 &&
+           (size_t)2 * ksb * nacc * R * N <= LINEAR_PART_CAP)
+        ksb *= 2;
+    return ksb;
+}
+
 template <typename T, int EPI>
 static void linear_dispatch(hipStream_t s, const LinearArgs<T>& a) {
-    const int grid = FM_CEIL(a.N, 16);
+    const int tiles = FM_CEIL(a.N, 16);
+    dim3 grid(tiles, linear_ksb(a.N, a.K, a.R, EPI == EPI_SWIGLU ? 2 : 1, a.part != nullptr && a.tickets != nullptr));
     if (a.R <= 16)
-        linear_kernel<T, 1, EPI><<<grid, 512, 0, s>>>(a);
-    else if (a.R <= 32)
-        linear_kernel<T, 2, EPI><<<grid, 512, 0, s>>>(a);
-    else
-        linear_kernel<T, 4, EPI><<<grid, 512, 0, s>>>(a);
+        linear_kernel<T, 1, EPI, 8><<<grid, 512, 0, s>>>(a);
+    else if (a.R <= 32) {
+        if (fm_tuning().linear_u32 == 8)
+            linear_kernel<T, 2, EPI, 8><<<grid, 512, 0, s>>>(a);
+        else
+            linear_kernel<T, 2, EPI, 4><<<grid, 512, 0, s>>>(a);
+    } else
+        linear_kernel<T, 4, EPI, 4><<<grid, 512, 0, s>>>(a);
 }
 template <typename T> void launch_linear(hipStream_t s, const LinearArgs<T>& a, int epi) {
     switch (epi) {

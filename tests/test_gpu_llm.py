@@ -225,6 +225,80 @@ def test_decode_frames_matches_generate(golden):
         np.testing.assert_array_equal(got, single[s])
 
 
+@pytest.fixture
+def knob():
+    """fm_tune knobs set by a test, restored to their defaults afterwards."""
+    from fishmi import native
+
+    set_ = {}
+
+    def put(key, value, default):
+        set_[key] = default
+        native.tune(key, value)
+
+    yield put
+    for k, d in set_.items():
+        native.tune(k, d)
+
+
+@pytest.mark.parametrize("bgemv", [0, 1])
+@pytest.mark.parametrize("n", [12, 20])
+def test_batched_slots_past_gemv_match_single(n, bgemv, golden, knob):
+    """Config-3 batching past the batch-1 GEMV (n > 8 slots) gives each slot its own batch-1
+    greedy stream (fp32 mode): the MFMA linear_kernel (default) and the opt-in batched weight
+    stream bgemv_kernel (one or two MFMA column groups)."""
+    from fishmi.llm import DualARModel
+
+    knob("bgemv", bgemv, 0)
+
+    m, g, cfg = _model("llm_b", "fp32", golden, max_slots=n)
+    rng = np.random.default_rng(7)
+    prompts = []
+    for s in range(n):
+        p = g["prompt"].copy()
+        p[0, 1:5] = rng.integers(16, cfg.semantic_begin_id, 4)
+        prompts.append(p)
+    n_new = 10
+    single = [m.generate(p, n_new, top_k=1, slot=s, mask_im_end=True) for s, p in enumerate(prompts)]
+    sp = DualARModel.sampling(top_k=1, mask_im_end=True)
+    firsts = [m.prefill(s, p, sp) for s, p in enumerate(prompts)]
+    fr = m.decode_frames(list(range(n)), n_new - 1)
+    for s in range(n):
+        got = np.concatenate([firsts[s][:, None], fr[:, s, :].T], axis=1)
+        np.testing.assert_array_equal(got, single[s])
+
+
+@pytest.mark.parametrize("knobs", [{"bgemv": 1}, {"linear_fill": 1024}])
+def test_batched_wide_split_k_matches_single(knobs, golden, knob):
+    """S2-Pro widths, 20 slots: the opt-in split-K forms (bgemv_kernel, and linear_kernel with
+    linear_fill) -- sc1 partials + ticketed last-slice reduction -- reproduce every slot's batch-1
+    greedy stream (fp32 mode)."""
+    from fishmi.llm import DualARModel
+
+    for k, v in knobs.items():
+        knob(k, v, 0)
+
+    g = golden("llm_wide_bf16.npz")
+    cfg = _cfg("llm_wide")
+    n = 20
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "fp32", n)
+    rng = np.random.default_rng(9)
+    prompts = []
+    for s in range(n):
+        p = g["prompt"].copy()
+        p[0, 1:5] = rng.integers(16, cfg.semantic_begin_id, 4)
+        prompts.append(p)
+    n_new = 4
+    single = [m.generate(p, n_new, top_k=1, slot=s, mask_im_end=True) for s, p in enumerate(prompts)]
+    sp = DualARModel.sampling(top_k=1, mask_im_end=True)
+    firsts = [m.prefill(s, p, sp) for s, p in enumerate(prompts)]
+    fr = m.decode_frames(list(range(n)), n_new - 1)
+    for s in range(n):
+        got = np.concatenate([firsts[s][:, None], fr[:, s, :].T], axis=1)
+        np.testing.assert_array_equal(got, single[s])
+    m.close()
+
+
 def test_long_context_split_attention_matches_oracle(golden):
     """Contexts longer than one attention block's rows (256 here) take the split path of the
     decode attention (per-split partials + last-arriver combine): greedy stream == oracle."""
