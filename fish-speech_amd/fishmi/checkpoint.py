@@ -271,3 +271,73 @@ def iter_synth(shapes, seed: int, rule) -> Iterator[tuple]:
 def env_bool(name: str, default: bool = False) -> bool:
     v = os.environ.get(name)
     return default if v is None else v not in ("0", "", "false", "False")
+
+
+ENCODER_RATES = (2, 4, 8, 8)   # DAC encoder_rates (modded_dac_vq.yaml)
+ENCODER_WINDOW = 512           # EncoderBlock transformer window: getattr(partial, "window_size", 512)
+
+
+def codec_encoder_tensor_shapes(c: CodecConfig, encoder_dim: int = 64,
+                                enc_layers=(0, 0, 0, 4)) -> "OrderedDict[str, tuple]":
+    """Encode-side keys of the modded DAC state dict: Encoder (modded_dac.py:623-709), the
+    quantizer's downsample + pre_module (rvq.py:193-276) and the VQ in_proj (descript)."""
+    s = OrderedDict()
+    D, cd = c.latent, c.codebook_dim
+
+    def wn(p, co, ci, k):
+        s[p + "conv.parametrizations.weight.original0"] = (co, 1, 1)
+        s[p + "conv.parametrizations.weight.original1"] = (co, ci, k)
+        s[p + "conv.bias"] = (co,)
+
+    def transformer(p, dim, layers, heads, hd, inter):
+        for l in range(layers):
+            q = f"{p}layers.{l}."
+            s[q + "attention.wqkv.weight"] = (3 * heads * hd, dim)
+            s[q + "attention.wo.weight"] = (dim, heads * hd)
+            s[q + "feed_forward.w1.weight"] = (inter, dim)
+            s[q + "feed_forward.w3.weight"] = (inter, dim)
+            s[q + "feed_forward.w2.weight"] = (dim, inter)
+            s[q + "ffn_norm.weight"] = (dim,)
+            s[q + "attention_norm.weight"] = (dim,)
+            s[q + "attention_layer_scale.gamma"] = (dim,)
+            s[q + "ffn_layer_scale.gamma"] = (dim,)
+        if layers:
+            s[p + "norm.weight"] = (dim,)
+
+    wn("encoder.block.0.", encoder_dim, 1, 7)
+    d = encoder_dim
+    for b, (st, nl) in enumerate(zip(ENCODER_RATES, enc_layers)):
+        h, d = d, d * 2
+        p = f"encoder.block.{b + 1}.block."
+        for r in range(3):
+            rp = f"{p}{r}.block."
+            s[rp + "0.alpha"] = (1, h, 1)
+            wn(rp + "1.", h, h, 7)
+            s[rp + "2.alpha"] = (1, h, 1)
+            wn(rp + "3.", h, h, 1)
+        s[p + "3.alpha"] = (1, h, 1)
+        wn(p + "4.", d, h, 2 * st)
+        transformer(p + "5.", d, nl, d // 64, 64, 3 * d)
+    s["encoder.block.5.alpha"] = (1, d, 1)
+    wn("encoder.block.6.", D, d, 3)
+    for i in range(2):
+        p = f"quantizer.downsample.{i}."
+        s[p + "0.conv.weight"] = (D, D, 2)
+        s[p + "0.conv.bias"] = (D,)
+        s[p + "1.dwconv.conv.weight"] = (D, 1, 7)
+        s[p + "1.dwconv.conv.bias"] = (D,)
+        s[p + "1.norm.weight"] = (D,)
+        s[p + "1.norm.bias"] = (D,)
+        s[p + "1.pwconv1.weight"] = (4 * D, D)
+        s[p + "1.pwconv1.bias"] = (4 * D,)
+        s[p + "1.pwconv2.weight"] = (D, 4 * D)
+        s[p + "1.pwconv2.bias"] = (D,)
+        s[p + "1.gamma"] = (D,)
+    transformer("quantizer.pre_module.", D, c.t_layers, c.t_heads, c.t_head_dim, c.t_inter)
+    for q in range(c.n_codebooks + 1):
+        p = ("quantizer.semantic_quantizer.quantizers.0." if q == 0
+             else f"quantizer.quantizer.quantizers.{q - 1}.")
+        s[p + "in_proj.weight_g"] = (cd, 1, 1)
+        s[p + "in_proj.weight_v"] = (cd, D, 1)
+        s[p + "in_proj.bias"] = (cd,)
+    return s

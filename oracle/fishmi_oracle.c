@@ -865,10 +865,11 @@ static void rms_rows(const float* x, int T, int D, const float* w, float eps, fl
     }
 }
 
-/* WindowLimitedTransformer.forward (modded_dac.py:418-439) on x [T][D] in place. */
-static int window_transformer(orc_codec* m, float* x, int T) {
+/* WindowLimitedTransformer.forward (modded_dac.py:418-439) on x [T][D] in place: layers at
+   `pre`layers.<l>., final norm `pre`norm.weight; causal window `window`. */
+static int window_transformer_at(orc_codec* m, const char* pre, float* x, int T, int D, int H, int hd,
+                                 int I, int nlayers, int window) {
     const orc_codec_config* c = &m->c;
-    const int D = c->latent, H = c->t_heads, hd = c->t_head_dim, I = c->t_inter;
     int bad = 0;
     char nm[200];
     float* xn = (float*)malloc(sizeof(float) * (size_t)T * D);
@@ -890,10 +891,9 @@ static int window_transformer(orc_codec* m, float* x, int T) {
             }
         }
     }
-    const char* pre = "quantizer.post_module.layers.";
-    for (int l = 0; l < c->t_layers; ++l) {
+    for (int l = 0; l < nlayers; ++l) {
 #define CW(var, suffix, cnt) \
-    snprintf(nm, sizeof nm, "%s%d.%s", pre, l, suffix); const float* var = cget(m, nm, cnt, &bad);
+    snprintf(nm, sizeof nm, "%slayers.%d.%s", pre, l, suffix); const float* var = cget(m, nm, cnt, &bad);
         CW(an, "attention_norm.weight", D);
         CW(wqkv, "attention.wqkv.weight", (int64_t)3 * H * hd * D);
         CW(wo, "attention.wo.weight", (int64_t)D * H * hd);
@@ -924,7 +924,7 @@ static int window_transformer(orc_codec* m, float* x, int T) {
         for (int t = 0; t < T; ++t)
             for (int h = 0; h < H; ++h) {
                 const float* q = qkv + (size_t)t * ld + h * hd;
-                int j0 = t - c->window + 1;
+                int j0 = t - window + 1;
                 if (j0 < 0) j0 = 0;
                 float sc[4096];
                 float mx = -INFINITY;
@@ -955,7 +955,8 @@ static int window_transformer(orc_codec* m, float* x, int T) {
         for (size_t i = 0; i < (size_t)T * D; ++i) x[i] = x[i] + o[i] * fg[i % D];
     }
     if (!bad) {
-        const float* nw = cget(m, "quantizer.post_module.norm.weight", D, &bad);
+        snprintf(nm, sizeof nm, "%snorm.weight", pre);
+        const float* nw = cget(m, nm, D, &bad);
         if (!bad) {
             rms_rows(x, T, D, nw, c->norm_eps, xn);
             memcpy(x, xn, sizeof(float) * (size_t)T * D);
@@ -963,6 +964,12 @@ static int window_transformer(orc_codec* m, float* x, int T) {
     }
     free(xn); free(qkv); free(y); free(t1); free(t3); free(o); free(tab);
     return bad ? -1 : 0;
+}
+
+static int window_transformer(orc_codec* m, float* x, int T) {
+    const orc_codec_config* c = &m->c;
+    return window_transformer_at(m, "quantizer.post_module.", x, T, c->latent, c->t_heads, c->t_head_dim,
+                                 c->t_inter, c->t_layers, c->window);
 }
 
 /* ConvNeXtBlock (rvq.py:129-191) on x [D][L] in place. */
@@ -1217,4 +1224,251 @@ int orc_op_rope(const float* x, const float* tab_rows /* rows x hd */, int rows,
     memcpy(y, x, sizeof(float) * (size_t)rows * hd);
     for (int r = 0; r < rows; ++r) rope(&tmp, y + (size_t)r * hd, tab_rows + (size_t)r * hd, hd);
     return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Codec ENCODE (fp32): DAC.encode (modded_dac.py:874-923)                              */
+/* ------------------------------------------------------------------------------------ */
+/* causal strided conv (CausalConvNet, modded_dac.py:59-90): left pad k - s, L % s == 0 (so no
+   extra right pad), Lo = L / s.  w [Co][Ci][k]; y [Co][Lo] */
+static void conv1d_causal_strided(const float* x, int Ci, int L, const float* w, const float* b, int Co,
+                                  int k, int s, float* y) {
+    const int Lo = L / s, pad = k - s;
+#pragma omp parallel for schedule(static)
+    for (int co = 0; co < Co; ++co) {
+        float* yr = y + (size_t)co * Lo;
+        for (int t = 0; t < Lo; ++t) yr[t] = b ? b[co] : 0.f;
+        for (int ci = 0; ci < Ci; ++ci) {
+            const float* xr = x + (size_t)ci * L;
+            const float* wr = w + ((size_t)co * Ci + ci) * k;
+            for (int t = 0; t < Lo; ++t)
+                for (int j = 0; j < k; ++j) {
+                    int src = t * s + j - pad;
+                    if (src >= 0) yr[t] += wr[j] * xr[src];
+                }
+        }
+    }
+}
+
+static int wn_conv_strided(orc_codec* m, const char* pre, const float* x, int Ci, int L, int Co, int k,
+                           int s, float* y) {
+    int bad = 0;
+    char nm[220];
+    snprintf(nm, sizeof nm, "%sconv.parametrizations.weight.original0", pre);
+    const float* g = cget(m, nm, Co, &bad);
+    snprintf(nm, sizeof nm, "%sconv.parametrizations.weight.original1", pre);
+    const float* v = cget(m, nm, (int64_t)Co * Ci * k, &bad);
+    snprintf(nm, sizeof nm, "%sconv.bias", pre);
+    const float* b = cget(m, nm, Co, &bad);
+    if (bad) return -1;
+    float* w = wn_fold(g, v, Co, Ci * k);
+    conv1d_causal_strided(x, Ci, L, w, b, Co, k, s, y);
+    free(w);
+    return 0;
+}
+
+/* ResidualUnit (modded_dac.py:600-620), causal: x += conv1(snake(conv7_dil(snake(x)))) */
+static int residual_unit(orc_codec* m, const char* pre, float* x, int C, int L, int dil) {
+    int bad = 0;
+    char nm[220];
+    snprintf(nm, sizeof nm, "%s0.alpha", pre);
+    const float* a0 = cget(m, nm, C, &bad);
+    snprintf(nm, sizeof nm, "%s2.alpha", pre);
+    const float* a2 = cget(m, nm, C, &bad);
+    if (bad) return -1;
+    float* t = (float*)malloc(sizeof(float) * (size_t)C * L);
+    float* u = (float*)malloc(sizeof(float) * (size_t)C * L);
+    memcpy(t, x, sizeof(float) * (size_t)C * L);
+    snake(t, a0, C, L);
+    snprintf(nm, sizeof nm, "%s1.", pre);
+    int rc = wn_conv(m, nm, t, C, L, C, 7, dil, u);
+    if (!rc) {
+        snake(u, a2, C, L);
+        snprintf(nm, sizeof nm, "%s3.", pre);
+        rc = wn_conv(m, nm, u, C, L, C, 1, 1, t);
+    }
+    if (!rc)
+        for (size_t i = 0; i < (size_t)C * L; ++i) x[i] += t[i];
+    free(t); free(u);
+    return rc;
+}
+
+/* [C][L] <-> [L][C] */
+static float* transpose_cl(const float* x, int C, int L) {
+    float* y = (float*)malloc(sizeof(float) * (size_t)C * L);
+    for (int c = 0; c < C; ++c)
+        for (int t = 0; t < L; ++t) y[(size_t)t * C + c] = x[(size_t)c * L + t];
+    return y;
+}
+
+/* descript 1.0.0 VectorQuantize.forward (restated, eval): z_e = in_proj(r); nearest codebook
+   entry of the l2-normalised z_e among the l2-normalised codebook (argmax of -dist, first
+   index on ties, dist = |e|^2 - 2 e.c + |c|^2); z_q = z_e + (codebook[idx] - z_e);
+   out = out_proj(z_q).  r, out: [D][T]. */
+static int vq_stage(orc_codec* m, const char* pre, int cbn, const float* r, int T, int32_t* codes, float* out) {
+    const int D = m->c.latent, cd = m->c.codebook_dim;
+    int bad = 0;
+    char nm[220];
+#define QW(var, suffix, cnt) \
+    snprintf(nm, sizeof nm, "%s%s", pre, suffix); const float* var = cget(m, nm, cnt, &bad);
+    QW(ig, "in_proj.weight_g", cd);
+    QW(iv, "in_proj.weight_v", (int64_t)cd * D);
+    QW(ib, "in_proj.bias", cd);
+    QW(og, "out_proj.weight_g", D);
+    QW(ov, "out_proj.weight_v", (int64_t)D * cd);
+    QW(ob, "out_proj.bias", D);
+    QW(cbw, "codebook.weight", (int64_t)cbn * cd);
+#undef QW
+    if (bad) return -1;
+    float* wi = wn_fold(ig, iv, cd, D);
+    float* wo = wn_fold(og, ov, D, cd);
+    float* cn = (float*)malloc(sizeof(float) * (size_t)cbn * cd);
+    float* cn2 = (float*)malloc(sizeof(float) * cbn);
+    for (int i = 0; i < cbn; ++i) {
+        float ss = 0.f;
+        for (int j = 0; j < cd; ++j) ss += cbw[(size_t)i * cd + j] * cbw[(size_t)i * cd + j];
+        float nrm = sqrtf(ss);
+        if (nrm < 1e-12f) nrm = 1e-12f;
+        float s2 = 0.f;
+        for (int j = 0; j < cd; ++j) {
+            cn[(size_t)i * cd + j] = cbw[(size_t)i * cd + j] / nrm;
+            s2 += cn[(size_t)i * cd + j] * cn[(size_t)i * cd + j];
+        }
+        cn2[i] = s2;
+    }
+#pragma omp parallel for schedule(static)
+    for (int t = 0; t < T; ++t) {
+        float ze[64], en[64], zq[64];
+        for (int j = 0; j < cd; ++j) {
+            float acc = 0.f;
+            for (int d = 0; d < D; ++d) acc += wi[(size_t)j * D + d] * r[(size_t)d * T + t];
+            ze[j] = acc + ib[j];
+        }
+        float ss = 0.f;
+        for (int j = 0; j < cd; ++j) ss += ze[j] * ze[j];
+        float nrm = sqrtf(ss);
+        if (nrm < 1e-12f) nrm = 1e-12f;
+        float e2 = 0.f;
+        for (int j = 0; j < cd; ++j) { en[j] = ze[j] / nrm; e2 += en[j] * en[j]; }
+        int best = 0;
+        float bv = -INFINITY;
+        for (int i = 0; i < cbn; ++i) {
+            float dot = 0.f;
+            for (int j = 0; j < cd; ++j) dot += en[j] * cn[(size_t)i * cd + j];
+            float nd = -((e2 - 2.f * dot) + cn2[i]);
+            if (nd > bv) { bv = nd; best = i; }
+        }
+        codes[t] = best;
+        for (int j = 0; j < cd; ++j) zq[j] = ze[j] + (cbw[(size_t)best * cd + j] - ze[j]);
+        for (int d = 0; d < D; ++d) {
+            float acc = 0.f;
+            for (int j = 0; j < cd; ++j) acc += wo[(size_t)d * cd + j] * zq[j];
+            out[(size_t)d * T + t] = acc + ob[d];
+        }
+    }
+    free(wi); free(wo); free(cn); free(cn2);
+    return 0;
+}
+
+/* DAC.encode: audio (n samples, mono) right-padded to a multiple of 2048 (modded_dac.py:
+   906-909); Encoder (modded_dac.py:670-709, strides 2/4/8/8, transformer of enc_layers layers
+   in the last block with window enc_window); quantizer: downsample x2 x2 (rvq.py:250-262),
+   pre_module (window c->window), semantic VQ then 9 residual VQ stages on z - semantic_z
+   (rvq.py:293-315).  codes: (nq+1) x T row-major with T = ceil(n / 2048).  Optional taps:
+   z_enc [D][4T], z_pre [D][T].  Returns T or -1. */
+int orc_codec_encode(orc_codec* m, const float* audio, int n, int encoder_dim, int enc_layers,
+                     int enc_window, int32_t* codes, float* z_enc_out, float* z_pre_out) {
+    const orc_codec_config* c = &m->c;
+    const int D = c->latent, nq = c->n_codebooks;
+    const int rates[4] = {2, 4, 8, 8};
+    const int T = (n + 2047) / 2048, L0 = T * 2048;
+    char nm[220];
+    float* x = (float*)calloc((size_t)L0, sizeof(float));
+    memcpy(x, audio, sizeof(float) * (size_t)n);
+    float* y = (float*)malloc(sizeof(float) * (size_t)encoder_dim * L0);
+    if (wn_conv(m, "encoder.block.0.", x, 1, L0, encoder_dim, 7, 1, y)) { free(x); free(y); return -1; }
+    free(x);
+    x = y;
+    int d = encoder_dim, L = L0;
+    for (int b = 0; b < 4; ++b) {
+        const int h = d, s = rates[b];
+        d *= 2;
+        char pre[160];
+        const int dils[3] = {1, 3, 9};
+        for (int r = 0; r < 3; ++r) {
+            snprintf(pre, sizeof pre, "encoder.block.%d.block.%d.block.", b + 1, r);
+            if (residual_unit(m, pre, x, h, L, dils[r])) { free(x); return -1; }
+        }
+        int bad = 0;
+        snprintf(nm, sizeof nm, "encoder.block.%d.block.3.alpha", b + 1);
+        const float* al = cget(m, nm, h, &bad);
+        if (bad) { free(x); return -1; }
+        snake(x, al, h, L);
+        y = (float*)malloc(sizeof(float) * (size_t)d * (L / s));
+        snprintf(pre, sizeof pre, "encoder.block.%d.block.4.", b + 1);
+        if (wn_conv_strided(m, pre, x, h, L, d, 2 * s, s, y)) { free(x); free(y); return -1; }
+        free(x);
+        x = y;
+        L /= s;
+        if (b == 3 && enc_layers > 0) {
+            float* xt = transpose_cl(x, d, L);
+            snprintf(pre, sizeof pre, "encoder.block.%d.block.5.", b + 1);
+            if (window_transformer_at(m, pre, xt, L, d, d / 64, 64, 3 * d, enc_layers, enc_window)) {
+                free(xt); free(x); return -1;
+            }
+            free(x);
+            x = transpose_cl(xt, L, d);
+            free(xt);
+        }
+    }
+    {
+        int bad = 0;
+        const float* al = cget(m, "encoder.block.5.alpha", d, &bad);
+        if (bad) { free(x); return -1; }
+        snake(x, al, d, L);
+        y = (float*)malloc(sizeof(float) * (size_t)D * L);
+        if (wn_conv(m, "encoder.block.6.", x, d, L, D, 3, 1, y)) { free(x); free(y); return -1; }
+        free(x);
+        x = y;
+    }
+    if (z_enc_out) memcpy(z_enc_out, x, sizeof(float) * (size_t)D * L);
+    /* quantizer.downsample: CausalConvNet(k=2, s=2) + ConvNeXtBlock, twice */
+    for (int i = 0; i < 2; ++i) {
+        int bad = 0;
+        snprintf(nm, sizeof nm, "quantizer.downsample.%d.0.conv.weight", i);
+        const float* w = cget(m, nm, (int64_t)D * D * 2, &bad);
+        snprintf(nm, sizeof nm, "quantizer.downsample.%d.0.conv.bias", i);
+        const float* b = cget(m, nm, D, &bad);
+        if (bad) { free(x); return -1; }
+        y = (float*)malloc(sizeof(float) * (size_t)D * (L / 2));
+        conv1d_causal_strided(x, D, L, w, b, D, 2, 2, y);
+        free(x);
+        x = y;
+        L /= 2;
+        snprintf(nm, sizeof nm, "quantizer.downsample.%d.1.", i);
+        if (convnext(m, nm, x, D, L)) { free(x); return -1; }
+    }
+    {
+        float* xt = transpose_cl(x, D, L);
+        if (window_transformer_at(m, "quantizer.pre_module.", xt, L, D, c->t_heads, c->t_head_dim, c->t_inter,
+                                  c->t_layers, c->window)) {
+            free(xt); free(x); return -1;
+        }
+        free(x);
+        x = transpose_cl(xt, L, D);
+        free(xt);
+    }
+    if (z_pre_out) memcpy(z_pre_out, x, sizeof(float) * (size_t)D * L);
+    /* semantic stage on z, then the residual stages on z - semantic_z */
+    float* q = (float*)malloc(sizeof(float) * (size_t)D * L);
+    int rc = vq_stage(m, "quantizer.semantic_quantizer.quantizers.0.", c->semantic_codebook_size, x, L, codes, q);
+    for (size_t i = 0; !rc && i < (size_t)D * L; ++i) x[i] -= q[i];
+    for (int k = 0; !rc && k < nq; ++k) {
+        char pre[160];
+        snprintf(pre, sizeof pre, "quantizer.quantizer.quantizers.%d.", k);
+        rc = vq_stage(m, pre, c->codebook_size, x, L, codes + (size_t)(k + 1) * L, q);
+        for (size_t i = 0; !rc && i < (size_t)D * L; ++i) x[i] -= q[i];
+    }
+    free(q); free(x);
+    return rc ? -1 : T;
 }

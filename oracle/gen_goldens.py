@@ -47,6 +47,7 @@ import ref_stubs  # noqa: E402
 ref_stubs.install()
 
 import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
 from safetensors.torch import save_file  # noqa: E402
 
 from fishmi import synth  # noqa: E402
@@ -345,7 +346,7 @@ CODEC_FULL = dict(encoder_dim=64, latent=1024, decoder_dim=1536, n_codebooks=9,
                   t_layers=8, t_heads=16, t_head_dim=64, t_inter=3072, window=128)
 
 
-def build_codec(spec: dict, seed: int):
+def build_codec(spec: dict, seed: int, enc_layers=None):
     from fish_speech.models.dac.modded_dac import DAC, ModelArgs, WindowLimitedTransformer
     from fish_speech.models.dac.rvq import DownsampleResidualVectorQuantize
 
@@ -358,23 +359,25 @@ def build_codec(spec: dict, seed: int):
     quant = DownsampleResidualVectorQuantize(
         input_dim=spec["latent"], n_codebooks=spec["n_codebooks"],
         codebook_size=spec["codebook_size"], codebook_dim=spec["codebook_dim"],
-        quantizer_dropout=0.5, downsample_factor=[2, 2], post_module=post, pre_module=None,
+        quantizer_dropout=0.5, downsample_factor=[2, 2], post_module=post,
+        pre_module=(WindowLimitedTransformer(causal=True, window_size=spec["window"], input_dim=spec["latent"],
+                                             config=tcfg) if enc_layers else None),
         semantic_codebook_size=spec["semantic_codebook_size"])
     gen = functools.partial(ModelArgs, block_size=8192, n_local_heads=-1, head_dim=64,
                             rope_base=10000, norm_eps=1e-5, dropout_rate=0.1,
                             attn_dropout_rate=0.1, channels_first=True)
     dac = DAC(encoder_dim=spec["encoder_dim"], encoder_rates=[2, 4, 8, 8],
               decoder_dim=spec["decoder_dim"], decoder_rates=[8, 8, 4, 2], quantizer=quant,
-              sample_rate=44100, causal=True, encoder_transformer_layers=[0, 0, 0, 0],
+              sample_rate=44100, causal=True, encoder_transformer_layers=enc_layers or [0, 0, 0, 0],
               decoder_transformer_layers=[0, 0, 0, 0], transformer_general_config=gen)
     sd = dac.state_dict()
     keys = [(k, tuple(v.shape)) for k, v in sd.items()
-            if k.startswith("decoder.") or k.startswith("quantizer.")]
+            if enc_layers or k.startswith("decoder.") or k.startswith("quantizer.")]
     state = synth_state(keys, seed, synth.codec_rule)
     state = OrderedDict((k, v.float()) for k, v in state.items())
     err = dac.load_state_dict(state, strict=False)
     assert not err.unexpected_keys, err.unexpected_keys
-    missing = [k for k in err.missing_keys if not k.startswith("encoder.")]
+    missing = [k for k in err.missing_keys if enc_layers or not k.startswith("encoder.")]
     assert not missing, missing
     return dac.eval()
 
@@ -415,6 +418,70 @@ def run_codec(name, spec, seed, T, clamp_test: bool):
           f"{res['prefix_maxdiff']:.3g}; bf16-vs-fp32 rms "
           f"{np.sqrt(np.mean((res['wave_bf16'] - res['wave_fp32'])**2)):.3g} "
           f"(signal rms {np.sqrt(np.mean(res['wave_fp32']**2)):.3g})")
+
+
+# --------------------------------------------------------------------------------------
+# Codec ENCODE: DAC.encode (modded_dac.py:874-923) = Encoder
+# (modded_dac.py:623-709) + DownsampleResidualVectorQuantize.forward (rvq.py:293-343) with the
+# descript 1.0.0 VQ encode restated in ref_stubs (parity at that boundary unpinned, as for decode)
+# --------------------------------------------------------------------------------------
+def encode_audio(n, seed):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / 44100.0
+    x = 0.4 * np.sin(2 * np.pi * 220 * t) + 0.2 * np.sin(2 * np.pi * 1375 * t + 0.3)
+    x = x * (0.6 + 0.4 * np.sin(2 * np.pi * 3 * t)) + 0.05 * rng.standard_normal(n)
+    return x.astype(np.float32)
+
+
+def run_codec_enc(name, spec, seed, n_samples, enc_layers):
+    dac = build_codec(spec, seed, enc_layers)
+    audio = encode_audio(n_samples, seed + 2)
+    margins = []
+
+    def track(vq):
+        orig = vq.decode_latents
+
+        def dl(latents):
+            enc = F.normalize(latents.transpose(1, 2).reshape(-1, latents.shape[1]))
+            cbk = F.normalize(vq.codebook.weight)
+            dist = enc.pow(2).sum(1, keepdim=True) - 2 * enc @ cbk.t() + cbk.pow(2).sum(1, keepdim=True).t()
+            top2 = torch.topk(-dist, 2, dim=1).values
+            margins.append((top2[:, 0] - top2[:, 1]).numpy().copy())
+            return orig(latents)
+
+        vq.decode_latents = dl
+
+    for vq in list(dac.quantizer.semantic_quantizer.quantizers) + list(dac.quantizer.quantizer.quantizers):
+        track(vq)
+    res = {"audio": audio, "synth_seed": seed, "spec": json.dumps(spec),
+           "enc_layers": np.array(enc_layers, np.int32), "torch_version": torch.__version__}
+    with torch.inference_mode():
+        x = torch.from_numpy(audio)[None, None]
+        t0 = time.time()
+        codes, lens = dac.encode(x)
+        dt = time.time() - t0
+        res["codes"] = codes.numpy().astype(np.int32)
+        res["lens"] = lens.numpy().astype(np.int32)
+        res["margin"] = np.stack(margins[:codes.shape[1]], 0).astype(np.float32)  # [nq+1][T]
+        # intermediate taps: encoder output (before the quantizer) and the quantizer's input to
+        # the first VQ stage (after downsample + pre_module)
+        pad = (-audio.shape[0]) % dac.frame_length
+        xp = F.pad(x, (0, pad))
+        z = dac.encoder(xp)
+        res["z_enc"] = z.float().numpy()
+        zq = dac.quantizer.pre_module(dac.quantizer.downsample(z))
+        res["z_pre"] = zq.float().numpy()
+    np.savez_compressed(os.path.join(GOLD, f"{name}.npz"), **res)
+    print(f"{name}: {n_samples} samples -> codes {res['codes'].shape} in {dt:.1f}s; "
+          f"min margin {res['margin'].min():.3g}; z_enc {res['z_enc'].shape} z_pre {res['z_pre'].shape}")
+
+
+def cmd_codec_enc():
+    run_codec_enc("codec_enc_tiny", CODEC_TINY, seed=41, n_samples=6 * 2048 - 700, enc_layers=[0, 0, 0, 2])
+
+
+def cmd_codec_enc_full():
+    run_codec_enc("codec_enc_full", CODEC_FULL, seed=43, n_samples=8 * 2048 - 300, enc_layers=[0, 0, 0, 4])
 
 
 def cmd_codec():

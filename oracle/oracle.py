@@ -15,7 +15,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "fish-speech_amd"))
 
-from fishmi.checkpoint import codec_tensor_shapes, llm_tensor_shapes  # noqa: E402
+from fishmi.checkpoint import (ENCODER_WINDOW, codec_encoder_tensor_shapes,  # noqa: E402
+                               codec_tensor_shapes, llm_tensor_shapes)
 from fishmi.config import CodecConfig, CodecConfigC, DualARConfig  # noqa: E402
 from fishmi.synth import codec_rule, llm_rule  # noqa: E402
 
@@ -61,6 +62,8 @@ def lib():
         L.orc_codec_synth_tensor.argtypes = [vp, ctypes.c_char_p, i64, ctypes.c_uint64, ctypes.c_float, ctypes.c_int]
         L.orc_codec_decode.argtypes = [vp, i32p, ctypes.c_int, f32p, f32p]
         L.orc_codec_free.argtypes = [vp]
+        L.orc_codec_encode.argtypes = [vp, f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, i32p,
+                                       f32p, f32p]
         _lib = L
     return _lib
 
@@ -174,6 +177,23 @@ class OracleCodec:
         for name, shape in codec_tensor_shapes(self.cfg).items():
             c, e = codec_rule(name)
             _check(lib().orc_codec_synth_tensor(self.h, name.encode(), int(np.prod(shape)), seed, c, e))
+
+    def synth_encoder(self, seed: int, encoder_dim: int, enc_layers):
+        for name, shape in codec_encoder_tensor_shapes(self.cfg, encoder_dim, enc_layers).items():
+            c, e = codec_rule(name)
+            _check(lib().orc_codec_synth_tensor(self.h, name.encode(), int(np.prod(shape)), seed, c, e))
+
+    def encode(self, audio: np.ndarray, encoder_dim: int, enc_layers: int, taps=False):
+        """DAC.encode (modded_dac.py:874-923): -> codes (nq+1, T) [, z_enc (D, 4T), z_pre (D, T)]."""
+        a = np.ascontiguousarray(audio, np.float32).reshape(-1)
+        T = (a.size + self.cfg.hop - 1) // self.cfg.hop
+        codes = np.zeros((self.cfg.n_codebooks + 1, T), np.int32)
+        ze = np.zeros((self.cfg.latent, 4 * T), np.float32) if taps else None
+        zp = np.zeros((self.cfg.latent, T), np.float32) if taps else None
+        n = _check(lib().orc_codec_encode(self.h, _f32p(a), a.size, encoder_dim, enc_layers, ENCODER_WINDOW,
+                                          _i32p(codes), _f32p(ze) if taps else None, _f32p(zp) if taps else None))
+        assert n == T
+        return (codes, ze, zp) if taps else codes
 
     def decode(self, codes: np.ndarray, want_latent=False):
         cd = np.ascontiguousarray(codes, np.int32)

@@ -103,6 +103,26 @@ def install() -> None:
         def decode_code(self, embed_id):
             return F.embedding(embed_id, self.codebook.weight).transpose(1, 2)
 
+        # encode side (descript-audio-codec 1.0.0 dac/nn/quantize.py VectorQuantize.forward /
+        # decode_latents, restated): in_proj, nearest codebook entry by l2-normalised
+        # distance, straight-through z_q, out_proj.  Losses are training-only and omitted.
+        def decode_latents(self, latents):
+            b = latents.shape[0]
+            enc = latents.transpose(1, 2).reshape(-1, latents.shape[1])
+            enc = F.normalize(enc)
+            cbk = F.normalize(self.codebook.weight)
+            dist = enc.pow(2).sum(1, keepdim=True) - 2 * enc @ cbk.t() + cbk.pow(2).sum(1, keepdim=True).t()
+            indices = (-dist).max(1)[1].reshape(b, -1)
+            return self.decode_code(indices), indices
+
+        def forward(self, z):
+            z_e = self.in_proj(z)
+            z_q, indices = self.decode_latents(z_e)
+            z_q = z_e + (z_q - z_e).detach()
+            z_q = self.out_proj(z_q)
+            zero = torch.zeros(z.shape[0])
+            return z_q, zero, zero, indices, z_e
+
     class ResidualVectorQuantize(nn.Module):
         def __init__(self, input_dim=512, n_codebooks=9, codebook_size=1024,
                      codebook_dim=8, quantizer_dropout=0.0):
@@ -117,6 +137,24 @@ def install() -> None:
                 for i in range(n_codebooks)
             )
             self.quantizer_dropout = quantizer_dropout
+
+        # descript 1.0.0 ResidualVectorQuantize.forward, eval mode (no quantizer dropout)
+        def forward(self, z, n_quantizers=None):
+            z_q = 0
+            residual = z
+            codes, latents = [], []
+            if n_quantizers is None:
+                n_quantizers = self.n_codebooks
+            zero = torch.zeros(z.shape[0])
+            for i, quantizer in enumerate(self.quantizers):
+                if i >= n_quantizers:
+                    break
+                z_q_i, _, _, indices_i, z_e_i = quantizer(residual)
+                z_q = z_q + z_q_i
+                residual = residual - z_q_i
+                codes.append(indices_i)
+                latents.append(z_e_i)
+            return z_q, torch.stack(codes, dim=1), torch.cat(latents, dim=1), zero, zero
 
         def from_codes(self, codes):
             z_q = 0.0

@@ -244,3 +244,37 @@ def test_bf16_wide_real_widths(golden):
             a = int(col[c + 1])
         pos = T + i
         x = col.reshape(-1, 1)
+
+
+def _codec_enc(name, golden):
+    g = golden(f"{name}.npz")
+    spec = json.loads(str(g["spec"]))
+    cfg = CodecConfig.from_spec(spec)
+    c = O.OracleCodec(cfg)
+    c.synth(int(g["synth_seed"]))
+    el = [int(v) for v in g["enc_layers"]]
+    c.synth_encoder(int(g["synth_seed"]), spec["encoder_dim"], el)
+    return c, g, cfg, spec, el
+
+
+def _codes_match(codes, g, tol):
+    """Codes equal to the reference's wherever its nearest/second-nearest margin exceeds tol
+    (an fp32 reassociation can only flip a decision closer than that)."""
+    ref, margin = g["codes"][0], g["margin"]
+    firm = margin > tol
+    assert firm.mean() > 0.9
+    np.testing.assert_array_equal(codes[firm], ref[firm])
+    assert codes.shape == ref.shape and int(g["lens"][0]) == ref.shape[1]
+
+
+@pytest.mark.parametrize("name", ["codec_enc_tiny", "codec_enc_full"])
+def test_codec_encode_matches_reference(name, golden):
+    """DAC.encode (modded_dac.py:874-923): encoder output, quantizer input (after downsample +
+    pre_module) and all 10 codebooks' codes vs the reference run on the same audio (right-padded
+    to a multiple of 2048 samples)."""
+    c, g, cfg, spec, el = _codec_enc(name, golden)
+    codes, ze, zp = c.encode(g["audio"], spec["encoder_dim"], el[-1], taps=True)
+    for got, ref in ((ze, g["z_enc"][0]), (zp, g["z_pre"][0])):
+        err = np.sqrt(np.mean((got - ref) ** 2)) / np.sqrt(np.mean(ref ** 2))
+        assert err < 1e-4, err
+    _codes_match(codes, g, 1e-5)
