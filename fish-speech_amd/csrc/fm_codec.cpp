@@ -34,6 +34,11 @@ struct DBlock {
     PackedW ct;
     RU ru[3];
 };
+struct EBlock {  // EncoderBlock (modded_dac.py:623-667): 3 residual units, snake, strided conv
+    RU ru[3];
+    void* a3;
+    PackedW down;  // k = 2s, stride s, as a 2-tap conv over the [L/s][s*Ci] view
+};
 
 // Streamed decode (fm_codec_decode_chunk): the codec is causal end to end, so chunk k of a
 // stream is decoded exactly like the matching rows of the one-shot decode when every causal
@@ -74,6 +79,19 @@ struct fm_codec {
     void *st_ct[4] = {}, *st_c7[4][3] = {};
     std::vector<std::pair<void*, size_t>> st_all;
     int spos = 0;                           // frames already streamed
+    // encode side (fm_codec_enable_encoder / fm_codec_encode)
+    int enc_dim = 0, enc_layers = 0;        // enc_dim 0: encoder not enabled
+    EBlock eblk[4];
+    PackedW e_c0, e_cf, ds[2], ds_pw1[2], ds_pw2[2];
+    void *e_a5 = nullptr, *ds_dw[2] = {}, *ds_db[2] = {}, *ds_lw[2] = {}, *ds_lb[2] = {}, *ds_gm[2] = {};
+    std::vector<TLayer> etl, ptl;
+    void *etnorm = nullptr, *ptnorm = nullptr;
+    VqEncPtrs vqe{};
+    void *e_audio = nullptr, *e_x = nullptr, *e_alt = nullptr, *e_c = nullptr, *e_z = nullptr, *e_xn = nullptr;
+    void *e_qkv = nullptr, *e_att = nullptr, *e_g1 = nullptr, *e_g3 = nullptr, *e_zenc = nullptr;
+    void *e_u0 = nullptr, *e_u1 = nullptr, *e_zpre = nullptr;
+    float* e_r = nullptr;
+    int32_t* e_codes = nullptr;
     double last_ms = 0, flops = 0, total_ms = 0, total_flops = 0;
     int64_t launches = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -179,6 +197,75 @@ static void build_inventory(fm_codec* m) {
     wn("decoder.model.6.", 1, cin, 7, false);
 }
 
+// encode-side keys (mirrors fishmi/checkpoint.codec_encoder_tensor_shapes)
+static const int ENC_RATES[4] = {2, 4, 8, 8};
+static constexpr int ENC_WINDOW = 512;  // EncoderBlock transformer: getattr(partial, "window_size", 512)
+static void add_tlayers(fm_codec* m, const std::string& pre, int dim, int layers, int HD, int I) {
+    for (int l = 0; l < layers; ++l) {
+        std::string p = pre + "layers." + std::to_string(l) + ".";
+        add(m, p + "attention.wqkv.weight", (int64_t)3 * HD * dim);
+        add(m, p + "attention.wo.weight", (int64_t)dim * HD);
+        add(m, p + "feed_forward.w1.weight", (int64_t)I * dim);
+        add(m, p + "feed_forward.w3.weight", (int64_t)I * dim);
+        add(m, p + "feed_forward.w2.weight", (int64_t)dim * I);
+        add(m, p + "ffn_norm.weight", dim);
+        add(m, p + "attention_norm.weight", dim);
+        add(m, p + "attention_layer_scale.gamma", dim);
+        add(m, p + "ffn_layer_scale.gamma", dim);
+    }
+    if (layers) add(m, pre + "norm.weight", dim);
+}
+static void build_encoder_inventory(fm_codec* m) {
+    const fm_codec_config& c = m->c;
+    const int D = c.latent, cd = c.codebook_dim;
+    auto wn = [&](const std::string& p, int co, int ci, int k) {
+        add(m, p + "conv.parametrizations.weight.original0", co);
+        add(m, p + "conv.parametrizations.weight.original1", (int64_t)co * ci * k);
+        add(m, p + "conv.bias", co);
+    };
+    wn("encoder.block.0.", m->enc_dim, 1, 7);
+    int d = m->enc_dim;
+    for (int b = 0; b < 4; ++b) {
+        const int h = d;
+        d *= 2;
+        std::string p = "encoder.block." + std::to_string(b + 1) + ".block.";
+        for (int r = 0; r < 3; ++r) {
+            std::string rp = p + std::to_string(r) + ".block.";
+            add(m, rp + "0.alpha", h);
+            wn(rp + "1.", h, h, 7);
+            add(m, rp + "2.alpha", h);
+            wn(rp + "3.", h, h, 1);
+        }
+        add(m, p + "3.alpha", h);
+        wn(p + "4.", d, h, 2 * ENC_RATES[b]);
+        if (b == 3) add_tlayers(m, p + "5.", d, m->enc_layers, d, 3 * d);
+    }
+    add(m, "encoder.block.5.alpha", d);
+    wn("encoder.block.6.", D, d, 3);
+    for (int i = 0; i < 2; ++i) {
+        std::string p = "quantizer.downsample." + std::to_string(i) + ".";
+        add(m, p + "0.conv.weight", (int64_t)D * D * 2);
+        add(m, p + "0.conv.bias", D);
+        add(m, p + "1.dwconv.conv.weight", (int64_t)D * 7);
+        add(m, p + "1.dwconv.conv.bias", D);
+        add(m, p + "1.norm.weight", D);
+        add(m, p + "1.norm.bias", D);
+        add(m, p + "1.pwconv1.weight", (int64_t)4 * D * D);
+        add(m, p + "1.pwconv1.bias", 4 * D);
+        add(m, p + "1.pwconv2.weight", (int64_t)4 * D * D);
+        add(m, p + "1.pwconv2.bias", D);
+        add(m, p + "1.gamma", D);
+    }
+    add_tlayers(m, "quantizer.pre_module.", D, c.t_layers, c.t_heads * c.t_head_dim, c.t_inter);
+    for (int q = 0; q <= c.n_codebooks; ++q) {
+        std::string p = q == 0 ? "quantizer.semantic_quantizer.quantizers.0."
+                               : "quantizer.quantizer.quantizers." + std::to_string(q - 1) + ".";
+        add(m, p + "in_proj.weight_g", cd);
+        add(m, p + "in_proj.weight_v", (int64_t)cd * D);
+        add(m, p + "in_proj.bias", cd);
+    }
+}
+
 static float* raw(fm_codec* m, const std::string& n) {
     auto it = m->w.find(n);
     FMCHECK(it != m->w.end() && it->second.set, "codec tensor not set: " + n);
@@ -240,6 +327,146 @@ static PackedW prep_wn_conv(fm_codec* m, const std::string& p, int Ci, int Co, i
     const float* w = fold(m, p + "conv.parametrizations.weight.original0", p + "conv.parametrizations.weight.original1",
                           Co, Ci * k);
     return prep(m, w, 0, Ci, Co, k, 1, dil, raw(m, p + "conv.bias"));
+}
+
+// conv weight rearranged on the host (fp32 [Co][Ci'][k']) then prepared as kind 0
+static PackedW prep_host(fm_codec* m, const std::vector<float>& w, int Ci, int Co, int k, const float* bias) {
+    float* d = nullptr;
+    HIPCHK(hipMalloc(&d, w.size() * 4));
+    HIPCHK(hipMemcpy(d, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+    PackedW p = prep(m, d, 0, Ci, Co, k, 1, 1, bias);  // prep synchronises before returning
+    HIPCHK(hipFree(d));
+    return p;
+}
+static std::vector<float> to_host(fm_codec* m, const float* d, size_t n) {
+    std::vector<float> h(n);
+    HIPCHK(hipStreamSynchronize(m->stream));
+    HIPCHK(hipMemcpy(h.data(), d, n * 4, hipMemcpyDeviceToHost));
+    return h;
+}
+// causal conv k = 2s, stride s (CausalConvNet, modded_dac.py:59-90; left pad k - s, no right pad
+// when L % s == 0): out[t] = sum_j W[j] x[ts + j - s] = tap0 . x'[t-1] + tap1 . x'[t] over the
+// contiguous view x'[L/s][s*Ci] of a time-major x, with x'[t][jj*Ci + ci] = x[ts + jj][ci]
+static PackedW prep_strided(fm_codec* m, const float* wdev, int Ci, int Co, int s, const float* bias) {
+    const std::vector<float> w = to_host(m, wdev, (size_t)Co * Ci * 2 * s);
+    std::vector<float> o((size_t)Co * s * Ci * 2);
+    for (int co = 0; co < Co; ++co)
+        for (int ci = 0; ci < Ci; ++ci)
+            for (int jj = 0; jj < s; ++jj)
+                for (int tap = 0; tap < 2; ++tap)
+                    o[(((size_t)co * s + jj) * Ci + ci) * 2 + tap] = w[((size_t)co * Ci + ci) * 2 * s + tap * s + jj];
+    return prep_host(m, o, s * Ci, Co, 2, bias);
+}
+static void prep_tlayers(fm_codec* m, std::vector<TLayer>& tl, const std::string& pre, int dim, int layers, int HD,
+                         int I) {
+    tl.resize(layers);
+    for (int l = 0; l < layers; ++l) {
+        std::string p = pre + "layers." + std::to_string(l) + ".";
+        TLayer& L = tl[l];
+        L.an = as_T(m, raw(m, p + "attention_norm.weight"), dim);
+        L.fn = as_T(m, raw(m, p + "ffn_norm.weight"), dim);
+        L.ag = as_T(m, raw(m, p + "attention_layer_scale.gamma"), dim);
+        L.fg = as_T(m, raw(m, p + "ffn_layer_scale.gamma"), dim);
+        L.wqkv = prep(m, raw(m, p + "attention.wqkv.weight"), 3, dim, 3 * HD, 1, 1, 1, nullptr);
+        L.wo = prep(m, raw(m, p + "attention.wo.weight"), 3, HD, dim, 1, 1, 1, nullptr);
+        L.w1 = prep(m, raw(m, p + "feed_forward.w1.weight"), 3, dim, I, 1, 1, 1, nullptr);
+        L.w3 = prep(m, raw(m, p + "feed_forward.w3.weight"), 3, dim, I, 1, 1, 1, nullptr);
+        L.w2 = prep(m, raw(m, p + "feed_forward.w2.weight"), 3, I, dim, 1, 1, 1, nullptr);
+    }
+}
+
+static void finalize_encoder(fm_codec* m) {
+    const fm_codec_config& c = m->c;
+    const int D = c.latent, cd = c.codebook_dim;
+    FMCHECK(m->enc_dim % 8 == 0, "encoder_dim must be a multiple of 8");
+    FMCHECK(c.codebook_dim <= 16 && c.n_codebooks + 1 <= 16, "vq encode: codebook_dim <= 16, <= 16 stages");
+    {  // first conv: 1 input channel padded to 8 (the audio buffer is [L][8], channel 0 live)
+        const int e = m->enc_dim;
+        const float* w = fold(m, "encoder.block.0.conv.parametrizations.weight.original0",
+                              "encoder.block.0.conv.parametrizations.weight.original1", e, 7);
+        const std::vector<float> h = to_host(m, w, (size_t)e * 7);
+        std::vector<float> o((size_t)e * 8 * 7, 0.f);
+        for (int co = 0; co < e; ++co)
+            for (int j = 0; j < 7; ++j) o[((size_t)co * 8) * 7 + j] = h[(size_t)co * 7 + j];
+        m->e_c0 = prep_host(m, o, 8, e, 7, raw(m, "encoder.block.0.conv.bias"));
+    }
+    int d = m->enc_dim;
+    for (int b = 0; b < 4; ++b) {
+        const int h = d, st = ENC_RATES[b];
+        d *= 2;
+        std::string p = "encoder.block." + std::to_string(b + 1) + ".block.";
+        EBlock& B = m->eblk[b];
+        const int dils[3] = {1, 3, 9};
+        for (int r = 0; r < 3; ++r) {
+            std::string rp = p + std::to_string(r) + ".block.";
+            B.ru[r].a0 = as_T(m, raw(m, rp + "0.alpha"), h);
+            B.ru[r].a2 = as_T(m, raw(m, rp + "2.alpha"), h);
+            B.ru[r].c7 = prep_wn_conv(m, rp + "1.", h, h, 7, dils[r]);
+            B.ru[r].c1 = prep_wn_conv(m, rp + "3.", h, h, 1, 1);
+        }
+        B.a3 = as_T(m, raw(m, p + "3.alpha"), h);
+        const float* w = fold(m, p + "4.conv.parametrizations.weight.original0",
+                              p + "4.conv.parametrizations.weight.original1", d, h * 2 * st);
+        B.down = prep_strided(m, w, h, d, st, raw(m, p + "4.conv.bias"));
+        if (b == 3 && m->enc_layers) {
+            FMCHECK(d % 64 == 0, "encoder transformer: dim must be a multiple of 64");
+            prep_tlayers(m, m->etl, p + "5.", d, m->enc_layers, d, 3 * d);
+            m->etnorm = as_T(m, raw(m, p + "5.norm.weight"), d);
+        }
+    }
+    m->e_a5 = as_T(m, raw(m, "encoder.block.5.alpha"), d);
+    m->e_cf = prep_wn_conv(m, "encoder.block.6.", d, D, 3, 1);
+    for (int i = 0; i < 2; ++i) {
+        std::string p = "quantizer.downsample." + std::to_string(i) + ".";
+        // CausalConvNet(k=2, s=2): no padding, out[t] = W0 x[2t] + W1 x[2t+1] = one tap over [L/2][2D]
+        const std::vector<float> w = to_host(m, raw(m, p + "0.conv.weight"), (size_t)D * D * 2);
+        std::vector<float> o((size_t)D * 2 * D);
+        for (int co = 0; co < D; ++co)
+            for (int ci = 0; ci < D; ++ci)
+                for (int j = 0; j < 2; ++j) o[((size_t)co * 2 + j) * D + ci] = w[((size_t)co * D + ci) * 2 + j];
+        m->ds[i] = prep_host(m, o, 2 * D, D, 1, raw(m, p + "0.conv.bias"));
+        m->ds_dw[i] = as_T(m, raw(m, p + "1.dwconv.conv.weight"), (int64_t)D * 7);
+        m->ds_db[i] = as_T(m, raw(m, p + "1.dwconv.conv.bias"), D);
+        m->ds_lw[i] = as_T(m, raw(m, p + "1.norm.weight"), D);
+        m->ds_lb[i] = as_T(m, raw(m, p + "1.norm.bias"), D);
+        m->ds_pw1[i] = prep(m, raw(m, p + "1.pwconv1.weight"), 3, D, 4 * D, 1, 1, 1, raw(m, p + "1.pwconv1.bias"));
+        m->ds_pw2[i] = prep(m, raw(m, p + "1.pwconv2.weight"), 3, 4 * D, D, 1, 1, 1, raw(m, p + "1.pwconv2.bias"));
+        m->ds_gm[i] = as_T(m, raw(m, p + "1.gamma"), D);
+    }
+    const int HD = c.t_heads * c.t_head_dim;
+    prep_tlayers(m, m->ptl, "quantizer.pre_module.", D, c.t_layers, HD, c.t_inter);
+    m->ptnorm = as_T(m, raw(m, "quantizer.pre_module.norm.weight"), D);
+    for (int q = 0; q <= c.n_codebooks; ++q) {
+        std::string p = q == 0 ? "quantizer.semantic_quantizer.quantizers.0."
+                               : "quantizer.quantizer.quantizers." + std::to_string(q - 1) + ".";
+        m->vqe.wi[q] = fold(m, p + "in_proj.weight_g", p + "in_proj.weight_v", cd, D);
+        m->vqe.bi[q] = raw(m, p + "in_proj.bias");
+        m->vqe.cb[q] = raw(m, p + "codebook.weight");
+        m->vqe.wo[q] = m->rvq.w[q];
+        m->vqe.bo[q] = raw(m, p + "out_proj.bias");
+        m->vqe.cbn[q] = q == 0 ? c.semantic_codebook_size : c.codebook_size;
+    }
+    // buffers for max_frames code frames (L0 = 2048 T samples); every encoder stage holds
+    // L * channels <= L0 * enc_dim elements
+    const size_t Tm = m->max_frames, E = m->esz, L0 = 2048 * Tm, dF = (size_t)m->enc_dim * 16;
+    m->e_audio = m->dalloc(L0 * 8 * E);
+    m->e_x = m->dalloc(L0 * m->enc_dim * E);
+    m->e_alt = m->dalloc(L0 * m->enc_dim * E);
+    m->e_c = m->dalloc(L0 * m->enc_dim * E);
+    const size_t R4 = 4 * Tm, wmax = std::max(dF, (size_t)D);
+    const size_t imax = std::max(std::max(3 * dF, (size_t)c.t_inter), (size_t)4 * D);
+    m->e_z = m->dalloc(R4 * wmax * E);
+    m->e_xn = m->dalloc(R4 * wmax * E);
+    m->e_qkv = m->dalloc(R4 * 3 * wmax * E);
+    m->e_att = m->dalloc(R4 * wmax * E);
+    m->e_g1 = m->dalloc(R4 * imax * E);
+    m->e_g3 = m->dalloc(R4 * imax * E);
+    m->e_zenc = m->dalloc(R4 * D * E);
+    m->e_u0 = m->dalloc(2 * Tm * D * E);
+    m->e_u1 = m->dalloc(Tm * D * E);
+    m->e_zpre = m->dalloc(Tm * D * E);
+    m->e_r = (float*)m->dalloc(Tm * D * 4);
+    m->e_codes = (int32_t*)m->dalloc((size_t)(c.n_codebooks + 1) * Tm * 4);
 }
 
 static void finalize(fm_codec* m) {
@@ -353,6 +580,7 @@ static void finalize(fm_codec* m) {
     }
     m->Cb = m->dalloc(Tm * maxact * E);
     m->wave = (float*)m->dalloc(Tm * 2048 * 4);
+    if (m->enc_dim) finalize_encoder(m);
     HIPCHK(hipEventCreate(&m->e0));
     HIPCHK(hipEventCreate(&m->e1));
     HIPCHK(hipStreamSynchronize(m->stream));
@@ -394,6 +622,85 @@ template <typename T> struct CRun {
         launch_conv_gemm<T>(s, a);
         m->flops += 2.0 * Lq * W.nphase * (double)W.Co * W.ntaps * W.Ci;
         m->launches++;
+    }
+
+    // WindowLimitedTransformer.forward (modded_dac.py:418-439) on z [Tn][Dm] in place; the final
+    // norm goes to xn
+    void transformer(const std::vector<TLayer>& tl, const void* norm, int Tn, int Dm, int H, int hd, int I,
+                     int window, void* z, void* xn, void* qkv, void* att, void* g1, void* g3) {
+        const float eps = m->c.norm_eps;
+        for (const TLayer& L : tl) {
+            launch_rmsnorm<T>(s, (const T*)z, Dm, (const T*)L.an, Dm, eps, (T*)xn, Dm, Tn);
+            gemm(L.wqkv, xn, Dm, Tn, Tn, qkv, 3 * H * hd, CE_STORE);
+            launch_rope_qk<T>(s, (T*)qkv, Tn, H, hd, m->rope, 0);
+            launch_window_attn<T>(s, (const T*)qkv, Tn, H, hd, window, (T*)att, 0);
+            gemm(L.wo, att, H * hd, Tn, Tn, z, Dm, CE_STORE | CE_RES | CE_GAMMA, z, Dm, L.ag);
+            launch_rmsnorm<T>(s, (const T*)z, Dm, (const T*)L.fn, Dm, eps, (T*)xn, Dm, Tn);
+            gemm(L.w1, xn, Dm, Tn, Tn, g1, I, CE_STORE);
+            gemm(L.w3, xn, Dm, Tn, Tn, g3, I, CE_STORE);
+            launch_silu_mul<T>(s, (const T*)g1, (T*)g3, (size_t)Tn * I);
+            gemm(L.w2, g3, I, Tn, Tn, z, Dm, CE_STORE | CE_RES | CE_GAMMA, z, Dm, L.fg);
+        }
+        launch_rmsnorm<T>(s, (const T*)z, Dm, (const T*)norm, Dm, eps, (T*)xn, Dm, Tn);
+    }
+
+    // ConvNeXtBlock (rvq.py:129-191) of quantizer.downsample.<i> on u [L][D] in place
+    void ds_convnext(int i, void* u, int L) {
+        const int D = m->c.latent;
+        launch_dwconv_ln<T>(s, (const T*)u, L, D, (const T*)m->ds_dw[i], (const T*)m->ds_db[i],
+                            (const T*)m->ds_lw[i], (const T*)m->ds_lb[i], (T*)m->e_xn, 0);
+        gemm(m->ds_pw1[i], m->e_xn, D, L, L, m->e_g1, 4 * D, CE_STORE | CE_GELU);
+        gemm(m->ds_pw2[i], m->e_g1, 4 * D, L, L, u, D, CE_STORE | CE_RES | CE_GAMMA, u, D, m->ds_gm[i]);
+    }
+
+    // DAC.encode (modded_dac.py:874-923) on e_audio [2048 Tn][8]: Encoder (modded_dac.py:670-709)
+    // -> quantizer.downsample (rvq.py:250-262) -> pre_module -> semantic + residual VQ
+    // (rvq.py:303-315) -> e_codes [(nq+1)][Tn]
+    void encode(int Tn) {
+        const fm_codec_config& c = m->c;
+        const int D = c.latent;
+        int L = 2048 * Tn, h = m->enc_dim;
+        void* alt = m->e_alt;
+        void* spare = m->e_c;
+        gemm(m->e_c0, m->e_audio, 8, L, L, m->e_x, h, CE_STORE, nullptr, 0, nullptr, m->eblk[0].ru[0].a0, alt, h);
+        const void* fin_in = nullptr;  // snake(encoder.block.5) of the last encoder block's output
+        for (int b = 0; b < 4; ++b) {
+            const EBlock& B = m->eblk[b];
+            const int st = ENC_RATES[b], d = 2 * h;
+            for (int r = 0; r < 3; ++r) {  // ResidualUnit (modded_dac.py:600-620)
+                const RU& R = B.ru[r];
+                gemm(R.c7, alt, h, L, L, nullptr, 0, 0, nullptr, 0, nullptr, R.a2, spare, h);
+                const void* an = r < 2 ? B.ru[r + 1].a0 : B.a3;
+                gemm(R.c1, spare, h, L, L, m->e_x, h, (r < 2 ? CE_STORE : 0) | CE_RES, m->e_x, h, nullptr, an, alt, h);
+            }
+            const int Lo = L / st;
+            if (b < 3) {
+                gemm(B.down, alt, st * h, Lo, Lo, m->e_x, d, CE_STORE, nullptr, 0, nullptr, m->eblk[b + 1].ru[0].a0,
+                     spare, d);
+                std::swap(alt, spare);
+            } else if (m->enc_layers) {
+                gemm(B.down, alt, st * h, Lo, Lo, m->e_z, d, CE_STORE);
+                transformer(m->etl, m->etnorm, Lo, d, d / 64, 64, 3 * d, ENC_WINDOW, m->e_z, m->e_xn, m->e_qkv,
+                            m->e_att, m->e_g1, m->e_g3);
+                launch_snake<T>(s, (const T*)m->e_xn, d, (size_t)Lo * d, (const T*)m->e_a5, (T*)spare);
+                fin_in = spare;
+            } else {
+                gemm(B.down, alt, st * h, Lo, Lo, nullptr, 0, 0, nullptr, 0, nullptr, m->e_a5, spare, d);
+                fin_in = spare;
+            }
+            L = Lo;
+            h = d;
+        }
+        gemm(m->e_cf, fin_in, h, L, L, m->e_zenc, D, CE_STORE);  // z_enc [4 Tn][D]
+        // quantizer.downsample: CausalConvNet(k2 s2) as one tap over the [L/2][2D] view + ConvNeXt
+        gemm(m->ds[0], m->e_zenc, 2 * D, L / 2, L / 2, m->e_u0, D, CE_STORE);
+        ds_convnext(0, m->e_u0, L / 2);
+        gemm(m->ds[1], m->e_u0, 2 * D, L / 4, L / 4, m->e_u1, D, CE_STORE);
+        ds_convnext(1, m->e_u1, L / 4);
+        transformer(m->ptl, m->ptnorm, Tn, D, c.t_heads, c.t_head_dim, c.t_inter, c.window, m->e_u1, m->e_zpre,
+                    m->e_qkv, m->e_att, m->e_g1, m->e_g3);
+        launch_convert<float>(s, m->e_zpre, sizeof(T) == 2, (int64_t)Tn * D, m->e_r);
+        launch_vq_encode(s, m->e_r, Tn, D, c.n_codebooks + 1, c.codebook_dim, m->vqe, m->e_codes);
     }
 
     // streamed chunk: a causal reader's carried rows -> the prefix of its input buffer, and back
@@ -517,6 +824,51 @@ static DTensor& ctensor(fm_codec* m, const char* name, int64_t numel) {
     return t;
 }
 
+int fm_codec_enable_encoder(fm_codec* m, int encoder_dim, int enc_layers) {
+    return fm_guard([&] {
+        FMCHECK(m, "null handle");
+        FMCHECK(!m->finalized, "enable the encoder before finalize");
+        FMCHECK(!m->enc_dim, "encoder already enabled");
+        FMCHECK(encoder_dim >= 8 && encoder_dim % 8 == 0 && enc_layers >= 0 && enc_layers <= 16, "bad encoder shape");
+        m->enc_dim = encoder_dim;
+        m->enc_layers = enc_layers;
+        build_encoder_inventory(m);
+    });
+}
+
+int fm_codec_encode(fm_codec* m, const float* audio, int64_t n, int32_t* codes, int* T_out) {
+    return fm_guard([&] {
+        FMCHECK(m && audio && codes && T_out, "null argument");
+        FMCHECK(m->enc_dim, "encoder not enabled (fm_codec_enable_encoder)");
+        FMCHECK(n >= 1 && n <= (int64_t)m->max_frames * 2048, "audio must hold 1 .. 2048 * max_frames samples");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        const int T = (int)((n + 2047) / 2048);
+        // DAC.encode right-pads to a multiple of frame_length (modded_dac.py:906-909); one live
+        // channel of 8 (Ci % 8 == 0 for the implicit-GEMM conv)
+        std::vector<float> a8((size_t)T * 2048 * 8, 0.f);
+        for (int64_t i = 0; i < n; ++i) a8[(size_t)i * 8] = audio[i];
+        float* tmp = nullptr;
+        HIPCHK(hipMalloc(&tmp, a8.size() * 4));
+        HIPCHK(hipMemcpyAsync(tmp, a8.data(), a8.size() * 4, hipMemcpyHostToDevice, m->stream));
+        if (m->prec == FM_PREC_BF16) {
+            launch_convert<bf16_t>(m->stream, tmp, 0, (int64_t)a8.size(), (bf16_t*)m->e_audio);
+            CRun<bf16_t> r(m);
+            r.encode(T);
+        } else {
+            launch_convert<float>(m->stream, tmp, 0, (int64_t)a8.size(), (float*)m->e_audio);
+            CRun<float> r(m);
+            r.encode(T);
+        }
+        HIPCHK(hipGetLastError());
+        const int nq1 = m->c.n_codebooks + 1;
+        HIPCHK(hipMemcpyAsync(codes, m->e_codes, (size_t)nq1 * T * 4, hipMemcpyDeviceToHost, m->stream));
+        HIPCHK(hipStreamSynchronize(m->stream));
+        HIPCHK(hipFree(tmp));
+        *T_out = T;
+    });
+}
+
 int fm_codec_set_tensor(fm_codec* m, const char* name, const void* data, int dtype, int64_t numel) {
     return fm_guard([&] {
         FMCHECK(m && name && data, "null argument");
@@ -609,16 +961,22 @@ static void codec_decode(fm_codec* m, const int32_t* codes, int T, float* pcm, b
     }
 }
 
-// test hook: copy an intermediate of the last decode as fp32 (time-major):
-// 1 = transformer output [T][D], 2 = upsample-1 [2T][D], 3 = decoder input latent [4T][D]
+// test hook: copy an intermediate of the last decode / encode as fp32 (time-major):
+// 1 = transformer output [T][D], 2 = upsample-1 [2T][D], 3 = decoder input latent [4T][D],
+// 10 = encoder output [4T][D], 11 = quantizer input after downsample + pre_module [T][D]
 int fm_codec_debug_read(fm_codec* m, int stage, int T, float* out) {
     return fm_guard([&] {
         FMCHECK(m && out && m->finalized, "bad arguments");
-        FMCHECK(stage >= 1 && stage <= 3, "debug stage must be 1..3");
+        FMCHECK((stage >= 1 && stage <= 3) || ((stage == 10 || stage == 11) && m->enc_dim),
+                "debug stage must be 1..3 or 10..11");
         FMCHECK(T >= 1 && T <= m->max_frames, "bad T");
         const int D = m->c.latent;
-        const void* src = stage == 1 ? m->xn : stage == 2 ? m->u0 : m->u1;
-        const size_t n = (size_t)(stage == 1 ? 1 : stage == 2 ? 2 : 4) * T * D;
+        const void* src = stage == 1    ? m->xn
+                          : stage == 2  ? m->u0
+                          : stage == 3  ? m->u1
+                          : stage == 10 ? m->e_zenc
+                                        : m->e_zpre;
+        const size_t n = (size_t)(stage == 1 || stage == 11 ? 1 : stage == 2 ? 2 : 4) * T * D;
         std::vector<uint8_t> h(n * m->esz);
         HIPCHK(hipMemcpy(h.data(), src, h.size(), hipMemcpyDeviceToHost));
         for (size_t i = 0; i < n; ++i) {

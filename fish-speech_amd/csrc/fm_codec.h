@@ -45,6 +45,17 @@ struct RvqPtrs {
 };
 
 template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a);
+// encode side (fm_codec_encode)
+struct VqEncPtrs {
+    const float* wi[16];  // folded in_proj [cd][D]
+    const float* bi[16];  // in_proj bias [cd]
+    const float* cb[16];  // codebooks [cbn][cd]
+    const float* wo[16];  // folded out_proj [D][cd]
+    const float* bo[16];  // out_proj bias [D]
+    int cbn[16];
+};
+void launch_vq_encode(hipStream_t s, float* r, int Tn, int D, int nst, int cd, const VqEncPtrs& p, int32_t* codes);
+template <typename T> void launch_snake(hipStream_t s, const T* x, int C, size_t n, const T* alpha, T* y);
 template <typename T> void launch_silu_mul(hipStream_t s, const T* g, T* y, size_t n);
 template <typename T>
 void launch_rvq_decode(hipStream_t s, const int32_t* codes, int Tn, int nq1, int sem, int cbs, int cd,

@@ -12,7 +12,10 @@
 //   rvq_decode_kernel  rvq.py:352-366 + descript ResidualVectorQuantize.from_codes
 //   dwconv_ln_kernel   ConvNeXt depthwise causal k7 + LayerNorm (rvq.py:176-178)
 //   rope_qk_kernel / window_attn_kernel   WindowLimitedTransformer (modded_dac.py:349-439)
+#include <algorithm>
+
 #include "fm_codec.h"
+#include "fm_runtime.h"
 
 template <typename T> struct CF;
 template <> struct CF<bf16_t> {
@@ -223,11 +226,12 @@ __global__ void rope_qk_kernel(T* __restrict__ qkv, int Tn, int H, int hd, const
 }
 
 // grid (T, H), one wave; window <= 128, hd <= 64
-template <typename T>
+// NS scores per lane: window <= 64 * NS (decode post_module: 128; encoder block: 512)
+template <typename T, int NS>
 __global__ __launch_bounds__(64) void window_attn_kernel(const T* __restrict__ qkv, int Tn, int H, int hd,
                                                          int window, T* __restrict__ out, int npre) {
     __shared__ float qs[64];
-    __shared__ float ps[128];
+    __shared__ float ps[64 * NS];
     const int lane = threadIdx.x;
     const int t = blockIdx.x, h = blockIdx.y;
     const size_t ld3 = (size_t)3 * H * hd;
@@ -238,8 +242,11 @@ __global__ __launch_bounds__(64) void window_attn_kernel(const T* __restrict__ q
     if (j0 < -npre) j0 = -npre;
     const int nj = t - j0 + 1;
     const float scale = 1.0f / sqrtf((float)hd);
-    float sc[2] = {-INFINITY, -INFINITY};
-    for (int i = 0; i < 2; ++i) {
+    float sc[NS];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        sc[i] = -INFINITY;
         const int jj = lane + 64 * i;
         if (jj < nj) {
             const T* k = qkv + (ptrdiff_t)(j0 + jj) * (ptrdiff_t)ld3 + (size_t)(H + h) * hd;
@@ -252,19 +259,108 @@ __global__ __launch_bounds__(64) void window_attn_kernel(const T* __restrict__ q
             }
             sc[i] = dot * scale;
         }
+        mx = fmaxf(mx, sc[i]);
     }
-    const float m = wave_max(fmaxf(sc[0], sc[1]));
-    const float p0 = lane < nj ? expf(sc[0] - m) : 0.f;
-    const float p1 = lane + 64 < nj ? expf(sc[1] - m) : 0.f;
-    const float l = wave_sum(p0 + p1);
-    ps[lane] = p0;
-    ps[lane + 64] = p1;
+    const float m = wave_max(mx);
+    float psum = 0.f;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const float p = lane + 64 * i < nj ? expf(sc[i] - m) : 0.f;
+        ps[lane + 64 * i] = p;
+        psum += p;
+    }
+    const float l = wave_sum(psum);
     __syncthreads();
     if (lane < hd) {
         float o = 0.f;
         for (int jj = 0; jj < nj; ++jj)
             o += ps[jj] * ld(qkv + (ptrdiff_t)(j0 + jj) * (ptrdiff_t)ld3 + (size_t)(2 * H + h) * hd, lane);
         st(out, (size_t)t * H * hd + (size_t)h * hd + lane, o / l);
+    }
+}
+
+// Snake1d (descript, restated in oracle/ref_stubs.py) on a time-major [L][C] activation
+template <typename T>
+__global__ void snake_kernel(const T* __restrict__ x, int C, size_t n, const T* __restrict__ alpha, T* __restrict__ y) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        st(y, i, snake_f(ld(x, i), ld(alpha, (int)(i % C))));
+}
+
+// Residual VQ encode (descript 1.0.0 VectorQuantize.forward / decode_latents, eval; rvq.py:
+// 303-315 chains the semantic stage then the residual stages on z - semantic_z), fp32.  One
+// block per frame t; r (time-major [Tn][D], T) is the running residual, updated in place.
+// Stage q: z_e = in_proj(r) (cd outputs); nearest l2-normalised codebook row to the
+// l2-normalised z_e (argmax of -(|e|^2 - 2 e.c + |c|^2), lowest index on ties); z_q = z_e +
+// (codebook[idx] - z_e); r -= out_proj(z_q).
+__global__ __launch_bounds__(256) void vq_encode_kernel_f(float* __restrict__ rf, int Tn, int D, int nst, int cd,
+                                                          VqEncPtrs p, int32_t* __restrict__ codes) {
+    __shared__ float zs[16], en[16], zq[16];
+    __shared__ float bv[256];
+    __shared__ int bi[256];
+    const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float* r = rf + (size_t)t * D;
+    for (int q = 0; q < nst; ++q) {
+        for (int j = wave; j < cd; j += 4) {
+            const float* w = p.wi[q] + (size_t)j * D;
+            float acc = 0.f;
+            for (int d = lane; d < D; d += 64) acc += w[d] * r[d];
+            acc = wave_sum(acc);
+            if (lane == 0) zs[j] = acc + p.bi[q][j];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            float ss = 0.f;
+            for (int j = 0; j < cd; ++j) ss += zs[j] * zs[j];
+            const float nrm = fmaxf(sqrtf(ss), 1e-12f);
+            for (int j = 0; j < cd; ++j) en[j] = zs[j] / nrm;
+        }
+        __syncthreads();
+        float e2 = 0.f;
+        for (int j = 0; j < cd; ++j) e2 += en[j] * en[j];
+        float best = -INFINITY;
+        int bidx = 0x7fffffff;
+        const float* cb = p.cb[q];
+        for (int i = tid; i < p.cbn[q]; i += 256) {
+            float ss = 0.f;
+            for (int j = 0; j < cd; ++j) ss += cb[(size_t)i * cd + j] * cb[(size_t)i * cd + j];
+            const float nrm = fmaxf(sqrtf(ss), 1e-12f);
+            float dot = 0.f, c2 = 0.f;
+            for (int j = 0; j < cd; ++j) {
+                const float cn = cb[(size_t)i * cd + j] / nrm;
+                dot += en[j] * cn;
+                c2 += cn * cn;
+            }
+            const float nd = -((e2 - 2.f * dot) + c2);
+            if (nd > best) {  // i ascends per thread: strict > keeps the lowest index
+                best = nd;
+                bidx = i;
+            }
+        }
+        bv[tid] = best;
+        bi[tid] = bidx;
+        __syncthreads();
+        for (int off = 128; off > 0; off >>= 1) {
+            if (tid < off) {
+                const float ov = bv[tid + off];
+                const int oi = bi[tid + off];
+                if (ov > bv[tid] || (ov == bv[tid] && oi < bi[tid])) {
+                    bv[tid] = ov;
+                    bi[tid] = oi;
+                }
+            }
+            __syncthreads();
+        }
+        const int idx = bi[0];
+        if (tid < cd) zq[tid] = zs[tid] + (cb[(size_t)idx * cd + tid] - zs[tid]);
+        if (tid == 0) codes[(size_t)q * Tn + t] = idx;
+        __syncthreads();
+        for (int d = tid; d < D; d += 256) {
+            const float* w = p.wo[q] + (size_t)d * cd;
+            float acc = 0.f;
+            for (int j = 0; j < cd; ++j) acc += w[j] * zq[j];
+            r[d] -= acc + p.bo[q][d];
+        }
+        __syncthreads();
     }
 }
 
@@ -337,7 +433,19 @@ void launch_rope_qk(hipStream_t s, T* qkv, int Tn, int H, int hd, const float* t
 }
 template <typename T>
 void launch_window_attn(hipStream_t s, const T* qkv, int Tn, int H, int hd, int window, T* out, int npre) {
-    window_attn_kernel<T><<<dim3(Tn, H), 64, 0, s>>>(qkv, Tn, H, hd, window, out, npre);
+    FMCHECK(hd <= 64 && window <= 512, "window attention: head_dim <= 64, window <= 512");
+    if (window <= 128)
+        window_attn_kernel<T, 2><<<dim3(Tn, H), 64, 0, s>>>(qkv, Tn, H, hd, window, out, npre);
+    else
+        window_attn_kernel<T, 8><<<dim3(Tn, H), 64, 0, s>>>(qkv, Tn, H, hd, window, out, npre);
+}
+template <typename T>
+void launch_snake(hipStream_t s, const T* x, int C, size_t n, const T* alpha, T* y) {
+    snake_kernel<T><<<(unsigned)std::min<size_t>((n + 255) / 256, 8192), 256, 0, s>>>(x, C, n, alpha, y);
+}
+void launch_vq_encode(hipStream_t s, float* r, int Tn, int D, int nst, int cd, const VqEncPtrs& p, int32_t* codes) {
+    FMCHECK(nst >= 1 && nst <= 16 && cd >= 1 && cd <= 16, "vq encode: <= 16 stages, codebook_dim <= 16");
+    vq_encode_kernel_f<<<Tn, 256, 0, s>>>(r, Tn, D, nst, cd, p, codes);
 }
 void launch_wn_fold(hipStream_t s, const float* g, const float* v, int rows, int per, float* w) {
     wn_fold_kernel<<<rows, 256, 0, s>>>(g, v, per, w);
@@ -356,6 +464,7 @@ void launch_conv_weight(hipStream_t s, const float* w, int kind, int Ci, int Co,
                                       const T*, T*, int);                                            \
     template void launch_rope_qk<T>(hipStream_t, T*, int, int, int, const float*, int);              \
     template void launch_window_attn<T>(hipStream_t, const T*, int, int, int, int, T*, int);         \
+    template void launch_snake<T>(hipStream_t, const T*, int, size_t, const T*, T*);                 \
     template void launch_conv_weight<T>(hipStream_t, const float*, int, int, int, int, int, T*);
 CINST(bf16_t)
 CINST(float)

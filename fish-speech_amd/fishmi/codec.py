@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 from . import native
-from .checkpoint import Tensor, codec_tensor_shapes, load_codec_weights
+from .checkpoint import Tensor, codec_encoder_tensor_shapes, codec_tensor_shapes, load_codec_weights
 from .config import CodecConfig
 from .synth import codec_rule
 
@@ -70,6 +70,58 @@ class FishMICodec:
     def finalize(self):
         native.check(native.lib().fm_codec_finalize(self.h))
 
+    # ---- encode side: DAC.encode (modded_dac.py:874-923), voice-clone reference audio ----------
+    def enable_encoder(self, encoder_dim: int = 64, enc_layers=(0, 0, 0, 4)):
+        """Before load/synth + finalize: adds the encoder, quantizer.downsample / pre_module and
+        VQ in_proj tensors (the decode-only inventory is the default)."""
+        if tuple(enc_layers[:3]) != (0, 0, 0):
+            raise ValueError("only the last encoder block carries a transformer (modded_dac_vq.yaml)")
+        self.encoder_dim, self.enc_layers = encoder_dim, tuple(enc_layers)
+        native.check(native.lib().fm_codec_enable_encoder(self.h, encoder_dim, int(enc_layers[3])))
+
+    def _encoder_shapes(self):
+        return codec_encoder_tensor_shapes(self.cfg, self.encoder_dim, self.enc_layers)
+
+    def load_encoder_weights(self, weights: "dict[str, Tensor]"):
+        L = native.lib()
+        for name, shape in self._encoder_shapes().items():
+            if name not in weights:
+                raise KeyError(f"codec checkpoint lacks {name}")
+            t = weights[name]
+            a = np.ascontiguousarray(t.data if t.bf16 else np.asarray(t.data, np.float32))
+            native.check(L.fm_codec_set_tensor(self.h, name.encode(), a.ctypes.data_as(ctypes.c_void_p),
+                                               native.FM_DT_BF16 if t.bf16 else native.FM_DT_F32, a.size))
+
+    def synth_encoder(self, seed: int):
+        L = native.lib()
+        for name, shape in self._encoder_shapes().items():
+            c, e = codec_rule(name)
+            native.check(L.fm_codec_synth_tensor(self.h, name.encode(), int(np.prod(shape)), seed, c, e))
+
+    def encode_audio(self, audio: np.ndarray) -> np.ndarray:
+        """mono 44.1 kHz samples -> codes (n_codebooks+1, ceil(n/2048)) int32 (DAC.encode with the
+        right pad to a multiple of frame_length; lens = T)."""
+        a = np.ascontiguousarray(np.asarray(audio, np.float32).reshape(-1))
+        T = (a.size + self.frame_length - 1) // self.frame_length
+        codes = np.zeros((self.cfg.n_codebooks + 1, T), np.int32)
+        t_out = ctypes.c_int(0)
+        native.check(native.lib().fm_codec_encode(self.h, native.f32p(a), a.size, native.i32p(codes),
+                                                  ctypes.byref(t_out)))
+        assert t_out.value == T
+        return codes
+
+    def encode(self, audio_data, audio_lengths=None):
+        """DAC.encode(audio[B, 1, N], audio_lengths) -> (codes[B, C, T], lens[B])."""
+        x = np.asarray(audio_data, np.float32)
+        if x.ndim == 2:
+            x = x[:, None]
+        outs, lens = [], []
+        for b in range(x.shape[0]):
+            n = int(audio_lengths[b]) if audio_lengths is not None else x.shape[-1]
+            outs.append(self.encode_audio(x[b, 0, :x.shape[-1]]))
+            lens.append((n + self.frame_length - 1) // self.frame_length)
+        return np.stack(outs), np.array(lens, np.int64)
+
     def decode_codes(self, codes: np.ndarray) -> np.ndarray:
         """codes (C, T) int -> float32 PCM (2048*T,)."""
         cd = np.ascontiguousarray(codes, dtype=np.int32)
@@ -101,9 +153,11 @@ class FishMICodec:
 
     def debug_read(self, stage: int, T: int) -> np.ndarray:
         """Test hook: 1 = transformer output [T][D], 2 = first upsample [2T][D],
-        3 = decoder input latent [4T][D] of the last decode (fp32, time-major)."""
+        3 = decoder input latent [4T][D] of the last decode; 10 = encoder output [4T][D],
+        11 = quantizer input after downsample + pre_module [T][D] of the last encode (fp32,
+        time-major)."""
         D = self.cfg.latent
-        shape = {1: (T, D), 2: (2 * T, D), 3: (4 * T, D)}[stage]
+        shape = {1: (T, D), 2: (2 * T, D), 3: (4 * T, D), 10: (4 * T, D), 11: (T, D)}[stage]
         out = np.zeros(shape, np.float32)
         native.check(native.lib().fm_codec_debug_read(self.h, stage, T, native.f32p(out)))
         return out

@@ -25,7 +25,8 @@ ABI_SYMBOLS = [
     "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph", "fm_tune", "fm_debug_ts_read",
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
     "fm_codec_finalize", "fm_codec_decode", "fm_codec_stream_reset", "fm_codec_decode_chunk",
-    "fm_codec_profile_read", "fm_codec_debug_read", "fm_codec_close",
+    "fm_codec_profile_read", "fm_codec_debug_read", "fm_codec_enable_encoder", "fm_codec_encode",
+    "fm_codec_close",
 ]
 
 
@@ -86,6 +87,8 @@ def lib():
                                             ctypes.POINTER(ctypes.c_double)]
         L.fm_codec_close.argtypes = [vp]
         L.fm_codec_debug_read.argtypes = [vp, i32, i32, pf32]
+        L.fm_codec_enable_encoder.argtypes = [vp, i32, i32]
+        L.fm_codec_encode.argtypes = [vp, pf32, i64, pi32, ctypes.POINTER(ctypes.c_int)]
     _lib = L
     return L
 

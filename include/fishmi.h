@@ -168,6 +168,15 @@ int fm_codec_profile_read(fm_codec* h, double* total_ms, int64_t* launches, doub
    2 first upsample [2T][latent], 3 decoder input [4T][latent]); other stages' buffers are
    reused in place and are not readable. */
 int fm_codec_debug_read(fm_codec* h, int stage, int T, float* out);
+// Codec ENCODE (voice-clone reference audio -> codes), SURVEY.md §8f row 1.  Replaces
+// DAC.encode(audio[B,1,N], audio_lengths) -> (codes[B,C,T], lens) (fish_speech/models/dac/
+// modded_dac.py:874-923; caller vq_manager.py:24-52 encode_reference).  enable before
+// set_tensor/finalize: adds the encode-side tensors (Encoder, quantizer.downsample,
+// quantizer.pre_module, VQ in_proj) to the inventory; encoder_dim 64 and enc_layers 4 for
+// modded_dac_vq.yaml.  encode: mono 44.1 kHz fp32 samples (n <= 2048 * max_frames), right-padded
+// to a multiple of 2048; codes (caller-owned, (n_codebooks+1) x T row-major, T = ceil(n/2048)).
+int fm_codec_enable_encoder(fm_codec* h, int encoder_dim, int enc_layers);
+int fm_codec_encode(fm_codec* h, const float* audio, int64_t n, int32_t* codes, int* T_out);
 int fm_codec_close(fm_codec* h);
 
 #ifdef __cplusplus

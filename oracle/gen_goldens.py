@@ -446,7 +446,7 @@ def run_codec_enc(name, spec, seed, n_samples, enc_layers):
             cbk = F.normalize(vq.codebook.weight)
             dist = enc.pow(2).sum(1, keepdim=True) - 2 * enc @ cbk.t() + cbk.pow(2).sum(1, keepdim=True).t()
             top2 = torch.topk(-dist, 2, dim=1).values
-            margins.append((top2[:, 0] - top2[:, 1]).numpy().copy())
+            margins.append((top2[:, 0] - top2[:, 1]).float().numpy().copy())
             return orig(latents)
 
         vq.decode_latents = dl
@@ -471,6 +471,10 @@ def run_codec_enc(name, spec, seed, n_samples, enc_layers):
         res["z_enc"] = z.float().numpy()
         zq = dac.quantizer.pre_module(dac.quantizer.downsample(z))
         res["z_pre"] = zq.float().numpy()
+        # the reference's own bf16 run (the bound a bf16 build is held to)
+        dac_bf = dac.to(torch.bfloat16)
+        res["z_enc_bf16"] = dac_bf.encoder(xp.bfloat16()).float().numpy()
+        res["codes_bf16"] = dac_bf.encode(x.bfloat16())[0].numpy().astype(np.int32)
     np.savez_compressed(os.path.join(GOLD, f"{name}.npz"), **res)
     print(f"{name}: {n_samples} samples -> codes {res['codes'].shape} in {dt:.1f}s; "
           f"min margin {res['margin'].min():.3g}; z_enc {res['z_enc'].shape} z_pre {res['z_pre'].shape}")
