@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=32,
                     help="throughput leg (BASELINE config 3): concurrent streams per GPU (0: skip)")
     ap.add_argument("--batch-frames", type=int, default=256, help="throughput leg: frames decoded")
+    ap.add_argument("--encode-seconds", type=float, default=30.0,
+                    help="encode leg: seconds of reference audio through the codec encoder (0: skip)")
     return ap.parse_args()
 
 
@@ -114,6 +116,39 @@ def throughput_leg(llm, cfg, batch, frames, sync, dist, world):
             "value": round(world * batch * frames / FRAME_RATE / dt, 2), "unit": "audio-sec/wall-sec",
             "ms_per_frame": round(dt / frames * 1e3, 3),
             "per_stream_rtf": round(frames / FRAME_RATE / dt, 3)}
+
+
+def encode_leg(ccfg, device, seconds, seed):
+    """BASELINE config 5's voice-clone input: `seconds` of reference audio -> codes through the codec
+    ENCODER (DAC.encode, modded_dac_vq.yaml shapes, bf16, random-init weights, synthetic audio).
+    Device time from HIP events around the encode; FLOPs are the implicit-GEMM convs/linears."""
+    from fishmi.codec import FishMICodec
+
+    T = int(np.ceil(seconds * FRAME_RATE))
+    m = FishMICodec(ccfg, device, "bf16", max_frames=T)
+    m.enable_encoder(64, (0, 0, 0, 4))
+    m.synth(seed + 2)
+    m.synth_encoder(seed + 2)
+    m.finalize()
+    n = T * ccfg.hop
+    t = np.arange(n) / ccfg.sample_rate
+    audio = (0.4 * np.sin(2 * np.pi * 220 * t) + 0.05 * np.random.default_rng(seed).standard_normal(n)).astype(np.float32)
+    m.encode_audio(audio)  # warm-up
+    ms0, _, fl0 = m.profile()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        m.encode_audio(audio)
+    wall = (time.perf_counter() - t0) / reps
+    ms1, _, fl1 = m.profile()
+    dev_ms = (ms1 - ms0) / reps
+    tflops = (fl1 - fl0) / reps / (dev_ms * 1e-3) / 1e12
+    m.close()
+    return {"workload": f"codec encode of {n / ccfg.sample_rate:.1f} s of reference audio ({T} code frames), bf16",
+            "value": round(n / ccfg.sample_rate / wall, 2), "unit": "audio-sec/wall-sec",
+            "wall_ms": round(wall * 1e3, 2), "device_ms": round(dev_ms, 2),
+            "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": BF16_DENSE_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(tflops / BF16_DENSE_TFLOPS, 4)}}
 
 
 def cpu_baseline(cfg, ccfg, prompt, frames, n_frames, n_codec, seed):
@@ -239,6 +274,7 @@ def main():
     codec_tflops = (fl1 - fl0) / ((ms1 - ms0) * 1e-3) / 1e12
 
     thr = throughput_leg(llm, cfg, args.batch, args.batch_frames, sync, dist, world) if args.batch > 0 else None
+    enc = encode_leg(ccfg, local, args.encode_seconds, args.seed) if args.encode_seconds > 0 else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -286,6 +322,7 @@ def main():
                                "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                                "frac": round(codec_tflops / BF16_DENSE_TFLOPS, 4)},
             "throughput": thr,
+            "encode": enc,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

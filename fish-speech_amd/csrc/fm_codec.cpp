@@ -851,6 +851,8 @@ int fm_codec_encode(fm_codec* m, const float* audio, int64_t n, int32_t* codes, 
         float* tmp = nullptr;
         HIPCHK(hipMalloc(&tmp, a8.size() * 4));
         HIPCHK(hipMemcpyAsync(tmp, a8.data(), a8.size() * 4, hipMemcpyHostToDevice, m->stream));
+        m->flops = 0;
+        HIPCHK(hipEventRecord(m->e0, m->stream));
         if (m->prec == FM_PREC_BF16) {
             launch_convert<bf16_t>(m->stream, tmp, 0, (int64_t)a8.size(), (bf16_t*)m->e_audio);
             CRun<bf16_t> r(m);
@@ -861,10 +863,16 @@ int fm_codec_encode(fm_codec* m, const float* audio, int64_t n, int32_t* codes, 
             r.encode(T);
         }
         HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(m->e1, m->stream));
         const int nq1 = m->c.n_codebooks + 1;
         HIPCHK(hipMemcpyAsync(codes, m->e_codes, (size_t)nq1 * T * 4, hipMemcpyDeviceToHost, m->stream));
         HIPCHK(hipStreamSynchronize(m->stream));
         HIPCHK(hipFree(tmp));
+        float ms = 0;  // device time of the encode (fm_codec_profile_read totals decode + encode)
+        HIPCHK(hipEventElapsedTime(&ms, m->e0, m->e1));
+        m->last_ms = ms;
+        m->total_ms += ms;
+        m->total_flops += m->flops;
         *T_out = T;
     });
 }
