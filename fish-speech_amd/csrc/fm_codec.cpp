@@ -91,6 +91,7 @@ struct fm_codec {
     void *e_qkv = nullptr, *e_att = nullptr, *e_g1 = nullptr, *e_g3 = nullptr, *e_zenc = nullptr;
     void *e_u0 = nullptr, *e_u1 = nullptr, *e_zpre = nullptr;
     float* e_r = nullptr;
+    float* e_pcm = nullptr;                 // mono input samples (fp32)
     int32_t* e_codes = nullptr;
     double last_ms = 0, flops = 0, total_ms = 0, total_flops = 0;
     int64_t launches = 0;
@@ -449,6 +450,7 @@ static void finalize_encoder(fm_codec* m) {
     // buffers for max_frames code frames (L0 = 2048 T samples); every encoder stage holds
     // L * channels <= L0 * enc_dim elements
     const size_t Tm = m->max_frames, E = m->esz, L0 = 2048 * Tm, dF = (size_t)m->enc_dim * 16;
+    m->e_pcm = (float*)m->dalloc(L0 * 4);
     m->e_audio = m->dalloc(L0 * 8 * E);
     m->e_x = m->dalloc(L0 * m->enc_dim * E);
     m->e_alt = m->dalloc(L0 * m->enc_dim * E);
@@ -844,21 +846,17 @@ int fm_codec_encode(fm_codec* m, const float* audio, int64_t n, int32_t* codes, 
         HIPCHK(hipSetDevice(m->device));
         finalize(m);
         const int T = (int)((n + 2047) / 2048);
-        // DAC.encode right-pads to a multiple of frame_length (modded_dac.py:906-909); one live
-        // channel of 8 (Ci % 8 == 0 for the implicit-GEMM conv)
-        std::vector<float> a8((size_t)T * 2048 * 8, 0.f);
-        for (int64_t i = 0; i < n; ++i) a8[(size_t)i * 8] = audio[i];
-        float* tmp = nullptr;
-        HIPCHK(hipMalloc(&tmp, a8.size() * 4));
-        HIPCHK(hipMemcpyAsync(tmp, a8.data(), a8.size() * 4, hipMemcpyHostToDevice, m->stream));
+        // DAC.encode right-pads to a multiple of frame_length (modded_dac.py:906-909); the device
+        // expands the mono samples to 8 channels (one live: Ci % 8 == 0 for the implicit-GEMM conv)
+        HIPCHK(hipMemcpyAsync(m->e_pcm, audio, (size_t)n * 4, hipMemcpyHostToDevice, m->stream));
         m->flops = 0;
         HIPCHK(hipEventRecord(m->e0, m->stream));
         if (m->prec == FM_PREC_BF16) {
-            launch_convert<bf16_t>(m->stream, tmp, 0, (int64_t)a8.size(), (bf16_t*)m->e_audio);
+            launch_audio8<bf16_t>(m->stream, m->e_pcm, n, (int64_t)T * 2048, (bf16_t*)m->e_audio);
             CRun<bf16_t> r(m);
             r.encode(T);
         } else {
-            launch_convert<float>(m->stream, tmp, 0, (int64_t)a8.size(), (float*)m->e_audio);
+            launch_audio8<float>(m->stream, m->e_pcm, n, (int64_t)T * 2048, (float*)m->e_audio);
             CRun<float> r(m);
             r.encode(T);
         }
@@ -867,7 +865,6 @@ int fm_codec_encode(fm_codec* m, const float* audio, int64_t n, int32_t* codes, 
         const int nq1 = m->c.n_codebooks + 1;
         HIPCHK(hipMemcpyAsync(codes, m->e_codes, (size_t)nq1 * T * 4, hipMemcpyDeviceToHost, m->stream));
         HIPCHK(hipStreamSynchronize(m->stream));
-        HIPCHK(hipFree(tmp));
         float ms = 0;  // device time of the encode (fm_codec_profile_read totals decode + encode)
         HIPCHK(hipEventElapsedTime(&ms, m->e0, m->e1));
         m->last_ms = ms;

@@ -56,6 +56,7 @@ struct VqEncPtrs {
 };
 void launch_vq_encode(hipStream_t s, float* r, int Tn, int D, int nst, int cd, const VqEncPtrs& p, int32_t* codes);
 template <typename T> void launch_snake(hipStream_t s, const T* x, int C, size_t n, const T* alpha, T* y);
+template <typename T> void launch_audio8(hipStream_t s, const float* a, int64_t n, int64_t npad, T* y);
 template <typename T> void launch_silu_mul(hipStream_t s, const T* g, T* y, size_t n);
 template <typename T>
 void launch_rvq_decode(hipStream_t s, const int32_t* codes, int Tn, int nq1, int sem, int cbs, int cd,

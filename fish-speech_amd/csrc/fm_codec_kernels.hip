@@ -279,6 +279,14 @@ __global__ __launch_bounds__(64) void window_attn_kernel(const T* __restrict__ q
     }
 }
 
+// mono fp32 samples -> the encoder's [n_pad][8] input (channel 0 live, right pad = causal zeros of
+// DAC.encode's pad to a multiple of frame_length, modded_dac.py:906-909)
+template <typename T>
+__global__ void audio8_kernel(const float* __restrict__ a, int64_t n, int64_t npad, T* __restrict__ y) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npad * 8; i += (int64_t)gridDim.x * blockDim.x)
+        st(y, (size_t)i, (i & 7) == 0 && (i >> 3) < n ? a[i >> 3] : 0.f);
+}
+
 // Snake1d (descript, restated in oracle/ref_stubs.py) on a time-major [L][C] activation
 template <typename T>
 __global__ void snake_kernel(const T* __restrict__ x, int C, size_t n, const T* __restrict__ alpha, T* __restrict__ y) {
@@ -440,6 +448,10 @@ void launch_window_attn(hipStream_t s, const T* qkv, int Tn, int H, int hd, int 
         window_attn_kernel<T, 8><<<dim3(Tn, H), 64, 0, s>>>(qkv, Tn, H, hd, window, out, npre);
 }
 template <typename T>
+void launch_audio8(hipStream_t s, const float* a, int64_t n, int64_t npad, T* y) {
+    audio8_kernel<T><<<(unsigned)std::min<int64_t>((npad * 8 + 255) / 256, 8192), 256, 0, s>>>(a, n, npad, y);
+}
+template <typename T>
 void launch_snake(hipStream_t s, const T* x, int C, size_t n, const T* alpha, T* y) {
     snake_kernel<T><<<(unsigned)std::min<size_t>((n + 255) / 256, 8192), 256, 0, s>>>(x, C, n, alpha, y);
 }
@@ -465,6 +477,7 @@ void launch_conv_weight(hipStream_t s, const float* w, int kind, int Ci, int Co,
     template void launch_rope_qk<T>(hipStream_t, T*, int, int, int, const float*, int);              \
     template void launch_window_attn<T>(hipStream_t, const T*, int, int, int, int, T*, int);         \
     template void launch_snake<T>(hipStream_t, const T*, int, size_t, const T*, T*);                 \
+    template void launch_audio8<T>(hipStream_t, const float*, int64_t, int64_t, T*);                 \
     template void launch_conv_weight<T>(hipStream_t, const float*, int, int, int, int, int, T*);
 CINST(bf16_t)
 CINST(float)
