@@ -202,6 +202,7 @@ struct FmTuning {
     int bgemv_tpb = 4;       // bgemv max 16-row tiles per block sharing one staged X slice (1, 2, 4)
     int bgemv_lds_kb = 84;   // bgemv X-slice LDS budget (KiB) before splitting K
     int bgemv_fill = 512;    // bgemv: split K until the grid has this many blocks
+    int rmsnorm_block = 0;   // 1: block-per-row RMSNorm (the pre-vectorisation kernel), 0: wave-per-row when shapes allow
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
 };

@@ -1350,6 +1350,8 @@ int fm_tune(const char* key, int value) {
             t.linear_fill = value;
         } else if (k == "ksb_balance") {
             t.ksb_balance = value != 0;
+        } else if (k == "rmsnorm_block") {
+            t.rmsnorm_block = value != 0;
         } else if (k == "debug_ts") {  // (re)arm the per-block timestamp buffer; 0 frees it
             if (t.dbg) HIPCHK(hipFree(t.dbg));
             t.dbg = nullptr;

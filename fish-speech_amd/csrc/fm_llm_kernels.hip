@@ -72,6 +72,54 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const int32_t* __restr
 // =========================================================================================
 // RMSNorm (llama.py:989-1000): fp32 mean square, round(x*rstd), * weight, round
 // =========================================================================================
+// one wave per row (4 rows per block), 8 consecutive features per lane held in registers between
+// the sum of squares and the scaled store: one read of x, no block barrier.  Host: d % 8 == 0,
+// d <= 512 * RN_MAXC, ldx/ldy multiples of 8 and 16-byte aligned rows.
+constexpr int RN_MAXC = 8;
+template <typename T>
+__global__ __launch_bounds__(256) void rmsnorm_wave_kernel(const T* __restrict__ x, int ldx,
+                                                           const T* __restrict__ w, int d, float eps,
+                                                           T* __restrict__ y, int ldy, int R) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const T* xr = x + (size_t)r * ldx;
+    float v[RN_MAXC][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < RN_MAXC; ++c) {
+        const int i = 8 * (c * 64 + lane);
+        if (i < d) {
+            load8(xr + i, v[c]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+        }
+    }
+    ss = wave_sum(ss);
+    const float rs = 1.0f / sqrtf(ss / (float)d + eps);
+    T* yr = y + (size_t)r * ldy;
+#pragma unroll
+    for (int c = 0; c < RN_MAXC; ++c) {
+        const int i = 8 * (c * 64 + lane);
+        if (i < d) {
+            float g[8], o[8];
+            load8(w + i, g);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = rnd<T>(rnd<T>(v[c][j] * rs) * g[j]);
+            if constexpr (is_bf16<T>::value) {
+                u32x4_t pk;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    pk[j] = (__float_as_uint(o[2 * j]) >> 16) | (__float_as_uint(o[2 * j + 1]) & 0xffff0000u);
+                *reinterpret_cast<u32x4_t*>(yr + i) = pk;
+            } else {
+                *reinterpret_cast<f32x4_t*>(yr + i) = (f32x4_t){o[0], o[1], o[2], o[3]};
+                *reinterpret_cast<f32x4_t*>(yr + i + 4) = (f32x4_t){o[4], o[5], o[6], o[7]};
+            }
+        }
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const T* __restrict__ x, int ldx,
                                                       const T* __restrict__ w, int d, float eps,
@@ -723,7 +771,12 @@ void launch_gather_rows(hipStream_t s, const int32_t* codes, int ldc, int col, c
 template <typename T>
 void launch_rmsnorm(hipStream_t s, const T* x, int ldx, const T* w, int d, float eps, T* y,
                     int ldy, int R) {
-    rmsnorm_kernel<T><<<R, 256, 0, s>>>(x, ldx, w, d, eps, y, ldy);
+    const bool vec = d % 8 == 0 && d <= 512 * RN_MAXC && ldx % 8 == 0 && ldy % 8 == 0 &&
+                     ((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) % 16 == 0 && !fm_tuning().rmsnorm_block;
+    if (vec)
+        rmsnorm_wave_kernel<T><<<FM_CEIL(R, 4), 256, 0, s>>>(x, ldx, w, d, eps, y, ldy, R);
+    else
+        rmsnorm_kernel<T><<<R, 256, 0, s>>>(x, ldx, w, d, eps, y, ldy);
 }
 
 // K-slices for the batched decode path: enough blocks to cover the chip (>= tu.linear_fill), each

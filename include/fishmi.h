@@ -127,7 +127,7 @@ int fm_llm_kernel_bench(fm_llm* h, const char* kernel_class, int reps, double* a
                         int64_t* launches, int64_t* bytes);
 int fm_llm_use_graph(fm_llm* h, int enable);
 /* process-wide developer knobs of the decode GEMV ("gemv_nt" 0|1, "gemv_u" 2|4|8, "gemv_wpb" 4|8, "gemv_sk" 0|1, "gemv_sk_bpc" 1..4, "ksb_blocks" n, "ksb_balance"
-   0|1); they apply to launches recorded after the call (graphs captured earlier keep theirs). */
+   0|1, "rmsnorm_block" 0|1); they apply to launches recorded after the call (graphs captured earlier keep theirs). */
 int fm_tune(const char* key, int value);
 /* developer hook ("debug_ts" armed): per-block records of 8 words {tag = N<<32 | blockIdx.y<<16 |
    blockIdx.x, start, staged, streamed, end, 3 kernel-specific} of the decode GEMVs,
