@@ -46,8 +46,12 @@ def test_fp32_greedy_tokens_exact(name, golden):
     np.testing.assert_array_equal(out, ref)
 
 
+@pytest.mark.parametrize("rmsnorm_block", [0, 1])
 @pytest.mark.parametrize("name", ["llm_a", "llm_b"])
-def test_fp32_teacher_forced_logits(name, golden):
+def test_fp32_teacher_forced_logits(name, rmsnorm_block, golden, knob):
+    """Logits, hidden states and fast logits within 1e-4 of the reference's, with the
+    wave-per-row RMSNorm (default) and the block-per-row one (rmsnorm_block=1)."""
+    knob("rmsnorm_block", rmsnorm_block, 0)
     m, g, cfg = _model(name, "fp32", golden)
     T = g["prompt"].shape[1]
     seq = g["seq"]
