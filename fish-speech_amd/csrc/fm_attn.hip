@@ -271,6 +271,11 @@ __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
                 const float c = tab[2 * p], sn = tab[2 * p + 1];
                 qs[hh * hd + 2 * p] = rnd<T>(q0[i][u] * c - q1[i][u] * sn);
                 qs[hh * hd + 2 * p + 1] = rnd<T>(q1[i][u] * c + q0[i][u] * sn);
+                if (a.qdbg && sp == 0) {  // per-op test hook only
+                    float* qd = a.qdbg + ((size_t)r * a.nh + kvh * g + hh) * hd;
+                    qd[2 * p] = qs[hh * hd + 2 * p];
+                    qd[2 * p + 1] = qs[hh * hd + 2 * p + 1];
+                }
             }
         }
     }
@@ -585,6 +590,8 @@ __global__ __launch_bounds__(256) void sample_radix_kernel(SampleArgs a) {
     const SlotParams sp = a.sp[slot];
     const float* lg = a.logits + (size_t)r * a.ldl;
     const int Nl = a.Nl;
+    if (sp.force)  // teacher forcing: the logits row as the production graph produced it
+        for (int i = threadIdx.x; i < Nl; i += 256) a.tap[(size_t)slot * a.tap_ld + i] = lg[i];
     for (int i = threadIdx.x; i < Nl; i += 256) {
         float v = lg[i];
         if (a.slow && sp.mask_im_end && i == Nl - 1) v = -INFINITY;
@@ -725,15 +732,21 @@ __global__ __launch_bounds__(256) void sample_radix_kernel(SampleArgs a) {
             // never emit an out-of-range id (NaN logits leave no valid candidate): end the stream
             if (!((tok >= a.sb && tok <= a.se) || tok == a.im_end)) tok = a.im_end;
             if (lane == 0) {
-                col[0] = tok;
                 int c = tok - a.sb;
                 c = c < 0 ? 0 : (c > a.cb - 1 ? a.cb - 1 : c);
+                if (sp.force) {
+                    tok = a.force_cols[(size_t)slot * a.ldc];
+                    c = a.force_cols[(size_t)slot * a.ldc + 1];
+                }
+                col[0] = tok;
                 col[1] = c;
             }
         } else {
             const int code = sample_top<T>(cv, cid, K, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed,
                                            step, (uint32_t)a.draw, lane);
-            if (lane == 0) col[a.col_idx] = (code >= 0 && code < a.cb) ? code : 0;
+            if (lane == 0)
+                col[a.col_idx] = sp.force ? a.force_cols[(size_t)slot * a.ldc + a.col_idx]
+                                          : ((code >= 0 && code < a.cb) ? code : 0);
         }
     }
 }
@@ -826,6 +839,8 @@ __global__ __launch_bounds__(256) void sample_fast_kernel(SampleArgs a) {
     const SlotParams sp = a.sp[slot];
     const float* lg = a.logits + (size_t)r * a.ldl;
     const int Nl = a.Nl;
+    if (sp.force)  // teacher forcing: the logits row as the production graph produced it
+        for (int i = threadIdx.x; i < Nl; i += 256) a.tap[(size_t)slot * a.tap_ld + i] = lg[i];
     auto tok_of = [&](int i) { return a.slow ? (i < Nl - 1 ? a.sb + i : a.im_end) : i; };
     // this thread's values: indices threadIdx.x + 256 * i (coalesced loads, all in flight)
     float v[SF_PER];
@@ -1008,15 +1023,21 @@ __global__ __launch_bounds__(256) void sample_fast_kernel(SampleArgs a) {
         }
         if (!((tok >= a.sb && tok <= a.se) || tok == a.im_end)) tok = a.im_end;
         if (lane == 0) {
-            col[0] = tok;
             int c = tok - a.sb;
             c = c < 0 ? 0 : (c > a.cb - 1 ? a.cb - 1 : c);
+            if (sp.force) {
+                tok = a.force_cols[(size_t)slot * a.ldc];
+                c = a.force_cols[(size_t)slot * a.ldc + 1];
+            }
+            col[0] = tok;
             col[1] = c;
         }
     } else {
         const int code = sample_top<T>(cv, cid, K, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed, step,
                                        (uint32_t)a.draw, lane);
-        if (lane == 0) col[a.col_idx] = (code >= 0 && code < a.cb) ? code : 0;
+        if (lane == 0)
+            col[a.col_idx] = sp.force ? a.force_cols[(size_t)slot * a.ldc + a.col_idx]
+                                      : ((code >= 0 && code < a.cb) ? code : 0);
     }
 }
 

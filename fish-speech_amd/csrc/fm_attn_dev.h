@@ -103,6 +103,16 @@ __device__ __forceinline__ void fast_attn_head(const FastFusedArgs<T>& a, int r,
     };
     prep(q0, q1, qw0, qw1, a.qk_norm);
     prep(k0, k1, kw0, kw1, a.qk_norm);
+    if (a.qdbg) {  // per-op test hook only (fm_op_qk_rope)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            if (p < half) {
+                a.qdbg[((size_t)r * a.nh + h) * hd + 2 * p] = q0[u];
+                a.qdbg[((size_t)r * a.nh + h) * hd + 2 * p + 1] = q1[u];
+            }
+        }
+    }
     if (a.dbg) tz[2] = __builtin_amdgcn_s_memrealtime();
     if (h == kvh * g) {  // first q head of the group stores the new k / v
 #pragma unroll

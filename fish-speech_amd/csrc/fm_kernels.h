@@ -76,7 +76,8 @@ struct SlotParams {
     float temperature, top_p;
     int top_k, mask_im_end;
     uint64_t seed;
-    int step, pad;
+    int step;
+    int force;  // teacher forcing (fm_llm_force): the samplers emit force_cols[slot] and tap their logits
 };
 
 struct SampleArgs {
@@ -90,6 +91,11 @@ struct SampleArgs {
     unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
     int32_t* cols;        // [R][ldc]
     int ldc;
+    // teacher forcing (SlotParams.force): emitted tokens come from force_cols[slot][ldc] and the
+    // logits row is copied to tap + slot * tap_ld (parity hook on the production decode graph)
+    const int32_t* force_cols;
+    float* tap;
+    int tap_ld;
 };
 
 template <typename T>
@@ -146,6 +152,7 @@ template <typename T> struct FastFusedArgs {
     float scale;
     T* out;              // [R][nh*hd]
     unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
+    float* qdbg = nullptr;    // per-op test hook (fm_op_qk_rope): q after qk-norm + RoPE [R][nh][hd]
 };
 template <typename T> struct GemvArgs {
     const T* W;
@@ -262,6 +269,7 @@ template <typename T> struct AttnDecArgs {
     int* cnt;            // [R][nkv] arrival tickets (zeroed at allocation, reset by the last block)
     T* out;              // [R][nh*hd]
     unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
+    float* qdbg = nullptr;    // per-op test hook (fm_op_qk_rope): q after qk-norm + RoPE [R][nh][hd]
 };
 template <typename T> void launch_attn_decode(hipStream_t s, const AttnDecArgs<T>& a, int R);
 // decode attention for the small-batch path (see fm_attn.hip): a.cap rows per block, a.maxsplit =

@@ -105,6 +105,10 @@ struct fm_llm {
     int *frame_slot = nullptr, *frame_pos = nullptr, *prow_slot = nullptr, *prow_pos = nullptr;
     int32_t *tok_in = nullptr, *cols = nullptr, *ptok = nullptr, *ras = nullptr;
     SlotParams* sp = nullptr;
+    // teacher forcing on the production graph (fm_llm_force / fm_llm_read_logits)
+    int32_t* force_cols = nullptr;              // [max_slots][C1]
+    float *tap_slow = nullptr, *tap_fast = nullptr;  // [max_slots][Nhead], [max_slots][C-1][cb]
+    std::vector<int> host_force;
     int32_t* h_cols = nullptr;  // pinned [2][max_slots][C1]
     int32_t* h_hist = nullptr;  // pinned, grown on demand: [frames][n][C1] of fm_llm_decode_frames
     size_t h_hist_n = 0;
@@ -632,6 +636,9 @@ template <typename T> struct Run {
         a.cols = m->cols;
         a.ldc = m->C1;
         a.dbg = fm_tuning().dbg;
+        a.force_cols = m->force_cols;
+        a.tap = slow ? m->tap_slow : m->tap_fast + (size_t)(c - 1) * m->cb;
+        a.tap_ld = slow ? m->Nhead : (m->C - 1) * m->cb;
         return a;
     }
 
@@ -885,6 +892,10 @@ static void finalize(fm_llm* m) {
     m->ptok = (int32_t*)m->dalloc((size_t)PREFILL_CHUNK * m->C1 * 4);
     m->ras = (int32_t*)m->dalloc((size_t)n * m->C1 * 10 * 4);
     m->sp = (SlotParams*)m->dalloc(sizeof(SlotParams) * n);
+    m->force_cols = (int32_t*)m->dalloc((size_t)n * m->C1 * 4);
+    m->tap_slow = (float*)m->dalloc((size_t)n * m->Nhead * 4);
+    m->tap_fast = (float*)m->dalloc((size_t)n * std::max(m->C - 1, 1) * m->cb * 4);
+    m->host_force.assign(n, 0);
     HIPCHK(hipHostMalloc((void**)&m->h_cols, (size_t)2 * n * m->C1 * 4, hipHostMallocDefault));
     m->host_pos.assign(n, 0);
     m->host_step.assign(n, 0);
@@ -919,6 +930,9 @@ static void reset_slot(fm_llm* m, int slot, const fm_sampling* sp) {
     HIPCHK(hipMemsetAsync((char*)m->ras + (size_t)slot * m->C1 * 10 * 4, 0, (size_t)m->C1 * 10 * 4, m->stream));
     SlotParams p{};
     if (sp) {
+        // the samplers select the top_k candidates in one wave: top_k is 1..64 (the reference
+        // default is 30, inference.py:532; larger values would silently change the distribution)
+        FMCHECK(sp->top_k >= 1 && sp->top_k <= 64, "top_k must be in [1, 64]: got " + std::to_string(sp->top_k));
         p.temperature = sp->temperature;
         p.top_p = sp->top_p;
         p.top_k = sp->top_k;
@@ -930,6 +944,7 @@ static void reset_slot(fm_llm* m, int slot, const fm_sampling* sp) {
         p.top_k = 1;
     }
     p.step = 0;
+    p.force = m->host_force[slot];
     HIPCHK(hipMemcpyAsync(m->sp + slot, &p, sizeof p, hipMemcpyHostToDevice, m->stream));
     HIPCHK(hipStreamSynchronize(m->stream));
     m->host_step[slot] = 0;
@@ -1430,6 +1445,50 @@ int fm_llm_kernel_bench(fm_llm* m, const char* cls, int reps, double* avg_us, in
         if (avg_us) *avg_us = (double)ms * 1e3 / ((double)reps * rec.size());
         if (launches) *launches = (int64_t)rec.size();
         if (bytes) *bytes = b;
+    });
+}
+
+int fm_llm_force(fm_llm* m, int slot, const int32_t* col) {
+    return fm_guard([&] {
+        FMCHECK(m, "null handle");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        FMCHECK(slot >= 0 && slot < m->max_slots, "bad slot");
+        const int on = col != nullptr;
+        if (on) {
+            const fm_model_config& c = m->c;
+            FMCHECK((col[0] >= c.semantic_begin_id && col[0] <= c.semantic_end_id) || col[0] == c.im_end_id,
+                    "forced token is outside the sampler's support (semantic ids + <|im_end|>)");
+            for (int q = 1; q < m->C1; ++q)
+                FMCHECK(col[q] >= 0 && col[q] < m->cb, "forced codebook token out of range");
+            HIPCHK(hipMemcpyAsync(m->force_cols + (size_t)slot * m->C1, col, (size_t)m->C1 * 4,
+                                  hipMemcpyHostToDevice, m->stream));
+        }
+        m->host_force[slot] = on;
+        HIPCHK(hipMemcpyAsync(&m->sp[slot].force, &m->host_force[slot], sizeof(int), hipMemcpyHostToDevice,
+                              m->stream));
+        HIPCHK(hipStreamSynchronize(m->stream));
+    });
+}
+
+int fm_llm_read_logits(fm_llm* m, int slot, float* slow_logits, float* fast_logits) {
+    return fm_guard([&] {
+        FMCHECK(m && m->finalized, "null or unfinalized handle");
+        FMCHECK(slot >= 0 && slot < m->max_slots, "bad slot");
+        HIPCHK(hipSetDevice(m->device));
+        const fm_model_config& c = m->c;
+        std::vector<float> lg(m->Nhead);
+        HIPCHK(hipMemcpyAsync(lg.data(), m->tap_slow + (size_t)slot * m->Nhead, (size_t)m->Nhead * 4,
+                              hipMemcpyDeviceToHost, m->stream));
+        if (fast_logits && m->C > 1)
+            HIPCHK(hipMemcpyAsync(fast_logits, m->tap_fast + (size_t)slot * (m->C - 1) * m->cb,
+                                  (size_t)(m->C - 1) * m->cb * 4, hipMemcpyDeviceToHost, m->stream));
+        HIPCHK(hipStreamSynchronize(m->stream));
+        if (slow_logits) {
+            for (int i = 0; i < c.vocab_size; ++i) slow_logits[i] = -INFINITY;
+            for (int i = 0; i < m->nsem; ++i) slow_logits[c.semantic_begin_id + i] = lg[i];
+            slow_logits[c.im_end_id] = lg[m->nsem];
+        }
     });
 }
 

@@ -1,0 +1,265 @@
+// fm_ops.cpp -- per-op test hooks of libfishmi (include/fishmi.h, "per-op parity hooks").
+//
+// Each hook runs ONE production kernel of the decode path on caller-supplied operands, so the
+// GPU tests can hold the fused forms to the reference's per-op goldens (tests/golden/ops.npz):
+//   fm_op_rmsnorm   RMSNorm (llama.py:989-1000) as the decode path computes it: the GEMV
+//                   prologue (first layer / head: statistic from the row itself; later layers:
+//                   statistic from the producing GEMV's per-tile sums of squares), or the
+//                   standalone row kernel of the batched / prefill path
+//   fm_op_qk_rope   QK-norm (llama.py:861-863) + RoPE with the bf16 table (llama.py:1003-1037)
+//                   inside the fused decode attention kernels (slow attn_decode2, fast attn2)
+//   fm_op_embed     the Dual-AR input embedding (llama.py:399-420)
+//   fm_rope_table   the host-built bf16 cos/sin table (no device needed)
+// Operands are fp32 host arrays, converted to the precision's storage type (bf16 rounding is the
+// caller's business: pass bf16-valued floats for bit-level comparisons).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <vector>
+
+#include "fm_kernels.h"
+#include "fm_runtime.h"
+
+namespace {
+
+struct DevBufs {
+    std::vector<void*> ptrs;
+    ~DevBufs() {
+        for (void* p : ptrs) (void)hipFree(p);
+    }
+    void* alloc(size_t bytes) {
+        void* p = nullptr;
+        HIPCHK(hipMalloc(&p, bytes ? bytes : 16));
+        HIPCHK(hipMemset(p, 0, bytes ? bytes : 16));
+        ptrs.push_back(p);
+        return p;
+    }
+    // fp32 host -> device storage type T
+    template <typename T> T* upload(const float* h, size_t n, hipStream_t s) {
+        float* tmp = (float*)alloc(n * 4);
+        HIPCHK(hipMemcpy(tmp, h, n * 4, hipMemcpyHostToDevice));
+        T* d = (T*)alloc(n * sizeof(T));
+        launch_convert<T>(s, tmp, 0, (int64_t)n, d);
+        HIPCHK(hipGetLastError());
+        return d;
+    }
+};
+
+template <typename T> void download(const T* d, size_t n, float* out, hipStream_t s) {
+    std::vector<T> h(n);
+    HIPCHK(hipMemcpyAsync(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (size_t i = 0; i < n; ++i) {
+        if constexpr (sizeof(T) == 2) {
+            const uint32_t u = (uint32_t)h[i] << 16;
+            memcpy(&out[i], &u, 4);
+        } else {
+            out[i] = h[i];
+        }
+    }
+}
+
+struct StreamGuard {
+    hipStream_t s = nullptr;
+    explicit StreamGuard(int device) {
+        int n = 0;
+        FMCHECK(hipGetDeviceCount(&n) == hipSuccess && n > 0, "no HIP device visible");
+        FMCHECK(device >= 0 && device < n, "bad device index");
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    }
+    ~StreamGuard() {
+        if (s) (void)hipStreamDestroy(s);
+    }
+};
+
+template <typename T>
+void rmsnorm_t(hipStream_t s, int mode, const float* x, const float* w, int R, int d, float eps, float* y) {
+    DevBufs b;
+    T* xd = b.upload<T>(x, (size_t)R * d, s);
+    T* wd = b.upload<T>(w, (size_t)d, s);
+    T* yd = (T*)b.alloc((size_t)R * d * sizeof(T));
+    if (mode == 2) {
+        launch_rmsnorm<T>(s, xd, d, wd, d, eps, yd, d, R);
+    } else {
+        // a 16-row GEMV of zeros: only its prologue's X' (stored through xn_out) is looked at
+        T* wz = (T*)b.alloc((size_t)16 * d * sizeof(T));
+        T* yz = (T*)b.alloc((size_t)R * 16 * sizeof(T));
+        int* tickets = (int*)b.alloc(4096);
+        GemvArgs<T> a{};
+        a.W = wz;
+        a.nw = wd;
+        a.eps = eps;
+        a.R = R;
+        a.N = 16;
+        a.K = d;
+        a.Y = yz;
+        a.ldy = 16;
+        a.xn_out = yd;
+        a.ldxo = d;
+        a.tickets = tickets;
+        if (mode == 0) {  // PRO_NORM: first layer / head, statistic from the row itself
+            a.X = xd;
+            a.ldx = d;
+            launch_gemv<T>(s, a, PRO_NORM, EPI_STORE, 1);
+        } else {
+            // PRO_PRENORM: a zero-weight EPI_SLABFIN GEMV finalises x = round(x + round(0)) and
+            // its per-16-column sums of squares, exactly as the wo / w2 GEMVs do for the next norm
+            T* xz = (T*)b.alloc((size_t)R * 32 * sizeof(T));
+            T* wz2 = (T*)b.alloc((size_t)d * 32 * sizeof(T));
+            float* slab = (float*)b.alloc((size_t)R * d * 4);
+            float* ss = (float*)b.alloc((size_t)(d / 16) * R * 4);
+            T* xf = (T*)b.alloc((size_t)R * d * sizeof(T));
+            GemvArgs<T> f{};
+            f.W = wz2;
+            f.X = xz;
+            f.ldx = 32;
+            f.R = R;
+            f.N = d;
+            f.K = 32;
+            f.Yf = slab;
+            f.ldy = d;
+            f.res = xd;
+            f.ldr = d;
+            f.res_out = xf;
+            f.ldro = d;
+            f.ss_out = ss;
+            f.tickets = tickets;
+            f.eps = eps;
+            launch_gemv<T>(s, f, PRO_PLAIN, EPI_SLABFIN, 1);
+            a.X = xf;
+            a.ldx = d;
+            a.ss_in = ss;
+            launch_gemv<T>(s, a, PRO_PRENORM, EPI_STORE, 1);
+        }
+    }
+    HIPCHK(hipGetLastError());
+    download<T>(yd, (size_t)R * d, y, s);
+}
+
+template <typename T>
+void qk_rope_t(hipStream_t s, int kernel, const float* qkv, int nh, int nkv, int hd, const float* qn,
+               const float* kn, int qk_norm, float eps, float base, int pos, float* q_out, float* k_out) {
+    DevBufs b;
+    const int ld = (nh + 2 * nkv) * hd;
+    T* raw = b.upload<T>(qkv, (size_t)ld, s);
+    T* qnd = qk_norm ? b.upload<T>(qn, (size_t)hd, s) : (T*)b.alloc((size_t)hd * sizeof(T));
+    T* knd = qk_norm ? b.upload<T>(kn, (size_t)hd, s) : (T*)b.alloc((size_t)hd * sizeof(T));
+    const int S = (pos + 1 + 7) / 8 * 8;
+    auto tab = rope_table_host(S, hd, base);
+    float* rope = (float*)b.alloc(tab.size() * 4);
+    HIPCHK(hipMemcpy(rope, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+    const size_t stride = (size_t)nkv * S * hd;
+    T* kc = (T*)b.alloc(stride * sizeof(T));
+    T* vc = (T*)b.alloc(stride * sizeof(T));
+    T* out = (T*)b.alloc((size_t)nh * hd * sizeof(T));
+    float* qd = (float*)b.alloc((size_t)nh * hd * 4);
+    int* row = (int*)b.alloc(8);
+    const int rs[2] = {0, pos};
+    HIPCHK(hipMemcpy(row, rs, 8, hipMemcpyHostToDevice));
+    const float scale = 1.0f / sqrtf((float)hd);
+    if (kernel == 0) {  // slow decode attention (attn_decode2)
+        AttnDecArgs<T> a{raw, ld, row, row + 1, nh, nkv, hd, qk_norm, eps, qnd, knd, rope, kc, vc, stride, 0, S,
+                         1, scale, nullptr};
+        a.cap = attn2_cap(hd, nh / nkv, sizeof(T));
+        a.maxsplit = FM_CEIL(S, a.cap);
+        a.part = (float*)b.alloc((size_t)nh * a.maxsplit * (hd + 2) * 4);
+        a.cnt = (int*)b.alloc((size_t)nkv * 4);
+        a.out = out;
+        a.qdbg = qd;
+        launch_attn_decode2<T>(s, a, 1);
+    } else {  // fast-model attention (one wave per q head) at codebook position pos
+        FMCHECK(pos < 16, "fast attention positions are < 16");
+        FastFusedArgs<T> a{raw, ld, row, nh, nkv, hd, qk_norm, eps, qnd, knd, rope, kc, vc, stride, 0, S, pos,
+                           scale, out};
+        a.qdbg = qd;
+        launch_fast_attn2<T>(s, a, 1);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(q_out, qd, (size_t)nh * hd * 4, hipMemcpyDeviceToHost, s));
+    for (int h = 0; h < nkv; ++h) download<T>(kc + (size_t)h * S * hd + (size_t)pos * hd, hd, k_out + (size_t)h * hd, s);
+    HIPCHK(hipStreamSynchronize(s));
+}
+
+template <typename T>
+void embed_t(hipStream_t s, const int32_t* tok, int R, const float* emb, int V, const float* cbemb, int d, int C,
+             int cb, int sb, int se, int scale, float* x) {
+    DevBufs b;
+    T* e = b.upload<T>(emb, (size_t)V * d, s);
+    T* ce = b.upload<T>(cbemb, (size_t)C * cb * d, s);
+    int32_t* td = (int32_t*)b.alloc((size_t)R * (C + 1) * 4);
+    HIPCHK(hipMemcpy(td, tok, (size_t)R * (C + 1) * 4, hipMemcpyHostToDevice));
+    T* xd = (T*)b.alloc((size_t)R * d * sizeof(T));
+    launch_embed<T>(s, td, R, e, ce, d, C, cb, sb, se, scale, xd, nullptr);
+    HIPCHK(hipGetLastError());
+    download<T>(xd, (size_t)R * d, x, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int fm_op_rmsnorm(int device, int precision, int mode, const float* x, const float* w, int R, int d, float eps,
+                  float* y) {
+    return fm_guard([&] {
+        FMCHECK(x && w && y, "null argument");
+        FMCHECK(mode >= 0 && mode <= 2, "mode must be 0 (PRO_NORM), 1 (PRO_PRENORM) or 2 (row kernel)");
+        FMCHECK(R >= 1 && d >= 32 && d % 32 == 0, "need R >= 1 and d a multiple of 32");
+        FMCHECK(mode == 2 || (R <= 8 && d <= 4096), "GEMV prologue modes need R <= 8 and d <= 4096");
+        StreamGuard g(device);
+        if (precision == FM_PREC_BF16)
+            rmsnorm_t<bf16_t>(g.s, mode, x, w, R, d, eps, y);
+        else
+            rmsnorm_t<float>(g.s, mode, x, w, R, d, eps, y);
+    });
+}
+
+int fm_op_qk_rope(int device, int precision, int kernel, const float* qkv, int nh, int nkv, int hd, const float* qn,
+                  const float* kn, int qk_norm, float eps, float rope_base, int pos, float* q_out, float* k_out) {
+    return fm_guard([&] {
+        FMCHECK(qkv && q_out && k_out, "null argument");
+        FMCHECK(!qk_norm || (qn && kn), "qk_norm needs both norm weights");
+        FMCHECK(kernel == 0 || kernel == 1, "kernel must be 0 (slow attn_decode2) or 1 (fast attn2)");
+        FMCHECK(nh >= 1 && nkv >= 1 && nh % nkv == 0 && nh / nkv <= 16, "bad head counts");
+        FMCHECK(hd >= 8 && hd <= 256 && hd % 8 == 0, "bad head_dim");
+        FMCHECK(pos >= 0 && pos < 65536, "bad position");
+        StreamGuard g(device);
+        if (precision == FM_PREC_BF16)
+            qk_rope_t<bf16_t>(g.s, kernel, qkv, nh, nkv, hd, qn, kn, qk_norm, eps, rope_base, pos, q_out, k_out);
+        else
+            qk_rope_t<float>(g.s, kernel, qkv, nh, nkv, hd, qn, kn, qk_norm, eps, rope_base, pos, q_out, k_out);
+    });
+}
+
+int fm_op_embed(int device, int precision, const int32_t* tok, int R, const float* emb, int vocab,
+                const float* cbemb, int dim, int num_codebooks, int codebook_size, int semantic_begin_id,
+                int semantic_end_id, int scale_codebook_embeddings, float* x) {
+    return fm_guard([&] {
+        FMCHECK(tok && emb && cbemb && x && R >= 1 && dim % 8 == 0, "bad arguments");
+        for (int r = 0; r < R; ++r) {
+            FMCHECK(tok[(size_t)r * (num_codebooks + 1)] >= 0 && tok[(size_t)r * (num_codebooks + 1)] < vocab,
+                    "token id out of range");
+            for (int q = 1; q <= num_codebooks; ++q) {
+                const int v = tok[(size_t)r * (num_codebooks + 1) + q];
+                FMCHECK(v >= 0 && v < codebook_size, "codebook token out of range");
+            }
+        }
+        StreamGuard g(device);
+        if (precision == FM_PREC_BF16)
+            embed_t<bf16_t>(g.s, tok, R, emb, vocab, cbemb, dim, num_codebooks, codebook_size, semantic_begin_id,
+                            semantic_end_id, scale_codebook_embeddings, x);
+        else
+            embed_t<float>(g.s, tok, R, emb, vocab, cbemb, dim, num_codebooks, codebook_size, semantic_begin_id,
+                           semantic_end_id, scale_codebook_embeddings, x);
+    });
+}
+
+int fm_rope_table(int seq_len, int head_dim, float base, float* out) {
+    return fm_guard([&] {
+        FMCHECK(out && seq_len >= 1 && head_dim >= 2 && head_dim % 2 == 0, "bad arguments");
+        auto t = rope_table_host(seq_len, head_dim, base);
+        memcpy(out, t.data(), t.size() * 4);
+    });
+}
+
+}  // extern "C"

@@ -184,6 +184,46 @@ class DualARModel:
             native.f32p(fl) if nc is not None else None))
         return lg, hid, (fl if nc is not None else None)
 
+    # ---- teacher forcing on the production decode path ------------------------------------
+    def force(self, slot: int, col) -> None:
+        """While forced, the slot's samplers emit `col` (C+1 tokens) and tap their logits
+        (fm_llm_force); col=None stops forcing."""
+        if col is None:
+            native.check(native.lib().fm_llm_force(self.h, slot, None))
+            return
+        c = np.ascontiguousarray(col, dtype=np.int32).reshape(-1)
+        assert c.size == self.C1
+        native.check(native.lib().fm_llm_force(self.h, slot, native.i32p(c)))
+
+    def read_logits(self, slot: int = 0):
+        """(slow logits [V], fast logits [(C-1), cb]) the last forced frame's samplers were handed."""
+        lg = np.zeros(self.cfg.vocab_size, np.float32)
+        fl = np.zeros((max(self.cfg.num_codebooks - 1, 1), self.cfg.codebook_size), np.float32)
+        native.check(native.lib().fm_llm_read_logits(self.h, slot, native.f32p(lg), native.f32p(fl)))
+        return lg, fl[: self.cfg.num_codebooks - 1]
+
+    def teacher_decode(self, prompt: np.ndarray, cols: np.ndarray, slot: int = 0):
+        """The reference's teacher-forced loop (oracle/gen_goldens.py teacher_forced: prefill, then
+        one forward_generate per emitted column) on the production path: the prefill, then
+        n-1 single-frame decodes through the captured frame graph, each sampler forced to emit the
+        given column.  cols: (C+1, n).  Returns slow logits (n, V) and fast logits (n, C-1, cb)."""
+        cols = np.ascontiguousarray(cols, dtype=np.int32)
+        n = cols.shape[1]
+        slow = np.zeros((n, self.cfg.vocab_size), np.float32)
+        fast = np.zeros((n, self.cfg.num_codebooks - 1, self.cfg.codebook_size), np.float32)
+        sp = self.sampling(top_k=1)
+        try:
+            for i in range(n):
+                self.force(slot, cols[:, i])
+                if i == 0:
+                    self.prefill(slot, prompt, sp)
+                else:
+                    self.decode([slot])
+                slow[i], fast[i] = self.read_logits(slot)
+        finally:
+            self.force(slot, None)
+        return slow, fast
+
     # ---- accounting / profiling --------------------------------------------------------
     def frame_bytes(self, n: int, pos: int) -> int:
         return int(native.lib().fm_llm_frame_bytes(self.h, n, pos))

@@ -26,7 +26,8 @@ ABI_SYMBOLS = [
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
     "fm_codec_finalize", "fm_codec_decode", "fm_codec_stream_reset", "fm_codec_decode_chunk",
     "fm_codec_profile_read", "fm_codec_debug_read", "fm_codec_enable_encoder", "fm_codec_encode",
-    "fm_codec_close",
+    "fm_codec_close", "fm_llm_force", "fm_llm_read_logits", "fm_op_rmsnorm", "fm_op_qk_rope",
+    "fm_op_embed", "fm_rope_table",
 ]
 
 
@@ -74,6 +75,12 @@ def lib():
     L.fm_tune.argtypes = [ctypes.c_char_p, i32]
     L.fm_debug_ts_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), i64, ctypes.POINTER(ctypes.c_int64)]
     L.fm_llm_close.argtypes = [vp]
+    L.fm_llm_force.argtypes = [vp, i32, pi32]
+    L.fm_llm_read_logits.argtypes = [vp, i32, pf32, pf32]
+    L.fm_op_rmsnorm.argtypes = [i32, i32, i32, pf32, pf32, i32, i32, f32, pf32]
+    L.fm_op_qk_rope.argtypes = [i32, i32, i32, pf32, i32, i32, i32, pf32, pf32, i32, f32, f32, i32, pf32, pf32]
+    L.fm_op_embed.argtypes = [i32, i32, pi32, i32, pf32, i32, pf32, i32, i32, i32, i32, i32, i32, pf32]
+    L.fm_rope_table.argtypes = [i32, i32, f32, pf32]
     if hasattr(L, "fm_codec_open"):
         L.fm_codec_open.argtypes = [vp, i32, i32, i32, ctypes.POINTER(vp)]
         L.fm_codec_set_tensor.argtypes = [vp, ctypes.c_char_p, vp, i32, i64]

@@ -1,0 +1,68 @@
+"""Per-op parity hooks of libfishmi (include/fishmi.h, fm_op_*): one production kernel of the decode
+path on caller operands, used by tests/test_gpu_ops.py against the reference's per-op goldens.
+
+Reference semantics pinned (file:line in PoTaTo-Mika/fish-speech):
+  rmsnorm   RMSNorm.forward            llama.py:989-1000   (fp32 normalise, round, * weight, round)
+  qk_rope   nn.RMSNorm(head_dim) +     llama.py:861-863, 900-902 (one rounding incl. the weight)
+            apply_rotary_emb           llama.py:1025-1037 (bf16 cos/sin table, fp32 rotate, round)
+  embed     forward_generate embedding llama.py:399-420
+  rope_table precompute_freqs_cis      llama.py:1003-1022
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import native
+
+MODES = {"prologue_norm": 0, "prologue_prenorm": 1, "row_kernel": 2}
+
+
+def _prec(precision: str) -> int:
+    return native.FM_PREC_BF16 if precision == "bf16" else native.FM_PREC_FP32
+
+
+def rmsnorm(x, w, eps, precision="bf16", mode="prologue_prenorm", device=0):
+    x = np.ascontiguousarray(x, np.float32)
+    R, d = x.reshape(-1, x.shape[-1]).shape
+    w = np.ascontiguousarray(w, np.float32)
+    y = np.zeros((R, d), np.float32)
+    native.check(native.lib().fm_op_rmsnorm(device, _prec(precision), MODES[mode], native.f32p(x),
+                                            native.f32p(w), R, d, float(eps), native.f32p(y)))
+    return y.reshape(x.shape)
+
+
+def qk_rope(qkv_row, nh, nkv, hd, pos, rope_base, qn=None, kn=None, eps=1e-6, precision="bf16",
+            kernel="slow", device=0):
+    """q (nh, hd) and k (nkv, hd) after qk-norm (if weights given) and RoPE at `pos`."""
+    raw = np.ascontiguousarray(qkv_row, np.float32).reshape(-1)
+    assert raw.size == (nh + 2 * nkv) * hd
+    qk = qn is not None
+    qn_ = np.ascontiguousarray(qn if qk else np.ones(hd), np.float32)
+    kn_ = np.ascontiguousarray(kn if qk else np.ones(hd), np.float32)
+    q = np.zeros(nh * hd, np.float32)
+    k = np.zeros(nkv * hd, np.float32)
+    native.check(native.lib().fm_op_qk_rope(device, _prec(precision), 0 if kernel == "slow" else 1,
+                                            native.f32p(raw), nh, nkv, hd, native.f32p(qn_), native.f32p(kn_),
+                                            int(qk), float(eps), float(rope_base), int(pos), native.f32p(q),
+                                            native.f32p(k)))
+    return q.reshape(nh, hd), k.reshape(nkv, hd)
+
+
+def embed(tok, emb, cbemb, num_codebooks, codebook_size, semantic_begin_id, semantic_end_id, scale,
+          precision="bf16", device=0):
+    """tok: (R, C+1) rows (row r = one position's [text/semantic token, codes...])."""
+    t = np.ascontiguousarray(tok, np.int32)
+    emb = np.ascontiguousarray(emb, np.float32)
+    cbemb = np.ascontiguousarray(cbemb, np.float32)
+    R, d = t.shape[0], emb.shape[1]
+    x = np.zeros((R, d), np.float32)
+    native.check(native.lib().fm_op_embed(device, _prec(precision), native.i32p(t), R, native.f32p(emb),
+                                          emb.shape[0], native.f32p(cbemb), d, num_codebooks, codebook_size,
+                                          semantic_begin_id, semantic_end_id, int(scale), native.f32p(x)))
+    return x
+
+
+def rope_table(seq_len, head_dim, base):
+    out = np.zeros((seq_len, head_dim // 2, 2), np.float32)
+    native.check(native.lib().fm_rope_table(seq_len, head_dim, float(base), native.f32p(out)))
+    return out

@@ -126,6 +126,16 @@ int fm_llm_profile_read(fm_llm* h, const char* kernel_class, double* total_ms, i
 int fm_llm_kernel_bench(fm_llm* h, const char* kernel_class, int reps, double* avg_us,
                         int64_t* launches, int64_t* bytes);
 int fm_llm_use_graph(fm_llm* h, int enable);
+/* Teacher forcing on the PRODUCTION decode path (parity with the reference's own teacher-forced
+   forward_generate / forward_generate_fast, llama.py:390-466, 798-827): while a slot is forced,
+   every sampler of its frames (prefill and decode, graph-replayed or eager, batch-1 GEMV path or
+   batched path) emits the given column instead of its draw and copies the logits it was handed
+   to a per-slot tap.  col: (C+1) tokens of the next emitted column (row 0 a semantic id or
+   <|im_end|>), or NULL to stop forcing; set it before fm_llm_prefill / each fm_llm_decode.
+   read_logits: the last forced frame's slow logits (V floats, -inf outside the semantic rows and
+   <|im_end|>, bias NOT applied) and fast logits ((C-1) x codebook_size, codebooks 1..C-1). */
+int fm_llm_force(fm_llm* h, int slot, const int32_t* col);
+int fm_llm_read_logits(fm_llm* h, int slot, float* slow_logits, float* fast_logits);
 /* process-wide developer knobs of the decode GEMV ("gemv_nt" 0|1, "gemv_u" 2|4|8, "gemv_wpb" 4|8, "gemv_sk" 0|1, "gemv_sk_bpc" 1..4, "ksb_blocks" n, "ksb_balance"
    0|1, "rmsnorm_block" 0|1); they apply to launches recorded after the call (graphs captured earlier keep theirs). */
 int fm_tune(const char* key, int value);
@@ -134,6 +144,30 @@ int fm_tune(const char* key, int value);
    s_memrealtime ticks (100 MHz). */
 int fm_debug_ts_read(unsigned long long* out, int64_t max_records, int64_t* n_records);
 int fm_llm_close(fm_llm* h);
+
+/* ---- per-op parity hooks (tests): one production kernel on caller operands, fp32 host arrays
+   in/out (converted to the precision's storage type).  Each replaces nothing in the reference; they
+   pin the fused decode kernels to the reference's per-op semantics (tests/golden/ops.npz). */
+/* RMSNorm (llama.py:989-1000), R rows of d: mode 0 = the decode GEMV prologue computing the
+   statistic from the row (first layer, head), 1 = the prologue fed by the producing GEMV's per-tile
+   sums of squares (every later norm of the batch-1 path), 2 = the standalone row kernel (batched /
+   prefill path). */
+int fm_op_rmsnorm(int device, int precision, int mode, const float* x, const float* w, int R, int d,
+                  float eps, float* y);
+/* QK-norm (llama.py:861-863) + RoPE with the bf16 table (llama.py:1003-1037) at position pos, as the
+   fused decode attention computes them: kernel 0 = slow attn_decode2, 1 = fast-model attention.
+   qkv: one raw projection row [(nh + 2 nkv) * hd]; q_out [nh * hd], k_out [nkv * hd] (the k row as
+   written to the KV cache). */
+int fm_op_qk_rope(int device, int precision, int kernel, const float* qkv, int nh, int nkv, int hd,
+                  const float* qn, const float* kn, int qk_norm, float eps, float rope_base, int pos,
+                  float* q_out, float* k_out);
+/* Dual-AR input embedding (llama.py:399-420): tok R x (C+1) row-major, x R x dim. */
+int fm_op_embed(int device, int precision, const int32_t* tok, int R, const float* emb, int vocab,
+                const float* cbemb, int dim, int num_codebooks, int codebook_size, int semantic_begin_id,
+                int semantic_end_id, int scale_codebook_embeddings, float* x);
+/* the RoPE cos/sin table the library builds on the host (precompute_freqs_cis, llama.py:1003-1022):
+   out [seq_len][head_dim/2][2], bf16-valued floats.  No device needed. */
+int fm_rope_table(int seq_len, int head_dim, float base, float* out);
 
 /* ---- codec (modded DAC decode side, modded_dac_vq.yaml shapes) --------------------- */
 typedef struct fm_codec_config {

@@ -43,6 +43,7 @@ sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.join(REPO, "fish-speech_amd"))
 
 import ref_stubs  # noqa: E402
+import signals  # noqa: E402
 
 ref_stubs.install()
 
@@ -252,11 +253,18 @@ def run_llm_case(name, config, weights_dir, seed, log2_half, T, n_new, dtypes, p
         slow, fast, hid = teacher_forced(model, seq, T, n, dtype)
         tag = {torch.float32: "fp32", torch.bfloat16: "bf16"}[dtype]
         out = os.path.join(GOLD, f"{name}_{tag}.npz")
+        extra = {}
+        if dtype == torch.bfloat16:
+            # the same teacher-forced stream through the fp32 model: the reference's own bf16 error
+            # (slow/fast bf16 - fp32) is the bound a bf16 build is held to (tests/test_gpu_llm.py)
+            m32 = build_llm(config, weights_dir, seed, log2_half).to(torch.float32)
+            s32, f32, _ = teacher_forced(m32, seq, T, n, torch.float32)
+            extra = dict(slow_logits_f32=s32, fast_logits_f32=f32)
         np.savez_compressed(out, prompt=prompt.numpy().astype(np.int32),
                             seq=seq.numpy().astype(np.int32), slow_logits=slow,
                             fast_logits=fast, hidden=hid, synth_seed=seed,
                             log2_half=log2_half, torch_version=torch.__version__,
-                            threads=torch.get_num_threads())
+                            threads=torch.get_num_threads(), **extra)
         print(f"{name} {tag}: T={T} generated {n} frames in {time.time() - t0:.1f}s -> {out}")
         print("  first columns:", seq[:, T:T + 3].T.tolist())
 
@@ -288,12 +296,14 @@ def cmd_ops():
     m.weight.data = torch.from_numpy(rng.normal(1, 0.2, 256).astype(np.float32)).bfloat16()
     with torch.no_grad():
         out["rms_x"], out["rms_w"], out["rms_y"] = x.float(), m.weight.float(), m(x).float()
+        out["rms_y32"] = m.float()(x.float()).float()  # the fp32 model on the same values
     # qk-norm nn.RMSNorm(head_dim) on bf16 (llama.py:861-863)
     q = torch.from_numpy(rng.normal(0, 2, (2, 3, 4, 64)).astype(np.float32)).bfloat16()
     qn = torch.nn.RMSNorm(64, 1e-6).bfloat16()
     qn.weight.data = torch.from_numpy(rng.normal(1, 0.2, 64).astype(np.float32)).bfloat16()
     with torch.no_grad():
         out["qk_x"], out["qk_w"], out["qk_y"] = q.float(), qn.weight.float(), qn(q).float()
+        out["qk_y32"] = qn.float()(q.float()).float()
     # RoPE (llama.py:1003-1037)
     fc = llama.precompute_freqs_cis(64, 32, 10000)
     out["rope_table"] = fc.float()
@@ -302,6 +312,20 @@ def cmd_ops():
     out["rope_pos"] = pos.to(torch.int32)
     out["rope_x"] = xr.float()
     out["rope_y"] = llama.apply_rotary_emb(xr, fc[pos]).float()
+    out["rope_y32"] = llama.apply_rotary_emb(xr.float(), fc[pos]).float()
+    # Dual-AR input embedding (llama.py:399-420) captured at the first block's input, llm_a shapes
+    # (fish_qwen3_omni: scale_codebook_embeddings) with the synthetic weights of seed 11
+    for tag, dt in (("", torch.bfloat16), ("32", torch.float32)):
+        em = build_llm(LLM_A_CONFIG, None, seed=11, log2_half=3).to(dt)
+        ecfg = em.config
+        inp = make_prompt(ecfg, 20, 8).view(1, ecfg.num_codebooks + 1, 20)
+        got = {}
+        h = em.layers[0].register_forward_pre_hook(lambda mod, args: got.update(x=args[0].clone()))
+        with torch.no_grad():
+            em.forward_generate(inp)
+        h.remove()
+        out["emb_tok"] = inp[0].numpy().astype(np.int32)
+        out["emb_x" + tag] = got["x"][0].float()
     fc2 = llama.precompute_freqs_cis(4096, 128, 1000000)
     out["rope_table_big"] = fc2[::97].float()
     # logits_to_probs (inference.py:54-77) with bf16 temperature / top_p tensors
@@ -383,11 +407,8 @@ def build_codec(spec: dict, seed: int, enc_layers=None):
 
 
 def codec_codes(spec, T, seed):
-    rng = np.random.default_rng(seed)
-    c = np.zeros((1, spec["n_codebooks"] + 1, T), dtype=np.int64)
-    c[0, 0] = rng.integers(0, spec["semantic_codebook_size"], T)
-    c[0, 1:] = rng.integers(0, spec["codebook_size"], (spec["n_codebooks"], T))
-    return c
+    return signals.codec_codes(spec["n_codebooks"], spec["semantic_codebook_size"], spec["codebook_size"],
+                               T, seed)
 
 
 def run_codec(name, spec, seed, T, clamp_test: bool):
@@ -426,11 +447,7 @@ def run_codec(name, spec, seed, T, clamp_test: bool):
 # descript 1.0.0 VQ encode restated in ref_stubs (parity at that boundary unpinned, as for decode)
 # --------------------------------------------------------------------------------------
 def encode_audio(n, seed):
-    rng = np.random.default_rng(seed)
-    t = np.arange(n) / 44100.0
-    x = 0.4 * np.sin(2 * np.pi * 220 * t) + 0.2 * np.sin(2 * np.pi * 1375 * t + 0.3)
-    x = x * (0.6 + 0.4 * np.sin(2 * np.pi * 3 * t)) + 0.05 * rng.standard_normal(n)
-    return x.astype(np.float32)
+    return signals.reference_audio(n, seed)
 
 
 def run_codec_enc(name, spec, seed, n_samples, enc_layers):
@@ -496,6 +513,38 @@ def cmd_codec_full():
     run_codec("codec_full", CODEC_FULL, seed=37, T=4, clamp_test=False)
 
 
+def cmd_codec_long():
+    """Config-2 length (216 frames = 10 s) at the real modded_dac_vq.yaml shapes, so the post
+    transformer's 128-frame causal window (modded_dac.py:380-398) is crossed.  The waveform is kept
+    at two segments (frames [0, 8) and the last 40), in three reference modes: fp32; the CLI's
+    dac.to(bf16) (inference.py:416); and the engine's autocast(bf16) over fp32 weights
+    (vq_manager.py:16-21, fish_speech/inference_engine/__init__.py:179-192; CPU autocast here)."""
+    spec, seed, T, head, tail = CODEC_FULL, 37, 216, 8, 40
+    dac = build_codec(spec, seed)
+    codes = codec_codes(spec, T, seed + 101)
+    segs = lambda y: np.concatenate([y.reshape(-1)[: head * 2048], y.reshape(-1)[(T - tail) * 2048:]])
+    res = {"codes": codes.astype(np.int32), "synth_seed": seed, "spec": json.dumps(spec),
+           "torch_version": torch.__version__, "head_frames": head, "tail_frames": tail}
+    with torch.inference_mode():
+        t0 = time.time()
+        y32 = dac.from_indices(torch.from_numpy(codes.copy())).float().numpy()
+        res["wave_fp32"] = segs(y32)
+        print(f"codec_long fp32 {time.time() - t0:.1f}s")
+        with torch.autocast(device_type="cpu", dtype=torch.bfloat16):
+            ya = dac.from_indices(torch.from_numpy(codes.copy())).float().numpy()
+        res["wave_autocast"] = segs(ya)
+        ybf = dac.to(torch.bfloat16).from_indices(torch.from_numpy(codes.copy())).float().numpy()
+        res["wave_bf16"] = segs(ybf)
+    for k in ("wave_bf16", "wave_autocast"):
+        e = res[k] - res["wave_fp32"]
+        res[k + "_rms_err"] = float(np.sqrt(np.mean(e.astype(np.float64) ** 2)))
+        res[k + "_stft_db"] = signals.stft_logmag_error_db(res[k][head * 2048:], res["wave_fp32"][head * 2048:])
+    np.savez_compressed(os.path.join(GOLD, "codec_long.npz"), **res)
+    print(f"codec_long: T={T} in {time.time() - t0:.1f}s; signal rms {np.sqrt(np.mean(res['wave_fp32'] ** 2)):.4g}; "
+          f"bf16 rms err {res['wave_bf16_rms_err']:.4g} ({res['wave_bf16_stft_db']:.4g} dB); autocast rms err "
+          f"{res['wave_autocast_rms_err']:.4g} ({res['wave_autocast_stft_db']:.4g} dB)")
+
+
 # --------------------------------------------------------------------------------------
 # LLM at the real S2-Pro widths, reduced depth (synthetic weights, nothing committed but
 # the outputs).  Shapes per SURVEY.md §2.3.
@@ -505,7 +554,7 @@ LLM_WIDE_CONFIG = {
     "text_config": {
         "vocab_size": 155776, "n_layer": 2, "n_head": 32, "n_local_heads": 8,
         "head_dim": 128, "dim": 2560, "intermediate_size": 9728, "rope_base": 1000000,
-        "norm_eps": 1e-6, "max_seq_len": 64, "tie_word_embeddings": True,
+        "norm_eps": 1e-6, "max_seq_len": 128, "tie_word_embeddings": True,
         "attention_qkv_bias": False, "attention_o_bias": False, "attention_qk_norm": True,
     },
     "audio_decoder_config": {
@@ -523,24 +572,31 @@ def cmd_llm_wide():
         json.dump(LLM_WIDE_CONFIG, f, indent=1)
     from fish_speech.models.text2semantic import inference
 
+    T = 64  # >= 64 prompt tokens, then 16 single-column decode steps (SURVEY.md §8d config 2 shape)
     model = build_llm(LLM_WIDE_CONFIG, None, seed=41, log2_half=5).to(torch.bfloat16)
     cfg = model.config
-    prompt = make_prompt(cfg, 16, 3)
+    prompt = make_prompt(cfg, T, 3)
     t0 = time.time()
-    seq = inference.generate(model=model, prompt=prompt.clone(), max_new_tokens=4,
+    seq = inference.generate(model=model, prompt=prompt.clone(), max_new_tokens=17,
                              audio_masks=None, audio_parts=None, temperature=0.7, top_p=0.9,
                              top_k=1)
-    n = seq.shape[1] - 16
-    slow, fast, hid = teacher_forced(model, seq, 16, n, torch.bfloat16)
+    n = seq.shape[1] - T
+    slow, fast, hid = teacher_forced(model, seq, T, n, torch.bfloat16)
+    del model
+    m32 = build_llm(LLM_WIDE_CONFIG, None, seed=41, log2_half=5).to(torch.float32)
+    s32, f32, _ = teacher_forced(m32, seq, T, n, torch.float32)
+    del m32
     # keep the constrained rows only (semantic range + im_end); the rest are -inf
     keep = np.r_[IM_END_ID, cfg.semantic_begin_id:cfg.semantic_end_id + 1]
     np.savez_compressed(os.path.join(GOLD, "llm_wide_bf16.npz"),
                         prompt=prompt.numpy().astype(np.int32), seq=seq.numpy().astype(np.int32),
                         slow_rows=keep.astype(np.int32), slow_logits=slow[:, keep],
-                        fast_logits=fast, hidden=hid, synth_seed=41, log2_half=5,
-                        torch_version=torch.__version__, threads=torch.get_num_threads())
-    print(f"llm_wide: {n} frames in {time.time() - t0:.1f}s; first cols",
-          seq[:, 16:18].T.tolist())
+                        fast_logits=fast, hidden=hid, slow_logits_f32=s32[:, keep], fast_logits_f32=f32,
+                        synth_seed=41, log2_half=5, torch_version=torch.__version__,
+                        threads=torch.get_num_threads())
+    e_s = np.abs(slow[:, keep] - s32[:, keep])
+    print(f"llm_wide: T={T}, {n} frames in {time.time() - t0:.1f}s; reference bf16-vs-fp32 slow logits "
+          f"max {e_s.max():.4g} rms {np.sqrt((e_s ** 2).mean()):.4g}; first cols", seq[:, T:T + 2].T.tolist())
 
 
 # --------------------------------------------------------------------------------------

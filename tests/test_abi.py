@@ -37,3 +37,18 @@ def test_library_loads_without_gpu():
     assert L.fm_device_count() >= 0
     for s in _header_symbols():
         assert hasattr(L, s)
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libfishmi.so not built")
+def test_host_rope_table_matches_reference(golden):
+    """The bf16 cos/sin table the library builds on the host (fm_rope_table, no device) equals the
+    reference's precompute_freqs_cis (llama.py:1003-1022) bit for bit, both goldens of ops.npz."""
+    import numpy as np
+
+    from fishmi import ops
+
+    g = golden("ops.npz")
+    t = ops.rope_table(64, 32, 10000)
+    np.testing.assert_array_equal(t, g["rope_table"].reshape(t.shape))
+    t2 = ops.rope_table(4096, 128, 1000000)[::97]
+    np.testing.assert_array_equal(t2, g["rope_table_big"].reshape(t2.shape))
