@@ -37,10 +37,19 @@ class FishMICodec:
         self.h = h
 
     @classmethod
-    def from_checkpoint(cls, codec_pth, device=0, precision="bf16", max_frames=1024):
-        """load_codec_model / dac.inference.load_model (inference.py:395-417)."""
-        m = cls(CodecConfig(), device, precision, max_frames)
-        m.load_weights(load_codec_weights(codec_pth))
+    def from_checkpoint(cls, codec_pth, device=0, precision="bf16", max_frames=1024,
+                        cfg: CodecConfig = None, encoder: bool = False, encoder_dim: int = 64,
+                        enc_layers=(0, 0, 0, 4)):
+        """load_codec_model / dac.inference.load_model (inference.py:395-417,
+        fish_speech/models/dac/inference.py:23-47). `encoder=True` also loads the encode half
+        (Encoder, quantizer downsample / pre_module, VQ in_proj), which VQManager.encode_reference
+        needs (vq_manager.py:24-52); the decode-only inventory is the default."""
+        m = cls(cfg or CodecConfig(), device, precision, max_frames)
+        w = load_codec_weights(codec_pth)
+        if encoder:
+            m.enable_encoder(encoder_dim, enc_layers)
+            m.load_encoder_weights(w)
+        m.load_weights(w)
         m.finalize()
         return m
 

@@ -81,7 +81,9 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
     if isinstance(prompt_tokens, (list, tuple)):
         ptoks = [_codes(t) for t in prompt_tokens]
     elif prompt_tokens is not None:
-        ptoks = [_codes(prompt_tokens)]
+        # one (C, T) array: base_conversation wraps it together with a str prompt_text, as the
+        # reference does (inference.py:544-547)
+        ptoks = _codes(prompt_tokens)
     else:
         ptoks = None
     base = P.base_conversation(prompt_text, ptoks)

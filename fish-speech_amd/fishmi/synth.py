@@ -83,6 +83,9 @@ def codec_rule(name: str) -> tuple[float, int]:
     """(center, log2_half) for a modded-DAC decode-side tensor (modded_dac.py / rvq.py keys)."""
     if name.endswith(".alpha"):
         return 1.0, 1          # snake alpha in [0.5, 1.5)
+    if name == "decoder.model.6.conv.parametrizations.weight.original0":
+        return 0.0625, 6       # output conv gain: keeps the random-weight waveform off tanh's rails
+                               # (with g ~ 1 most samples sit at +-1 and parity only tests signs)
     if name.endswith("original0") or name.endswith("weight_g"):
         return 1.0, 2          # weight-norm gain g in [0.75, 1.25)
     if name.endswith("gamma"):

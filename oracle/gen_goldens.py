@@ -450,7 +450,10 @@ def encode_audio(n, seed):
     return signals.reference_audio(n, seed)
 
 
-def run_codec_enc(name, spec, seed, n_samples, enc_layers):
+def run_codec_enc(name, spec, seed, n_samples, enc_layers, tail_steps=None):
+    """tail_steps: keep only the last `tail_steps` encoder-transformer steps of the z_enc taps and
+    regenerate the audio in the test (signals.reference_audio(n_samples, audio_seed)), so a long
+    clip's fixture stays small."""
     dac = build_codec(spec, seed, enc_layers)
     audio = encode_audio(n_samples, seed + 2)
     margins = []
@@ -470,8 +473,9 @@ def run_codec_enc(name, spec, seed, n_samples, enc_layers):
 
     for vq in list(dac.quantizer.semantic_quantizer.quantizers) + list(dac.quantizer.quantizer.quantizers):
         track(vq)
-    res = {"audio": audio, "synth_seed": seed, "spec": json.dumps(spec),
-           "enc_layers": np.array(enc_layers, np.int32), "torch_version": torch.__version__}
+    res = {"audio": audio, "synth_seed": seed, "spec": json.dumps(spec), "audio_seed": seed + 2,
+           "n_samples": n_samples, "enc_layers": np.array(enc_layers, np.int32),
+           "torch_version": torch.__version__}
     with torch.inference_mode():
         x = torch.from_numpy(audio)[None, None]
         t0 = time.time()
@@ -492,6 +496,11 @@ def run_codec_enc(name, spec, seed, n_samples, enc_layers):
         dac_bf = dac.to(torch.bfloat16)
         res["z_enc_bf16"] = dac_bf.encoder(xp.bfloat16()).float().numpy()
         res["codes_bf16"] = dac_bf.encode(x.bfloat16())[0].numpy().astype(np.int32)
+    if tail_steps:
+        del res["audio"]
+        for k in ("z_enc", "z_enc_bf16"):
+            res[k] = np.ascontiguousarray(res[k][..., -tail_steps:])
+        res["tail_steps"] = tail_steps
     np.savez_compressed(os.path.join(GOLD, f"{name}.npz"), **res)
     print(f"{name}: {n_samples} samples -> codes {res['codes'].shape} in {dt:.1f}s; "
           f"min margin {res['margin'].min():.3g}; z_enc {res['z_enc'].shape} z_pre {res['z_pre'].shape}")
@@ -503,6 +512,25 @@ def cmd_codec_enc():
 
 def cmd_codec_enc_full():
     run_codec_enc("codec_enc_full", CODEC_FULL, seed=43, n_samples=8 * 2048 - 300, enc_layers=[0, 0, 0, 4])
+
+
+def cmd_codec_enc_long():
+    """160 code frames = 640 encoder-transformer steps (7.4 s): the encoder transformer's 512-step
+    causal window (modded_dac.py:380-398) is crossed, as in config 5's 30 s clip."""
+    run_codec_enc("codec_enc_long", CODEC_FULL, seed=47, n_samples=160 * 2048 - 300, enc_layers=[0, 0, 0, 4],
+                  tail_steps=96)
+
+
+def cmd_codec_keys():
+    """The state_dict key layout of the reference's own DAC at the real modded_dac_vq.yaml dims with
+    the encoder (enc_layers [0,0,0,4]): names and shapes only. Loader tests push a checkpoint with
+    exactly this layout through FishMICodec.from_checkpoint (dac/inference.py:23-47)."""
+    dac = build_codec(CODEC_FULL, 1, [0, 0, 0, 4])
+    keys = [[k, list(v.shape), str(v.dtype)] for k, v in dac.state_dict().items()]
+    with open(os.path.join(GOLD, "codec_keys.json"), "w") as f:
+        json.dump({"spec": CODEC_FULL, "enc_layers": [0, 0, 0, 4], "torch_version": torch.__version__,
+                   "keys": keys}, f, indent=0)
+    print(f"codec_keys: {len(keys)} tensors")
 
 
 def cmd_codec():
@@ -729,6 +757,7 @@ def cmd_engine():
 if __name__ == "__main__":
     cmds = sys.argv[1:] or ["all"]
     if cmds == ["all"]:
-        cmds = ["ops", "llm", "codec", "codec_full", "llm_wide", "prompt", "engine"]
+        cmds = ["ops", "llm", "codec", "codec_full", "codec_long", "codec_enc", "codec_enc_full",
+                "codec_enc_long", "codec_keys", "llm_wide", "prompt", "engine"]
     for c in cmds:
         globals()[f"cmd_{c}"]()

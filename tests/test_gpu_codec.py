@@ -95,3 +95,49 @@ def test_intermediate_latents_match_oracle(golden):
         x = m.debug_read(stage, T)
         assert np.abs(x - ref).max() <= 1e-4 * np.abs(ref).max(), stage
     assert np.abs(wave - wave_o).max() < 5e-3
+
+
+def _segments(g, wave):
+    """The fixture keeps frames [0, head) and the last `tail` frames of the 216-frame waveform."""
+    head, tail = int(g["head_frames"]), int(g["tail_frames"])
+    T = g["codes"].shape[-1]
+    w = wave.reshape(-1)
+    return np.concatenate([w[: head * 2048], w[(T - tail) * 2048:]]), head * 2048
+
+
+def test_long_fp32_matches_reference(golden):
+    """Config-2 length (216 frames): the post transformer's 128-frame causal window
+    (modded_dac.py:380-398) is crossed, so the window mask is checked against the reference."""
+    m, g = _codec("codec_long", golden, "fp32", max_frames=216)
+    got, _ = _segments(g, m.decode_codes(g["codes"][0]))
+    ref = g["wave_fp32"]
+    assert _rms(got - ref) <= 1e-3 * _rms(ref), (_rms(got - ref), _rms(ref))
+    m.close()
+
+
+@pytest.mark.parametrize("mode", ["one_shot", "streamed"])
+def test_long_bf16_within_reference_bf16_error(mode, golden):
+    """bf16 over 216 frames vs the reference fp32 waveform. Bounds are 1.5x the reference's own
+    bf16 error in both of its bf16 modes: the CLI's dac.to(bf16) (inference.py:416) and the engine's
+    autocast over fp32 weights (vq_manager.py:16-21). Two measures are used: RMS error, and the
+    multi-resolution STFT log-magnitude error in dB (oracle/signals.py). The
+    streamed decode uses 22-frame chunks, as config 5's vocoder does."""
+    import signals
+
+    m, g = _codec("codec_long", golden, "bf16", max_frames=216)
+    codes = g["codes"][0]
+    if mode == "one_shot":
+        wave = m.decode_codes(codes)
+    else:
+        m.stream_reset()
+        wave = np.concatenate([m.decode_chunk(np.ascontiguousarray(codes[:, t:t + 22]))
+                               for t in range(0, codes.shape[1], 22)])
+    got, head = _segments(g, wave)
+    ref = g["wave_fp32"]
+    err = _rms(got - ref)
+    db = signals.stft_logmag_error_db(got[head:], ref[head:])
+    for k in ("wave_bf16", "wave_autocast"):
+        assert err <= 1.5 * float(g[k + "_rms_err"]), (k, err, float(g[k + "_rms_err"]))
+        assert db <= 1.5 * float(g[k + "_stft_db"]), (k, db, float(g[k + "_stft_db"]))
+    assert np.abs(wave).max() <= 1.0
+    m.close()

@@ -19,14 +19,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _enc(name, golden, prec):
+def _enc(name, golden, prec, max_frames=16):
     from fishmi.codec import FishMICodec
     from fishmi.config import CodecConfig
 
     g = golden(f"{name}.npz")
     spec = json.loads(str(g["spec"]))
     cfg = CodecConfig.from_spec(spec)
-    m = FishMICodec(cfg, 0, prec, max_frames=16)
+    m = FishMICodec(cfg, 0, prec, max_frames=max_frames)
     m.enable_encoder(spec["encoder_dim"], [int(v) for v in g["enc_layers"]])
     m.synth(int(g["synth_seed"]))
     m.synth_encoder(int(g["synth_seed"]))
@@ -74,4 +74,37 @@ def test_encode_decode_round_trip_shapes(golden):
     assert codes.shape == (1, cfg.n_codebooks + 1, int(g["lens"][0])) and lens[0] == g["lens"][0]
     wave = m.decode_codes(codes[0])
     assert wave.shape == (2048 * codes.shape[2],) and np.isfinite(wave).all()
+    m.close()
+
+
+def _long_audio(g):
+    import signals
+
+    return signals.reference_audio(int(g["n_samples"]), int(g["audio_seed"]))
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_encode_long_crosses_window(prec, golden):
+    """160 code frames = 640 encoder-transformer steps: the encoder transformer's 512-step causal
+    window (modded_dac.py:380-398) is crossed, as it is for config 5's 30 s reference clip. The
+    fixture keeps the last 96 steps of the encoder output (past the window edge), the full
+    quantizer input and every code; the audio is regenerated from its seed (oracle/signals.py).
+    Bounds are the same as the short cases above."""
+    m, g, cfg = _enc("codec_enc_long", golden, prec, max_frames=160)
+    codes = m.encode_audio(_long_audio(g))
+    ref = g["codes"][0]
+    assert codes.shape == ref.shape
+    T, tail = ref.shape[1], int(g["tail_steps"])
+    z_enc = m.debug_read(10, T)[-tail:]
+    if prec == "fp32":
+        assert _rel(z_enc, g["z_enc"][0].T) < 1e-3
+        assert _rel(m.debug_read(11, T), g["z_pre"][0].T) < 1e-3
+        firm = g["margin"] > 1e-4
+        np.testing.assert_array_equal(codes[firm], ref[firm])
+        assert (codes == ref).mean() >= 0.9
+    else:
+        ref_err = _rel(g["z_enc_bf16"][0], g["z_enc"][0])
+        assert _rel(z_enc, g["z_enc"][0].T) <= 1.5 * ref_err, ref_err
+        ref_agree = (g["codes_bf16"][0] == ref).mean()
+        assert (codes == ref).mean() >= 0.75 * ref_agree, ((codes == ref).mean(), ref_agree)
     m.close()

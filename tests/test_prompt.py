@@ -73,3 +73,18 @@ def test_engine_device_and_precision_parsing():
     assert engine._device_index(torch.device("cuda", 2)) == 2 and engine._device_index(5) == 5
     assert engine._precision(torch.bfloat16) == "bf16" and engine._precision(torch.float32) == "fp32"
     assert engine._precision("bf16") == "bf16" and engine._precision("fp32") == "fp32"
+
+
+def test_single_prompt_text_and_tokens():
+    """generate_long(prompt_text="...", prompt_tokens=<one (C, T) array>) wraps both together
+    (inference.py:544-547): the system message is the same as for one-element lists, with a 2-D
+    VQ part."""
+    from fishmi import prompt as P
+
+    tok = P.FishTokenizer(os.path.join(GOLDEN, "tok_tiny"))
+    codes = np.random.default_rng(0).integers(0, 128, (10, 7))
+    one = P.base_conversation("reference one", codes)
+    lst = P.base_conversation(["reference one"], [codes])
+    assert one.messages[0].parts[-1].codes.shape == (10, 7)
+    np.testing.assert_array_equal(one.encode_for_inference(tok, num_codebooks=10)[0],
+                                  lst.encode_for_inference(tok, num_codebooks=10)[0])
