@@ -47,7 +47,11 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--batch", type=int, default=32,
                     help="throughput leg (BASELINE config 3): concurrent streams per GPU (0: skip)")
-    ap.add_argument("--batch-frames", type=int, default=256, help="throughput leg: frames decoded")
+    ap.add_argument("--batch-frames", type=int, default=512, help="throughput leg: frames per request")
+    ap.add_argument("--waves", type=int, default=1,
+                    help="throughput leg: requests = batch x GPUs x waves, pulled from rank 0's tick queue")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the in-run rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on the GEMV")
     ap.add_argument("--encode-seconds", type=float, default=30.0,
                     help="encode leg: seconds of reference audio through the codec encoder (0: skip)")
     return ap.parse_args()
@@ -82,25 +86,55 @@ def utterance(llm, codec, prompt, sp, frames, first_chunk):
                      total=t4 - t0)
 
 
-def throughput_leg(llm, cfg, batch, frames, sync, dist, world):
-    """BASELINE config 3 (config 4 at N GPUs): `batch` concurrent prompts per GPU with lengths
-    uniform in [16, 256] (seed 2), prefilled into their own KV slots, then decoded
-    together: one batched Dual-AR frame (slow pass + 10 fast passes + samplers of every stream)
-    per graph replay.  Returns aggregate audio-seconds per wall-second over all ranks."""
+def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world):
+    """BASELINE config 3 at N=1 (32 concurrent prompts per GPU) and config 4 at N=8 (256 requests
+    over 8 GPUs), end to end: rank 0 owns batch x world x waves requests (prompt lengths uniform in
+    [16, 256], seed 2; `frames` frames each) and hands them out through the tick queue
+    (fishmi/scheduler.py). Each rank prefills its requests into KV slots and decodes them together,
+    one batched Dual-AR frame per graph replay (slow pass + 10 fast passes + samplers of every
+    stream). It vocodes each finished stream through the streamed codec, and the int16 PCM is
+    gathered to rank 0 over RCCL. Value = audio seconds of PCM gathered at rank 0 / wall time
+    (max over ranks)."""
+    from fishmi import dp
+    from fishmi import scheduler as S
     from fishmi.llm import DualARModel
 
     rank = dist.get_rank() if dist is not None else 0
-    rng = np.random.default_rng(2 + 7919 * rank)
-    lens = rng.integers(16, 257, batch)
-    for s in range(batch):
-        llm.prefill(s, make_prompt(cfg, int(lens[s]), 5000 + 97 * rank + s),
-                    DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30, seed=31 * s + rank,
-                                         mask_im_end=True))
-    slots = list(range(batch))
-    llm.decode_frames(slots, 4)  # graph capture for n = batch
+    C1 = cfg.num_codebooks + 1
+    reqs = None
+    if rank == 0:
+        rng = np.random.default_rng(2)
+        n = batch * world * waves
+        lens = rng.integers(16, 257, n)
+        reqs = [S.Request(i, make_prompt(cfg, int(lens[i]), 5000 + i), frames, 31 * i + 7) for i in range(n)]
+    if dist is None:  # the tick queue runs on a one-rank gloo group at N=1
+        import torch.distributed as tdist
+
+        tdist.init_process_group("gloo", store=tdist.HashStore(), rank=0, world_size=1)
+    # graph capture of the batch-wide frame before the clock starts
+    warm = [s for s in range(batch)]
+    for s in warm:
+        llm.prefill(s, make_prompt(cfg, 16, 77 + s), DualARModel.sampling(mask_im_end=True))
+    llm.decode_frames(warm, 2)
+
+    def start(slot, req):
+        return llm.prefill(slot, req.prompt, DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30,
+                                                                  seed=req.seed, mask_im_end=True))
+
+    def step(slots, n):
+        return llm.decode_frames(slots, n)
+
+    def finish(slot, req, cols):
+        codec.stream_reset()
+        mx = codec.max_frames
+        pcm = np.concatenate([codec.decode_chunk(np.ascontiguousarray(cols[1:, t:t + mx]))
+                              for t in range(0, cols.shape[1], mx)])
+        return dp.pcm_to_int16(pcm)
+
     sync()
     t0 = time.perf_counter()
-    llm.decode_frames(slots, frames)
+    q = S.TickQueue(reqs, C1)
+    stats = S.serve(q, batch, start, step, finish, tick_frames=32)
     sync()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -109,13 +143,23 @@ def throughput_leg(llm, cfg, batch, frames, sync, dist, world):
         e = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         dt = float(e.item())
-    return {"workload": f"BASELINE config 3 per GPU: {batch} concurrent streams (prompt lengths "
-                        f"uniform 16-256, seed 2), {frames} batched Dual-AR frames each (top_k 30, "
-                        f"top_p 0.8, temp 0.8), hipGraph per frame; aggregate over {world} GPU(s)",
-            "batch_per_gpu": batch, "frames": frames,
-            "value": round(world * batch * frames / FRAME_RATE / dt, 2), "unit": "audio-sec/wall-sec",
-            "ms_per_frame": round(dt / frames * 1e3, 3),
-            "per_stream_rtf": round(frames / FRAME_RATE / dt, 3)}
+    else:
+        import torch.distributed as tdist
+
+        tdist.destroy_process_group()
+    if rank != 0:
+        return None
+    samples = sum(r.data.size for r in q.results)
+    audio_s = samples / 44100.0
+    return {"workload": f"BASELINE config {3 if world == 1 else 4}: {len(q.results)} requests (prompt lengths "
+                        f"uniform 16-256, seed 2; {frames} frames each, top_k 30, top_p 0.8, temp 0.8) over "
+                        f"{world} GPU(s), {batch} concurrent per GPU via rank 0's tick queue; end to end: "
+                        f"prefill + batched hipGraph decode + streamed codec decode + int16 PCM gathered "
+                        f"to rank 0",
+            "requests": len(q.results), "batch_per_gpu": batch, "frames": frames,
+            "value": round(audio_s / dt, 2), "unit": "audio-sec/wall-sec", "wall_s": round(dt, 3),
+            "decode_frames_rank0": stats["frames"], "ticks": stats["ticks"],
+            "per_stream_rtf": round(audio_s / len(q.results) / dt, 3)}
 
 
 def encode_leg(ccfg, device, seconds, seed):
@@ -181,9 +225,88 @@ def cpu_baseline(cfg, ccfg, prompt, frames, n_frames, n_codec, seed):
                        f"frames + codec of {frames} frames = {est:.1f}s")}
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` outside torch.distributed.run: start N rank processes through it (one per
+    GPU, RCCL rendezvous on 127.0.0.1) before this process touches the GPU, and exit with their
+    status. The driver's own launch (WORLD_SIZE set) skips this."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def pmc_gemv_traffic(timeout_s=150):
+    """HBM bytes per decode-GEMV launch at HEAD, measured in this run: two rocprofv3 --pmc passes
+    (FETCH_SIZE, then WRITE_SIZE; one counter group per pass) over scripts/pmc_probe.py in child
+    processes. FETCH_SIZE is doubled per the gfx950 wide-read correction (MI355X_MICROARCH.md §HBM).
+    Returns (bytes per launch or None, note)."""
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from rocprof_summary import load_pmc
+
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not on PATH"
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="fishmi_pmc_", dir="/tmp")
+        env = dict(os.environ, FISHMI_GRAPH="0")
+        cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", counter, "-d", d, "-o", "pmc", "--",
+               sys.executable, os.path.join(ROOT, "scripts", "pmc_probe.py")]
+        r = subprocess.run(cmd, env=env, cwd="/tmp", stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        dbs = glob.glob(os.path.join(d, "**", "*results.db"), recursive=True) + \
+            glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not dbs:
+            return None, f"rocprofv3 --pmc {counter} failed (rc {r.returncode}): {r.stderr[-300:].decode(errors='replace')}"
+        v = [x for name, xs in load_pmc(dbs[0], counter).items() if name.startswith("void gemv_kernel") for x in xs]
+        shutil.rmtree(d, ignore_errors=True)
+        if not v:
+            return None, f"no gemv_kernel dispatches in the {counter} pass"
+        vals[counter] = 1024.0 * sum(v) / len(v)
+    fetch = 2.0 * vals["FETCH_SIZE"]
+    return int(round(fetch + vals["WRITE_SIZE"])), (
+        f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes over scripts/pmc_probe.py in this run: "
+        f"{fetch / 1e6:.2f} MB fetched (FETCH_SIZE KB x1024 x2, gfx950 wide-read correction) + "
+        f"{vals['WRITE_SIZE'] / 1e6:.3f} MB written per gemv_kernel launch")
+
+
+def copy_peak_gbps(nbytes=2 << 30, reps=10):
+    """Measured device-to-device copy rate (read + write bytes / time; SURVEY.md §8d asks for the
+    measured STREAM-like peak beside the vendor figure). torch's copy kernel on the current stream,
+    HIP events."""
+    import torch
+
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbps = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return round(gbps, 1)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -259,11 +382,6 @@ def main():
     llm.decode_frames([0], 8)
     cls_ms = {c: llm.profile_read(c)[0] / 8 for c in ("linear", "attn", "rope", "norm", "sample", "other")}
     llm.profile(False)
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_gemv_r01.json")
-    if os.path.exists(pmc):
-        with open(pmc) as fh:
-            traffic = json.load(fh).get("hbm_bytes_per_launch")
 
     # frame-level: algorithmic frame bytes / graph-replayed frame time inside the timed region
     dec_s = np.mean([t["decode"] for t in tms]) / (args.frames - args.first_chunk)
@@ -273,8 +391,14 @@ def main():
     ms1, n1, fl1 = codec.profile()
     codec_tflops = (fl1 - fl0) / ((ms1 - ms0) * 1e-3) / 1e12
 
-    thr = throughput_leg(llm, cfg, args.batch, args.batch_frames, sync, dist, world) if args.batch > 0 else None
+    thr = throughput_leg(llm, codec, cfg, args.batch, args.batch_frames, args.waves, sync, dist, world) \
+        if args.batch > 0 else None
     enc = encode_leg(ccfg, local, args.encode_seconds, args.seed) if args.encode_seconds > 0 else None
+
+    copy_gbps = copy_peak_gbps() if rank == 0 else None
+    traffic, traffic_note = None, "not measured (--no-pmc or N>1)"
+    if rank == 0 and world == 1 and not args.no_pmc:
+        traffic, traffic_note = pmc_gemv_traffic()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -304,13 +428,16 @@ def main():
                        "global_batch": world, "frames": args.frames, "prompt_len": args.prompt_len,
                        "first_chunk_frames": args.first_chunk, "parallelism": f"dp{world}"},
             "p50_first_sample_ms": round(float(np.median(firsts)) * 1e3, 2),
+            "p90_first_sample_ms": round(float(np.percentile(firsts, 90)) * 1e3, 2),
             "per_stream_rtf": round(args.frames / FRAME_RATE / np.mean([t["total"] for t in tms]), 4),
             "breakdown_ms": {k: round(float(np.mean([t[k] for t in tms])) * 1e3, 2)
                              for k in ("prefill", "head", "decode", "codec", "total")},
             "roofline": {"kernel": "gemv_kernel (decode linear layers, fused norm/residual prologues)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "bytes_per_launch": int(per_launch),
+                         "traffic": traffic, "traffic_source": traffic_note,
+                         "copy_peak_measured": copy_gbps,
+                         "bytes_per_launch": int(per_launch),
                          "avg_launch_us": round(avg_us, 3), "launches_per_frame": int(lin_n),
                          "method": "one frame's GEMV launches replayed x20 as a graph, HIP events on "
                                    "the compute stream"},

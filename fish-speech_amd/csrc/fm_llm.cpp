@@ -878,7 +878,7 @@ static void finalize(fm_llm* m) {
         m->skpart_cap = 8ll << 20;  // 32 MiB of partial tiles
         m->skpart = (float*)m->dalloc((size_t)m->skpart_cap * sizeof(float), false);
     }
-    HIPCHK(hipMemset(m->attn_cnt, 0, (size_t)R * d.nkv * sizeof(int)));
+    HIPCHK(hipMemsetAsync(m->attn_cnt, 0, (size_t)R * d.nkv * sizeof(int), m->stream));
     m->slabA = (float*)m->dalloc((size_t)KSB_MAX * std::min(n, GEMV_MAX_ROWS) * dmax * 4);
     m->slabB = (float*)m->dalloc((size_t)KSB_MAX * std::min(n, GEMV_MAX_ROWS) * dmax * 4);
     m->logits = (float*)m->dalloc((size_t)n * m->Nhead * 4);

@@ -22,22 +22,32 @@
 
 namespace {
 
+// Every fill, copy and launch of a hook goes to the hook's own non-blocking stream, in order. (A
+// non-blocking stream does not wait for the null stream, so a null-stream hipMemset of a buffer
+// could land after a kernel on `s` has written it.)
 struct DevBufs {
+    hipStream_t s;
     std::vector<void*> ptrs;
+    explicit DevBufs(hipStream_t st) : s(st) {}
     ~DevBufs() {
+        (void)hipStreamSynchronize(s);
         for (void* p : ptrs) (void)hipFree(p);
     }
     void* alloc(size_t bytes) {
         void* p = nullptr;
         HIPCHK(hipMalloc(&p, bytes ? bytes : 16));
-        HIPCHK(hipMemset(p, 0, bytes ? bytes : 16));
+        HIPCHK(hipMemsetAsync(p, 0, bytes ? bytes : 16, s));
         ptrs.push_back(p);
         return p;
     }
+    void put(void* d, const void* h, size_t bytes) {
+        HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));  // the host array may be a temporary
+    }
     // fp32 host -> device storage type T
-    template <typename T> T* upload(const float* h, size_t n, hipStream_t s) {
+    template <typename T> T* upload(const float* h, size_t n) {
         float* tmp = (float*)alloc(n * 4);
-        HIPCHK(hipMemcpy(tmp, h, n * 4, hipMemcpyHostToDevice));
+        put(tmp, h, n * 4);
         T* d = (T*)alloc(n * sizeof(T));
         launch_convert<T>(s, tmp, 0, (int64_t)n, d);
         HIPCHK(hipGetLastError());
@@ -75,9 +85,9 @@ struct StreamGuard {
 
 template <typename T>
 void rmsnorm_t(hipStream_t s, int mode, const float* x, const float* w, int R, int d, float eps, float* y) {
-    DevBufs b;
-    T* xd = b.upload<T>(x, (size_t)R * d, s);
-    T* wd = b.upload<T>(w, (size_t)d, s);
+    DevBufs b(s);
+    T* xd = b.upload<T>(x, (size_t)R * d);
+    T* wd = b.upload<T>(w, (size_t)d);
     T* yd = (T*)b.alloc((size_t)R * d * sizeof(T));
     if (mode == 2) {
         launch_rmsnorm<T>(s, xd, d, wd, d, eps, yd, d, R);
@@ -140,15 +150,15 @@ void rmsnorm_t(hipStream_t s, int mode, const float* x, const float* w, int R, i
 template <typename T>
 void qk_rope_t(hipStream_t s, int kernel, const float* qkv, int nh, int nkv, int hd, const float* qn,
                const float* kn, int qk_norm, float eps, float base, int pos, float* q_out, float* k_out) {
-    DevBufs b;
+    DevBufs b(s);
     const int ld = (nh + 2 * nkv) * hd;
-    T* raw = b.upload<T>(qkv, (size_t)ld, s);
-    T* qnd = qk_norm ? b.upload<T>(qn, (size_t)hd, s) : (T*)b.alloc((size_t)hd * sizeof(T));
-    T* knd = qk_norm ? b.upload<T>(kn, (size_t)hd, s) : (T*)b.alloc((size_t)hd * sizeof(T));
+    T* raw = b.upload<T>(qkv, (size_t)ld);
+    T* qnd = qk_norm ? b.upload<T>(qn, (size_t)hd) : (T*)b.alloc((size_t)hd * sizeof(T));
+    T* knd = qk_norm ? b.upload<T>(kn, (size_t)hd) : (T*)b.alloc((size_t)hd * sizeof(T));
     const int S = (pos + 1 + 7) / 8 * 8;
     auto tab = rope_table_host(S, hd, base);
     float* rope = (float*)b.alloc(tab.size() * 4);
-    HIPCHK(hipMemcpy(rope, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+    b.put(rope, tab.data(), tab.size() * 4);
     const size_t stride = (size_t)nkv * S * hd;
     T* kc = (T*)b.alloc(stride * sizeof(T));
     T* vc = (T*)b.alloc(stride * sizeof(T));
@@ -156,7 +166,7 @@ void qk_rope_t(hipStream_t s, int kernel, const float* qkv, int nh, int nkv, int
     float* qd = (float*)b.alloc((size_t)nh * hd * 4);
     int* row = (int*)b.alloc(8);
     const int rs[2] = {0, pos};
-    HIPCHK(hipMemcpy(row, rs, 8, hipMemcpyHostToDevice));
+    b.put(row, rs, 8);
     const float scale = 1.0f / sqrtf((float)hd);
     if (kernel == 0) {  // slow decode attention (attn_decode2)
         AttnDecArgs<T> a{raw, ld, row, row + 1, nh, nkv, hd, qk_norm, eps, qnd, knd, rope, kc, vc, stride, 0, S,
@@ -184,11 +194,11 @@ void qk_rope_t(hipStream_t s, int kernel, const float* qkv, int nh, int nkv, int
 template <typename T>
 void embed_t(hipStream_t s, const int32_t* tok, int R, const float* emb, int V, const float* cbemb, int d, int C,
              int cb, int sb, int se, int scale, float* x) {
-    DevBufs b;
-    T* e = b.upload<T>(emb, (size_t)V * d, s);
-    T* ce = b.upload<T>(cbemb, (size_t)C * cb * d, s);
+    DevBufs b(s);
+    T* e = b.upload<T>(emb, (size_t)V * d);
+    T* ce = b.upload<T>(cbemb, (size_t)C * cb * d);
     int32_t* td = (int32_t*)b.alloc((size_t)R * (C + 1) * 4);
-    HIPCHK(hipMemcpy(td, tok, (size_t)R * (C + 1) * 4, hipMemcpyHostToDevice));
+    b.put(td, tok, (size_t)R * (C + 1) * 4);
     T* xd = (T*)b.alloc((size_t)R * d * sizeof(T));
     launch_embed<T>(s, td, R, e, ce, d, C, cb, sb, se, scale, xd, nullptr);
     HIPCHK(hipGetLastError());

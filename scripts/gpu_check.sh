@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests -x -v --timeout 120 --timeout-method
     > gpurun_out/gpu_tests_$TAG.log 2>&1 && tail -3 gpurun_out/gpu_tests_$TAG.log &&
 timeout -k 10 420 python -u bench.py > gpurun_out/bench_$TAG.log 2>&1 && tail -1 gpurun_out/bench_$TAG.log &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_$TAG -o run -- \
-    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench_$TAG.log 2>&1 &&
+    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pmc > gpurun_out/prof_bench_$TAG.log 2>&1 &&
 python3 scripts/rocprof_summary.py "$(find /tmp/prof_$TAG -name '*results.db' -print -quit)" \
     gpurun_out/prof_$TAG --bench gpurun_out/prof_bench_$TAG.log >> gpurun_out/prof_bench_$TAG.log 2>&1 &&
 echo GPU_CHECK_DONE
