@@ -15,6 +15,7 @@
 //                       top-p / temperature / multinomial with the shared counter RNG
 //                       (inference.py:43-93) and RAS (inference.py:117-144).
 #include "fm_kernels.h"
+#include "fm_runtime.h"
 #include "fm_attn_dev.h"
 
 // normalise (optional) + rope one head held as pairs by a wave (lane p owns pair p, p+64)
@@ -431,6 +432,227 @@ __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
             O += w * pp[(size_t)q * (hd + 2) + 2 + e];
         }
         st(a.out + (size_t)r * a.nh * hd + (size_t)(kvh * g + hh) * hd, e, O / L);
+    }
+}
+
+// Slow-model decode attention, v3: grid (R, nkv, maxsplit), 256 threads, ATT3_CH = 64 cached
+// positions per block (16 per wave), registers instead of LDS tiles for K / V.
+//   round trip 1: slot, pos and the raw q / k / v rows;
+//   round trip 2: every lane's K slice (one position, a quarter of hd) and V slice (four
+//   positions, eight dims), all loads issued together before the q-side arithmetic;
+//   scores: quarter dot products summed across the four 16-lane groups (two xor shuffles);
+//   softmax per head over the block's positions (wave per head); PV accumulated in registers per
+//   lane, summed across the 16-lane groups and the four waves.
+// The split holding `pos` normalises + ropes the new k (llama.py:894-910), writes k / v to the
+// cache (llama.py:205-214) and uses them in place of the cache rows it loaded.  One split writes
+// the output; several write (m, l, o) partials and the last-arriving one combines them (agent
+// release / acquire ticket, as attn_decode2).
+constexpr int ATT3_CH = 64;
+template <typename T>
+__global__ __launch_bounds__(256) void attn_dec3_kernel(AttnDecArgs<T> a) {
+    __shared__ float q_s[8][128];        // g <= 8 q heads, hd <= 128, fp32 (T-rounded values)
+    __shared__ float kv_new[2][128];     // the new position's k (normed, roped) and v
+    __shared__ float ps[8][ATT3_CH];     // scores, then probabilities
+    __shared__ float mls[8][2];          // per head (max, sum)
+    __shared__ float ored[4][8][128];    // per-wave PV partials
+    __shared__ int flag;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+    const int hd = a.hd, g = a.nh / a.nkv, half = hd >> 1;
+    const int slot = a.row_slot[r];
+    const int pos = a.row_pos[r];
+    const int npos = pos + 1;
+    const int nsp = (npos + ATT3_CH - 1) / ATT3_CH;
+    if (sp >= nsp) return;
+    const int j0 = sp * ATT3_CH, nj = min(ATT3_CH, npos - j0);
+    const bool owner = j0 + nj == npos;
+    const T* raw = a.qkv + (size_t)r * a.ldqkv;
+    // ---- round trip 1 (raw rows of this wave's items: q heads, then new k, new v) -----------
+    float x0[2][2], x1[2][2];
+    const int nitem = g + 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int it = wave + 4 * i;
+        const int row = it < g ? kvh * g + it : (it == g ? a.nh + kvh : a.nh + a.nkv + kvh);
+        const T* src = raw + (size_t)(it < nitem ? row : 0) * hd;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            const bool ok = it < nitem && p < half;
+            x0[i][u] = ok ? ld(src, 2 * p) : 0.f;
+            x1[i][u] = ok ? ld(src, 2 * p + 1) : 0.f;
+        }
+    }
+    // ---- round trip 2: K slice (position j0 + 16 w + (lane & 15), dims quarter lane >> 4) and
+    // V slices (positions j0 + 16 w + 4 it + (lane >> 4), dims 8 (lane & 15) .. + 8)
+    const size_t base = (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
+    T* kc = a.kc + base;
+    T* vc = a.vc + base;
+    const int qd = hd >> 2;                       // dims per quarter (<= 32)
+    const int jk = j0 + 16 * wave + (lane & 15);  // this lane's score position
+    const int qq = lane >> 4;
+    float kreg[32];
+    {
+        const T* krow = kc + (size_t)(jk < npos ? jk : npos - 1) * hd + qq * qd;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (8 * c < qd) load8(krow + 8 * c, *reinterpret_cast<float(*)[8]>(kreg + 8 * c));
+    }
+    float vreg[4][8];
+    const int vd = 8 * (lane & 15);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int jv = j0 + 16 * wave + 4 * it + (lane >> 4);
+        const T* vrow = vc + (size_t)(jv < npos ? jv : npos - 1) * hd + (vd < hd ? vd : 0);
+        load8(vrow, vreg[it]);
+    }
+    const float* tab = a.rope + (size_t)pos * hd;
+    // ---- q heads (+ new k / v in the owner): qk-norm (fp32 incl. weight, one rounding), RoPE
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int it = wave + 4 * i;
+        if (it >= nitem || (it >= g && !owner)) continue;
+        const bool isq = it < g, isk = it == g;
+        if (a.qk_norm && (isq || isk)) {
+            float ss = 0.f;
+            for (int u = 0; u < 2; ++u) ss += x0[i][u] * x0[i][u] + x1[i][u] * x1[i][u];
+            ss = wave_sum(ss);
+            const float rs = 1.0f / sqrtf(ss / (float)hd + a.eps);
+            const T* nw = isq ? a.qn : a.kn;
+            for (int u = 0; u < 2; ++u) {
+                const int p = lane + 64 * u;
+                if (p < half) {
+                    x0[i][u] = rnd<T>((x0[i][u] * rs) * ld(nw, 2 * p));
+                    x1[i][u] = rnd<T>((x1[i][u] * rs) * ld(nw, 2 * p + 1));
+                }
+            }
+        }
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            if (p >= half) break;
+            float y0 = x0[i][u], y1 = x1[i][u];
+            if (isq || isk) {
+                const float c = tab[2 * p], sn = tab[2 * p + 1];
+                y0 = rnd<T>(x0[i][u] * c - x1[i][u] * sn);
+                y1 = rnd<T>(x1[i][u] * c + x0[i][u] * sn);
+            }
+            if (isq) {
+                q_s[it][2 * p] = y0;
+                q_s[it][2 * p + 1] = y1;
+                if (a.qdbg && sp == 0) {  // per-op test hook only
+                    float* qdp = a.qdbg + ((size_t)r * a.nh + kvh * g + it) * hd;
+                    qdp[2 * p] = y0;
+                    qdp[2 * p + 1] = y1;
+                }
+            } else {
+                kv_new[isk ? 0 : 1][2 * p] = y0;
+                kv_new[isk ? 0 : 1][2 * p + 1] = y1;
+                T* dst = (isk ? kc : vc) + (size_t)pos * hd;
+                st(dst, 2 * p, y0);
+                st(dst, 2 * p + 1, y1);
+            }
+        }
+    }
+    __syncthreads();
+    // ---- scores: the new row comes from kv_new, not the cache rows loaded before it was written
+    if (owner && jk == pos) {
+#pragma unroll
+        for (int c = 0; c < 32; ++c)
+            if (c < qd) kreg[c] = kv_new[0][qq * qd + c];
+    }
+    for (int h = 0; h < g; ++h) {
+        float d = 0.f;
+#pragma unroll
+        for (int c = 0; c < 32; ++c)
+            if (c < qd) d += q_s[h][qq * qd + c] * kreg[c];
+        d += __shfl_xor(d, 16);
+        d += __shfl_xor(d, 32);
+        if (qq == 0) ps[h][16 * wave + (lane & 15)] = jk < npos ? d * a.scale : -INFINITY;
+    }
+    __syncthreads();
+    // ---- softmax over the block's positions, wave per head
+    for (int h = wave; h < g; h += 4) {
+        const float sc = ps[h][lane];
+        const float mx = wave_max(sc);
+        const float pe = lane < nj ? expf(sc - mx) : 0.f;
+        ps[h][lane] = pe;
+        const float l = wave_sum(pe);
+        if (lane == 0) {
+            mls[h][0] = mx;
+            mls[h][1] = l;
+        }
+    }
+    __syncthreads();
+    // ---- PV: this lane's four V rows x eight dims, every head
+    if (owner) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it)
+            if (j0 + 16 * wave + 4 * it + (lane >> 4) == pos)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) vreg[it][e] = vd + e < hd ? kv_new[1][vd + e] : 0.f;
+    }
+    for (int h = 0; h < g; ++h) {
+        float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const float p = ps[h][16 * wave + 4 * it + (lane >> 4)];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] += p * vreg[it][e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            o[e] += __shfl_xor(o[e], 16);
+            o[e] += __shfl_xor(o[e], 32);
+        }
+        if (lane < 16 && vd < hd)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ored[wave][h][vd + e] = o[e];
+    }
+    __syncthreads();
+    const bool single = nsp == 1;
+    float* part = a.part + (((size_t)r * a.nh + (size_t)kvh * g) * a.maxsplit + sp) * (hd + 2);
+    for (int idx = threadIdx.x; idx < g * hd; idx += 256) {
+        const int h = idx / hd, e = idx - h * hd;
+        const float o = (ored[0][h][e] + ored[1][h][e]) + (ored[2][h][e] + ored[3][h][e]);
+        if (single) {
+            st(a.out + (size_t)r * a.nh * hd + (size_t)(kvh * g + h) * hd, e, o / mls[h][1]);
+        } else {  // write-through (sc1): read back by the combining block without a fence
+            float* pp = part + (size_t)h * a.maxsplit * (hd + 2);
+            __hip_atomic_store(pp + 2 + e, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (e == 0) {
+                __hip_atomic_store(pp, mls[h][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(pp + 1, mls[h][1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if (single) return;
+    // ---- split combine by the last-arriving block of (row, kv head): sc1 partial stores drained by
+    // every wave, a relaxed agent ticket, sc1 loads in the combiner (the write-through hand-off of
+    // MI355X_MICROARCH.md, no release / acquire fence)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int t = __hip_atomic_fetch_add(a.cnt + (size_t)r * a.nkv + kvh, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        flag = t == nsp - 1;
+        if (t == nsp - 1) __hip_atomic_store(a.cnt + (size_t)r * a.nkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!flag) return;
+    const float* p0 = a.part + (((size_t)r * a.nh + (size_t)kvh * g) * a.maxsplit) * (hd + 2);
+    auto ldp = [](const float* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    for (int idx = threadIdx.x; idx < g * hd; idx += 256) {
+        const int h = idx / hd, e = idx - h * hd;
+        const float* pp = p0 + (size_t)h * a.maxsplit * (hd + 2);
+        float M = -INFINITY;
+        for (int q = 0; q < nsp; ++q) M = fmaxf(M, ldp(pp + (size_t)q * (hd + 2)));
+        float L = 0.f, O = 0.f;
+        for (int q = 0; q < nsp; ++q) {
+            const float w = expf(ldp(pp + (size_t)q * (hd + 2)) - M);
+            L += w * ldp(pp + (size_t)q * (hd + 2) + 1);
+            O += w * ldp(pp + (size_t)q * (hd + 2) + 2 + e);
+        }
+        st(a.out + (size_t)r * a.nh * hd + (size_t)(kvh * g + h) * hd, e, O / L);
     }
 }
 
@@ -1058,6 +1280,13 @@ template <typename T> void launch_attn_decode2(hipStream_t s, const AttnDecArgs<
     }
     attn_decode2_kernel<T><<<g1, 512, attn2_lds_bytes(a.hd, a.nh / a.nkv, a.cap, sizeof(T)), s>>>(a);
 }
+template <typename T> void launch_attn_decode3(hipStream_t s, const AttnDecArgs<T>& a0, int R) {
+    FMCHECK(a0.hd % 32 == 0 && a0.hd <= 128 && a0.nh % a0.nkv == 0 && a0.nh / a0.nkv <= 6,
+            "attn_dec3: hd a multiple of 32 up to 128, at most 6 q heads per kv head");
+    AttnDecArgs<T> a = a0;
+    a.maxsplit = FM_CEIL(a.S, ATT3_CH);
+    attn_dec3_kernel<T><<<dim3(R, a.nkv, a.maxsplit), 256, 0, s>>>(a);
+}
 template <typename T> void launch_fast_attn2(hipStream_t s, const FastFusedArgs<T>& a, int R) {
     fast_attn2_kernel<T><<<dim3(R, a.nh), 64, 0, s>>>(a);
 }
@@ -1076,6 +1305,8 @@ template void launch_attn_decode<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&
 template void launch_attn_decode<float>(hipStream_t, const AttnDecArgs<float>&, int);
 template void launch_attn_decode2<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
 template void launch_attn_decode2<float>(hipStream_t, const AttnDecArgs<float>&, int);
+template void launch_attn_decode3<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
+template void launch_attn_decode3<float>(hipStream_t, const AttnDecArgs<float>&, int);
 template void launch_fast_attn2<bf16_t>(hipStream_t, const FastFusedArgs<bf16_t>&, int);
 template void launch_fast_attn2<float>(hipStream_t, const FastFusedArgs<float>&, int);
 template void launch_fast_attn_fused<bf16_t>(hipStream_t, const FastFusedArgs<bf16_t>&, int);

@@ -1,0 +1,325 @@
+// fm_bstream.hip -- batched decode linears for 8 < R <= 32 rows (BASELINE config 3: 32 concurrent
+// utterances per GPU), and the residual finalise + RMSNorm that consumes their split-K slabs.
+//
+// At R = 32 a decode linear does 32 flop per weight byte: it is an HBM weight stream, not a GEMM.
+// Measured on gfx950 (scripts/bgemm_probe.hip, 36 layers of distinct S2-Pro weights):
+//   * staging the X slice in LDS caps the block at one per CU, and the in-flight weight bytes
+//     with it;
+//   * loading X B-fragments from L2 beside every weight fragment (16-row gathers) halves the
+//     stream rate;
+//   * split-K partials combined by the last-arriving block (ticket) put two memory round trips on
+//     every block's tail.
+// So X lives in VGPRs instead. Block = NW waves, one block per CU. Wave w owns the k-steps
+// [w*Sp/NW, (w+1)*Sp/NW) of the block's K part (at most SPW of them). Their B fragments, both
+// 16-column groups, are loaded once. The wave then streams the weight fragments of the block's
+// contiguous tile range at those k-steps through a ring of SPW*TPI fragments, the next TPI tiles
+// ahead. Per tile, the NW wave partials are summed through LDS (double-buffered, one barrier per
+// tile), and the epilogue runs on the full-K sum:
+//   EPI_STORE   Y = round(v + bias)                       (QKV, fast_project_in)
+//   EPI_SWIGLU8 row-interleaved W1||W3 tile -> 8 outputs round(silu(round(g))) * round(u)
+//   EPI_F32     logits as fp32 holding the T-rounded value
+//   EPI_SLAB    kparts > 1: fp32 partial slab [kp][R][ldy], no combine here. The consumer
+//               (finalize_norm_kernel) sums the slabs, so no block waits on another.
+// Weights use the packed fragment layout of fm_kernels.h, shared with the batch-1 GEMV.
+#include "fm_kernels.h"
+#include "fm_runtime.h"
+
+namespace {
+
+template <typename T> struct BsFrag;
+template <> struct BsFrag<bf16_t> {
+    typedef u32x4_t f;
+    static __device__ __forceinline__ f load_w(const bf16_t* blk, int lane) {
+        return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(blk + lane * 8));
+    }
+    static __device__ __forceinline__ f load_x(const bf16_t* p) { return *reinterpret_cast<const u32x4_t*>(p); }
+    static __device__ __forceinline__ f zero() { return (u32x4_t){0, 0, 0, 0}; }
+    static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                       __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+    }
+};
+template <> struct BsFrag<float> {
+    struct f {
+        f32x4_t lo, hi;
+    };
+    static __device__ __forceinline__ f load_w(const float* blk, int lane) {
+        f v;
+        v.lo = *reinterpret_cast<const f32x4_t*>(blk + lane * 4);
+        v.hi = *reinterpret_cast<const f32x4_t*>(blk + 256 + lane * 4);
+        return v;
+    }
+    static __device__ __forceinline__ f load_x(const float* p) {
+        f v;
+        v.lo = *reinterpret_cast<const f32x4_t*>(p);
+        v.hi = *reinterpret_cast<const f32x4_t*>(p + 4);
+        return v;
+    }
+    static __device__ __forceinline__ f zero() {
+        f v;
+        v.lo = v.hi = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        return v;
+    }
+    // lane l holds k = 8*(l>>4) + j of a 32-wide k block; MFMA j covers {8g + j}: exact f32
+    static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[j], b.lo[j], c, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[j], b.hi[j], c, 0, 0, 0);
+        return c;
+    }
+};
+
+constexpr int BS_MAXW = 16;  // waves per block
+
+__device__ __forceinline__ float silu_b(float a) { return a / (1.0f + expf(-a)); }
+
+template <typename T, int SPW, int TPI, int EPI>
+__global__ __launch_bounds__(BS_MAXW * 64) void bstream_kernel(BstreamArgs<T> a) {
+    using F = BsFrag<T>;
+    __shared__ f32x4_t red[2][BS_MAXW][2][64];
+    constexpr int U = SPW * TPI;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
+    const int kparts = a.kparts;
+    const int kp = blockIdx.x % kparts, gb = blockIdx.x / kparts, Gk = gridDim.x / kparts;
+    const int T_ = (a.N + 15) >> 4;
+    const int t0 = (int)((long long)gb * T_ / Gk), t1 = (int)((long long)(gb + 1) * T_ / Gk);
+    const int ntl = t1 - t0;
+    const int S = a.K >> 5, Sp = S / kparts, s0 = kp * Sp;
+    const int wa = s0 + wave * Sp / NW, nst = s0 + (wave + 1) * Sp / NW - wa;  // host: 1 <= nst <= SPW
+    const int r = lane & 15, g = lane >> 4;
+    // this wave's B fragments (rows >= R and steps >= nst are zero; loads clamped, never skipped)
+    typename F::f xa[SPW], xb[SPW];
+    {
+        const int ra = r < a.R ? r : a.R - 1, rb = 16 + r < a.R ? 16 + r : a.R - 1;
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int jj = j < nst ? j : nst - 1;
+            const size_t k = (size_t)(wa + jj) * 32 + 8 * g;
+            xa[j] = F::load_x(a.X + (size_t)ra * a.ldx + k);
+            xb[j] = F::load_x(a.X + (size_t)rb * a.ldx + k);
+            if (j >= nst || r >= a.R) xa[j] = F::zero();
+            if (j >= nst || 16 + r >= a.R) xb[j] = F::zero();
+        }
+    }
+    // weight stream: fragment f = (tile f / SPW, step min(f % SPW, nst - 1)); slots past the run
+    // re-load its last fragment (a cache hit) so the ring never needs a branch
+    const int flast = ntl * SPW - 1;
+    const T* wbase = a.W + ((size_t)t0 * S + wa) * 512;
+    typename F::f fa[U];
+    auto issue = [&](int f, int u) {
+        f = f < flast ? f : flast;
+        const int t = f / SPW, j = f - t * SPW;
+        fa[u] = F::load_w(wbase + ((size_t)t * S + (j < nst ? j : nst - 1)) * 512, lane);
+    };
+#pragma unroll
+    for (int u = 0; u < U; ++u) issue(u, u);
+
+    for (int t = 0; t < ntl; t += TPI) {
+#pragma unroll
+        for (int tt = 0; tt < TPI; ++tt) {
+            f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+            for (int j = 0; j < SPW; ++j) {
+                const int u = tt * SPW + j;
+                acc0 = F::mma(fa[u], xa[j], acc0);
+                acc1 = F::mma(fa[u], xb[j], acc1);
+                issue((t + TPI) * SPW + u, u);
+                __builtin_amdgcn_sched_barrier(0);  // each refill right behind its consumer
+            }
+            const int buf = (t + tt) & 1;
+            red[buf][wave][0][lane] = acc0;
+            red[buf][wave][1][lane] = acc1;
+            __syncthreads();  // buf is rewritten two tiles later, behind the next tile's barrier
+            const int tile = t0 + t + tt;
+            if (t + tt < ntl) {
+                // 16 rows x R columns; C/D map of a 16x16 accumulator: row = 4*(lane>>4)+i, col = lane&15
+                if constexpr (EPI == EPI_SWIGLU8) {
+                    for (int o = threadIdx.x; o < 8 * a.R; o += blockDim.x) {
+                        const int col = o >> 3, row = o & 7;
+                        const int cg = col >> 4, i = row & 3;
+                        const int lg = 16 * (row >> 2) + (col & 15), lu = 16 * ((row + 8) >> 2) + (col & 15);
+                        float vg = 0.f, vu = 0.f;
+                        for (int w = 0; w < NW; ++w) {
+                            vg += red[buf][w][cg][lg][i];
+                            vu += red[buf][w][cg][lu][i];
+                        }
+                        const int n = tile * 8 + row;
+                        if (n < (a.N >> 1)) st(a.Y, (size_t)col * a.ldy + n, rnd<T>(silu_b(rnd<T>(vg))) * rnd<T>(vu));
+                    }
+                } else {
+                    for (int o = threadIdx.x; o < 16 * a.R; o += blockDim.x) {
+                        const int col = o >> 4, row = o & 15;
+                        const int cg = col >> 4, ln = 16 * (row >> 2) + (col & 15), i = row & 3;
+                        float v = 0.f;
+                        for (int w = 0; w < NW; ++w) v += red[buf][w][cg][ln][i];
+                        const int n = tile * 16 + row;
+                        if (n >= a.N) continue;
+                        if constexpr (EPI == EPI_SLAB) {
+                            a.Yf[((size_t)kp * a.R + col) * a.ldy + n] = v;
+                        } else {
+                            if (a.bias) v += ld(a.bias, n);
+                            if constexpr (EPI == EPI_STORE)
+                                st(a.Y, (size_t)col * a.ldy + n, v);
+                            else
+                                a.Yf[(size_t)col * a.ldy + n] = rnd<T>(v);
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// x = round(res + round(sum_kp slab[kp] + bias)) (llama.py:841-842 residual, the split-K sum in fp32
+// rounded once like the reference's one linear output), then optionally xn = RMSNorm(x) with two
+// roundings (llama.py:989-1000).  One 512-thread block per row: every thread's slab, residual and
+// norm-weight loads (<= FN_CPT chunks of 8) are issued together, one round trip, then a block sum.
+constexpr int FN_THREADS = 512, FN_CPT = 2;  // d <= 8 * FN_THREADS * FN_CPT
+template <typename T>
+__global__ __launch_bounds__(FN_THREADS) void finalize_norm_kernel(FinalizeArgs<T> a) {
+    __shared__ float red_s[FN_THREADS / 64];
+    const int r = blockIdx.x;
+    float v[FN_CPT][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < FN_CPT; ++c) {
+        const int i = 8 * (threadIdx.x + FN_THREADS * c);
+        if (i < a.d) {
+            float y[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, x[8];
+            for (int q = 0; q < a.kparts; ++q) {
+                const float* sp = a.slab + ((size_t)q * a.R + r) * a.lds + i;
+                const f32x4_t p0 = *reinterpret_cast<const f32x4_t*>(sp);
+                const f32x4_t p1 = *reinterpret_cast<const f32x4_t*>(sp + 4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    y[j] += p0[j];
+                    y[4 + j] += p1[j];
+                }
+            }
+            if (a.bias) {
+                float b[8];
+                load8(a.bias + i, b);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) y[j] += b[j];
+            }
+            load8(a.res + (size_t)r * a.ldr + i, x);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                v[c][j] = rnd<T>(x[j] + rnd<T>(y[j]));
+                ss += v[c][j] * v[c][j];
+            }
+            T* xo = a.x_out + (size_t)r * a.ldx + i;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) st(xo, j, v[c][j]);
+        }
+    }
+    if (!a.nw) return;
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red_s[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < FN_THREADS / 64; ++w) ss += red_s[w];
+    const float rs = 1.0f / sqrtf(ss / (float)a.d + a.eps);
+#pragma unroll
+    for (int c = 0; c < FN_CPT; ++c) {
+        const int i = 8 * (threadIdx.x + FN_THREADS * c);
+        if (i < a.d) {
+            float w[8];
+            load8(a.nw + i, w);
+            T* xn = a.xn_out + (size_t)r * a.ldxn + i;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) st(xn, j, rnd<T>(rnd<T>(v[c][j] * rs) * w[j]));
+        }
+    }
+}
+
+template <typename T, int SPW, int TPI>
+void bs_go(hipStream_t s, const BstreamArgs<T>& a, int epi, int G, int NW) {
+    dim3 grid(G), block(NW * 64);
+    switch (epi) {
+        case EPI_STORE: bstream_kernel<T, SPW, TPI, EPI_STORE><<<grid, block, 0, s>>>(a); break;
+        case EPI_SWIGLU8: bstream_kernel<T, SPW, TPI, EPI_SWIGLU8><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32: bstream_kernel<T, SPW, TPI, EPI_F32><<<grid, block, 0, s>>>(a); break;
+        case EPI_SLAB: bstream_kernel<T, SPW, TPI, EPI_SLAB><<<grid, block, 0, s>>>(a); break;
+        default: FMCHECK(false, "bstream: unsupported epilogue");
+    }
+}
+
+int bs_num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    }
+    return n;
+}
+
+}  // namespace
+
+// Geometry for one linear (bf16 numbers from scripts/bgemm_probe.hip, S2-Pro shapes):
+//   whole-K epilogues: kparts 1, 16 waves, 5 k-steps per wave at K = 2560 (TPI 2);
+//   EPI_SLAB: kparts 4 at K = 4096 (8 waves x 4 steps), kparts 8 at K = 9728 (8 waves x 4-5).
+// SPW is the smallest instantiated ring width >= ceil(Sp / NW).  fp32 holds twice the VGPRs per
+// fragment, so it runs TPI 1 (validation mode only).
+BstreamPlan bstream_plan(int N, int K, int R, int epi, size_t esz) {
+    BstreamPlan p{};
+    const FmTuning& tu = fm_tuning();
+    const int S = K / 32, tiles = (N + 15) / 16;
+    if (R < 1 || R > 32 || K % 32 || S < 1) return p;
+    int kparts = 1;
+    if (epi == EPI_SLAB) {
+        kparts = tu.bstream_kparts > 0 ? tu.bstream_kparts : (S >= 256 ? 8 : (S >= 128 ? 4 : (S >= 64 ? 2 : 1)));
+        while (kparts > 1 && (S % kparts || S / kparts < 8)) kparts /= 2;
+    }
+    const int Sp = S / kparts;
+    int NW = epi == EPI_SLAB ? 8 : 16;
+    if (tu.bstream_nw > 0) NW = tu.bstream_nw;
+    NW = std::min(NW, Sp);
+    const int spw_need = (Sp + NW - 1) / NW;
+    const int spws[] = {2, 4, 5, 8};
+    int spw = 0;
+    for (int c : spws)
+        if (c >= spw_need) {
+            spw = c;
+            break;
+        }
+    if (!spw) return p;
+    int G = std::min(bs_num_cus(), tiles * kparts);
+    G = std::max(kparts, G / kparts * kparts);
+    p.ok = true;
+    p.kparts = kparts;
+    p.nw = NW;
+    p.spw = spw;
+    p.tpi = (esz == 2 && spw <= 5) ? 2 : 1;
+    p.grid = G;
+    return p;
+}
+
+template <typename T> bool launch_bstream(hipStream_t s, const BstreamArgs<T>& a0, int epi, const BstreamPlan& p) {
+    if (!p.ok) return false;
+    BstreamArgs<T> a = a0;
+    a.kparts = p.kparts;
+    FMCHECK(epi == EPI_SLAB || p.kparts == 1, "bstream: split K only into slabs");
+    FMCHECK(epi != EPI_SWIGLU8 || a.N % 16 == 0, "bstream: SwiGLU8 needs whole interleaved tiles");
+#define BSG(SPW, TPI)                                    \
+    if (p.spw == SPW && p.tpi == TPI) {                  \
+        bs_go<T, SPW, TPI>(s, a, epi, p.grid, p.nw);     \
+        return true;                                     \
+    }
+    BSG(2, 2) BSG(4, 2) BSG(5, 2) BSG(2, 1) BSG(4, 1) BSG(5, 1) BSG(8, 1)
+#undef BSG
+    return false;
+}
+
+template <typename T> void launch_finalize_norm(hipStream_t s, const FinalizeArgs<T>& a) {
+    FMCHECK(a.d % 8 == 0 && a.d <= 8 * FN_THREADS * FN_CPT && a.lds % 4 == 0, "finalize_norm: bad row width");
+    finalize_norm_kernel<T><<<a.R, FN_THREADS, 0, s>>>(a);
+}
+
+template bool launch_bstream<bf16_t>(hipStream_t, const BstreamArgs<bf16_t>&, int, const BstreamPlan&);
+template bool launch_bstream<float>(hipStream_t, const BstreamArgs<float>&, int, const BstreamPlan&);
+template void launch_finalize_norm<bf16_t>(hipStream_t, const FinalizeArgs<bf16_t>&);
+template void launch_finalize_norm<float>(hipStream_t, const FinalizeArgs<float>&);

@@ -209,6 +209,10 @@ struct FmTuning {
     int bgemv_tpb = 4;       // bgemv max 16-row tiles per block sharing one staged X slice (1, 2, 4)
     int bgemv_lds_kb = 84;   // bgemv X-slice LDS budget (KiB) before splitting K
     int bgemv_fill = 512;    // bgemv: split K until the grid has this many blocks
+    int attn3 = 1;           // 1: slow decode attention on attn_dec3_kernel, 0: attn_decode2_kernel
+    int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)
+    int bstream_kparts = 0;  // bstream EPI_SLAB K parts (0: by K)
+    int bstream_nw = 0;      // bstream waves per block (0: 16 whole-K, 8 split-K)
     int rmsnorm_block = 0;   // 1: block-per-row RMSNorm (the pre-vectorisation kernel), 0: wave-per-row when shapes allow
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
@@ -246,6 +250,39 @@ BgemvPlan bgemv_plan(int N, int K, int R, size_t esz);
 template <typename T> void launch_bgemv(hipStream_t s, const BgemvArgs<T>& a, int epi);
 // stream-K decode GEMV; returns false (nothing launched) when the shape is not eligible
 template <typename T> bool launch_gemv_sk(hipStream_t s, const GemvArgs<T>& a, int pro, int epi);
+
+// ---- batched decode weight streaming with register-resident X, 8 < R <= 32 (fm_bstream.hip) ---
+template <typename T> struct BstreamArgs {
+    const T* W;      // packed MFMA-fragment layout [tiles][K/32][512]
+    const T* bias;   // [N] or null (EPI_STORE / EPI_F32; EPI_SLAB leaves it to finalize_norm)
+    const T* X;      // [R][ldx]
+    int ldx, R, N, K;
+    T* Y;            // EPI_STORE / EPI_SWIGLU8 [R][ldy]
+    int ldy;         // also the row stride of Yf
+    float* Yf;       // EPI_F32 [R][ldy] | EPI_SLAB partial slabs [kparts][R][ldy]
+    int kparts = 1;  // set by the launcher from the plan
+};
+struct BstreamPlan {
+    bool ok = false;
+    int kparts = 1, nw = 0, spw = 0, tpi = 1, grid = 0;
+};
+BstreamPlan bstream_plan(int N, int K, int R, int epi, size_t esz);
+template <typename T> bool launch_bstream(hipStream_t s, const BstreamArgs<T>& a, int epi, const BstreamPlan& p);
+// x_out = round(res + round(sum of kparts slabs + bias)); if nw: xn_out = RMSNorm(x_out) * nw
+template <typename T> struct FinalizeArgs {
+    const float* slab;  // [kparts][R][lds]
+    int kparts, lds;
+    const T* bias;      // [d] or null
+    const T* res;       // [R][ldr]
+    int ldr;
+    T* x_out;           // [R][ldx] (may alias res)
+    int ldx;
+    const T* nw;        // norm weight [d] or null (no norm)
+    float eps;
+    T* xn_out;          // [R][ldxn]
+    int ldxn, d, R;
+};
+template <typename T> void launch_finalize_norm(hipStream_t s, const FinalizeArgs<T>& a);
 
 // ---- fused decode attention / sampler (fm_attn.hip) ------------------------------------------
 template <typename T> struct AttnDecArgs {
@@ -287,6 +324,9 @@ inline int attn2_cap(int hd, int g, size_t esz) {
     c = c > 256 ? 256 : c;
     return (int)(c & ~15L);
 }
+// decode attention v3 (fm_attn.hip attn_dec3_kernel): 64 positions per block in registers,
+// maxsplit set by the launcher (ceil(S / 64)); a.part must hold [R][nh][ceil(S / 64)][hd + 2]
+template <typename T> void launch_attn_decode3(hipStream_t s, const AttnDecArgs<T>& a, int R);
 template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFusedArgs<T>& a, int R);
 // fast-model attention, one wave per q head (cpos < 16 cached rows, hd <= 256)
 template <typename T> void launch_fast_attn2(hipStream_t s, const FastFusedArgs<T>& a, int R);

@@ -27,6 +27,7 @@ static constexpr int PREFILL_CHUNK = 256;
 static constexpr int ATTN_SPLIT = 64;
 static constexpr int GEMV_MAX_ROWS = 8;  // frames with <= 8 streams take the fused GEMV path
 static constexpr int KSB_MAX = 8;
+static constexpr int BS_KPARTS = 8;  // most K parts of a bstream slab (fm_bstream.hip)
 
 // split-K factor across blocks for a GEMV with N output rows: >= ~512 blocks when possible,
 // K/(32*ksb) integral, LDS staging within budget.
@@ -101,6 +102,7 @@ struct fm_llm {
     float* skpart = nullptr;              // stream-K partial tiles
     long long skpart_cap = 0;  // [Rmax][nkv] arrival tickets of attn_decode2 (kept zero between launches)
     float *slabA = nullptr, *slabB = nullptr;  // split-K partials of wo / w2 (small-batch path)
+    float *bsA = nullptr, *bsB = nullptr;      // bstream K-part slabs of wo / w2 (batched path)
     // rows / slots
     int *frame_slot = nullptr, *frame_pos = nullptr, *prow_slot = nullptr, *prow_pos = nullptr;
     int32_t *tok_in = nullptr, *cols = nullptr, *ptok = nullptr, *ras = nullptr;
@@ -220,6 +222,9 @@ template <typename T> struct Run {
 
     void linear(const void* W, const void* W2, const void* bias, const void* X, int ldx, int R, int N,
                 int K, void* Y, int ldy, const void* res, int ldr, float* Yf, int epi, const char* cls) {
+        if (bs_use(R, false) && !W2 && !res && (epi == EPI_F32 || epi == EPI_STORE) &&
+            bs_linear(W, bias, X, ldx, R, N, K, Y, ldy, Yf, epi))
+            return;  // heads / fast_project_in of a batched frame
         LinearArgs<T> a{(const T*)W, (const T*)W2, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y,
                         ldy, (const T*)res, ldr, Yf};
         if (R > GEMV_MAX_ROWS && R <= 64) {  // batched decode: split-K over the idle CUs
@@ -245,15 +250,88 @@ template <typename T> struct Run {
     }
 
     // TransformerBlock.forward (llama.py:838-843) on R rows; x is updated in place.
+    // ---- batched decode (8 < R <= 32 rows, one per slot) on bstream_kernel (fm_bstream.hip) ----
+    // Wo and W2 leave fp32 K-part slabs; finalize_norm_kernel sums them into the residual row and
+    // applies the next RMSNorm, so W2's finalise is deferred to the next block's start (or flush()).
+    struct BsPending {
+        bool on = false;
+        const float* slab = nullptr;
+        int kparts = 0, d = 0, R = 0;
+        void* res = nullptr;  // residual rows (h) ...
+        void* out = nullptr;  // ... + round(sum of slabs) -> out (x)
+    } pend;
+    // slow-model decode attention: attn_dec3 (registers, 64 positions per block) for the batched
+    // frame (B=32: 35.7 vs 38.1 us per layer), attn_decode2 (LDS tiles, 32-row blocks) at B <= 8,
+    // where it is the faster of the two (B=1 frame 4.28 vs 4.52 ms)
+    void attn_slow(const AttnDecArgs<T>& aa, int R) {
+        if (fm_tuning().attn3 && R > GEMV_MAX_ROWS && aa.hd % 32 == 0 && aa.hd <= 128 && aa.nh / aa.nkv <= 6)
+            launch_attn_decode3<T>(s, aa, R);
+        else
+            launch_attn_decode2<T>(s, aa, R);
+    }
+    bool bs_frame = false;  // inside a batched decode frame (rows are distinct slots)
+    bool bs_use(int R, bool) const {
+        return fm_tuning().bstream && bs_frame && R > GEMV_MAX_ROWS && R <= 32 && m->bsA;
+    }
+    // one bstream linear; returns false (nothing launched) when the shape is not eligible
+    bool bs_linear(const void* W, const void* bias, const void* X, int ldx, int R, int N, int K, void* Y, int ldy,
+                   float* Yf, int epi, int* kparts_out = nullptr) {
+        const BstreamPlan p = bstream_plan(N, K, R, epi, E);
+        if (!p.ok) return false;
+        BstreamArgs<T> a{(const T*)W, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y, ldy, Yf};
+        const int64_t bytes = (int64_t)N * K * E + (int64_t)R * K * E +
+                              (int64_t)R * N * (epi == EPI_SLAB ? 4 * p.kparts : (epi == EPI_F32 ? 4 : E));
+        const double flops = 2.0 * R * N * K;
+        hipStream_t st = s;
+        auto go = [st, a, epi, p] { FMCHECK(launch_bstream<T>(st, a, epi, p), "bstream: no kernel for the plan"); };
+        m->prof.record("linear", bytes, go);
+        m->prof.run(s, "linear", bytes, flops, go);
+        if (kparts_out) *kparts_out = p.kparts;
+        return true;
+    }
+    void finalize_norm(const float* slab, int kparts, const void* bias, const void* res, void* out, const void* nw,
+                       void* xn, int d, int R) {
+        FinalizeArgs<T> f{slab, kparts, d, (const T*)bias, (const T*)res, d, (T*)out, d, (const T*)nw,
+                          m->c.norm_eps, (T*)xn, d, d, R};
+        m->prof.run(s, "norm", 0, 0, [&] { launch_finalize_norm<T>(s, f); });
+    }
+    // finalise a W2 left pending by the last block of a stack (no norm)
+    void flush() {
+        if (!pend.on) return;
+        pend.on = false;
+        finalize_norm(pend.slab, pend.kparts, nullptr, pend.res, pend.out, nullptr, nullptr, pend.d, pend.R);
+    }
+    // the stack's input rows x are final unless a previous block left W2 pending on them
+    void bs_norm_in(const StackDims& d, const LayerW& L, int R, void* xb, void* xnb) {
+        if (pend.on) {
+            FMCHECK(pend.out == xb && pend.R == R && pend.d == d.dim, "bstream: pending residual mismatch");
+            pend.on = false;
+            finalize_norm(pend.slab, pend.kparts, nullptr, pend.res, xb, L.an, xnb, d.dim, R);
+        } else {
+            m->prof.run(s, "norm", 0, 0, [&] {
+                launch_rmsnorm<T>(s, (const T*)xb, d.dim, (const T*)L.an, d.dim, m->c.norm_eps, (T*)xnb, d.dim, R);
+            });
+        }
+    }
+
     void block(const StackDims& d, const LayerW& L, int R, const int* rslot, const int* rpos,
                int fixed_pos, bool is_fast, void* kc, void* vc, size_t sstride, size_t loff, int Sc,
                const float* rope, void* xb, void* hb, void* xnb) {
         const float eps = m->c.norm_eps;
-        m->prof.run(s, "norm", 0, 0, [&] {
-            launch_rmsnorm<T>(s, (const T*)xb, d.dim, (const T*)L.an, d.dim, eps, (T*)xnb, d.dim, R);
-        });
-        linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
-               nullptr, EPI_STORE, "linear");
+        const bool bs = bs_use(R, is_fast);
+        if (bs) {
+            bs_norm_in(d, L, R, xb, xnb);
+            if (!bs_linear(L.wqkv, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, EPI_STORE))
+                linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
+                       nullptr, EPI_STORE, "linear");
+        } else {
+            flush();
+            m->prof.run(s, "norm", 0, 0, [&] {
+                launch_rmsnorm<T>(s, (const T*)xb, d.dim, (const T*)L.an, d.dim, eps, (T*)xnb, d.dim, R);
+            });
+            linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
+                   nullptr, EPI_STORE, "linear");
+        }
         const float scale = 1.0f / sqrtf((float)d.hd);
         // One row per slot (batched decode frames, every fast pass): the fused decode attention
         // kernels of the small-batch path do QK-norm, RoPE and the KV write themselves.  Prompt
@@ -269,7 +347,7 @@ template <typename T> struct Run {
             aa.cnt = m->attn_cnt;
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
-            m->prof.run(s, "attn", 0, 0, [&] { launch_attn_decode2<T>(s, aa, R); });
+            m->prof.run(s, "attn", 0, 0, [&] { attn_slow(aa, R); });
         } else if (is_fast && fm_tuning().batched_fused_attn && fixed_pos >= 0 && fixed_pos < 16 && d.hd <= 256) {
             FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), rslot, d.nh, d.nkv, d.hd, d.qk_norm, eps,
                                 (const T*)L.qn, (const T*)L.kn, rope, (T*)kc, (T*)vc, sstride, loff, Sc,
@@ -290,18 +368,36 @@ template <typename T> struct Run {
                 m->prof.run(s, "attn", 0, 0, [&] { launch_fast_attn<T>(s, fa, R); });
             }
         }
-        linear(L.wo, nullptr, L.bo, m->att, d.nq(), R, d.dim, d.nq(), hb, d.dim, xb, d.dim, nullptr,
-               EPI_RESID, "linear");
-        m->prof.run(s, "norm", 0, 0, [&] {
-            launch_rmsnorm<T>(s, (const T*)hb, d.dim, (const T*)L.fn, d.dim, eps, (T*)xnb, d.dim, R);
-        });
-        linear(L.w13, nullptr, nullptr, xnb, d.dim, R, 2 * d.inter, d.dim, m->act2, 2 * d.inter, nullptr, 0,
-               nullptr, EPI_STORE, "linear");
-        m->prof.run(s, "other", 0, 0, [&] {
-            launch_swiglu_i8<T>(s, (const T*)m->act2, 2 * d.inter, (T*)m->act, d.inter, d.inter, R);
-        });
-        linear(L.w2, nullptr, nullptr, m->act, d.inter, R, d.dim, d.inter, xb, d.dim, hb, d.dim, nullptr,
-               EPI_RESID, "linear");
+        int kp = 0;
+        if (bs && bs_linear(L.wo, nullptr, m->att, d.nq(), R, d.dim, d.nq(), nullptr, d.dim, m->bsA, EPI_SLAB, &kp)) {
+            finalize_norm(m->bsA, kp, L.bo, xb, hb, L.fn, xnb, d.dim, R);  // h = x + wo(att); xn = ffn_norm(h)
+        } else {
+            linear(L.wo, nullptr, L.bo, m->att, d.nq(), R, d.dim, d.nq(), hb, d.dim, xb, d.dim, nullptr,
+                   EPI_RESID, "linear");
+            m->prof.run(s, "norm", 0, 0, [&] {
+                launch_rmsnorm<T>(s, (const T*)hb, d.dim, (const T*)L.fn, d.dim, eps, (T*)xnb, d.dim, R);
+            });
+        }
+        if (!(bs && bs_linear(L.w13, nullptr, xnb, d.dim, R, 2 * d.inter, d.dim, m->act, d.inter, nullptr,
+                              EPI_SWIGLU8))) {
+            linear(L.w13, nullptr, nullptr, xnb, d.dim, R, 2 * d.inter, d.dim, m->act2, 2 * d.inter, nullptr, 0,
+                   nullptr, EPI_STORE, "linear");
+            m->prof.run(s, "other", 0, 0, [&] {
+                launch_swiglu_i8<T>(s, (const T*)m->act2, 2 * d.inter, (T*)m->act, d.inter, d.inter, R);
+            });
+        }
+        if (bs && bs_linear(L.w2, nullptr, m->act, d.inter, R, d.dim, d.inter, nullptr, d.dim, m->bsB, EPI_SLAB, &kp)) {
+            pend.on = true;  // x = h + w2(act): finalised by the next block's norm, or flush()
+            pend.slab = m->bsB;
+            pend.kparts = kp;
+            pend.d = d.dim;
+            pend.R = R;
+            pend.res = hb;
+            pend.out = xb;
+        } else {
+            linear(L.w2, nullptr, nullptr, m->act, d.inter, R, d.dim, d.inter, xb, d.dim, hb, d.dim, nullptr,
+                   EPI_RESID, "linear");
+        }
     }
 
     // ---------------- small-batch (<= 8 streams) fused path --------------------------------
@@ -397,7 +493,7 @@ template <typename T> struct Run {
             aa.cnt = m->attn_cnt;
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
-            m->prof.run(s, "attn", 0, 0, [&] { launch_attn_decode2<T>(s, aa, n); });
+            m->prof.run(s, "attn", 0, 0, [&] { attn_slow(aa, n); });
         } else if (!fuse && !att_wo) {
             m->prof.run(s, "attn", 0, 0, [&] {
                 if (cpos < 16 && d.hd <= 256)
@@ -581,6 +677,7 @@ template <typename T> struct Run {
         for (int l = 0; l < m->sd.n_layer; ++l)
             block(m->sd, m->slow[l], R, rslot, rpos, -1, false, m->kc, m->vc, m->slot_stride,
                   (size_t)l * m->layer_stride, m->S, m->rope, m->x, m->h, m->xn);
+        flush();
     }
 
     // final norm -> constrained head logits; hidden for the fast model (llama.py:447-466, 826)
@@ -605,6 +702,7 @@ template <typename T> struct Run {
         for (int l = 0; l < m->fdm.n_layer; ++l)
             block(m->fdm, m->fast[l], n, m->frame_slot, nullptr, cpos, true, m->fkc, m->fvc,
                   m->fslot_stride, (size_t)l * m->flayer_stride, m->C, m->frope, m->fx, m->fh, m->fxn);
+        flush();
         if (with_head) {
             m->prof.run(s, "norm", 0, 0, [&] {
                 launch_rmsnorm<T>(s, (const T*)m->fx, c.fast_dim, (const T*)m->fnorm, c.fast_dim,
@@ -672,10 +770,12 @@ template <typename T> struct Run {
                             (T*)m->x, m->frame_slot);
         });
         rows_distinct_slots = true;
+        bs_frame = true;
         slow_layers(n, m->frame_slot, m->frame_pos);
         rows_distinct_slots = false;
         head_and_hidden(m->x, n);
         frame_tail(n, true, true);
+        bs_frame = false;
         launch_finish(s, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10,
                       m->C1, 1, m->sp);
     }
@@ -881,6 +981,10 @@ static void finalize(fm_llm* m) {
     HIPCHK(hipMemsetAsync(m->attn_cnt, 0, (size_t)R * d.nkv * sizeof(int), m->stream));
     m->slabA = (float*)m->dalloc((size_t)KSB_MAX * std::min(n, GEMV_MAX_ROWS) * dmax * 4);
     m->slabB = (float*)m->dalloc((size_t)KSB_MAX * std::min(n, GEMV_MAX_ROWS) * dmax * 4);
+    if (n > GEMV_MAX_ROWS) {  // [BS_KPARTS][32][dmax] fp32 each
+        m->bsA = (float*)m->dalloc((size_t)BS_KPARTS * 32 * dmax * 4, false);
+        m->bsB = (float*)m->dalloc((size_t)BS_KPARTS * 32 * dmax * 4, false);
+    }
     m->logits = (float*)m->dalloc((size_t)n * m->Nhead * 4);
     m->flogits = (float*)m->dalloc((size_t)n * m->cb * 4);
     m->frame_slot = (int*)m->dalloc(n * 4);
@@ -1365,6 +1469,16 @@ int fm_tune(const char* key, int value) {
             t.linear_fill = value;
         } else if (k == "ksb_balance") {
             t.ksb_balance = value != 0;
+        } else if (k == "attn3") {
+            t.attn3 = value != 0;
+        } else if (k == "bstream") {
+            t.bstream = value != 0;
+        } else if (k == "bstream_kparts") {
+            FMCHECK(value == 0 || value == 1 || value == 2 || value == 4 || value == 8, "bstream_kparts must be 0, 1, 2, 4 or 8");
+            t.bstream_kparts = value;
+        } else if (k == "bstream_nw") {
+            FMCHECK(value >= 0 && value <= 16, "bstream_nw must be in [0, 16]");
+            t.bstream_nw = value;
         } else if (k == "rmsnorm_block") {
             t.rmsnorm_block = value != 0;
         } else if (k == "debug_ts") {  // (re)arm the per-block timestamp buffer; 0 frees it

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "fm_kernels.h"
@@ -168,16 +169,22 @@ void qk_rope_t(hipStream_t s, int kernel, const float* qkv, int nh, int nkv, int
     const int rs[2] = {0, pos};
     b.put(row, rs, 8);
     const float scale = 1.0f / sqrtf((float)hd);
-    if (kernel == 0) {  // slow decode attention (attn_decode2)
+    if (kernel == 0 || kernel == 2) {  // slow decode attention
         AttnDecArgs<T> a{raw, ld, row, row + 1, nh, nkv, hd, qk_norm, eps, qnd, knd, rope, kc, vc, stride, 0, S,
                          1, scale, nullptr};
         a.cap = attn2_cap(hd, nh / nkv, sizeof(T));
-        a.maxsplit = FM_CEIL(S, a.cap);
+        a.maxsplit = FM_CEIL(S, std::min(a.cap, 16));  // covers both kernels' split counts
         a.part = (float*)b.alloc((size_t)nh * a.maxsplit * (hd + 2) * 4);
         a.cnt = (int*)b.alloc((size_t)nkv * 4);
         a.out = out;
         a.qdbg = qd;
-        launch_attn_decode2<T>(s, a, 1);
+        // kernel 0: attn_decode2 (the B <= 8 decode path), 2: attn_dec3 (the batched frame)
+        if (kernel == 2) {
+            launch_attn_decode3<T>(s, a, 1);
+        } else {
+            a.maxsplit = FM_CEIL(S, a.cap);
+            launch_attn_decode2<T>(s, a, 1);
+        }
     } else {  // fast-model attention (one wave per q head) at codebook position pos
         FMCHECK(pos < 16, "fast attention positions are < 16");
         FastFusedArgs<T> a{raw, ld, row, nh, nkv, hd, qk_norm, eps, qnd, knd, rope, kc, vc, stride, 0, S, pos,
@@ -229,7 +236,7 @@ int fm_op_qk_rope(int device, int precision, int kernel, const float* qkv, int n
     return fm_guard([&] {
         FMCHECK(qkv && q_out && k_out, "null argument");
         FMCHECK(!qk_norm || (qn && kn), "qk_norm needs both norm weights");
-        FMCHECK(kernel == 0 || kernel == 1, "kernel must be 0 (slow attn_decode2) or 1 (fast attn2)");
+        FMCHECK(kernel >= 0 && kernel <= 2, "kernel must be 0 (slow attn_decode2), 1 (fast attn2) or 2 (slow attn_dec3)");
         FMCHECK(nh >= 1 && nkv >= 1 && nh % nkv == 0 && nh / nkv <= 16, "bad head counts");
         FMCHECK(hd >= 8 && hd <= 256 && hd % 8 == 0, "bad head_dim");
         FMCHECK(pos >= 0 && pos < 65536, "bad position");

@@ -54,7 +54,7 @@ def test_rmsnorm(mode, precision, golden):
     _check(y, ref, precision)
 
 
-@pytest.mark.parametrize("kernel", ["slow", "fast"])
+@pytest.mark.parametrize("kernel", ["slow", "slow3", "fast"])
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_qk_norm(kernel, precision, golden):
     """qk-norm alone: position 0 (RoPE is the identity there), every head of ops.npz's q fed both
@@ -71,7 +71,7 @@ def test_qk_norm(kernel, precision, golden):
             _check(k, ref[i, j], precision)
 
 
-@pytest.mark.parametrize("kernel", ["slow", "fast"])
+@pytest.mark.parametrize("kernel", ["slow", "slow3", "fast"])
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_rope(kernel, precision, golden):
     """RoPE with the bf16 cos/sin table at the golden positions (the fast model's kernel only covers
