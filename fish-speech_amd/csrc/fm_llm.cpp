@@ -1174,28 +1174,31 @@ int fm_llm_finalize(fm_llm* m) {
     });
 }
 
+// pos0 > 0 continues a slot whose positions [0, pos0) already hold the KV of the same tokens
+// (prefix reuse across generate_long batches); the prompt suffix runs at pos0 .. pos0 + T - 1
 static void do_prefill(fm_llm* m, int slot, const int32_t* tokens, int T, const fm_sampling* sp,
-                       int32_t* first_col) {
+                       int32_t* first_col, int pos0 = 0) {
     FMCHECK(slot >= 0 && slot < m->max_slots, "bad slot");
-    FMCHECK(T >= 1 && T < m->c.max_seq_len, "prompt length must be in [1, max_seq_len)");
+    FMCHECK(T >= 1 && pos0 >= 0 && pos0 + T < m->c.max_seq_len, "prompt must end before max_seq_len");
+    FMCHECK(pos0 <= m->host_pos[slot], "prefix reuse past the slot's cached positions");
     check_tokens(m, tokens, T);
     reset_slot(m, slot, sp);
     const int32_t one = slot;
     m->uploaded_slots.clear();
     HIPCHK(hipMemcpyAsync(m->frame_slot, &one, 4, hipMemcpyHostToDevice, m->stream));
     with_prec(m, [&](auto& r) {
-        const void* last = r.prefill_slow(slot, tokens, T, 0);
+        const void* last = r.prefill_slow(slot, tokens, T, pos0);
         const void* hid = r.head_small(last, false, 1, 1);
         r.frame_tail_small(1, false, true, hid);
     });
-    int pos = T - 1;  // finish() advances it to T: the first decode frame runs at position T
+    int pos = pos0 + T - 1;  // finish() advances it: the first decode frame runs at pos0 + T
     HIPCHK(hipMemcpyAsync(m->frame_pos, &pos, 4, hipMemcpyHostToDevice, m->stream));
     launch_finish(m->stream, 1, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras,
                   m->C1 * 10, m->C1, 0, m->sp);
     HIPCHK(hipMemcpyAsync(m->h_cols, m->cols, (size_t)m->C1 * 4, hipMemcpyDeviceToHost, m->stream));
     HIPCHK(hipStreamSynchronize(m->stream));
     m->prof.collect();
-    m->host_pos[slot] = T;
+    m->host_pos[slot] = pos0 + T;
     m->host_step[slot] = 1;
     m->uploaded_slots.clear();
     if (first_col) memcpy(first_col, m->h_cols, (size_t)m->C1 * 4);
@@ -1268,18 +1271,17 @@ int fm_llm_decode_frames(fm_llm* m, const int32_t* slots, int n, int nframes, in
     });
 }
 
-int fm_llm_generate(fm_llm* m, int slot, const int32_t* prompt, int T, int max_new, const fm_sampling* sp,
-                    int32_t* out, int* n_out) {
-    return fm_guard([&] {
+static void do_generate(fm_llm* m, int slot, const int32_t* prompt, int T, int pos0, int max_new,
+                        const fm_sampling* sp, int32_t* out, int* n_out) {
         FMCHECK(m && prompt && out && n_out, "null argument");
         HIPCHK(hipSetDevice(m->device));
         finalize(m);
         const fm_model_config& c = m->c;
-        if (max_new <= 0 || T + max_new > c.max_seq_len) max_new = c.max_seq_len - T;
+        if (max_new <= 0 || pos0 + T + max_new > c.max_seq_len) max_new = c.max_seq_len - pos0 - T;
         FMCHECK(max_new >= 1, "prompt leaves no room to generate");
         const int C1 = m->C1;
         int32_t col[64];
-        do_prefill(m, slot, prompt, T, sp, col);
+        do_prefill(m, slot, prompt, T, sp, col, pos0);
         for (int q = 0; q < C1; ++q) out[(size_t)q * max_new] = col[q];
         int n = 1;
         upload_frame_rows(m, &slot, 1);
@@ -1308,10 +1310,26 @@ int fm_llm_generate(fm_llm* m, int slot, const int32_t* prompt, int T, int max_n
         m->prof.collect();
         (void)hipEventDestroy(ev[0]);
         (void)hipEventDestroy(ev[1]);
-        m->host_pos[slot] = T + issued;  // device advanced once per issued frame
+        m->host_pos[slot] = pos0 + T + issued;  // device advanced once per issued frame
         m->host_step[slot] = 1 + issued;
         m->uploaded_slots.clear();
         *n_out = n;
+}
+
+int fm_llm_generate(fm_llm* m, int slot, const int32_t* prompt, int T, int max_new, const fm_sampling* sp,
+                    int32_t* out, int* n_out) {
+    return fm_guard([&] { do_generate(m, slot, prompt, T, 0, max_new, sp, out, n_out); });
+}
+
+int fm_llm_generate_at(fm_llm* m, int slot, const int32_t* suffix, int T, int pos0, int max_new,
+                       const fm_sampling* sp, int32_t* out, int* n_out) {
+    return fm_guard([&] { do_generate(m, slot, suffix, T, pos0, max_new, sp, out, n_out); });
+}
+
+int fm_llm_slot_pos(fm_llm* m, int slot, int* pos) {
+    return fm_guard([&] {
+        FMCHECK(m && pos && slot >= 0 && slot < m->max_slots, "bad arguments");
+        *pos = m->host_pos[slot];
     });
 }
 

@@ -66,10 +66,18 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
                   top_p: float = 0.9, top_k: int = 30, repetition_penalty: float = 1.1,
                   temperature: float = 1.0, compile: bool = False, iterative_prompt: bool = True,
                   chunk_length: int = 512, prompt_text: Optional[Union[str, List[str]]] = None,
-                  prompt_tokens=None, seed: Optional[int] = None) -> Iterator[GenerateResponse]:
+                  prompt_tokens=None, seed: Optional[int] = None,
+                  reuse_prefix: bool = True) -> Iterator[GenerateResponse]:
     """inference.py:523-733 on the native model.  `device`, `decode_one_token`, `compile`,
     `iterative_prompt` and `repetition_penalty` are accepted for signature compatibility; like
-    the reference, repetition_penalty is not applied (RAS is, inside the sampler)."""
+    the reference, repetition_penalty is not applied (RAS is, inside the sampler).
+
+    The reference re-prefills the whole growing conversation for every text batch
+    (inference.py:620-724).  With reuse_prefix, each batch after the first keeps the slot's KV for
+    the longest prefix its new prompt shares with what the slot already ran (the previous prompt
+    plus the columns fed back while generating), and prefills only the rest (fm_llm_generate_at).
+    The prompt tokens are the same, so the codes are the same up to the fp32 accumulation order of
+    the reused positions (decode-path vs prefill-path kernels; tests/test_gpu_engine.py)."""
     if not (0 < top_p <= 1):
         raise AssertionError("top_p must be in (0, 1]")
     if not (0 < temperature < 2):
@@ -95,6 +103,7 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
     for sample_idx in range(num_samples):
         conv = copy.deepcopy(base)
         t0 = time.perf_counter()
+        cached = None  # (C+1, P) tokens whose KV the slot holds at positions [0, P)
         for batch_idx, batch_text in enumerate(batches):
             conv.append(P.Message(role="user", parts=[P.TextPart(text=batch_text)]))
             gen = copy.deepcopy(conv)
@@ -103,8 +112,21 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
             if encoded.shape[1] > max_len - 2048:
                 raise ValueError(f"Prompt is too long: {encoded.shape[1]} > {max_len - 2048}")
             s = int(rng.integers(0, 2**63 - 1)) if seed is None else seed + 1000003 * sample_idx + batch_idx
-            y = model.generate(encoded.astype(np.int32), max_new_tokens, temperature=temperature,
-                               top_p=top_p, top_k=top_k, seed=s)
+            enc = encoded.astype(np.int32)
+            L = 0
+            if reuse_prefix and cached is not None:
+                n = min(cached.shape[1], enc.shape[1] - 1)  # at least one new position to prefill
+                same = np.all(cached[:, :n] == enc[:, :n], axis=0)
+                L = int(n if same.all() else np.argmin(same))
+            if L > 0:
+                y = model.generate_at(enc[:, L:], L, max_new_tokens, temperature=temperature, top_p=top_p,
+                                      top_k=top_k, seed=s)
+            else:
+                y = model.generate(enc, max_new_tokens, temperature=temperature, top_p=top_p, top_k=top_k,
+                                   seed=s)
+            if reuse_prefix and hasattr(model, "slot_pos"):
+                fed = model.slot_pos() - enc.shape[1]  # columns fed back while decoding
+                cached = np.concatenate([enc, y[:, :fed]], axis=1)
             codes = np.ascontiguousarray(y[1:, :-1])  # y[1:, prompt_length:-1] of the reference
             if (codes < 0).any():
                 raise AssertionError(f"Negative code found: {codes}")

@@ -172,6 +172,27 @@ class DualARModel:
                                                   ctypes.byref(sp), native.i32p(out), ctypes.byref(n)))
         return out[:, : n.value]
 
+    def generate_at(self, suffix: np.ndarray, pos0: int, max_new_tokens: int, temperature=0.7, top_p=0.9,
+                    top_k=30, seed=0, slot=0, mask_im_end=False) -> np.ndarray:
+        """generate() whose prompt = the slot's cached positions [0, pos0) + `suffix`
+        (fm_llm_generate_at: only the suffix is prefilled).  Returns the emitted columns."""
+        p = np.ascontiguousarray(suffix, dtype=np.int32)
+        T = p.shape[1]
+        mx = max_new_tokens if (max_new_tokens and pos0 + T + max_new_tokens <= self.cfg.max_seq_len) \
+            else self.cfg.max_seq_len - pos0 - T
+        out = np.zeros((self.C1, mx), np.int32)
+        n = ctypes.c_int(0)
+        sp = self.sampling(temperature, top_p, top_k, seed, mask_im_end)
+        native.check(native.lib().fm_llm_generate_at(self.h, slot, native.i32p(p), T, int(pos0), mx,
+                                                     ctypes.byref(sp), native.i32p(out), ctypes.byref(n)))
+        return out[:, : n.value]
+
+    def slot_pos(self, slot: int = 0) -> int:
+        """Positions of `slot` whose KV is written (its prompt + the columns fed back so far)."""
+        v = ctypes.c_int(0)
+        native.check(native.lib().fm_llm_slot_pos(self.h, slot, ctypes.byref(v)))
+        return v.value
+
     def teacher_step(self, x: np.ndarray, pos0: int, next_col=None, slot: int = 0):
         xx = np.ascontiguousarray(x, dtype=np.int32)
         lg = np.zeros(self.cfg.vocab_size, np.float32)

@@ -104,6 +104,15 @@ int fm_llm_decode_frames(fm_llm* h, const int32_t* slots, int n, int nframes, in
    (stops after emitting <|im_end|> unless mask_im_end). */
 int fm_llm_generate(fm_llm* h, int slot, const int32_t* prompt, int T, int max_new,
                     const fm_sampling* sp, int32_t* out, int* n_out);
+/* generate() continuing a slot's cached prefix: positions [0, pos0) keep the KV of tokens the
+   slot already ran (the previous generate_long batch's prompt and fed columns), the prompt suffix
+   ((C+1) x T) is prefilled at pos0 .. pos0 + T - 1, then decoding as fm_llm_generate.  Replaces
+   the whole-conversation re-prefill of generate_long (inference.py:620-724) for the shared
+   prefix.  pos0 must not exceed fm_llm_slot_pos. */
+int fm_llm_generate_at(fm_llm* h, int slot, const int32_t* suffix, int T, int pos0, int max_new,
+                       const fm_sampling* sp, int32_t* out, int* n_out);
+/* positions of the slot whose KV is written (prompt + fed columns of its last generate) */
+int fm_llm_slot_pos(fm_llm* h, int slot, int* pos);
 /* teacher forcing for parity: run S positions of x ((C+1) x S) from pos0 on slot (pos0 == 0
    resets the slot), return the last position's slow logits (V, with the semantic bias NOT
    applied), the fast hidden (fast_dim), and -- when next_col != NULL -- the fast logits

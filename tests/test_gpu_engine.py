@@ -58,6 +58,37 @@ def test_generate_long_matches_reference(golden, tmp_path):
         np.testing.assert_array_equal(o.codes, g[f"codes_{i}"])
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_prefix_reuse_equals_reprefill(golden, tmp_path, precision):
+    """generate_long's later batches keep the slot's KV for the prefix they share
+    with the previous batch's prompt and fed columns, and prefill only the rest.  The codes equal
+    the whole-conversation re-prefill (the reference's own flow, inference.py:620-724) in fp32 and
+    bf16, and fewer positions are prefilled."""
+    from fishmi import engine
+    from fishmi.llm import DualARModel
+
+    g = golden("engine.npz")
+    m = DualARModel.from_pretrained(_ckpt(tmp_path), device=0, precision=precision, max_length=2560)
+    calls = []
+    gen_at = m.generate_at
+
+    def spy(suffix, pos0, *a, **k):
+        calls.append((pos0, suffix.shape[1]))
+        return gen_at(suffix, pos0, *a, **k)
+
+    m.generate_at = spy
+    req = _request(g)
+    reused = [o.codes for o in engine.generate_long(model=m, reuse_prefix=True, **req) if o.action == "sample"]
+    full = [o.codes for o in engine.generate_long(model=m, reuse_prefix=False, **req) if o.action == "sample"]
+    assert len(reused) == len(full) >= 3
+    for a, b in zip(reused, full):
+        np.testing.assert_array_equal(a, b)
+    assert len(calls) == len(full) - 1 and all(p0 > 0 for p0, _ in calls)
+    if precision == "fp32":
+        for i, c in enumerate(reused):
+            np.testing.assert_array_equal(c, g[f"codes_{i}"])
+
+
 def test_worker_queue_contract(golden, tmp_path):
     """launch_thread_safe_queue: FIFO requests, sample* + next per request, an exception becomes
     status="error" and the worker keeps serving, None stops it (inference.py:748-799)."""
