@@ -1,0 +1,198 @@
+"""Wire-compatible HTTP API on libfishmi: the drop-in for tools/api_server.py.
+
+Routes and contract, as the reference serves them (tools/server/views.py, api_utils.py):
+  GET|POST /v1/health          {"status": "ok"}
+  POST /v1/tts                 ServeTTSRequest as application/json or application/msgpack;
+                               streaming: WAV header then int16 little-endian PCM chunks, one per
+                               text batch (format must be wav, else 400); otherwise a whole file in
+                               `format` (wav; pcm = raw int16; mp3/opus need encoders absent here: 400).
+                               400 when the text exceeds --max-text-length, 500 on engine errors.
+  POST /v1/vqgan/encode        msgpack {"audios": [wav bytes]} -> {"tokens": [[[int]]]}
+  POST /v1/vqgan/decode        msgpack {"tokens": [[[int]]]} -> {"audios": [float16 PCM bytes]}.
+                               The reference's batch_vqgan_decode calls DAC.decode(x, feature_lengths),
+                               which its DAC does not have, so this route is broken
+                               there; here it decodes each token matrix through the codec.
+  GET  /v1/references/list     {"success": true, "reference_ids": [...]}
+Optional bearer auth (--api-key): 401 "Invalid token" otherwise (tools/api_server.py:33-45).
+
+    python -m fishmi.server --llama-checkpoint-path DIR --decoder-checkpoint-path codec.pth
+"""
+import argparse
+import io
+import logging
+from typing import Optional
+
+import numpy as np
+
+from . import tts as TTS
+
+log = logging.getLogger("fishmi.server")
+
+
+def _content_type(fmt: str) -> str:
+    return {"wav": "audio/wav", "flac": "audio/flac", "mp3": "audio/mpeg", "opus": "audio/ogg"}.get(
+        fmt, "application/octet-stream")
+
+
+def create_app(engine: "TTS.TTSInferenceEngine", max_text_length: int = 0, api_key: Optional[str] = None):
+    import msgpack
+    from fastapi import FastAPI, HTTPException, Request
+    from fastapi.responses import JSONResponse, Response, StreamingResponse
+
+    app = FastAPI(title="Fish Speech API (libfishmi)", version="1.5.0")
+
+    @app.middleware("http")
+    async def auth(request: Request, call_next):
+        if api_key is not None:
+            h = request.headers.get("authorization", "")
+            if not h.lower().startswith("bearer ") or h[7:].strip() != api_key:
+                return JSONResponse({"detail": "Invalid token"}, status_code=401)
+        return await call_next(request)
+
+    async def body(request: Request) -> dict:
+        ct = request.headers.get("content-type", "").split(";")[0].strip().lower()
+        raw = await request.body()
+        if ct == "application/msgpack":
+            return msgpack.unpackb(raw, raw=False)
+        if ct in ("application/json", ""):
+            import json
+
+            return json.loads(raw or b"{}")
+        raise HTTPException(415, detail="Accept: application/msgpack, application/json")
+
+    def wants_json(request: Request) -> bool:
+        q = request.query_params.get("format", "").strip().lower()
+        if q in {"json", "application/json", "msgpack", "application/msgpack"}:
+            return q in ("json", "application/json")
+        accept = request.headers.get("accept", "").lower()
+        return "application/json" in accept and "application/msgpack" not in accept
+
+    def respond(request: Request, obj: dict):
+        if wants_json(request):  # bytes fields travel base64-encoded in JSON
+            import base64
+
+            def enc(v):
+                if isinstance(v, bytes):
+                    return base64.b64encode(v).decode()
+                if isinstance(v, list):
+                    return [enc(x) for x in v]
+                return v
+
+            return JSONResponse({k: enc(v) for k, v in obj.items()})
+        return Response(msgpack.packb(obj, use_bin_type=True), media_type="application/msgpack")
+
+    @app.get("/v1/health")
+    @app.post("/v1/health")
+    async def health():
+        return {"status": "ok"}
+
+    @app.post("/v1/tts")
+    async def tts(request: Request):
+        try:
+            req = TTS.ServeTTSRequest(**(await body(request)))
+        except HTTPException:
+            raise
+        except Exception as e:
+            raise HTTPException(422, detail=str(e))
+        sr = engine.decoder_model.sample_rate
+        if max_text_length > 0 and len(req.text) > max_text_length:
+            raise HTTPException(400, detail=f"Text is too long, max length is {max_text_length}")
+        if req.streaming and req.format != "wav":
+            raise HTTPException(400, detail="Streaming only supports WAV format")
+        headers = {"Content-Disposition": f"attachment; filename=audio.{req.format}"}
+        if req.streaming:
+            gen = TTS.inference_wrapper(req, engine)
+            try:  # the header (and any immediate engine error) before the response starts
+                first = next(gen)
+            except TTS.EngineError as e:
+                raise HTTPException(500, detail=str(e))
+
+            def stream():
+                # the status line is already out once the header is: an engine error ends the
+                # body early, as the reference's HTTPException inside its stream generator does
+                yield first
+                try:
+                    for chunk in gen:
+                        if isinstance(chunk, bytes):
+                            yield chunk
+                except TTS.EngineError as e:
+                    log.error("TTS stream aborted: %s", e)
+
+            return StreamingResponse(stream(), media_type=_content_type("wav"), headers=headers)
+        if req.format not in ("wav", "pcm"):
+            raise HTTPException(400, detail=f"format {req.format!r} needs an encoder absent from this build")
+        audio = None
+        try:
+            for chunk in TTS.inference_wrapper(req, engine):
+                if isinstance(chunk, np.ndarray):
+                    audio = chunk
+        except TTS.EngineError as e:
+            raise HTTPException(500, detail=str(e))
+        data = TTS.wav_bytes(audio, sr) if req.format == "wav" else \
+            (np.clip(audio, -1, 1) * 32767).astype("<i2").tobytes()
+        return Response(data, media_type=_content_type(req.format), headers=headers)
+
+    @app.post("/v1/vqgan/encode")
+    async def vqgan_encode(request: Request):
+        d = await body(request)
+        try:
+            tokens = [engine.encode_reference(a, True).tolist() for a in d["audios"]]
+        except Exception as e:
+            log.error("VQGAN encode failed: %s", e)
+            raise HTTPException(500, detail="Failed to encode audio")
+        return respond(request, {"tokens": tokens})
+
+    @app.post("/v1/vqgan/decode")
+    async def vqgan_decode(request: Request):
+        d = await body(request)
+        try:
+            audios = [engine.decode_vq_tokens(np.asarray(t, np.int32)).astype(np.float16).tobytes()
+                      for t in d["tokens"]]
+        except Exception as e:
+            log.error("VQGAN decode failed: %s", e)
+            raise HTTPException(500, detail="Failed to decode tokens to audio")
+        return respond(request, {"audios": audios})
+
+    @app.get("/v1/references/list")
+    async def list_refs(request: Request):
+        return respond(request, {"success": True, "reference_ids": engine.list_reference_ids(), "message": "Success"})
+
+    return app
+
+
+def build_engine(llama_checkpoint_path: str, decoder_checkpoint_path: str, device=0, precision="bf16",
+                 compile: bool = False, max_frames: int = 2048):
+    """ModelManager (tools/server/model_manager.py): the LLM worker + the codec with its encoder."""
+    from .codec import FishMICodec
+    from .engine import launch_thread_safe_queue
+
+    q = launch_thread_safe_queue(llama_checkpoint_path, device, precision, compile)
+    codec = FishMICodec.from_checkpoint(decoder_checkpoint_path, device, precision, max_frames, encoder=True)
+    return TTS.TTSInferenceEngine(q, codec, precision, compile)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["tts"], default="tts")
+    ap.add_argument("--llama-checkpoint-path", default="checkpoints/s2-pro")
+    ap.add_argument("--decoder-checkpoint-path", default="checkpoints/s2-pro/codec.pth")
+    ap.add_argument("--decoder-config-name", default="modded_dac_vq")
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--half", action="store_true")
+    ap.add_argument("--compile", action="store_true")
+    ap.add_argument("--max-text-length", type=int, default=0)
+    ap.add_argument("--listen", default="127.0.0.1:8080")
+    ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--api-key", default=None)
+    a = ap.parse_args(argv)
+    import uvicorn
+
+    from .engine import _device_index
+
+    engine = build_engine(a.llama_checkpoint_path, a.decoder_checkpoint_path, _device_index(a.device), "bf16")
+    host, port = a.listen.rsplit(":", 1)
+    uvicorn.run(create_app(engine, a.max_text_length, a.api_key), host=host, port=int(port), workers=1)
+
+
+if __name__ == "__main__":
+    main()

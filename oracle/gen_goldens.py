@@ -754,10 +754,44 @@ def cmd_engine():
     print("engine:", [o.action for o in outs], [res[k].shape for k in res if k.startswith("codes_")])
 
 
+def cmd_engine_clone():
+    """BASELINE config 5's chain at tiny shapes: reference audio -> the reference's own DAC.encode
+    (codec_enc_tiny weights, fp32; vq_manager.py:24-52) -> those codes as the voice-clone prompt of
+    the reference's generate_long (llm_a weights, tiny tokenizer, greedy fp32, several speaker
+    batches) -> codes.  The GPU test runs the same chain through fm_codec_encode + the native
+    generate_long."""
+    import copy as _copy
+
+    from fish_speech.models.text2semantic import inference
+    from fish_speech.tokenizer import FishTokenizer
+
+    dac = build_codec(CODEC_TINY, 41, [0, 0, 0, 2])
+    n = 9 * 2048 - 500
+    audio = encode_audio(n, 77)
+    with torch.inference_mode():
+        ref_codes = dac.encode(torch.from_numpy(audio)[None, None])[0][0]
+    cfg = _copy.deepcopy(LLM_A_CONFIG)
+    cfg["text_config"]["max_seq_len"] = 2560
+    model = build_llm(cfg, None, seed=11, log2_half=3).to(torch.float32)
+    model.tokenizer = FishTokenizer(os.path.join(GOLD, "tok_tiny"))
+    text = "<|speaker:0|>Read this aloud. <|speaker:0|>Then a second sentence follows here."
+    outs = list(inference.generate_long(model=model, device="cpu", decode_one_token=inference.decode_one_token_ar,
+                                        text=text, max_new_tokens=9, top_p=0.9, top_k=1, temperature=0.7,
+                                        chunk_length=30, prompt_text=["the reference transcript"],
+                                        prompt_tokens=[ref_codes.clone()]))
+    res = {"text": np.array(text), "audio_seed": 77, "n_samples": n, "ref_codes": ref_codes.numpy().astype(np.int32),
+           "prompt_text": np.array("the reference transcript"),
+           "actions": np.array(json.dumps([o.action for o in outs]))}
+    for i, o in enumerate([o for o in outs if o.action == "sample"]):
+        res[f"codes_{i}"] = o.codes.numpy().astype(np.int32)
+    np.savez_compressed(os.path.join(GOLD, "engine_clone.npz"), **res)
+    print("engine_clone:", res["ref_codes"].shape, [o.action for o in outs],
+          [res[k].shape for k in res if k.startswith("codes_")])
+
 if __name__ == "__main__":
     cmds = sys.argv[1:] or ["all"]
     if cmds == ["all"]:
         cmds = ["ops", "llm", "codec", "codec_full", "codec_long", "codec_enc", "codec_enc_full",
-                "codec_enc_long", "codec_keys", "llm_wide", "prompt", "engine"]
+                "codec_enc_long", "codec_keys", "llm_wide", "prompt", "engine", "engine_clone"]
     for c in cmds:
         globals()[f"cmd_{c}"]()

@@ -1,0 +1,195 @@
+"""Engine and HTTP wire layer (fishmi.tts / fishmi.server) against the reference's contract
+(fish_speech/inference_engine/__init__.py:41-131, tools/server/inference.py:12-45,
+tools/server/views.py:146-205, tools/api_server.py:33-45), on CPU with a scripted LLM worker and a
+numpy codec stand-in.  The GPU path (real worker + HIP codec) is tests/test_gpu_tts.py."""
+import io
+import queue
+import threading
+import wave
+
+import numpy as np
+import pytest
+
+fastapi = pytest.importorskip("fastapi")
+msgpack = pytest.importorskip("msgpack")
+
+
+class FakeCodec:
+    sample_rate = 44100
+    frame_length = 2048
+    device = "cpu"
+
+    def __init__(self):
+        self.encoded = []
+
+    def decode_codes(self, codes):
+        c = np.asarray(codes)
+        t = np.arange(c.shape[1] * self.frame_length, dtype=np.float32)
+        return (0.5 * np.sin(t * 0.01 + float(c[0, 0]))).astype(np.float32)
+
+    def encode_audio(self, audio):
+        self.encoded.append(audio.size)
+        return np.full((10, (audio.size + 2047) // 2048), 7, np.int32)
+
+
+def fake_worker(batches, fail=False):
+    """Scripted B1 worker: one (10, n) code matrix per text batch, then "next" (or an error)."""
+    from fishmi.engine import GenerateResponse, WrappedGenerateResponse
+
+    q = queue.Queue()
+    seen = []
+
+    def run():
+        while True:
+            item = q.get()
+            if item is None:
+                return
+            seen.append(item.request)
+            if fail:
+                item.response_queue.put(WrappedGenerateResponse("error", RuntimeError("boom")))
+                continue
+            for i, n in enumerate(batches):
+                codes = np.full((10, n), i + 1, np.int32)
+                item.response_queue.put(WrappedGenerateResponse("success", GenerateResponse("sample", codes, f"b{i}")))
+            item.response_queue.put(WrappedGenerateResponse("success", GenerateResponse("next")))
+
+    threading.Thread(target=run, daemon=True).start()
+    return q, seen
+
+
+def _engine(batches=(3, 2), fail=False, tmp_path=None):
+    from fishmi.tts import TTSInferenceEngine
+
+    q, seen = fake_worker(batches, fail)
+    eng = TTSInferenceEngine(q, FakeCodec(), references_dir=str(tmp_path) if tmp_path else "references")
+    return eng, seen
+
+
+def _wav(x, sr=22050, width=2):
+    buf = io.BytesIO()
+    with wave.open(buf, "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(width)
+        w.setframerate(sr)
+        w.writeframes((x * 32767).astype("<i2").tobytes())
+    return buf.getvalue()
+
+
+def test_engine_streaming_results():
+    from fishmi.tts import ServeTTSRequest, wav_chunk_header
+
+    eng, seen = _engine()
+    res = list(eng.inference(ServeTTSRequest(text="hello", streaming=True, seed=3)))
+    assert [r.code for r in res] == ["header", "segment", "segment", "final"]
+    assert res[0].audio[1].tobytes() == wav_chunk_header(44100)
+    segs = [r.audio[1] for r in res[1:3]]
+    assert [s.size for s in segs] == [3 * 2048, 2 * 2048]
+    np.testing.assert_array_equal(res[-1].audio[1], np.concatenate(segs))
+    assert seen[0]["text"] == "hello" and seen[0]["seed"] == 3 and seen[0]["chunk_length"] == 200
+
+
+def test_engine_error_and_empty():
+    from fishmi.tts import ServeTTSRequest
+
+    eng, _ = _engine(fail=True)
+    res = list(eng.inference(ServeTTSRequest(text="x")))
+    # the reference yields the worker's error, then (no segments) its "No audio generated" error
+    assert [r.code for r in res] == ["error", "error"] and "boom" in str(res[0].error)
+    eng, _ = _engine(batches=())
+    res = list(eng.inference(ServeTTSRequest(text="x")))
+    assert res[-1].code == "error" and "No audio" in str(res[-1].error)
+
+
+def test_references_encoded_once_per_hash(tmp_path):
+    from fishmi.tts import ServeReferenceAudio, ServeTTSRequest
+
+    eng, seen = _engine(tmp_path=tmp_path)
+    ref = ServeReferenceAudio(audio=_wav(np.sin(np.arange(22050) * 0.05)), text="ref text")
+    list(eng.inference(ServeTTSRequest(text="a", references=[ref], use_memory_cache="on")))
+    list(eng.inference(ServeTTSRequest(text="b", references=[ref], use_memory_cache="on")))
+    assert eng.decoder_model.encoded == [44100]  # resampled 22.05 -> 44.1 kHz, encoded once
+    assert seen[1]["prompt_text"] == ["ref text"] and seen[1]["prompt_tokens"][0].shape == (10, 22)
+    # reference_id folder with .wav + .lab
+    d = tmp_path / "alice"
+    d.mkdir()
+    (d / "a.wav").write_bytes(_wav(np.zeros(4410), 44100))
+    (d / "a.lab").write_text("alice says hi")
+    list(eng.inference(ServeTTSRequest(text="c", reference_id="alice")))
+    assert seen[2]["prompt_text"] == ["alice says hi"] and eng.list_reference_ids() == ["alice"]
+
+
+def test_read_wav_formats():
+    from fishmi.tts import read_wav
+
+    x = (0.25 * np.sin(np.arange(1000) * 0.1)).astype(np.float32)
+    np.testing.assert_allclose(read_wav(_wav(x, 44100), 44100), x, atol=1e-4)
+    with pytest.raises(ValueError):
+        read_wav(b"ID3\x03mp3data...", 44100)
+
+
+def _client(**kw):
+    from fastapi.testclient import TestClient
+
+    from fishmi.server import create_app
+
+    eng, seen = _engine(**{k: v for k, v in kw.items() if k in ("batches", "fail")})
+    app = create_app(eng, max_text_length=kw.get("max_text_length", 0), api_key=kw.get("api_key"))
+    return TestClient(app), eng, seen
+
+
+def test_http_health_and_auth():
+    c, _, _ = _client(api_key="sekrit")
+    assert c.get("/v1/health").status_code == 401
+    r = c.get("/v1/health", headers={"Authorization": "Bearer sekrit"})
+    assert r.status_code == 200 and r.json() == {"status": "ok"}
+    c, _, _ = _client()
+    assert c.post("/v1/health").json() == {"status": "ok"}
+
+
+def test_http_tts_wav_and_stream_json_and_msgpack():
+    from fishmi.tts import wav_chunk_header
+
+    c, eng, _ = _client()
+    r = c.post("/v1/tts", json={"text": "hello"})
+    assert r.status_code == 200 and r.headers["content-type"] == "audio/wav"
+    with wave.open(io.BytesIO(r.content)) as w:
+        assert w.getframerate() == 44100 and w.getnframes() == 5 * 2048
+    body = msgpack.packb({"text": "hello", "streaming": True}, use_bin_type=True)
+    r = c.post("/v1/tts", content=body, headers={"Content-Type": "application/msgpack"})
+    assert r.status_code == 200
+    hdr = wav_chunk_header(44100)
+    assert r.content[: len(hdr)] == hdr
+    pcm = np.frombuffer(r.content[len(hdr):], "<i2")
+    exp = np.concatenate([(eng.decoder_model.decode_codes(np.full((10, n), i + 1)) * 32768).astype(np.int16)
+                          for i, n in enumerate((3, 2))])
+    np.testing.assert_array_equal(pcm, exp)  # the reference's x * 32768 -> int16 chunks
+
+
+def test_http_tts_errors():
+    c, _, _ = _client(max_text_length=5)
+    assert c.post("/v1/tts", json={"text": "too long text"}).status_code == 400
+    c, _, _ = _client()
+    assert c.post("/v1/tts", json={"text": "x", "streaming": True, "format": "mp3"}).status_code == 400
+    assert c.post("/v1/tts", json={"text": "x", "chunk_length": 5}).status_code == 422
+    c, _, _ = _client(fail=True)
+    assert c.post("/v1/tts", json={"text": "x"}).status_code == 500
+    # streaming: the header has gone out before the worker fails, so the body just ends there
+    from fishmi.tts import wav_chunk_header
+
+    r = c.post("/v1/tts", json={"text": "x", "streaming": True})
+    assert r.status_code == 200 and r.content == wav_chunk_header(44100)
+
+
+def test_http_vqgan_routes():
+    c, eng, _ = _client()
+    wav = _wav(np.zeros(44100 + 100), 44100)
+    r = c.post("/v1/vqgan/encode", content=msgpack.packb({"audios": [wav]}, use_bin_type=True),
+               headers={"Content-Type": "application/msgpack"})
+    tok = msgpack.unpackb(r.content, raw=False)["tokens"]
+    assert np.asarray(tok).shape == (1, 10, 22)
+    r = c.post("/v1/vqgan/decode?format=json", json={"tokens": [[[1] * 4] * 10]})
+    assert r.status_code == 200
+    r = c.post("/v1/vqgan/decode", content=msgpack.packb({"tokens": [[[1] * 4] * 10]}, use_bin_type=True),
+               headers={"Content-Type": "application/msgpack"})
+    a = np.frombuffer(msgpack.unpackb(r.content, raw=False)["audios"][0], np.float16)
+    assert a.size == 4 * 2048
