@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--batch-frames", type=int, default=512, help="throughput leg: frames per request")
     ap.add_argument("--waves", type=int, default=1,
                     help="throughput leg: requests = batch x GPUs x waves, pulled from rank 0's tick queue")
+    ap.add_argument("--longform-turns", type=int, default=4,
+                    help="config-5 leg: speaker turns (0: skip), each --longform-frames frames")
+    ap.add_argument("--longform-frames", type=int, default=323, help="config-5 leg: frames per turn (15 s)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the in-run rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on the GEMV")
     ap.add_argument("--encode-seconds", type=float, default=30.0,
@@ -193,6 +196,77 @@ def encode_leg(ccfg, device, seconds, seed):
             "wall_ms": round(wall * 1e3, 2), "device_ms": round(dev_ms, 2),
             "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": BF16_DENSE_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(tflops / BF16_DENSE_TFLOPS, 4)}}
+
+
+def longform_leg(ccfg, device, turns, frames_per_turn, seed):
+    """BASELINE config 5 on one GPU: voice clone from 30 s of reference audio (codec encode), then
+    `turns` speaker turns of `frames_per_turn` frames through the native generate_long (conversation
+    growing with each turn's codes, prefix KV reused), codes streamed 22 frames at a time into the
+    causal streamed vocoder.  Synthetic S2-Pro weights and a synthetic tokenizer at the S2-Pro vocab
+    layout; <|im_end|> masked so every turn has its full length.  Timed from the request (reference
+    audio in host memory) to the last PCM sample."""
+    import tempfile
+
+    from fishmi import engine as E
+    from fishmi.codec import FishMICodec
+    from fishmi.config import S2_PRO_CONFIG, S2_PRO_IM_END_ID, DualARConfig
+    from fishmi.llm import DualARModel
+    from fishmi.prompt import FishTokenizer
+    from fishmi.synth import write_synthetic_tokenizer
+
+    cfg = DualARConfig._from_fish_qwen3_omni(S2_PRO_CONFIG)
+    cfg.im_end_id = S2_PRO_IM_END_ID
+    cfg.max_seq_len = 4096  # generate_long refuses prompts longer than max_seq_len - 2048
+    llm = DualARModel.synthetic(cfg, seed=seed, log2_half=5, device=device, precision="bf16", max_slots=1)
+    tdir = tempfile.mkdtemp(prefix="fishmi_tok_", dir="/tmp")
+    llm.tokenizer = FishTokenizer(write_synthetic_tokenizer(tdir, cfg.vocab_size, S2_PRO_IM_END_ID,
+                                                            cfg.semantic_begin_id))
+    ref_frames = int(np.ceil(30.0 * FRAME_RATE))
+    codec = FishMICodec(ccfg, device, "bf16", max_frames=ref_frames)
+    codec.enable_encoder(64, (0, 0, 0, 4))
+    codec.synth(seed + 1)
+    codec.synth_encoder(seed + 1)
+    codec.finalize()
+    n = ref_frames * ccfg.hop
+    t = np.arange(n) / ccfg.sample_rate
+    audio = (0.4 * np.sin(2 * np.pi * 220 * t) * (0.6 + 0.4 * np.sin(2 * np.pi * 3 * t)) +
+             0.05 * np.random.default_rng(seed).standard_normal(n)).astype(np.float32)
+    words = "the quick brown fox jumps over a lazy dog while the river runs past the old mill "
+    text = " ".join(f"<|speaker:{i % 2}|>" + (words * 2)[: 150 + 7 * i] for i in range(turns))
+
+    def run():
+        t0 = time.perf_counter()
+        ptok = codec.encode_audio(audio)
+        firsts, samples, turn_t0 = [], 0, t0
+        for o in E.generate_long(model=llm, text=text, max_new_tokens=frames_per_turn, top_p=0.8, top_k=30,
+                                 temperature=0.8, chunk_length=200, prompt_text=["a thirty second reference"],
+                                 prompt_tokens=[ptok], seed=seed, stream_frames=22, mask_im_end=True):
+            if o.action != "sample":
+                continue
+            if o.stream == 0:
+                codec.stream_reset()
+            pcm = codec.decode_chunk(o.codes)
+            samples += pcm.size
+            now = time.perf_counter()
+            if o.stream == 0:
+                firsts.append(now - turn_t0)  # turn start (previous turn's last PCM) -> first PCM
+            turn_t0 = now
+        return time.perf_counter() - t0, firsts, samples, ptok.shape[1]
+
+    run()  # warm-up: graph capture, tokenizer, allocation
+    wall, firsts, samples, ref_codes = run()
+    llm.close()
+    codec.close()
+    audio_s = samples / ccfg.sample_rate
+    f = np.array(firsts) * 1e3
+    return {"workload": f"BASELINE config 5: voice clone from {n / ccfg.sample_rate:.1f} s of reference audio "
+                        f"({ref_codes} code frames, HIP encode) + {turns} speaker turns x {frames_per_turn} frames "
+                        f"through generate_long (prefix KV reused across turns), codes streamed 22 frames at a "
+                        f"time into the causal streamed vocoder; bf16, synthetic weights + tokenizer",
+            "value": round(audio_s / wall, 3), "unit": "audio-sec/wall-sec", "audio_s": round(audio_s, 2),
+            "wall_s": round(wall, 3), "first_sample_ms": round(float(f[0]), 2),
+            "turn_first_chunk_ms_p50": round(float(np.median(f)), 2),
+            "turn_first_chunk_ms_p90": round(float(np.percentile(f, 90)), 2)}
 
 
 def cpu_baseline(cfg, ccfg, prompt, frames, n_frames, n_codec, seed):
@@ -394,6 +468,8 @@ def main():
     thr = throughput_leg(llm, codec, cfg, args.batch, args.batch_frames, args.waves, sync, dist, world) \
         if args.batch > 0 else None
     enc = encode_leg(ccfg, local, args.encode_seconds, args.seed) if args.encode_seconds > 0 else None
+    longf = longform_leg(ccfg, local, args.longform_turns, args.longform_frames, args.seed) \
+        if args.longform_turns > 0 and rank == 0 else None
 
     copy_gbps = copy_peak_gbps() if rank == 0 else None
     traffic, traffic_note = None, "not measured (--no-pmc or N>1)"
@@ -450,6 +526,7 @@ def main():
                                "frac": round(codec_tflops / BF16_DENSE_TFLOPS, 4)},
             "throughput": thr,
             "encode": enc,
+            "longform": longf,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -1214,6 +1214,16 @@ int fm_llm_prefill(fm_llm* m, int slot, const int32_t* tokens, int T, const fm_s
     });
 }
 
+int fm_llm_prefill_at(fm_llm* m, int slot, const int32_t* suffix, int T, int pos0, const fm_sampling* sp,
+                      int32_t* first_col) {
+    return fm_guard([&] {
+        FMCHECK(m && suffix, "null argument");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        do_prefill(m, slot, suffix, T, sp, first_col, pos0);
+    });
+}
+
 int fm_llm_decode(fm_llm* m, const int32_t* slots, int n, int32_t* cols) {
     return fm_guard([&] {
         FMCHECK(m && slots && n >= 1 && n <= m->max_slots, "bad arguments");

@@ -36,6 +36,10 @@ class GenerateResponse:
     action: Literal["sample", "next"]
     codes: Optional[np.ndarray] = None
     text: Optional[str] = None
+    # streaming (generate_long(stream_frames=K) only): index of this chunk within its text batch.
+    # The chunks of one batch are consecutive code columns of one causal stream: vocode them with
+    # the codec's carried state (FishMICodec.stream_reset at chunk 0, then decode_chunk).
+    stream: Optional[int] = None
 
 
 @dataclass
@@ -67,7 +71,8 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
                   temperature: float = 1.0, compile: bool = False, iterative_prompt: bool = True,
                   chunk_length: int = 512, prompt_text: Optional[Union[str, List[str]]] = None,
                   prompt_tokens=None, seed: Optional[int] = None,
-                  reuse_prefix: bool = True) -> Iterator[GenerateResponse]:
+                  reuse_prefix: bool = True, stream_frames: int = 0,
+                  mask_im_end: bool = False) -> Iterator[GenerateResponse]:
     """inference.py:523-733 on the native model.  `device`, `decode_one_token`, `compile`,
     `iterative_prompt` and `repetition_penalty` are accepted for signature compatibility; like
     the reference, repetition_penalty is not applied (RAS is, inside the sampler).
@@ -77,7 +82,12 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
     the longest prefix its new prompt shares with what the slot already ran (the previous prompt
     plus the columns fed back while generating), and prefills only the rest (fm_llm_generate_at).
     The prompt tokens are the same, so the codes are the same up to the fp32 accumulation order of
-    the reused positions (decode-path vs prefill-path kernels; tests/test_gpu_engine.py)."""
+    the reused positions (decode-path vs prefill-path kernels; tests/test_gpu_engine.py).
+
+    stream_frames > 0 (BASELINE config 5's streamed vocoder): each batch's codes are yielded as they
+    are decoded, `stream_frames` columns at a time (GenerateResponse.stream = chunk index), instead of
+    once per batch; their concatenation equals the batch's codes.  mask_im_end: fixed-length
+    generation for benchmarks (the semantic bias keeps <|im_end|> at -inf)."""
     if not (0 < top_p <= 1):
         raise AssertionError("top_p must be in (0, 1]")
     if not (0 < temperature < 2):
@@ -118,23 +128,58 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
                 n = min(cached.shape[1], enc.shape[1] - 1)  # at least one new position to prefill
                 same = np.all(cached[:, :n] == enc[:, :n], axis=0)
                 L = int(n if same.all() else np.argmin(same))
-            if L > 0:
+            if stream_frames > 0:
+                y, fed_cols = yield from _stream_batch(model, enc, L, max_new_tokens, stream_frames, batch_text,
+                                                       model.sampling(temperature, top_p, top_k, s, mask_im_end))
+            elif L > 0:
                 y = model.generate_at(enc[:, L:], L, max_new_tokens, temperature=temperature, top_p=top_p,
-                                      top_k=top_k, seed=s)
+                                      top_k=top_k, seed=s, mask_im_end=mask_im_end)
             else:
                 y = model.generate(enc, max_new_tokens, temperature=temperature, top_p=top_p, top_k=top_k,
-                                   seed=s)
+                                   seed=s, mask_im_end=mask_im_end)
             if reuse_prefix and hasattr(model, "slot_pos"):
                 fed = model.slot_pos() - enc.shape[1]  # columns fed back while decoding
-                cached = np.concatenate([enc, y[:, :fed]], axis=1)
+                cached = np.concatenate([enc, (fed_cols if stream_frames > 0 else y)[:, :fed]], axis=1)
             codes = np.ascontiguousarray(y[1:, :-1])  # y[1:, prompt_length:-1] of the reference
             if (codes < 0).any():
                 raise AssertionError(f"Negative code found: {codes}")
             dt = time.perf_counter() - t0
             log.info("Batch %d: generated %d frames in %.2fs", batch_idx, y.shape[1], dt)
             conv.append(P.Message(role="assistant", parts=[P.VQPart(codes=codes)], modality="voice"))
-            yield GenerateResponse(action="sample", codes=codes, text=batch_text)
+            if stream_frames <= 0:
+                yield GenerateResponse(action="sample", codes=codes, text=batch_text)
         yield GenerateResponse(action="next")
+
+
+def _stream_batch(model, enc, L, max_new_tokens, stream_frames, text, sp):
+    """One generate() of generate_long, decoded `stream_frames` frames at a time (prefill, then
+    decode_frames chunks on slot 0): yields the confirmed code columns of each chunk, returns
+    (y (C+1, n) as generate() would, every column fed back to the model)."""
+    T = enc.shape[1]
+    mx = max_new_tokens if (max_new_tokens and T + max_new_tokens <= model.cfg.max_seq_len) \
+        else model.cfg.max_seq_len - T
+    im_end = model.cfg.im_end_id
+    cols = [model.prefill(0, enc[:, L:], sp, pos0=L)]
+    fed = []
+    done = cols[0][0] == im_end or mx <= 1
+    emitted, chunk = 0, 0
+    while not done:
+        k = min(stream_frames, mx - len(cols))
+        out = model.decode_frames([0], k)[:, 0, :]
+        fed.extend([cols[-1]] + list(out[:-1]))  # frame j feeds the column sampled before it
+        for c in out:
+            cols.append(c)
+            if c[0] == im_end or len(cols) >= mx:
+                done = True
+                break
+        # every column but the newest is final (the newest may be the batch's dropped last column)
+        if len(cols) - 1 > emitted:
+            part = np.stack(cols[emitted:len(cols) - 1], axis=1)[1:]
+            yield GenerateResponse(action="sample", codes=np.ascontiguousarray(part), text=text, stream=chunk)
+            emitted, chunk = len(cols) - 1, chunk + 1
+    y = np.stack(cols, axis=1)
+    fed_cols = np.stack(fed, axis=1) if fed else y[:, :0]
+    return y, fed_cols
 
 
 def _device_index(device) -> int:

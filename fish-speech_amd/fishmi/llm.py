@@ -136,12 +136,18 @@ class DualARModel:
         return native.SamplingC(float(temperature), float(top_p), int(top_k), int(seed) & (2**64 - 1),
                                 int(bool(mask_im_end)))
 
-    def prefill(self, slot: int, prompt: np.ndarray, sampling) -> np.ndarray:
+    def prefill(self, slot: int, prompt: np.ndarray, sampling, pos0: int = 0) -> np.ndarray:
+        """Prefill `prompt` into `slot` (pos0 > 0: after the slot's cached positions [0, pos0),
+        fm_llm_prefill_at); returns the first emitted column (C+1,)."""
         p = np.ascontiguousarray(prompt, dtype=np.int32)
         assert p.shape[0] == self.C1
         col = np.zeros(self.C1, np.int32)
-        native.check(native.lib().fm_llm_prefill(self.h, slot, native.i32p(p), p.shape[1],
-                                                 ctypes.byref(sampling), native.i32p(col)))
+        if pos0:
+            native.check(native.lib().fm_llm_prefill_at(self.h, slot, native.i32p(p), p.shape[1], int(pos0),
+                                                        ctypes.byref(sampling), native.i32p(col)))
+        else:
+            native.check(native.lib().fm_llm_prefill(self.h, slot, native.i32p(p), p.shape[1],
+                                                     ctypes.byref(sampling), native.i32p(col)))
         return col
 
     def decode(self, slots) -> np.ndarray:

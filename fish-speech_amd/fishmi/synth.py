@@ -97,3 +97,41 @@ def codec_rule(name: str) -> tuple[float, int]:
     if "codebook.weight" in name:
         return 0.0, 0          # codebook vectors in [-1, 1)
     return 0.0, 5
+
+
+def write_synthetic_tokenizer(path: str, vocab_size: int, im_end_id: int, semantic_begin_id: int,
+                              n_semantic: int = 4096) -> str:
+    """A tokenizer.json for synthetic-weight runs at a real model's vocabulary layout (there is no
+    checkpoint tokenizer on the box): single characters at low ids, <|im_end|> and the other chat
+    specials just below the semantic range (Qwen-style), <|semantic:i|> at semantic_begin_id + i, the
+    rest reserved.  Returns the directory (FishTokenizer(path) loads it)."""
+    import json
+    import os
+
+    from tokenizers import AddedToken, Regex, Tokenizer, models, pre_tokenizers
+
+    specials = {"<|endoftext|>": im_end_id - 2, "<|im_start|>": im_end_id - 1, "<|im_end|>": im_end_id,
+                "<|text|>": im_end_id + 1, "<|voice|>": im_end_id + 2, "<|interleave|>": im_end_id + 3,
+                "<|audio_start|>": im_end_id + 4, "<|audio_end|>": im_end_id + 5, "<|audio_pad|>": im_end_id + 6}
+    for i in range(5):
+        specials[f"<|speaker:{i}|>"] = im_end_id + 10 + i
+    assert max(specials.values()) < semantic_begin_id and semantic_begin_id + n_semantic <= vocab_size
+    chars = [chr(c) for c in range(32, 127)] + ["\n"]
+    vocab = {ch: 16 + i for i, ch in enumerate(chars)}
+    vocab["[UNK]"] = 15
+    vocab.update(specials)
+    sem = [f"<|semantic:{i}|>" for i in range(n_semantic)]
+    for i, t in enumerate(sem):
+        vocab[t] = semantic_begin_id + i
+    used = set(vocab.values())
+    for i in range(vocab_size):
+        if i not in used:
+            vocab[f"<|reserved_{i}|>"] = i
+    tk = Tokenizer(models.WordLevel(vocab=vocab, unk_token="[UNK]"))
+    tk.pre_tokenizer = pre_tokenizers.Split(Regex("."), behavior="isolated")
+    tk.add_special_tokens([AddedToken(t, special=True, normalized=False) for t in list(specials) + sem])
+    os.makedirs(path, exist_ok=True)
+    tk.save(os.path.join(path, "tokenizer.json"))
+    with open(os.path.join(path, "tokenizer_config.json"), "w") as f:
+        json.dump({"tokenizer_class": "PreTrainedTokenizerFast", "eos_token": "<|endoftext|>"}, f)
+    return path

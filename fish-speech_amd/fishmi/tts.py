@@ -153,7 +153,7 @@ class TTSInferenceEngine:
     decoder_model: a FishMICodec (its encoder enabled for voice-clone references)."""
 
     def __init__(self, llama_queue: "queue.Queue", decoder_model, precision="bf16", compile: bool = False,
-                 references_dir: str = "references"):
+                 references_dir: str = "references", stream_frames: int = 22):
         self.llama_queue = llama_queue
         self.decoder_model = decoder_model
         self.precision = precision
@@ -162,6 +162,9 @@ class TTSInferenceEngine:
         self.ref_by_id: dict = {}
         self.ref_by_hash: dict = {}
         self._codec_lock = threading.Lock()  # one codec handle, called from request threads
+        # streaming requests with latency="balanced": codes arrive `stream_frames` columns at a time
+        # (generate_long(stream_frames=...)) and are vocoded as one causal stream per text batch
+        self.stream_frames = stream_frames
 
     # ---- references (reference_loader.py) -------------------------------------------------
     def encode_reference(self, reference_audio: bytes, enable_reference_audio: bool = True):
@@ -216,6 +219,8 @@ class TTSInferenceEngine:
                        chunk_length=req.chunk_length, prompt_tokens=prompt_tokens, prompt_text=prompt_texts)
         if req.seed is not None:
             request["seed"] = int(req.seed)
+        if req.streaming and req.latency == "balanced" and self.stream_frames > 0:
+            request["stream_frames"] = self.stream_frames
         rq: "queue.Queue" = queue.Queue()
         self.llama_queue.put(GenerateRequest(request=request, response_queue=rq))
         return rq
@@ -228,6 +233,11 @@ class TTSInferenceEngine:
             return self.decoder_model.decode_codes(c)
 
     def get_audio_segment(self, result: GenerateResponse) -> np.ndarray:
+        if result.stream is not None:  # a chunk of one batch's causal stream: carried codec state
+            with self._codec_lock:
+                if result.stream == 0:
+                    self.decoder_model.stream_reset()
+                return np.asarray(self.decoder_model.decode_chunk(np.asarray(result.codes)), np.float32)
         return np.asarray(self.decode_vq_tokens(result.codes), np.float32)
 
     # ---- main entry (inference_engine/__init__.py:41-131) -----------------------------------

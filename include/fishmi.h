@@ -111,6 +111,9 @@ int fm_llm_generate(fm_llm* h, int slot, const int32_t* prompt, int T, int max_n
    prefix.  pos0 must not exceed fm_llm_slot_pos. */
 int fm_llm_generate_at(fm_llm* h, int slot, const int32_t* suffix, int T, int pos0, int max_new,
                        const fm_sampling* sp, int32_t* out, int* n_out);
+/* fm_llm_prefill continuing the slot's cached positions [0, pos0): the suffix runs at pos0 .. */
+int fm_llm_prefill_at(fm_llm* h, int slot, const int32_t* suffix, int T, int pos0, const fm_sampling* sp,
+                      int32_t* first_col);
 /* positions of the slot whose KV is written (prompt + fed columns of its last generate) */
 int fm_llm_slot_pos(fm_llm* h, int slot, int* pos);
 /* teacher forcing for parity: run S positions of x ((C+1) x S) from pos0 on slot (pos0 == 0

@@ -115,3 +115,40 @@ def test_tts_engine_and_http_stream(golden, tmp_path):
     pcm = np.frombuffer(r.content[len(hdr):], "<i2")
     np.testing.assert_array_equal(pcm, np.concatenate([(s * 32768).astype(np.int16) for s in segs]))
     q.put(None)
+
+
+def test_streamed_generation_and_vocoding(golden, tmp_path):
+    """generate_long(stream_frames=K) yields each batch's codes K columns at a time; their
+    concatenation equals the batch's codes from the one-shot flow (same seed), and the engine's
+    latency="balanced" stream vocodes them as one causal stream: the PCM equals the one-shot decode
+    of the batch's codes (the codec is causal end to end)."""
+    from fishmi import engine as E
+    from fishmi.llm import DualARModel
+    from fishmi.tts import ServeTTSRequest, TTSInferenceEngine
+
+    m = DualARModel.from_pretrained(_ckpt(tmp_path), device=0, precision="bf16", max_length=2560)
+    kw = dict(model=m, text="<|speaker:0|>Streaming turn one, long enough to fill most of a batch by itself. "
+                             "<|speaker:1|>Streaming turn two, which has to land in a second text batch.",
+              max_new_tokens=23, top_p=0.8, temperature=0.8, chunk_length=100, seed=7)
+    whole = [o for o in E.generate_long(**kw) if o.action == "sample"]
+    chunks = [o for o in E.generate_long(stream_frames=5, **kw) if o.action == "sample"]
+    assert all(c.stream is not None for c in chunks) and max(c.codes.shape[1] for c in chunks) <= 5
+    per_batch, cur = [], None
+    for c in chunks:
+        if c.stream == 0:
+            cur = []
+            per_batch.append(cur)
+        cur.append(c.codes)
+    assert len(per_batch) == len(whole) == 2
+    for w, parts in zip(whole, per_batch):
+        np.testing.assert_array_equal(np.concatenate(parts, axis=1), w.codes)
+    codec = _codec(golden)
+    q = E.launch_thread_safe_queue(None, 0, "bf16", model=m)
+    eng = TTSInferenceEngine(q, codec, stream_frames=5)
+    res = list(eng.inference(ServeTTSRequest(text=kw["text"], max_new_tokens=23, chunk_length=100, seed=7,
+                                             streaming=True, latency="balanced")))
+    segs = [r.audio[1] for r in res if r.code == "segment"]
+    assert len(segs) == len(chunks)
+    np.testing.assert_array_equal(np.concatenate(segs),
+                                  np.concatenate([codec.decode_codes(w.codes) for w in whole]))
+    q.put(None)
