@@ -216,7 +216,7 @@ def longform_leg(ccfg, device, turns, frames_per_turn, seed):
 
     cfg = DualARConfig._from_fish_qwen3_omni(S2_PRO_CONFIG)
     cfg.im_end_id = S2_PRO_IM_END_ID
-    cfg.max_seq_len = 4096  # generate_long refuses prompts longer than max_seq_len - 2048
+    cfg.max_seq_len = 5120  # generate_long refuses prompts longer than max_seq_len - 2048
     llm = DualARModel.synthetic(cfg, seed=seed, log2_half=5, device=device, precision="bf16", max_slots=1)
     tdir = tempfile.mkdtemp(prefix="fishmi_tok_", dir="/tmp")
     llm.tokenizer = FishTokenizer(write_synthetic_tokenizer(tdir, cfg.vocab_size, S2_PRO_IM_END_ID,
