@@ -663,7 +663,7 @@ template <typename T>
 __global__ __launch_bounds__(64) void fast_attn2_kernel(FastFusedArgs<T> a) {
     unsigned long long tz[7] = {0, 0, 0, 0, 0, 0, 0};
     DBG_TS(tz, 0)
-    fast_attn_head<T, false>(a, blockIdx.x, blockIdx.y, threadIdx.x, tz);
+    fast_attn_head<T>(a, blockIdx.x, blockIdx.y, threadIdx.x, tz);
     if (a.dbg && threadIdx.x == 0) {
         tz[4] = __builtin_amdgcn_s_memrealtime();
         dbg_record(a.dbg, 0xFFFE, (unsigned)a.cpos, tz);

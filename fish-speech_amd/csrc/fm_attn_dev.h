@@ -1,42 +1,30 @@
-// Device-side fast-model attention for one (row, q head), shared by the standalone
-// fast_attn2_kernel (fm_attn.hip) and the fused tail of the QKV GEMV (fm_gemv.hip, EPI_QKVATT).
+// Device-side fast-model attention: one (row, q head) per wave for fast_attn2_kernel (fm_attn.hip),
+// and the LDS-staged form the Wo GEMV's PRO_FATT prologue runs (fm_gemv.hip).
 //
 // Fast-model attention at codebook position cpos (llama.py:947-975), every rounding of the
 // reference's matmul-softmax-matmul kept: ONE wave per q head, no LDS, no barrier.  Lane l owns
 // dimension pairs l, l+64 (RoPE pairs).  Each wave recomputes the new k (qk-norm + RoPE, cheap) so
 // waves never wait on each other; the first q head of each kv group writes k/v of cpos to the fast
-// cache.  COH: read the raw q/k/v projections with agent-coherent (write-through-visible) loads --
-// the fused tail reads rows other workgroups of the same launch have just written.
+// cache.
 #pragma once
 #include "fm_common.h"
 #include "fm_kernels.h"
 
 constexpr int FAST_ATTN_MAXJ = 16;  // cached rows a wave keeps in registers (cpos < 16)
 
-// (p[0], p[1]) as floats; COH: one agent-scope relaxed load per 32-bit word (sc1, bypasses the
-// non-coherent per-XCD L2 lines another XCD may hold)
-template <typename T, bool COH>
-__device__ __forceinline__ void ld_pair(const T* p, float& x0, float& x1) {
+// (p[0], p[1]) as floats
+template <typename T> __device__ __forceinline__ void ld_pair(const T* p, float& x0, float& x1) {
     if constexpr (sizeof(T) == 2) {
-        uint32_t w;
-        if constexpr (COH)
-            w = __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-            w = *reinterpret_cast<const uint32_t*>(p);
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
         x0 = __uint_as_float(w << 16);
         x1 = __uint_as_float(w & 0xffff0000u);
     } else {
-        if constexpr (COH) {
-            x0 = __hip_atomic_load(reinterpret_cast<const float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            x1 = __hip_atomic_load(reinterpret_cast<const float*>(p) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            x0 = ld(p, 0);
-            x1 = ld(p, 1);
-        }
+        x0 = ld(p, 0);
+        x1 = ld(p, 1);
     }
 }
 
-template <typename T, bool COH>
+template <typename T>
 __device__ __forceinline__ void fast_attn_head(const FastFusedArgs<T>& a, int r, int h, int lane,
                                                unsigned long long (&tz)[7]) {
     const int hd = a.hd, g = a.nh / a.nkv, kvh = h / g, cpos = a.cpos, half = hd >> 1;
@@ -49,9 +37,9 @@ __device__ __forceinline__ void fast_attn_head(const FastFusedArgs<T>& a, int r,
         const int p = lane + 64 * u;
         const bool ok = p < half;
         const int pp = ok ? p : 0;
-        ld_pair<T, COH>(raw + (size_t)h * hd + 2 * pp, q0[u], q1[u]);
-        ld_pair<T, COH>(raw + (size_t)(a.nh + kvh) * hd + 2 * pp, k0[u], k1[u]);
-        ld_pair<T, COH>(raw + (size_t)(a.nh + a.nkv + kvh) * hd + 2 * pp, v0[u], v1[u]);
+        ld_pair<T>(raw + (size_t)h * hd + 2 * pp, q0[u], q1[u]);
+        ld_pair<T>(raw + (size_t)(a.nh + kvh) * hd + 2 * pp, k0[u], k1[u]);
+        ld_pair<T>(raw + (size_t)(a.nh + a.nkv + kvh) * hd + 2 * pp, v0[u], v1[u]);
         qw0[u] = a.qk_norm ? ld(a.qn, 2 * pp) : 1.f;
         qw1[u] = a.qk_norm ? ld(a.qn, 2 * pp + 1) : 1.f;
         kw0[u] = a.qk_norm ? ld(a.kn, 2 * pp) : 1.f;
@@ -72,8 +60,8 @@ __device__ __forceinline__ void fast_attn_head(const FastFusedArgs<T>& a, int r,
             for (int u = 0; u < 2; ++u) {
                 const int p = lane + 64 * u;
                 const int pp = p < half ? p : 0;
-                ld_pair<T, false>(kc + (size_t)j * hd + 2 * pp, K0[j][u], K1[j][u]);
-                ld_pair<T, false>(vc + (size_t)j * hd + 2 * pp, V0[j][u], V1[j][u]);
+                ld_pair<T>(kc + (size_t)j * hd + 2 * pp, K0[j][u], K1[j][u]);
+                ld_pair<T>(vc + (size_t)j * hd + 2 * pp, V0[j][u], V1[j][u]);
                 if (p >= half) K0[j][u] = K1[j][u] = V0[j][u] = V1[j][u] = 0.f;
             }
         }

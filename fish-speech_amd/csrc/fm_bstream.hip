@@ -23,52 +23,9 @@
 // Weights use the packed fragment layout of fm_kernels.h, shared with the batch-1 GEMV.
 #include "fm_kernels.h"
 #include "fm_runtime.h"
+#include "fm_frag.h"
 
 namespace {
-
-template <typename T> struct BsFrag;
-template <> struct BsFrag<bf16_t> {
-    typedef u32x4_t f;
-    static __device__ __forceinline__ f load_w(const bf16_t* blk, int lane) {
-        return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(blk + lane * 8));
-    }
-    static __device__ __forceinline__ f load_x(const bf16_t* p) { return *reinterpret_cast<const u32x4_t*>(p); }
-    static __device__ __forceinline__ f zero() { return (u32x4_t){0, 0, 0, 0}; }
-    static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
-                                                       __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
-    }
-};
-template <> struct BsFrag<float> {
-    struct f {
-        f32x4_t lo, hi;
-    };
-    static __device__ __forceinline__ f load_w(const float* blk, int lane) {
-        f v;
-        v.lo = *reinterpret_cast<const f32x4_t*>(blk + lane * 4);
-        v.hi = *reinterpret_cast<const f32x4_t*>(blk + 256 + lane * 4);
-        return v;
-    }
-    static __device__ __forceinline__ f load_x(const float* p) {
-        f v;
-        v.lo = *reinterpret_cast<const f32x4_t*>(p);
-        v.hi = *reinterpret_cast<const f32x4_t*>(p + 4);
-        return v;
-    }
-    static __device__ __forceinline__ f zero() {
-        f v;
-        v.lo = v.hi = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-        return v;
-    }
-    // lane l holds k = 8*(l>>4) + j of a 32-wide k block; MFMA j covers {8g + j}: exact f32
-    static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[j], b.lo[j], c, 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[j], b.hi[j], c, 0, 0, 0);
-        return c;
-    }
-};
 
 constexpr int BS_MAXW = 16;  // waves per block
 
@@ -76,7 +33,7 @@ __device__ __forceinline__ float silu_b(float a) { return a / (1.0f + expf(-a));
 
 template <typename T, int SPW, int TPI, int EPI>
 __global__ __launch_bounds__(BS_MAXW * 64) void bstream_kernel(BstreamArgs<T> a) {
-    using F = BsFrag<T>;
+    using F = Frag<T>;
     __shared__ f32x4_t red[2][BS_MAXW][2][64];
     constexpr int U = SPW * TPI;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
@@ -96,8 +53,8 @@ __global__ __launch_bounds__(BS_MAXW * 64) void bstream_kernel(BstreamArgs<T> a)
         for (int j = 0; j < SPW; ++j) {
             const int jj = j < nst ? j : nst - 1;
             const size_t k = (size_t)(wa + jj) * 32 + 8 * g;
-            xa[j] = F::load_x(a.X + (size_t)ra * a.ldx + k);
-            xb[j] = F::load_x(a.X + (size_t)rb * a.ldx + k);
+            xa[j] = F::load(a.X + (size_t)ra * a.ldx + k);
+            xb[j] = F::load(a.X + (size_t)rb * a.ldx + k);
             if (j >= nst || r >= a.R) xa[j] = F::zero();
             if (j >= nst || 16 + r >= a.R) xb[j] = F::zero();
         }
@@ -110,7 +67,7 @@ __global__ __launch_bounds__(BS_MAXW * 64) void bstream_kernel(BstreamArgs<T> a)
     auto issue = [&](int f, int u) {
         f = f < flast ? f : flast;
         const int t = f / SPW, j = f - t * SPW;
-        fa[u] = F::load_w(wbase + ((size_t)t * S + (j < nst ? j : nst - 1)) * 512, lane);
+        fa[u] = F::template load_w<true>(wbase + ((size_t)t * S + (j < nst ? j : nst - 1)) * 512, lane);
     };
 #pragma unroll
     for (int u = 0; u < U; ++u) issue(u, u);

@@ -16,51 +16,7 @@
 
 #include "fm_codec.h"
 #include "fm_runtime.h"
-
-template <typename T> struct CF;
-template <> struct CF<bf16_t> {
-    typedef u32x4_t f;
-    static __device__ __forceinline__ f wload(const bf16_t* blk, int lane) {
-        return *reinterpret_cast<const u32x4_t*>(blk + lane * 8);
-    }
-    static __device__ __forceinline__ f xload(const bf16_t* p, bool valid) {
-        u32x4_t v = *reinterpret_cast<const u32x4_t*>(p);
-        const uint32_t m = valid ? 0xffffffffu : 0u;
-        return (u32x4_t){v[0] & m, v[1] & m, v[2] & m, v[3] & m};
-    }
-    static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
-                                                       __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
-    }
-};
-template <> struct CF<float> {
-    struct f {
-        f32x4_t lo, hi;
-    };
-    static __device__ __forceinline__ f wload(const float* blk, int lane) {
-        f v;
-        v.lo = *reinterpret_cast<const f32x4_t*>(blk + lane * 4);
-        v.hi = *reinterpret_cast<const f32x4_t*>(blk + 256 + lane * 4);
-        return v;
-    }
-    static __device__ __forceinline__ f xload(const float* p, bool valid) {
-        f v;
-        v.lo = *reinterpret_cast<const f32x4_t*>(p);
-        v.hi = *reinterpret_cast<const f32x4_t*>(p + 4);
-        if (!valid) {
-            v.lo = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-            v.hi = v.lo;
-        }
-        return v;
-    }
-    static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[j], b.lo[j], c, 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[j], b.hi[j], c, 0, 0, 0);
-        return c;
-    }
-};
+#include "fm_frag.h"
 
 __device__ __forceinline__ float snake_f(float y, float al) {
     const float s = sinf(al * y);
@@ -70,7 +26,7 @@ __device__ __forceinline__ float snake_f(float y, float al) {
 // block = 4 waves, block tile 64 time x 64 channels, wave tile 32 x 32 (2x2 MFMA 16x16x32)
 template <typename T>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
-    using F = CF<T>;
+    using F = Frag<T>;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int tq0 = blockIdx.x * 64 + (wave & 1) * 32;
     const int co0 = blockIdx.y * 64 + (wave >> 1) * 32;
@@ -96,15 +52,15 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
         tap = kin ? tap : a.ntaps - 1;
         const int ci0 = kin ? kl - tap * a.Ci : 0;
         const int sh = a.shift[tap];
-        typename F::f fa0 = F::wload(wb + ((size_t)ct0 * S + s) * 512, lane);
-        typename F::f fa1 = F::wload(wb + ((size_t)(c1 ? ct0 + 1 : ct0) * S + s) * 512, lane);
+        typename F::f fa0 = F::load_w(wb + ((size_t)ct0 * S + s) * 512, lane);
+        typename F::f fa1 = F::load_w(wb + ((size_t)(c1 ? ct0 + 1 : ct0) * S + s) * 512, lane);
         typename F::f fb[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int row = tq[u] - sh;
             const bool valid = kin && row >= a.lo && row < a.Lx;
             const int rc = row < a.lo ? a.lo : (row >= a.Lx ? a.Lx - 1 : row);
-            fb[u] = F::xload(a.x + (ptrdiff_t)rc * a.ldx + ci0, valid);
+            fb[u] = F::load_masked(a.x + (ptrdiff_t)rc * a.ldx + ci0, valid);
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {

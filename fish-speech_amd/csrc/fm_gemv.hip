@@ -20,45 +20,7 @@
 #include "fm_kernels.h"
 #include "fm_runtime.h"
 #include "fm_attn_dev.h"
-
-template <typename T> struct GFrag;
-template <> struct GFrag<bf16_t> {
-    typedef u32x4_t f;
-    template <bool NT> static __device__ __forceinline__ f load_w(const bf16_t* blk, int lane) {
-        const u32x4_t* p = reinterpret_cast<const u32x4_t*>(blk + lane * 8);
-        if constexpr (NT) return __builtin_nontemporal_load(p);
-        else return *p;
-    }
-    static __device__ __forceinline__ f load_lds(const bf16_t* p) { return *reinterpret_cast<const u32x4_t*>(p); }
-    static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
-                                                       __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
-    }
-};
-template <> struct GFrag<float> {
-    struct f {
-        f32x4_t lo, hi;
-    };
-    template <bool NT> static __device__ __forceinline__ f load_w(const float* blk, int lane) {
-        f v;
-        v.lo = *reinterpret_cast<const f32x4_t*>(blk + lane * 4);
-        v.hi = *reinterpret_cast<const f32x4_t*>(blk + 256 + lane * 4);
-        return v;
-    }
-    static __device__ __forceinline__ f load_lds(const float* p) {
-        f v;
-        v.lo = *reinterpret_cast<const f32x4_t*>(p);
-        v.hi = *reinterpret_cast<const f32x4_t*>(p + 4);
-        return v;
-    }
-    static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[j], b.lo[j], c, 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[j], b.hi[j], c, 0, 0, 0);
-        return c;
-    }
-};
+#include "fm_frag.h"
 
 __device__ __forceinline__ float silu_g(float a) { return a / (1.0f + expf(-a)); }
 
@@ -102,7 +64,7 @@ void gemv_kernel(GemvArgs<T> a) {
     // row per stream (2 items per thread at R = 1), and its register budget is what lets the
     // 1216-block W1||W3 grid stay resident (5 waves per SIMD)
     constexpr int PRE_N = PRO == PRO_PRENORM ? 3 : GEMV_PRE;
-    using G = GFrag<T>;
+    using G = Frag<T>;
     constexpr int NACC = (EPI == EPI_SWIGLU) ? 2 : 1;
     constexpr int NTH = WPB * 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -355,7 +317,7 @@ void gemv_kernel(GemvArgs<T> a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (i + u < nmy) {
-                const typename G::f xb = G::load_lds(xp + (size_t)(i + u) * 32);
+                const typename G::f xb = G::load(xp + (size_t)(i + u) * 32);
                 acc0 = G::mma(fa[u], xb, acc0);
                 if constexpr (NACC == 2) acc1 = G::mma(fb[u], xb, acc1);
             }
@@ -435,16 +397,6 @@ void gemv_kernel(GemvArgs<T> a) {
             const size_t yi = (size_t)col * a.ldy + n;
             if constexpr (EPI == EPI_STORE) {
                 st(a.Y, yi, v0);
-            } else if constexpr (EPI == EPI_QKVATT) {  // write-through: read back by another block
-                if constexpr (sizeof(T) == 2) {
-                    const float rv = rnd<T>(v0);
-                    __hip_atomic_store(reinterpret_cast<unsigned short*>(a.Y) + yi,
-                                       (unsigned short)(__float_as_uint(rv) >> 16), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    __hip_atomic_store(reinterpret_cast<float*>(a.Y) + yi, v0, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
             } else if constexpr (EPI == EPI_SWIGLU) {
                 const float ga = rnd<T>(v0), ub = rnd<T>(v1);
                 st(a.Y, yi, rnd<T>(silu_g(ga)) * ub);
@@ -452,36 +404,6 @@ void gemv_kernel(GemvArgs<T> a) {
                 a.Yf[yi] = rnd<T>(v0);
             }
         }
-    }
-    if constexpr (EPI == EPI_QKVATT) {
-        // Ticket on the tile's kv group (its q heads, k head and v head rows); the group's last
-        // block runs the group's fast-model attention, one wave per (row, q head).  Hand-off in the
-        // write-through form: sc1 stores drained by every wave, relaxed agent ticket, sc1 loads of
-        // the raw projections in fast_attn_head<T, true>.
-        const FastFusedArgs<T>& at = a.att;
-        const int hd = at.hd, g = at.nh / at.nkv, qr = at.nh * hd, kr = at.nkv * hd;
-        const int grp = n0 < qr ? n0 / (g * hd) : (n0 < qr + kr ? (n0 - qr) / hd : (n0 - qr - kr) / hd);
-        const int need = (g + 2) * hd / 16;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const int t = __hip_atomic_fetch_add(a.att_tickets + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int last = t == need - 1;
-            if (last) __hip_atomic_store(a.att_tickets + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            flag[0] = last;
-        }
-        __syncthreads();
-        if (flag[0]) {
-            unsigned long long tz[7] = {0, 0, 0, 0, 0, 0, 0};
-            if (a.dbg) tz[0] = __builtin_amdgcn_s_memrealtime();
-            for (int it = wave; it < R * g; it += WPB) fast_attn_head<T, true>(at, it / g, grp * g + it % g, lane, tz);
-            if (a.dbg && lane == 0) {
-                tz[4] = __builtin_amdgcn_s_memrealtime();
-                dbg_record(a.dbg, 0xFFFC, (unsigned)at.cpos, tz);
-            }
-        }
-        stamp();
-        return;
     }
     if constexpr (EPI == EPI_SLABFIN) {
         // The last-arriving K-slice block of this 16-column tile finalises the residual stream:
@@ -590,375 +512,10 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
     GO(PRO_PLAIN, EPI_STORE) GO(PRO_PLAIN, EPI_SLABFIN) GO(PRO_PLAIN, EPI_F32) GO(PRO_PLAIN, EPI_SLAB)
     GO(PRO_NORM, EPI_STORE) GO(PRO_NORM, EPI_SWIGLU) GO(PRO_NORM, EPI_F32)
     GO(PRO_PRENORM, EPI_STORE) GO(PRO_PRENORM, EPI_SWIGLU) GO(PRO_PRENORM, EPI_F32)
-    GO(PRO_NORM, EPI_QKVATT) GO(PRO_PRENORM, EPI_QKVATT) GO(PRO_PRENORM, EPI_SWIGLU8)
+    GO(PRO_PRENORM, EPI_SWIGLU8)
     GO(PRO_FATT, EPI_SLABFIN)
 #undef GO
 }
 
 template void launch_gemv<bf16_t>(hipStream_t, const GemvArgs<bf16_t>&, int, int, int);
 template void launch_gemv<float>(hipStream_t, const GemvArgs<float>&, int, int, int);
-
-// =============================================================================================
-// Stream-K decode GEMV.  grid = (CUs x bpc) persistent blocks of 8 waves.  The fragment space of
-// the packed weight ([tile][k-step] x 1 KiB, one contiguous HBM stream) is cut into equal
-// contiguous runs, one per wave: u in [gw*U/W, (gw+1)*U/W).  Every block stages the whole
-// X' (all K) once; a wave keeps one accumulator per tile it touches (at most two when a run is
-// shorter than a tile), writes each as a write-through (sc1) partial after its run, drains,
-// and takes a ticket on the tile; the tile's last contributor combines the partials in
-// contributor order (deterministic) and applies the epilogue.  No cross-block barrier, no
-// fence (cdna_hip_programming.md §5 split-K recipe, write-through form).
-// =============================================================================================
-__host__ __device__ inline int sk_first_wave(long long x, int Wact, long long Utot) {
-    return (int)(((x + 1) * Wact - 1) / Utot);  // max gw with floor(gw * Utot / Wact) <= x
-}
-
-template <typename T, int PRO, int EPI, bool NT, int U>
-__global__ __launch_bounds__(512) void gemv_sk_kernel(GemvArgs<T> a) {
-    using G = GFrag<T>;
-    constexpr int WPB = 8, NTH = 512;
-    constexpr int NACC = (EPI == EPI_SWIGLU) ? 2 : 1;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int R = a.R, K = a.K, S = K >> 5;
-    const int ntile = (a.N + 15) >> 4;
-    const int xstride = K + 8;
-    T* xs = reinterpret_cast<T*>(smem);
-    float* ssq = reinterpret_cast<float*>(smem + (size_t)R * xstride * sizeof(T));  // [WPB][16*R]
-    float* rsl = ssq + WPB * 16 * GEMV_RMAX;                                        // [WPB][GEMV_RMAX]
-    const unsigned long long ts0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    unsigned long long tsa = 0, tsb = 0, tsc = 0;
-
-    const long long Utot = (long long)ntile * S;
-    const int Wact = (int)(Utot < (long long)gridDim.x * WPB ? Utot : (long long)gridDim.x * WPB);
-    const int gw = blockIdx.x * WPB + wave;
-    const bool active = gw < Wact;
-    const int u0 = active ? (int)((long long)gw * Utot / Wact) : 0;
-    const int u1 = active ? (int)((long long)(gw + 1) * Utot / Wact) : 0;
-    const int ulast = u1 > u0 ? u1 - 1 : 0;
-    const int r = lane & 15, g = lane >> 4;
-    typename G::f fa[U], fb[NACC == 2 ? U : 1];
-    auto issue = [&](int i, int u) {  // branch-free ring (see gemv_kernel)
-        const int uj = u0 + i < ulast ? u0 + i : ulast;
-        fa[u] = G::template load_w<NT>(a.W + (size_t)uj * 512, lane);
-        if constexpr (NACC == 2) fb[u] = G::template load_w<NT>(a.W2 + (size_t)uj * 512, lane);
-    };
-
-    // ---------------- prologue: X'[r][0 .. K) -> LDS, once per block -------------------------------
-    if constexpr (PRO == PRO_NORM) {
-        __shared__ float red_s[16];
-        const int nch = K >> 3;
-        const bool writer = blockIdx.x == 0;
-        for (int rr = 0; rr < R; ++rr) {
-            const int xi = a.xidx ? a.xidx[(size_t)rr * a.xidx_ld + a.xidx_col] : rr;
-            const T* xr = a.X + (size_t)xi * a.ldx;
-            float xv[4][8], wv[4][8];
-            float ss = 0.f;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int c = threadIdx.x + NTH * j;
-                if (c < nch) {
-                    load8(a.nw + 8 * c, wv[j]);
-                    load8(xr + 8 * c, xv[j]);
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) ss += xv[j][u] * xv[j][u];
-                }
-            }
-            ss = block_sum(ss, red_s);
-            const float rs = 1.0f / sqrtf(ss / (float)K + a.eps);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int c = threadIdx.x + NTH * j;
-                if (c >= nch) continue;
-                float xn[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) xn[u] = rnd<T>(rnd<T>(xv[j][u] * rs) * wv[j][u]);
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    st(xs, (size_t)rr * xstride + 8 * c + u, xn[u]);
-                    if (writer && a.xn_out) st(a.xn_out, (size_t)rr * a.ldxo + 8 * c + u, xn[u]);
-                }
-            }
-            __syncthreads();
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) issue(u, u);
-    } else {
-        const int nch = K >> 3, nitem = R * nch;
-        C8<T> xc[GEMV_PRE], wc[PRO == PRO_PRENORM ? GEMV_PRE : 1];
-#pragma unroll
-        for (int q = 0; q < GEMV_PRE; ++q) {
-            const int it = threadIdx.x + NTH * q;
-            if (it < nitem) {
-                const int rr = it / nch, cc = it - rr * nch;
-                xc[q] = load_c8(a.X + (size_t)rr * a.ldx + 8 * cc);
-                if constexpr (PRO == PRO_PRENORM) {
-                    if (!(a.pro_exp & 2)) wc[q] = load_c8(a.nw + 8 * cc);
-                    else wc[q] = xc[q];
-                }
-            }
-        }
-        float ssl[GEMV_RMAX];
-        if constexpr (PRO == PRO_PRENORM) {
-            const int nt = K >> 4;  // K <= 4096 (host)
-#pragma unroll
-            for (int rr = 0; rr < GEMV_RMAX; ++rr) {
-                ssl[rr] = 0.f;
-                if (rr < R && (a.pro_exp & 1)) ssl[rr] = (float)K / 64.0f;  // EXPERIMENT: no loads, rs ~ 1
-                if (rr < R && !(a.pro_exp & 1)) {
-                    float v[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int t = lane + 64 * j;
-                        v[j] = a.ss_in[(size_t)(t < nt ? t : nt - 1) * R + rr];
-                    }
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) ssl[rr] += (lane + 64 * j < nt) ? v[j] : 0.f;
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) issue(u, u);
-        tsa = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (PRO == PRO_PRENORM && (a.pro_exp & 4)) {  // EXPERIMENT: stage raw x (no normalise)
-#pragma unroll
-            for (int q = 0; q < GEMV_PRE; ++q) {
-                const int it = threadIdx.x + NTH * q;
-                if (it < nitem) {
-                    const int rr = it / nch, cc = it - rr * nch;
-                    *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) = xc[q];
-                }
-            }
-        } else if constexpr (PRO == PRO_PRENORM) {
-            // per-row 1/rms in this wave's LDS slot (a register array indexed by the runtime row
-            // would be spilled to scratch: one more memory round trip per read)
-            float* rsw = rsl + wave * GEMV_RMAX;
-#pragma unroll
-            for (int rr = 0; rr < GEMV_RMAX; ++rr) {
-                const float v = rr < R ? 1.0f / sqrtf(wave_sum(ssl[rr]) / (float)K + a.eps) : 0.f;
-                if (lane == 0) rsw[rr] = v;
-            }
-            __builtin_amdgcn_wave_barrier();
-            tsb = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-            const bool writer = blockIdx.x == 0 && a.xn_out;
-            auto put = [&](int rr, int cc, const C8<T>& xq, const C8<T>& wq) {
-                float xv[8], wv[8];
-                c8_to_f(xq, xv);
-                c8_to_f(wq, wv);
-                const float rs = rsw[rr];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const float xn = rnd<T>(rnd<T>(xv[u] * rs) * wv[u]);
-                    st(xs, (size_t)rr * xstride + 8 * cc + u, xn);
-                    if (writer) st(a.xn_out, (size_t)rr * a.ldxo + 8 * cc + u, xn);
-                }
-            };
-#pragma unroll
-            for (int q = 0; q < GEMV_PRE; ++q) {
-                const int it = threadIdx.x + NTH * q;
-                if (it < nitem) put(it / nch, it - (it / nch) * nch, xc[q], wc[q]);
-            }
-            for (int it = threadIdx.x + NTH * GEMV_PRE; it < nitem; it += NTH) {
-                const int rr = it / nch, cc = it - rr * nch;
-                put(rr, cc, load_c8(a.X + (size_t)rr * a.ldx + 8 * cc), load_c8(a.nw + 8 * cc));
-            }
-            tsc = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-        } else {
-#pragma unroll
-            for (int q = 0; q < GEMV_PRE; ++q) {
-                const int it = threadIdx.x + NTH * q;
-                if (it < nitem) {
-                    const int rr = it / nch, cc = it - rr * nch;
-                    *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) = xc[q];
-                }
-            }
-            for (int it = threadIdx.x + NTH * GEMV_PRE; it < nitem; it += NTH) {
-                const int rr = it / nch, cc = it - rr * nch;
-                *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) =
-                    load_c8(a.X + (size_t)rr * a.ldx + 8 * cc);
-            }
-        }
-    }
-    __syncthreads();
-    const unsigned long long ts1 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-
-    // ---------------- tile finisher: partial -> ticket -> (last) combine + epilogue ------------
-    auto finish = [&](int t, const f32x4_t& c0, const f32x4_t& c1) {
-        const int fw = sk_first_wave((long long)t * S, Wact, Utot);
-        const int lw = sk_first_wave((long long)(t + 1) * S - 1, Wact, Utot);
-        const int nc = lw - fw + 1, ci = gw - fw;
-        float* pt = a.part + (size_t)t * a.maxc * NACC * 16 * R;
-        if ((lane & 15) < R) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = 4 * (lane >> 4) + i, col = lane & 15;
-                __hip_atomic_store(pt + ((size_t)ci * NACC * 16 + row) * R + col, c0[i], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                if constexpr (NACC == 2)
-                    __hip_atomic_store(pt + ((size_t)ci * NACC * 16 + 16 + row) * R + col, c1[i], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        int tk = 0;
-        if (lane == 0) tk = __hip_atomic_fetch_add(a.tickets + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        tk = __shfl(tk, 0);
-        if (tk != nc - 1) return;
-        if (lane == 0) __hip_atomic_store(a.tickets + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        float* sq = ssq + wave * 16 * GEMV_RMAX;
-        for (int o = lane; o < 16 * R; o += 64) {
-            const int row = o / R, col = o - row * R;
-            const int n = t * 16 + row;
-            float v0 = 0.f, v1 = 0.f;
-            for (int q = 0; q < nc; ++q) {
-                v0 += __hip_atomic_load(pt + ((size_t)q * NACC * 16 + row) * R + col, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-                if constexpr (NACC == 2)
-                    v1 += __hip_atomic_load(pt + ((size_t)q * NACC * 16 + 16 + row) * R + col, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (n >= a.N) {
-                if constexpr (EPI == EPI_SLABFIN) sq[row * R + col] = 0.f;
-                continue;
-            }
-            if (a.bias) v0 += ld(a.bias, n);
-            const size_t yi = (size_t)col * a.ldy + n;
-            if constexpr (EPI == EPI_STORE) {
-                st(a.Y, yi, v0);
-            } else if constexpr (EPI == EPI_QKVATT) {  // write-through: read back by another block
-                if constexpr (sizeof(T) == 2) {
-                    const float rv = rnd<T>(v0);
-                    __hip_atomic_store(reinterpret_cast<unsigned short*>(a.Y) + yi,
-                                       (unsigned short)(__float_as_uint(rv) >> 16), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    __hip_atomic_store(reinterpret_cast<float*>(a.Y) + yi, v0, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-            } else if constexpr (EPI == EPI_SWIGLU) {
-                st(a.Y, yi, rnd<T>(silu_g(rnd<T>(v0))) * rnd<T>(v1));
-            } else if constexpr (EPI == EPI_F32) {
-                a.Yf[yi] = rnd<T>(v0);
-            } else {  // EPI_SLABFIN: x = round(res + round(y)), and the tile's sums of squares
-                const int ri = a.residx ? a.residx[(size_t)col * a.xidx_ld + a.xidx_col] : col;
-                const float x = rnd<T>(ld(a.res + (size_t)ri * a.ldr, n) + rnd<T>(v0));
-                st(a.res_out, (size_t)col * a.ldro + n, x);
-                sq[row * R + col] = x * x;
-            }
-        }
-        if constexpr (EPI == EPI_SLABFIN) {
-            __builtin_amdgcn_wave_barrier();
-            if (lane < R) {
-                float s2 = 0.f;
-                for (int row = 0; row < 16; ++row) s2 += sq[row * R + lane];
-                a.ss_out[(size_t)t * R + lane] = s2;
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-    };
-
-    // ---------------- main loop: this wave's contiguous run, ring of U fragments ----------------
-    if (active) {
-        int tcur = u0 / S, tend = (tcur + 1) * S;
-        int tprev = -1;
-        f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, p0 = acc0, p1 = acc0;
-        const T* xrow = xs + (size_t)(r < R ? r : R - 1) * xstride + 8 * g;
-        const int n = u1 - u0;
-        for (int i = 0; i < n; i += U) {
-#pragma unroll
-            for (int uu = 0; uu < U; ++uu) {
-                const int uj = u0 + i + uu;
-                if (uj < u1) {
-                    if (uj == tend) {  // tile switch: park the finished accumulator
-                        if (tprev >= 0) finish(tprev, p0, p1);  // a third tile: only when a run exceeds a tile
-                        tprev = tcur;
-                        p0 = acc0;
-                        p1 = acc1;
-                        acc0 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-                        acc1 = acc0;
-                        ++tcur;
-                        tend += S;
-                    }
-                    const typename G::f xb = G::load_lds(xrow + (size_t)(uj - tcur * S) * 32);
-                    acc0 = G::mma(fa[uu], xb, acc0);
-                    if constexpr (NACC == 2) acc1 = G::mma(fb[uu], xb, acc1);
-                }
-                issue(i + uu + U, uu);
-            }
-        }
-        if (tprev >= 0) finish(tprev, p0, p1);
-        finish(tcur, acc0, acc1);
-    }
-    if (a.dbg && lane == 0 && active) {
-        const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
-        const unsigned long long slot = atomicAdd(a.dbg, 1ull);
-        if (slot < (1ull << 20)) {
-            unsigned long long* q = a.dbg + 8 + slot * 8;
-            q[0] = ((unsigned long long)a.N << 32) | ((unsigned long long)wave << 16) | blockIdx.x;
-            q[1] = ts0;
-            q[2] = ts1;
-            q[3] = t3;
-            q[4] = t3;
-            q[5] = tsa;
-            q[6] = tsb;
-            q[7] = tsc;
-        }
-    }
-}
-
-template <typename T, int PRO, int EPI, bool NT, int U>
-static void gemv_sk_go(hipStream_t s, const GemvArgs<T>& a0, int nblk, size_t lds) {
-    GemvArgs<T> a = a0;
-    a.dbg = fm_tuning().dbg;
-    a.pro_exp = fm_tuning().pro_exp;
-    static bool big = false;
-    if (lds > 64 * 1024 && !big) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_sk_kernel<T, PRO, EPI, NT, U>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        big = true;
-    }
-    gemv_sk_kernel<T, PRO, EPI, NT, U><<<nblk, 512, lds, s>>>(a);
-}
-
-static int sk_num_cus() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    }
-    return n;
-}
-
-template <typename T> bool launch_gemv_sk(hipStream_t s, const GemvArgs<T>& a0, int pro, int epi) {
-    const FmTuning& tu = fm_tuning();
-    if (!tu.gemv_sk || a0.R > GEMV_RMAX || !a0.part || !a0.tickets) return false;
-    if (pro == PRO_PRENORM && a0.K > 4096) return false;
-    if (pro == PRO_NORM && a0.K > 4 * 512 * 8) return false;
-    const size_t lds = (size_t)a0.R * (a0.K + 8) * sizeof(T) + (size_t)8 * 17 * GEMV_RMAX * sizeof(float);
-    if (lds > 150 * 1024) return false;
-    const int nacc = epi == EPI_SWIGLU ? 2 : 1;
-    const int ntile = (a0.N + 15) / 16, S = a0.K / 32;
-    const int nblk = sk_num_cus() * tu.gemv_sk_bpc;
-    const long long Utot = (long long)ntile * S;
-    const int Wact = (int)std::min<long long>(Utot, (long long)nblk * 8);
-    // contributors per tile <= ceil(S * Wact / Utot) + 1
-    const int maxc = (int)(((long long)S * Wact + Utot - 1) / Utot) + 1;
-    if ((long long)ntile * maxc * nacc * 16 * a0.R > a0.part_cap) return false;
-    GemvArgs<T> a = a0;
-    a.maxc = maxc;
-    const int U = tu.gemv_u == 8 ? 8 : 4;
-#define SKGO(P, E)                                                                       \
-    if (pro == P && epi == E) {                                                         \
-        if (U == 8) gemv_sk_go<T, P, E, true, 8>(s, a, nblk, lds);                       \
-        else gemv_sk_go<T, P, E, true, 4>(s, a, nblk, lds);                              \
-        return true;                                                                     \
-    }
-    SKGO(PRO_PLAIN, EPI_STORE) SKGO(PRO_PLAIN, EPI_SLABFIN) SKGO(PRO_PLAIN, EPI_F32)
-    SKGO(PRO_NORM, EPI_STORE) SKGO(PRO_NORM, EPI_SWIGLU) SKGO(PRO_NORM, EPI_F32)
-    SKGO(PRO_PRENORM, EPI_STORE) SKGO(PRO_PRENORM, EPI_SWIGLU) SKGO(PRO_PRENORM, EPI_F32)
-#undef SKGO
-    return false;
-}
-
-template bool launch_gemv_sk<bf16_t>(hipStream_t, const GemvArgs<bf16_t>&, int, int);
-template bool launch_gemv_sk<float>(hipStream_t, const GemvArgs<float>&, int, int);

@@ -129,12 +129,9 @@ enum { PRO_PLAIN = 0, PRO_NORM = 1, PRO_PRENORM = 3, PRO_FATT = 4 };
 // PRO_FATT (fast model, one row, cpos < 16): X' is the fast-model attention output, recomputed by
 // every block from the raw QKV row and the cached K/V rows staged in LDS (llama.py:947-975), so
 // the Wo GEMV needs no separate attention launch; blockIdx.x == 0 writes the new k / v of cpos.
-enum { EPI_SLAB = 4, EPI_SLABFIN = 5, EPI_QKVATT = 6, EPI_SWIGLU8 = 7 };
+enum { EPI_SLAB = 4, EPI_SLABFIN = 5, EPI_SWIGLU8 = 7 };
 // EPI_SWIGLU8: W is the row-interleaved W1||W3 (each 16-row tile = 8 gate rows then the same 8 up
 // rows, see pack_w13 in fm_llm.cpp); a tile yields 8 SwiGLU outputs, N = 2 * intermediate.
-// EPI_QKVATT (fast model, cpos < 16, whole K per block): the QKV GEMV stores its tile write-through,
-// takes a ticket on the tile's kv group, and the group's last-arriving block runs the fast-model
-// attention of that group's q heads (fm_attn_dev.h) -- no separate attention launch.
 
 template <typename T> struct FastFusedArgs {
     const T* qkv;
@@ -179,12 +176,7 @@ template <typename T> struct GemvArgs {
     T* xn_out;               // optional (ksb == 1): block (0,0) stores X' (normalised row) here
     int ldxo;
     unsigned long long* dbg; // developer timestamps (fm_tune "debug_ts"); null in production
-    float* part;             // stream-K: per-(tile, contributor) partial tiles (sc1), capacity part_cap
-    long long part_cap;      //   floats
-    int maxc;                // stream-K: contributor slots per tile (set by the launcher)
-    int pro_exp;             // EXPERIMENT knob (see FmTuning)
-    FastFusedArgs<T> att;    // EPI_QKVATT: the attention the group's last block runs
-    int* att_tickets;        // EPI_QKVATT: per-kv-group arrival counters (zero between launches)
+    FastFusedArgs<T> att;    // PRO_FATT: the fast-model attention the prologue recomputes
     int fatt_off;            // PRO_FATT: byte offset of the attention staging area in LDS (launcher)
 };
 // developer knobs for the decode GEMV (fm_tune): weight load policy and split-K policy
@@ -192,23 +184,14 @@ struct FmTuning {
     int gemv_nt = 1;         // 1: non-temporal weight loads (each weight byte is read once a frame)
     int gemv_u = 8;          // weight fragments in flight per wave (2, 4 or 8)
     int gemv_wpb = 4;        // waves per block (4 or 8) sharing one 16-row tile
-    int gemv_sk = 0;         // 1: stream-K decode GEMV (one persistent block per CU), 0: tiled
-    int gemv_sk_bpc = 1;     // stream-K blocks per CU
-    int pro_exp = 0;         // EXPERIMENT: 1 skip tile-sum loads, 2 skip norm-weight loads, 3 both
     int sampler_fast = 1;    // 1: two-stage register top-K sampler, 0: LDS radix-select sampler
     int attn_cap = 32;       // slow decode attention rows per block cap (0: the LDS-budget maximum)
-    int attn_fuse = 0;       // 1: fast-model attention fused into the QKV GEMV's tail (EPI_QKVATT)
     int attn_wo = 0;         // 1: fast-model attention recomputed in the Wo GEMV's prologue (PRO_FATT, R == 1; measured 0.37 ms/frame slower)
     int ksb_blocks = 512;    // split K until the grid has at least this many blocks
     int batched_fused_attn = 1;  // batched decode (one row per slot): fused QK-norm/RoPE/KV-write attention kernels
     int attn_cap_batched = 128;  // rows per block of the batched decode attention (one row per slot)
     int linear_u32 = 4;      // linear_kernel weight fragments in flight per wave at 16 < R <= 32 (4 or 8)
     int linear_fill = 0;     // batched linear_kernel: split K until this many blocks (0: never; measured slower)
-    int bgemv = 0;           // 1: batched decode linears (8 < R <= 32) on bgemv_kernel (measured slower at B=32), 0: linear_kernel
-    int bgemv_u = 8;         // bgemv weight fragments in flight per wave (4 or 8)
-    int bgemv_tpb = 4;       // bgemv max 16-row tiles per block sharing one staged X slice (1, 2, 4)
-    int bgemv_lds_kb = 84;   // bgemv X-slice LDS budget (KiB) before splitting K
-    int bgemv_fill = 512;    // bgemv: split K until the grid has this many blocks
     int attn3 = 1;           // 1: slow decode attention on attn_dec3_kernel, 0: attn_decode2_kernel
     int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)
     int bstream_kparts = 0;  // bstream EPI_SLAB K parts (0: by K)
@@ -227,29 +210,6 @@ inline size_t gemv_lds_bytes(int R, int Kb, size_t esz) {
            8 * 8 * sizeof(float);
 }
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb);
-
-// ---- batched decode weight streaming, 8 < R <= 32 rows (fm_bgemv.hip) ---------------------------
-template <typename T> struct BgemvArgs {
-    const T* W;      // packed MFMA-fragment layout [tiles][K/32][512]
-    const T* bias;   // [N] or null
-    const T* X;      // [R][ldx]
-    int ldx, R, N, K;
-    T* Y;            // EPI_STORE / EPI_RESID [R][ldy]
-    int ldy;
-    const T* res;    // EPI_RESID residual [R][ldr] (may alias Y)
-    int ldr;
-    float* Yf;       // EPI_F32 [R][ldy]
-    float* part;     // split-K partials [ksb][R][N] (<= LINEAR_PART_CAP floats)
-    int* tickets;    // one arrival counter per block column (zero between launches)
-    int tpb = 1;     // set by the launcher
-};
-struct BgemvPlan {
-    int tpb, ksb;
-};
-BgemvPlan bgemv_plan(int N, int K, int R, size_t esz);
-template <typename T> void launch_bgemv(hipStream_t s, const BgemvArgs<T>& a, int epi);
-// stream-K decode GEMV; returns false (nothing launched) when the shape is not eligible
-template <typename T> bool launch_gemv_sk(hipStream_t s, const GemvArgs<T>& a, int pro, int epi);
 
 // ---- batched decode weight streaming with register-resident X, 8 < R <= 32 (fm_bstream.hip) ---
 template <typename T> struct BstreamArgs {

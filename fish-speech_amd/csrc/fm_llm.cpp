@@ -96,11 +96,10 @@ struct fm_llm {
     float *part = nullptr, *logits = nullptr, *flogits = nullptr;
     void* act2 = nullptr;  // batched path: [R][2 * inter] output of the interleaved W1||W3
     int* attn_cnt = nullptr;
-    int* att_tickets = nullptr;           // EPI_QKVATT per-kv-group arrival counters
     float *ssX = nullptr, *ssH = nullptr;  // per-16-column tile sums of squares of the residual rows
-    int* tickets = nullptr;               // EPI_SLABFIN / stream-K arrival counters (zero between launches)
-    float* skpart = nullptr;              // stream-K partial tiles
-    long long skpart_cap = 0;  // [Rmax][nkv] arrival tickets of attn_decode2 (kept zero between launches)
+    int* tickets = nullptr;               // EPI_SLABFIN / linear split-K arrival counters (zero between launches)
+    float* skpart = nullptr;              // linear_kernel split-K partial tiles
+    long long skpart_cap = 0;             //   floats
     float *slabA = nullptr, *slabB = nullptr;  // split-K partials of wo / w2 (small-batch path)
     float *bsA = nullptr, *bsB = nullptr;      // bstream K-part slabs of wo / w2 (batched path)
     // rows / slots
@@ -232,19 +231,11 @@ template <typename T> struct Run {
             a.part = m->skpart;
             a.tickets = m->tickets;
         }
-        const bool bg = fm_tuning().bgemv && R > GEMV_MAX_ROWS && R <= 32 && epi != EPI_SWIGLU && K % 32 == 0;
-        BgemvArgs<T> b{(const T*)W, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y, ldy, (const T*)res, ldr,
-                       Yf, m->skpart, m->tickets};
         const int64_t wbytes = (int64_t)N * K * E * (epi == EPI_SWIGLU ? 2 : 1);
         const int64_t bytes = wbytes + (int64_t)R * K * E + (int64_t)R * N * (epi == EPI_F32 ? 4 : E);
         const double flops = 2.0 * R * N * K * (epi == EPI_SWIGLU ? 2 : 1);
         hipStream_t st = s;
-        auto go = [st, a, b, bg, epi] {
-            if (bg)
-                launch_bgemv<T>(st, b, epi);
-            else
-                launch_linear<T>(st, a, epi);
-        };
+        auto go = [st, a, epi] { launch_linear<T>(st, a, epi); };
         m->prof.record(cls, bytes, go);
         m->prof.run(s, cls, bytes, flops, go);
     }
@@ -411,12 +402,8 @@ template <typename T> struct Run {
         const int64_t bytes = wbytes + (int64_t)a.R * a.K * E;
         const double flops = 2.0 * a.R * a.N * a.K * (epi == EPI_SWIGLU ? 2 : 1);
         hipStream_t st = s;
-        a.part = m->skpart;
-        a.part_cap = m->skpart_cap;
         if (!a.tickets) a.tickets = m->tickets;
-        auto go = [st, a, pro, epi, ksb] {
-            if (!launch_gemv_sk<T>(st, a, pro, epi)) launch_gemv<T>(st, a, pro, epi, ksb);
-        };
+        auto go = [st, a, pro, epi, ksb] { launch_gemv<T>(st, a, pro, epi, ksb); };
         m->prof.record(cls, bytes, go);
         m->prof.run(s, cls, bytes, flops, go);
     }
@@ -446,11 +433,9 @@ template <typename T> struct Run {
                             (T*)m->fvc, m->fslot_stride, (size_t)layer * m->flayer_stride, m->C, cpos,
                             scale, (T*)m->att};
         fa.dbg = fm_tuning().dbg;
-        // fast model: attention runs in the QKV GEMV's tail (EPI_QKVATT) when it fits the tail
-        const bool fuse = is_fast && fm_tuning().attn_fuse && cpos < 16 && d.nkv <= 256 && d.hd <= 256 &&
-                          d.hd % 16 == 0 && d.nh % d.nkv == 0;
-        // ... or recomputed by every block of the Wo GEMV (PRO_FATT, one row): no attention launch
-        const bool att_wo = is_fast && !fuse && fm_tuning().attn_wo && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
+        // fast model: attention recomputed by every block of the Wo GEMV (PRO_FATT, one row) --
+        // no attention launch (fm_tune attn_wo; measured slower, kept under test)
+        const bool att_wo = is_fast && fm_tuning().attn_wo && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
                             d.hd <= 128 && d.nh % d.nkv == 0 && (d.nq() / kp.wo) % d.hd == 0 && d.nqkv() % 8 == 0;
         // QKV (+ attention_norm)
         {
@@ -463,11 +448,7 @@ template <typename T> struct Run {
             a.K = d.dim;
             a.Y = (T*)m->qkv;
             a.ldy = d.nqkv();
-            const int epi = fuse ? EPI_QKVATT : EPI_STORE;
-            if (fuse) {
-                a.att = fa;
-                a.att_tickets = m->att_tickets;
-            }
+            const int epi = EPI_STORE;
             if (first) {
                 a.X = (const T*)x_in;
                 a.ldx = ldx_in;
@@ -494,7 +475,7 @@ template <typename T> struct Run {
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
             m->prof.run(s, "attn", 0, 0, [&] { attn_slow(aa, n); });
-        } else if (!fuse && !att_wo) {
+        } else if (!att_wo) {
             m->prof.run(s, "attn", 0, 0, [&] {
                 if (cpos < 16 && d.hd <= 256)
                     launch_fast_attn2<T>(s, fa, n);
@@ -968,7 +949,6 @@ static void finalize(fm_llm* m) {
     m->maxsplit = FM_CEIL(m->S, ATTN_SPLIT);
     m->part = (float*)m->dalloc((size_t)R * d.nh * std::max(m->maxsplit, FM_CEIL(m->S, 16)) * (d.hd + 2) * 4, false);
     m->attn_cnt = (int*)m->dalloc((size_t)R * d.nkv * sizeof(int));  // tickets: zeroed
-    m->att_tickets = (int*)m->dalloc(256 * sizeof(int));
     m->ssX = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
     m->ssH = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
     {
@@ -1453,37 +1433,14 @@ int fm_tune(const char* key, int value) {
         } else if (k == "attn_cap") {
             FMCHECK(value == 0 || (value >= 16 && value % 16 == 0), "attn_cap must be 0 or a multiple of 16");
             t.attn_cap = value;
-        } else if (k == "attn_fuse") {
-            t.attn_fuse = value != 0;
         } else if (k == "attn_wo") {
             t.attn_wo = value != 0;
-        } else if (k == "pro_exp") {
-            t.pro_exp = value;
-        } else if (k == "gemv_sk") {
-            t.gemv_sk = value != 0;
-        } else if (k == "gemv_sk_bpc") {
-            FMCHECK(value >= 1 && value <= 4, "gemv_sk_bpc must be in [1, 4]");
-            t.gemv_sk_bpc = value;
         } else if (k == "gemv_wpb") {
             FMCHECK(value == 4 || value == 8, "gemv_wpb must be 4 or 8");
             t.gemv_wpb = value;
         } else if (k == "ksb_blocks") {
             FMCHECK(value >= 1, "ksb_blocks must be >= 1");
             t.ksb_blocks = value;
-        } else if (k == "bgemv") {
-            t.bgemv = value != 0;
-        } else if (k == "bgemv_u") {
-            FMCHECK(value == 4 || value == 8, "bgemv_u must be 4 or 8");
-            t.bgemv_u = value;
-        } else if (k == "bgemv_tpb") {
-            FMCHECK(value == 1 || value == 2 || value == 4, "bgemv_tpb must be 1, 2 or 4");
-            t.bgemv_tpb = value;
-        } else if (k == "bgemv_lds_kb") {
-            FMCHECK(value >= 16 && value <= 140, "bgemv_lds_kb must be in [16, 140]");
-            t.bgemv_lds_kb = value;
-        } else if (k == "bgemv_fill") {
-            FMCHECK(value >= 1, "bgemv_fill must be >= 1");
-            t.bgemv_fill = value;
         } else if (k == "attn_cap_batched") {
             FMCHECK(value == 0 || (value >= 16 && value % 16 == 0), "attn_cap_batched must be 0 or a multiple of 16");
             t.attn_cap_batched = value;

@@ -14,6 +14,7 @@
 //   sample_kernel ............ inference.py:43-93, 117-144 (top-k / top-p / temperature /
 //                              RAS with the reference's rounding; no full-vocab sort)
 #include "fm_kernels.h"
+#include "fm_frag.h"
 
 // =========================================================================================
 // embeddings
@@ -187,45 +188,6 @@ template void launch_swiglu_i8<bf16_t>(hipStream_t, const bf16_t*, int, bf16_t*,
 template void launch_swiglu_i8<float>(hipStream_t, const float*, int, float*, int, int, int);
 template void launch_pack<float>(hipStream_t, const float*, int, int, float*);
 
-template <typename T> struct Mfma;
-template <> struct Mfma<bf16_t> {
-    typedef u32x4_t frag;  // 8 bf16 along k
-    static __device__ __forceinline__ frag load(const bf16_t* p) {
-        return *reinterpret_cast<const u32x4_t*>(p);
-    }
-    static __device__ __forceinline__ frag load_packed(const bf16_t* blk, int lane) {
-        return *reinterpret_cast<const u32x4_t*>(blk + lane * 8);
-    }
-    static __device__ __forceinline__ f32x4_t mma(frag a, frag b, f32x4_t c) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
-                                                       __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
-    }
-};
-template <> struct Mfma<float> {
-    struct frag {
-        f32x4_t lo, hi;
-    };
-    static __device__ __forceinline__ frag load(const float* p) {
-        frag f;
-        f.lo = *reinterpret_cast<const f32x4_t*>(p);
-        f.hi = *reinterpret_cast<const f32x4_t*>(p + 4);
-        return f;
-    }
-    static __device__ __forceinline__ frag load_packed(const float* blk, int lane) {
-        frag f;
-        f.lo = *reinterpret_cast<const f32x4_t*>(blk + lane * 4);
-        f.hi = *reinterpret_cast<const f32x4_t*>(blk + 256 + lane * 4);
-        return f;
-    }
-    // lane l holds k = 8*(l>>4) + j of a 32-wide k block; MFMA j covers {8g + j}: exact f32
-    static __device__ __forceinline__ f32x4_t mma(frag a, frag b, f32x4_t c) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[j], b.lo[j], c, 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[j], b.hi[j], c, 0, 0, 0);
-        return c;
-    }
-};
 
 __device__ __forceinline__ float silu_f(float a) { return a / (1.0f + expf(-a)); }
 
@@ -252,7 +214,7 @@ __device__ __forceinline__ void linear_epi(const LinearArgs<T>& a, int n, int co
 // as gemv_kernel's EPI_SLABFIN).
 template <typename T, int NCG, int EPI, int U>
 __global__ __launch_bounds__(512) void linear_kernel(LinearArgs<T> a) {
-    using M = Mfma<T>;
+    using M = Frag<T>;
     constexpr int NACC = (EPI == EPI_SWIGLU) ? 2 : 1;
     __shared__ f32x4_t red[8][NACC * NCG][64];
     __shared__ int last_flag;
@@ -280,11 +242,11 @@ __global__ __launch_bounds__(512) void linear_kernel(LinearArgs<T> a) {
         }
         int s = s0;
         for (; s + U <= s1; s += U) {
-            typename M::frag fa[NACC][U], fb[NCG][U];
+            typename M::f fa[NACC][U], fb[NCG][U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                fa[0][u] = M::load_packed(wp + (size_t)(s + u) * 512, lane);
-                if constexpr (NACC == 2) fa[1][u] = M::load_packed(wp2 + (size_t)(s + u) * 512, lane);
+                fa[0][u] = M::load_w(wp + (size_t)(s + u) * 512, lane);
+                if constexpr (NACC == 2) fa[1][u] = M::load_w(wp2 + (size_t)(s + u) * 512, lane);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -298,12 +260,12 @@ __global__ __launch_bounds__(512) void linear_kernel(LinearArgs<T> a) {
                     for (int q = 0; q < NACC; ++q) acc[q][c] = M::mma(fa[q][u], fb[c][u], acc[q][c]);
         }
         for (; s < s1; ++s) {
-            typename M::frag fa0 = M::load_packed(wp + (size_t)s * 512, lane);
-            typename M::frag fa1;
-            if constexpr (NACC == 2) fa1 = M::load_packed(wp2 + (size_t)s * 512, lane);
+            typename M::f fa0 = M::load_w(wp + (size_t)s * 512, lane);
+            typename M::f fa1;
+            if constexpr (NACC == 2) fa1 = M::load_w(wp2 + (size_t)s * 512, lane);
 #pragma unroll
             for (int c = 0; c < NCG; ++c) {
-                typename M::frag fb = M::load(xp[c] + (size_t)s * 32);
+                typename M::f fb = M::load(xp[c] + (size_t)s * 32);
                 acc[0][c] = M::mma(fa0, fb, acc[0][c]);
                 if constexpr (NACC == 2) acc[1][c] = M::mma(fa1, fb, acc[1][c]);
             }

@@ -3,7 +3,10 @@
 Mirrors the reference's seams (fish_speech/models/text2semantic/llama.py and inference.py):
   * ``DualARModel.from_pretrained(path)``  <- BaseTransformer.from_pretrained (llama.py:479-593)
   * ``model.generate(prompt, ...)``         <- inference.generate (inference.py:241-359)
-  * ``model.decode_one_token(...)``         <- decode_one_token_ar (inference.py:96-181), batched
+  * ``model.decode_frames(slots, n)``       <- decode_n_tokens over decode_one_token_ar
+                                               (inference.py:96-238), batched over slots
+  * ``DecodeOneToken(model)``               <- the injected ``decode_one_token`` operator itself
+                                               (inference.py:96-107, injected at :195 and :250)
   * ``model.teacher_step(...)``             <- forward_generate + forward_generate_fast
 """
 from __future__ import annotations
@@ -274,3 +277,74 @@ class DualARModel:
 
     def use_graph(self, enable: bool):
         native.check(native.lib().fm_llm_use_graph(self.h, int(enable)))
+
+
+class DecodeOneToken:
+    """The reference's injected per-step operator, ``decode_one_token_ar(model, x, input_pos,
+    temperature, top_p, top_k, semantic_logit_bias, audio_masks, audio_parts, previous_tokens)``
+    (inference.py:96-181), on one slot of a DualARModel.  Pass it as ``generate(...,
+    decode_one_token=op)`` / ``decode_n_tokens(..., decode_one_token=op)`` (inference.py:195, 250),
+    or call it for the prefill step as generate() does (inference.py:323-333).
+
+    The slot owns the KV cache and the RAS window, so the call checks that the caller's state is
+    the one the slot holds rather than re-deriving it:
+      * x (1, C+1, T), T > 1: a prefill at positions input_pos = [p0, p0 + T); p0 must be 0 or a
+        position the slot has already cached (prefix reuse, fm_llm_prefill_at);
+      * x (1, C+1, 1): one frame at input_pos == the slot's next position, x == the column this
+        operator returned last (decode_n_tokens feeds back exactly that);
+      * temperature / top_p / top_k are fixed by the prefill (the reference keeps them for the
+        whole generate); semantic_logit_bias must be the reference's (0 on the semantic range and
+        <|im_end|>, -inf elsewhere, inference.py:308-320) -- the compact head is exact only there;
+      * audio_parts must be None (the prompt side encodes text and VQ codes only).
+    Returns a (C+1, 1) int64 tensor on x's device, like the reference."""
+
+    def __init__(self, model: DualARModel, slot: int = 0, seed: int = 0):
+        self.m = model
+        self.slot = slot
+        self.seed = seed
+        self._last = None
+        self._params = None
+        self._bias_ok = set()
+
+    def _check_bias(self, bias):
+        if bias is None or id(bias) in self._bias_ok:
+            return
+        cfg = self.m.cfg
+        b = bias.detach().float().reshape(-1).cpu().numpy()
+        want = np.full(cfg.vocab_size, -np.inf, np.float32)
+        want[cfg.semantic_begin_id: cfg.semantic_end_id + 1] = 0.0
+        want[cfg.im_end_id] = 0.0
+        if b.shape != want.shape or not np.array_equal(b, want):
+            raise ValueError("semantic_logit_bias differs from generate()'s (inference.py:308-320)")
+        self._bias_ok.add(id(bias))
+
+    def __call__(self, model, x, input_pos, temperature, top_p, top_k, semantic_logit_bias,
+                 audio_masks=None, audio_parts=None, previous_tokens=None):
+        import torch
+
+        if audio_parts is not None:
+            raise NotImplementedError("audio_parts (continuous audio embeddings) are not on this path")
+        self._check_bias(semantic_logit_bias)
+        xx = x.detach().reshape(self.m.C1, -1).to("cpu", torch.int32).numpy()
+        ip = np.asarray(input_pos.detach().reshape(-1).cpu().numpy(), np.int64)
+        params = (float(temperature), float(top_p), int(top_k))
+        T = xx.shape[1]
+        if T > 1 or ip[0] == 0:
+            p0 = int(ip[0])
+            if p0 and p0 > self.m.slot_pos(self.slot):
+                raise ValueError(f"prefill at {p0} past the slot's cached positions")
+            sp = DualARModel.sampling(*params, seed=self.seed)
+            col = self.m.prefill(self.slot, xx, sp, pos0=p0)
+            self._params = params
+        else:
+            if self._last is None:
+                raise ValueError("decode step before a prefill on this slot")
+            if params != self._params:
+                raise ValueError("temperature / top_p / top_k changed after the prefill")
+            if int(ip[0]) != self.m.slot_pos(self.slot):
+                raise ValueError(f"input_pos {int(ip[0])} != the slot's next position {self.m.slot_pos(self.slot)}")
+            if not np.array_equal(xx[:, 0], self._last):
+                raise ValueError("x is not the column this operator emitted last")
+            col = self.m.decode([self.slot])[0]
+        self._last = np.asarray(col, np.int32).copy()
+        return torch.from_numpy(self._last.astype(np.int64)).reshape(self.m.C1, 1).to(x.device)

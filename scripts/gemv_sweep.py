@@ -19,8 +19,7 @@ m = DualARModel.synthetic(cfg, seed=0, log2_half=5, device=0, precision="bf16", 
 p = np.zeros((cfg.num_codebooks + 1, 64), np.int32)
 p[0] = np.random.default_rng(1).integers(16, cfg.semantic_begin_id, 64)
 sp = DualARModel.sampling(mask_im_end=True)
-configs = [dict(gemv_sk=1, gemv_u=u, gemv_sk_bpc=b) for b in (1, 2) for u in (4, 8)]
-configs += [dict(gemv_sk=0, gemv_u=4, gemv_wpb=8), dict(gemv_sk=0, gemv_u=8, gemv_wpb=4)]
+configs = [dict(gemv_u=u, gemv_wpb=w) for u in (4, 8) for w in (4, 8)]
 for c in configs:
     for k, v in c.items():
         native.tune(k, v)

@@ -46,6 +46,47 @@ def test_fp32_greedy_tokens_exact(name, golden):
     np.testing.assert_array_equal(out, ref)
 
 
+def _reference_loop(op, prompt, max_new, cfg, top_k):
+    """generate() + decode_n_tokens() control flow (inference.py:241-359, 184-238) around an
+    injected decode_one_token operator, as the reference drives it."""
+    import torch
+
+    C1 = cfg.num_codebooks + 1
+    T = prompt.shape[1]
+    x = torch.from_numpy(prompt.astype(np.int32)).view(1, C1, T)
+    temperature, top_p = torch.tensor(0.7), torch.tensor(0.9)
+    bias = torch.full((1, 1, cfg.vocab_size), float("-inf"))
+    bias[0, 0, cfg.semantic_begin_id: cfg.semantic_end_id + 1] = 0.0
+    bias[0, 0, cfg.im_end_id] = 0.0
+    first = op(None, x, torch.arange(0, T), temperature, top_p, top_k, bias, None, None)
+    cols = [first]
+    cur, pos = first.view(1, C1, -1), torch.tensor([T], dtype=torch.int)
+    prev = torch.zeros((C1, 16), dtype=torch.int)
+    for _ in range(max_new - 1):
+        nxt = op(None, cur, pos, temperature, top_p, top_k, bias, None, None, previous_tokens=prev).clone()
+        pos += 1
+        cur = nxt.view(1, C1, -1)
+        prev = prev.roll(-1, dims=1)
+        prev[:, -1] = nxt.view(C1, -1)[:, 0]
+        cols.append(nxt)
+        if cur[0, 0, -1] == cfg.im_end_id:
+            break
+    return torch.cat(cols, dim=1).numpy()
+
+
+@pytest.mark.parametrize("name", ["llm_a", "llm_b"])
+def test_decode_one_token_operator_in_reference_loop(name, golden):
+    """B2: DecodeOneToken driven by the reference's generate/decode_n_tokens loop (prefill call,
+    then one call per frame with the fed-back column) reproduces the reference's greedy tokens."""
+    from fishmi.llm import DecodeOneToken
+
+    m, g, cfg = _model(name, "fp32", golden)
+    T = g["prompt"].shape[1]
+    ref = g["seq"][:, T:]
+    out = _reference_loop(DecodeOneToken(m), g["prompt"], ref.shape[1], cfg, top_k=1)
+    np.testing.assert_array_equal(out, ref)
+
+
 @pytest.mark.parametrize("rmsnorm_block", [0, 1])
 @pytest.mark.parametrize("name", ["llm_a", "llm_b"])
 def test_fp32_teacher_step_prefill_path_logits(name, rmsnorm_block, golden, knob):
@@ -351,15 +392,15 @@ def knob():
         native.tune(k, d)
 
 
-@pytest.mark.parametrize("bgemv", [0, 1])
+@pytest.mark.parametrize("bstream", [1, 0])
 @pytest.mark.parametrize("n", [12, 20])
-def test_batched_slots_past_gemv_match_single(n, bgemv, golden, knob):
+def test_batched_slots_past_gemv_match_single(n, bstream, golden, knob):
     """Config-3 batching past the batch-1 GEMV (n > 8 slots) gives each slot its own batch-1
-    greedy stream (fp32 mode): the MFMA linear_kernel (default) and the opt-in batched weight
-    stream bgemv_kernel (one or two MFMA column groups)."""
+    greedy stream (fp32 mode): the register-resident weight stream bstream_kernel (default) and the
+    MFMA linear_kernel (fm_tune bstream=0)."""
     from fishmi.llm import DualARModel
 
-    knob("bgemv", bgemv, 0)
+    knob("bstream", bstream, 1)
 
     m, g, cfg = _model("llm_b", "fp32", golden, max_slots=n)
     rng = np.random.default_rng(7)
@@ -378,15 +419,16 @@ def test_batched_slots_past_gemv_match_single(n, bgemv, golden, knob):
         np.testing.assert_array_equal(got, single[s])
 
 
-@pytest.mark.parametrize("knobs", [{"bgemv": 1}, {"linear_fill": 1024}])
+@pytest.mark.parametrize("knobs", [{}, {"bstream": 0}, {"bstream": 0, "linear_fill": 1024}])
 def test_batched_wide_split_k_matches_single(knobs, golden, knob):
-    """S2-Pro widths, 20 slots: the opt-in split-K forms (bgemv_kernel, and linear_kernel with
-    linear_fill) -- sc1 partials + ticketed last-slice reduction -- reproduce every slot's batch-1
-    greedy stream (fp32 mode)."""
+    """S2-Pro widths, 20 slots: bstream_kernel's K-part slabs + finalize_norm (default), whole-K
+    linear_kernel, and linear_kernel's opt-in split K (linear_fill: sc1 partials + ticketed
+    last-slice reduction) reproduce every slot's batch-1 greedy stream (fp32 mode)."""
     from fishmi.llm import DualARModel
 
+    defaults = {"bstream": 1, "linear_fill": 0}
     for k, v in knobs.items():
-        knob(k, v, 0)
+        knob(k, v, defaults[k])
 
     g = golden("llm_wide_bf16.npz")
     cfg = _cfg("llm_wide")
