@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--longform-turns", type=int, default=4,
                     help="config-5 leg: speaker turns (0: skip), each --longform-frames frames")
     ap.add_argument("--longform-frames", type=int, default=323, help="config-5 leg: frames per turn (15 s)")
+    ap.add_argument("--no-int8", action="store_true", help="skip the opt-in weight-only int8 leg")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the in-run rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on the GEMV")
     ap.add_argument("--encode-seconds", type=float, default=30.0,
@@ -269,6 +270,45 @@ def longform_leg(ccfg, device, turns, frames_per_turn, seed):
             "turn_first_chunk_ms_p90": round(float(np.percentile(f, 90)), 2)}
 
 
+def int8_leg(cfg, codec, args, local):
+    """Config 2 with weight-only int8 linears (opt-in; tools/llama/quantize.py's
+    per-channel rule applied on the device to the same synthetic weights): the same utterance loop,
+    and the int8 decode GEMV's roofline at its own algorithmic bytes (1 byte per weight)."""
+    from fishmi.llm import DualARModel
+
+    llm = DualARModel.synthetic(cfg, seed=args.seed, log2_half=5, device=local, precision="bf16",
+                                max_slots=1, quant="int8")
+    def go(step):
+        sp = DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30, seed=7919 * step, mask_im_end=True)
+        return utterance(llm, codec, make_prompt(cfg, args.prompt_len, 1000 * step), sp, args.frames,
+                         args.first_chunk)[1]
+
+    go(-1)
+    import torch
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tms = [go(k) for k in range(args.steps)]
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    pos = args.prompt_len + args.frames // 2
+    llm.prefill(0, make_prompt(cfg, args.prompt_len, 99), DualARModel.sampling(mask_im_end=True))
+    llm.decode_frames([0], args.frames // 2)
+    avg_us, n, b = llm.kernel_bench("linear", reps=20)
+    dec_s = np.mean([t["decode"] for t in tms]) / (args.frames - args.first_chunk)
+    fb = llm.frame_bytes(1, pos)
+    llm.close()
+    ach = b / n / (avg_us * 1e-6) / 1e9
+    return {"workload": "config 2 as above with weight-only int8 linears (round(round(x.q) * scale), "
+                        "biases dropped, as WeightOnlyInt8Linear); opt-in, off the bf16 parity contract",
+            "value": round(args.steps * args.frames / FRAME_RATE / el, 4), "unit": "audio-sec/wall-sec",
+            "ms_per_frame": round(dec_s * 1e3, 4), "bytes_per_frame": int(fb),
+            "frame_frac": round(fb / dec_s / 1e9 / HBM_PEAK_GBPS, 4),
+            "gemv": {"achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBPS, 4), "bytes_per_launch": int(b / n),
+                     "avg_launch_us": round(avg_us, 3), "launches_per_frame": int(n)}}
+
+
 def cpu_baseline(cfg, ccfg, prompt, frames, n_frames, n_codec, seed):
     """The C oracle (oracle/, a restatement of the reference's CPU path) at full S2-Pro shapes on
     the host cores: prompt pass + n_frames decode frames and a codec decode of n_codec frames,
@@ -471,6 +511,10 @@ def main():
     longf = longform_leg(ccfg, local, args.longform_turns, args.longform_frames, args.seed) \
         if args.longform_turns > 0 and rank == 0 else None
 
+    q8 = None
+    if rank == 0 and not args.no_int8:
+        llm.close()
+        q8 = int8_leg(cfg, codec, args, local)
     copy_gbps = copy_peak_gbps() if rank == 0 else None
     traffic, traffic_note = None, "not measured (--no-pmc or N>1)"
     if rank == 0 and world == 1 and not args.no_pmc:
@@ -527,6 +571,7 @@ def main():
             "throughput": thr,
             "encode": enc,
             "longform": longf,
+            "int8": q8,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

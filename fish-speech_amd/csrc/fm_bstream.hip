@@ -101,6 +101,10 @@ __global__ __launch_bounds__(BS_MAXW * 64) void bstream_kernel(BstreamArgs<T> a)
                             vg += red[buf][w][cg][lg][i];
                             vu += red[buf][w][cg][lu][i];
                         }
+                        if (a.wscale) {  // weight-only int8: round(round(acc) * scale) per packed row
+                            vg = rnd<T>(rnd<T>(vg) * ld(a.wscale, tile * 16 + row));
+                            vu = rnd<T>(rnd<T>(vu) * ld(a.wscale, tile * 16 + 8 + row));
+                        }
                         const int n = tile * 8 + row;
                         if (n < (a.N >> 1)) st(a.Y, (size_t)col * a.ldy + n, rnd<T>(silu_b(rnd<T>(vg))) * rnd<T>(vu));
                     }
@@ -115,6 +119,7 @@ __global__ __launch_bounds__(BS_MAXW * 64) void bstream_kernel(BstreamArgs<T> a)
                         if constexpr (EPI == EPI_SLAB) {
                             a.Yf[((size_t)kp * a.R + col) * a.ldy + n] = v;
                         } else {
+                            if (a.wscale) v = rnd<T>(rnd<T>(v) * ld(a.wscale, n));
                             if (a.bias) v += ld(a.bias, n);
                             if constexpr (EPI == EPI_STORE)
                                 st(a.Y, (size_t)col * a.ldy + n, v);
@@ -159,6 +164,12 @@ __global__ __launch_bounds__(FN_THREADS) void finalize_norm_kernel(FinalizeArgs<
                 load8(a.bias + i, b);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) y[j] += b[j];
+            }
+            if (a.wscale) {  // weight-only int8 linear output
+                float sc[8];
+                load8(a.wscale + i, sc);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) y[j] = rnd<T>(rnd<T>(y[j]) * sc[j]);
             }
             load8(a.res + (size_t)r * a.ldr + i, x);
 #pragma unroll

@@ -10,8 +10,17 @@
 //   load_masked(p, valid)   the same, zeroed when !valid (the load itself is unconditional)
 //   zero()                  an all-zero fragment
 //   mma(a, b, c)            c += a . b over the 32-wide k block
+//   dq8(raw, f0, f1)        16 int8 weights (one int8 unit of a lane: 8 k of k-step 2u, then 8 k
+//                           of k-step 2u + 1) as two exact T fragments (weight-only int8)
 #pragma once
 #include "fm_common.h"
+
+// (float)(int8) of byte j of w: exact, and exact again in bf16 (|q| <= 128 needs 8 bits)
+__device__ __forceinline__ float i8f(uint32_t w, int j) { return (float)(int)(int8_t)(w >> (8 * j)); }
+// two floats holding bf16-exact values -> one word of packed bf16 (their high halves)
+__device__ __forceinline__ uint32_t hi_pair(float lo, float hi) {
+    return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
+}
 
 template <typename T> struct Frag;
 
@@ -29,6 +38,18 @@ template <> struct Frag<bf16_t> {
         return (u32x4_t){v[0] & m, v[1] & m, v[2] & m, v[3] & m};
     }
     static __device__ __forceinline__ f zero() { return (u32x4_t){0, 0, 0, 0}; }
+    static __device__ __forceinline__ void dq8(u32x4_t raw, f& f0, f& f1) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            f& o = h ? f1 : f0;
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                const uint32_t v = raw[2 * h + w];
+                o[2 * w] = hi_pair(i8f(v, 0), i8f(v, 1));
+                o[2 * w + 1] = hi_pair(i8f(v, 2), i8f(v, 3));
+            }
+        }
+    }
     static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
                                                        __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
@@ -55,6 +76,15 @@ template <> struct Frag<float> {
         f v;
         v.lo = v.hi = (f32x4_t){0.f, 0.f, 0.f, 0.f};
         return v;
+    }
+    static __device__ __forceinline__ void dq8(u32x4_t raw, f& f0, f& f1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f0.lo[j] = i8f(raw[0], j);
+            f0.hi[j] = i8f(raw[1], j);
+            f1.lo[j] = i8f(raw[2], j);
+            f1.hi[j] = i8f(raw[3], j);
+        }
     }
     static __device__ __forceinline__ f load_masked(const float* p, bool valid) {
         f v = load(p);

@@ -57,9 +57,13 @@ constexpr int GEMV_PRE = 8;   // (row, chunk) items of X preloaded per thread be
 constexpr int gemv_wpe(int pro, int epi) { return pro == PRO_PRENORM && epi == EPI_SWIGLU8 ? 5 : (pro == PRO_FATT ? 1 : 3); }
 
 // WPB waves per block share one 16-row tile, each streaming a contiguous run of its k-steps.
-template <typename T, int PRO, int EPI, bool NT, int U, int WPB>
+// Q8 (weight-only int8): the weight stream is a.Wq, one ring slot = one 64-k unit (1 KiB per wave,
+// as a T fragment is), dequantised exactly to two T fragments in registers; each output is
+// round(round(acc) * wscale[row]) (WeightOnlyInt8Linear.forward, quantize.py:228-229).
+template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(gemv_wpe(PRO, EPI))))
 void gemv_kernel(GemvArgs<T> a) {
+    static_assert(!(Q8 && (EPI == EPI_SWIGLU || EPI == EPI_SLAB || PRO == PRO_FATT)), "no int8 form");
     // X items preloaded per thread ahead of the weight ring: PRO_PRENORM's operand is one dim-wide
     // row per stream (2 items per thread at R = 1), and its register budget is what lets the
     // 1216-block W1||W3 grid stay resident (5 waves per SIMD)
@@ -71,7 +75,7 @@ void gemv_kernel(GemvArgs<T> a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n0 = blockIdx.x * 16;
     const int ks = blockIdx.y;
-    const int Kb = a.K / gridDim.y;  // host guarantees a multiple of 32
+    const int Kb = a.K / gridDim.y;  // host guarantees a multiple of 32 (64 with Q8)
     const int kbeg = ks * Kb;
     const int R = a.R;
     const int xstride = Kb + 8;  // +16 B per row: conflict-free ds_read_b128 across rows
@@ -84,20 +88,29 @@ void gemv_kernel(GemvArgs<T> a) {
     const unsigned long long ts0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long tsA = 0, tsB = 0;  // PRO_PRENORM: tile sums staged / X' written
     const int r = lane & 15, g = lane >> 4;
-    const int S = a.K >> 5, Sb = Kb >> 5, sb0 = ks * Sb;
+    constexpr int KU = Q8 ? 64 : 32;  // k per ring slot
+    const int S = a.K / KU, Sb = Kb / KU, sb0 = ks * Sb;
     const int wa = (wave * Sb) / WPB, wb = ((wave + 1) * Sb) / WPB, nmy = wb - wa;
-    typename G::f fa[U], fb[NACC == 2 ? U : 1];
+    typename G::f fa[Q8 ? 1 : U], fb[NACC == 2 ? U : 1];
+    u32x4_t fq[Q8 ? U : 1];
     // Fragment i of the run into ring slot u.  Branch-free on purpose: a load under a branch makes
     // the compiler drain vmcnt(0) before every MFMA (no pipelining at all), so tail slots re-load
     // the run's last fragment (a cache hit) instead of being predicated off.
     const int ilast = nmy > 0 ? nmy - 1 : 0;
-    const size_t run0 = ((size_t)blockIdx.x * S + sb0 + (nmy > 0 ? wa : 0)) * 512;
-    const T* wrun = a.W + run0;
+    const size_t run0 = ((size_t)blockIdx.x * S + sb0 + (nmy > 0 ? wa : 0)) * (Q8 ? 1024 : 512);
+    const T* wrun = Q8 ? nullptr : a.W + run0;
     const T* wrun2 = (EPI == EPI_SWIGLU) ? a.W2 + run0 : nullptr;
+    const unsigned char* qrun = Q8 ? a.Wq + run0 : nullptr;
     auto issue = [&](int i, int u) {
-        const size_t off = (size_t)(i < ilast ? i : ilast) * 512;
-        fa[u] = G::template load_w<NT>(wrun + off, lane);
-        if constexpr (NACC == 2) fb[u] = G::template load_w<NT>(wrun2 + off, lane);
+        const size_t ii = (size_t)(i < ilast ? i : ilast);
+        if constexpr (Q8) {
+            const u32x4_t* p = reinterpret_cast<const u32x4_t*>(qrun + ii * 1024 + lane * 16);
+            if constexpr (NT) fq[u] = __builtin_nontemporal_load(p);
+            else fq[u] = *p;
+        } else {
+            fa[u] = G::template load_w<NT>(wrun + ii * 512, lane);
+            if constexpr (NACC == 2) fb[u] = G::template load_w<NT>(wrun2 + ii * 512, lane);
+        }
     };
 
     // ---------------- prologue: X'[r][kbeg .. kbeg+Kb) -> LDS ----------------------------------
@@ -311,19 +324,31 @@ void gemv_kernel(GemvArgs<T> a) {
 
     const unsigned long long ts1 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     // ---------------- main loop: ring of U fragments per wave ------------------------------------
-    const T* xp = xs + (size_t)(r < R ? r : R - 1) * xstride + (size_t)wa * 32 + 8 * g;
+    const T* xp = xs + (size_t)(r < R ? r : R - 1) * xstride + (size_t)wa * KU + 8 * g;
     f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     for (int i = 0; i < nmy; i += U) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (i + u < nmy) {
-                const typename G::f xb = G::load(xp + (size_t)(i + u) * 32);
-                acc0 = G::mma(fa[u], xb, acc0);
-                if constexpr (NACC == 2) acc1 = G::mma(fb[u], xb, acc1);
+                if constexpr (Q8) {
+                    typename G::f w0, w1;
+                    G::dq8(fq[u], w0, w1);
+                    acc0 = G::mma(w0, G::load(xp + (size_t)(i + u) * 64), acc0);
+                    acc0 = G::mma(w1, G::load(xp + (size_t)(i + u) * 64 + 32), acc0);
+                } else {
+                    const typename G::f xb = G::load(xp + (size_t)(i + u) * 32);
+                    acc0 = G::mma(fa[u], xb, acc0);
+                    if constexpr (NACC == 2) acc1 = G::mma(fb[u], xb, acc1);
+                }
             }
             issue(i + u + U, u);
         }
     }
+    // weight-only int8 output: round(round(acc) * scale of the packed row)
+    auto wsc = [&](float v, int prow) {
+        if constexpr (Q8) return rnd<T>(rnd<T>(v) * ld(a.wscale, prow));
+        else return v;
+    };
     // cross-wave reduction: only the R live columns of the 16x16 accumulator tile go to LDS
     if ((lane & 15) < R) {
 #pragma unroll
@@ -366,6 +391,8 @@ void gemv_kernel(GemvArgs<T> a) {
                 v0 += red[(w * 16 + row) * R + col];
                 v1 += red[(w * 16 + row + 8) * R + col];
             }
+            v0 = wsc(v0, n0 + row);
+            v1 = wsc(v1, n0 + row + 8);
             st(a.Y, (size_t)col * a.ldy + n, rnd<T>(silu_g(rnd<T>(v0))) * rnd<T>(v1));
         }
         stamp();
@@ -393,6 +420,7 @@ void gemv_kernel(GemvArgs<T> a) {
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
         } else {
+            v0 = wsc(v0, n);
             if (a.bias) v0 += ld(a.bias, n);
             const size_t yi = (size_t)col * a.ldy + n;
             if constexpr (EPI == EPI_STORE) {
@@ -439,7 +467,7 @@ void gemv_kernel(GemvArgs<T> a) {
                     y += __hip_atomic_load(a.Yf + ((size_t)q * R + col) * a.ldy + n, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
             const int ri = a.residx ? a.residx[(size_t)col * a.xidx_ld + a.xidx_col] : col;
-            const float x = rnd<T>(ld(a.res + (size_t)ri * a.ldr, n) + rnd<T>(y));
+            const float x = rnd<T>(ld(a.res + (size_t)ri * a.ldr, n) + rnd<T>(wsc(y, n)));
             st(a.res_out, (size_t)col * a.ldro + n, x);
             float sq = x * x;
 #pragma unroll
@@ -450,17 +478,17 @@ void gemv_kernel(GemvArgs<T> a) {
     stamp();
 }
 
-template <typename T, int PRO, int EPI, bool NT, int U, int WPB>
+template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8 = false>
 static void gemv_launch(hipStream_t s, const GemvArgs<T>& a0, dim3 grid, size_t lds) {
     GemvArgs<T> a = a0;
     a.dbg = fm_tuning().dbg;
     static bool big = false;  // > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
     if (lds > 64 * 1024 && !big) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<T, PRO, EPI, NT, U, WPB>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<T, PRO, EPI, NT, U, WPB, Q8>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         big = true;
     }
-    gemv_kernel<T, PRO, EPI, NT, U, WPB><<<grid, WPB * 64, lds, s>>>(a);
+    gemv_kernel<T, PRO, EPI, NT, U, WPB, Q8><<<grid, WPB * 64, lds, s>>>(a);
 }
 
 template <typename T, int PRO, int EPI, bool NT, int U>
@@ -497,6 +525,13 @@ static void gemv_go(hipStream_t s, const GemvArgs<T>& a, int ksb) {
         gemv_go_u<T, PRO, EPI, false>(s, b, grid, lds);
 }
 
+// weight-only int8: one configuration (non-temporal, 8 units in flight per wave, 4 waves)
+template <typename T, int PRO, int EPI>
+static void gemv_go_q8(hipStream_t s, const GemvArgs<T>& a, int ksb) {
+    FMCHECK(a.K % (64 * ksb) == 0 && a.wscale, "int8 GEMV: K slices must be whole 64-k units, scales set");
+    gemv_launch<T, PRO, EPI, true, 8, 4, true>(s, a, dim3(FM_CEIL(a.N, 16), ksb), gemv_lds_bytes(a.R, a.K / ksb, sizeof(T)));
+}
+
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb) {
     // PRO_PRENORM stages the [K/16][R] tile sums in the 256 * R floats of the reduction buffer
     FMCHECK(pro != PRO_PRENORM || (a.K <= 4096 && a.R <= GEMV_RMAX), "PRO_PRENORM needs K <= 4096, R <= 8");
@@ -504,6 +539,18 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
                                 (a.K / ksb) % a.att.hd == 0 && a.att.hd % 16 == 0 && a.att.hd <= 16 * FATT_MAXPP &&
                                 a.att.ldqkv % 8 == 0),
             "PRO_FATT needs one row, cpos < 16, whole heads per K slice");
+    if (a.Wq) {
+#define GQ(P, E)                                           \
+    if (pro == P && epi == E) {                            \
+        gemv_go_q8<T, P, E>(s, a, ksb);                    \
+        return;                                            \
+    }
+        GQ(PRO_PLAIN, EPI_STORE) GQ(PRO_PLAIN, EPI_SLABFIN) GQ(PRO_PLAIN, EPI_F32)
+        GQ(PRO_NORM, EPI_STORE) GQ(PRO_NORM, EPI_F32)
+        GQ(PRO_PRENORM, EPI_STORE) GQ(PRO_PRENORM, EPI_F32) GQ(PRO_PRENORM, EPI_SWIGLU8)
+#undef GQ
+        FMCHECK(false, "int8 GEMV: no kernel for this prologue / epilogue");
+    }
 #define GO(P, E)                                           \
     if (pro == P && epi == E) {                            \
         gemv_go<T, P, E>(s, a, ksb);                       \

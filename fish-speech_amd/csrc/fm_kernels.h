@@ -13,6 +13,16 @@ enum { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_F32 = 3 };
 // the row-interleaved W1||W3 (batched path)
 template <typename T> void launch_swiglu_i8(hipStream_t s, const T* t, int ldt, T* act, int lda, int inter, int R);
 template <typename T> void launch_pack(hipStream_t s, const T* src, int N, int K, T* dst);
+// Weight-only int8 (tools/llama/quantize.py:22-52, 190-232).
+// quant_rows: per row n of a row-major [N][K] weight w (values as T): m = max(-min(min w, 0),
+// max(max w, 0)), s = max(m / 127.5, FLT_EPSILON) in fp32, q = clamp(rint(w / s), -128, 127);
+// writes q (int8 row-major), scale[n] = bf16(s) (held in T), and rewrites w with T(q) (exact).
+template <typename T> void launch_quant_rows(hipStream_t s, T* w, int N, int K, int8_t* q, T* scale);
+// int8 row-major -> T row-major (exact), for the kernels that read T fragments of q
+template <typename T> void launch_i8_to(hipStream_t s, const int8_t* q, int64_t n, T* dst);
+// int8 row-major [N][K] -> the int8 decode-GEMV layout: [ceil(N/16)][K/64] units of 1 KiB, lane l
+// (row l & 15, k-offset 8 * (l >> 4)) holding 8 bytes of k-step 2u then 8 bytes of k-step 2u + 1
+void launch_pack_q8(hipStream_t s, const int8_t* src, int N, int K, int8_t* dst);
 
 template <typename T> struct LinearArgs {
     const T* W;      // [N(padded to 16)][K] row-major (nn.Linear layout)
@@ -29,6 +39,9 @@ template <typename T> struct LinearArgs {
     // counter per 16-row tile (zero between launches; the last-arriving block resets it)
     float* part = nullptr;
     int* tickets = nullptr;
+    // weight-only int8 (tools/llama/quantize.py WeightOnlyInt8Linear): W holds the int8 values
+    // exactly and every output is round(round(acc) * wscale[n]) (not with EPI_SWIGLU)
+    const T* wscale = nullptr;
 };
 
 template <typename T> struct QkArgs {
@@ -178,6 +191,10 @@ template <typename T> struct GemvArgs {
     unsigned long long* dbg; // developer timestamps (fm_tune "debug_ts"); null in production
     FastFusedArgs<T> att;    // PRO_FATT: the fast-model attention the prologue recomputes
     int fatt_off;            // PRO_FATT: byte offset of the attention staging area in LDS (launcher)
+    // weight-only int8: Wq replaces W (packed [tiles][K/64][64 lanes][16 B], fm_kernels.h) and
+    // each output is round(round(acc) * wscale[packed row]) (WeightOnlyInt8Linear, quantize.py:228-229)
+    const unsigned char* Wq;
+    const T* wscale;
 };
 // developer knobs for the decode GEMV (fm_tune): weight load policy and split-K policy
 struct FmTuning {
@@ -221,6 +238,7 @@ template <typename T> struct BstreamArgs {
     int ldy;         // also the row stride of Yf
     float* Yf;       // EPI_F32 [R][ldy] | EPI_SLAB partial slabs [kparts][R][ldy]
     int kparts = 1;  // set by the launcher from the plan
+    const T* wscale = nullptr;  // weight-only int8 row scales (EPI_SLAB: applied by finalize_norm)
 };
 struct BstreamPlan {
     bool ok = false;
@@ -241,6 +259,7 @@ template <typename T> struct FinalizeArgs {
     float eps;
     T* xn_out;          // [R][ldxn]
     int ldxn, d, R;
+    const T* wscale = nullptr;  // weight-only int8: round(res + round(round(sum) * wscale[n]))
 };
 template <typename T> void launch_finalize_norm(hipStream_t s, const FinalizeArgs<T>& a);
 

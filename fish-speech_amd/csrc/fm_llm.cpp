@@ -120,12 +120,25 @@ struct fm_llm {
     std::map<int, hipGraphExec_t> graphs;
     Profiler prof;
     std::vector<void*> allocs;
+    // weight-only int8 (fm_llm_set_quant): packed T pointer of a linear -> its int8 form
+    int quant = FM_QUANT_NONE;
+    struct QInfo {
+        const unsigned char* q8 = nullptr;  // packed int8 decode-GEMV layout
+        const void* scale = nullptr;        // [rows padded to 16] in packed row order
+    };
+    std::map<const void*, QInfo> qmap;
+    const QInfo* qinfo(const void* W) const {
+        auto it = qmap.find(W);
+        return it == qmap.end() ? nullptr : &it->second;
+    }
 
     ~fm_llm() {
         if (device >= 0) (void)hipSetDevice(device);
         for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
-        for (auto& kv : w)
+        for (auto& kv : w) {
             if (kv.second.p) (void)hipFree(kv.second.p);
+            if (kv.second.q) (void)hipFree(kv.second.q);
+        }
         for (void* p : allocs) (void)hipFree(p);
         if (h_cols) (void)hipHostFree(h_cols);
         if (h_hist) (void)hipHostFree(h_hist);
@@ -226,6 +239,7 @@ template <typename T> struct Run {
             return;  // heads / fast_project_in of a batched frame
         LinearArgs<T> a{(const T*)W, (const T*)W2, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y,
                         ldy, (const T*)res, ldr, Yf};
+        if (const auto* q = m->qinfo(W)) a.wscale = (const T*)q->scale;
         if (R > GEMV_MAX_ROWS && R <= 64) {  // batched decode: split-K over the idle CUs
             FMCHECK(m->skpart_cap >= (long long)LINEAR_PART_CAP, "split-K partial buffer too small");
             a.part = m->skpart;
@@ -250,6 +264,7 @@ template <typename T> struct Run {
         int kparts = 0, d = 0, R = 0;
         void* res = nullptr;  // residual rows (h) ...
         void* out = nullptr;  // ... + round(sum of slabs) -> out (x)
+        const void* sc = nullptr;  // weight-only int8 row scales of w2
     } pend;
     // slow-model decode attention: attn_dec3 (registers, 64 positions per block) for the batched
     // frame (B=32: 35.7 vs 38.1 us per layer), attn_decode2 (LDS tiles, 32-row blocks) at B <= 8,
@@ -270,6 +285,7 @@ template <typename T> struct Run {
         const BstreamPlan p = bstream_plan(N, K, R, epi, E);
         if (!p.ok) return false;
         BstreamArgs<T> a{(const T*)W, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y, ldy, Yf};
+        if (const auto* q = m->qinfo(W)) a.wscale = (const T*)q->scale;
         const int64_t bytes = (int64_t)N * K * E + (int64_t)R * K * E +
                               (int64_t)R * N * (epi == EPI_SLAB ? 4 * p.kparts : (epi == EPI_F32 ? 4 : E));
         const double flops = 2.0 * R * N * K;
@@ -280,24 +296,28 @@ template <typename T> struct Run {
         if (kparts_out) *kparts_out = p.kparts;
         return true;
     }
+    const void* wscale(const void* W) const {
+        const auto* q = m->qinfo(W);
+        return q ? q->scale : nullptr;
+    }
     void finalize_norm(const float* slab, int kparts, const void* bias, const void* res, void* out, const void* nw,
-                       void* xn, int d, int R) {
+                       void* xn, int d, int R, const void* sc) {
         FinalizeArgs<T> f{slab, kparts, d, (const T*)bias, (const T*)res, d, (T*)out, d, (const T*)nw,
-                          m->c.norm_eps, (T*)xn, d, d, R};
+                          m->c.norm_eps, (T*)xn, d, d, R, (const T*)sc};
         m->prof.run(s, "norm", 0, 0, [&] { launch_finalize_norm<T>(s, f); });
     }
     // finalise a W2 left pending by the last block of a stack (no norm)
     void flush() {
         if (!pend.on) return;
         pend.on = false;
-        finalize_norm(pend.slab, pend.kparts, nullptr, pend.res, pend.out, nullptr, nullptr, pend.d, pend.R);
+        finalize_norm(pend.slab, pend.kparts, nullptr, pend.res, pend.out, nullptr, nullptr, pend.d, pend.R, pend.sc);
     }
     // the stack's input rows x are final unless a previous block left W2 pending on them
     void bs_norm_in(const StackDims& d, const LayerW& L, int R, void* xb, void* xnb) {
         if (pend.on) {
             FMCHECK(pend.out == xb && pend.R == R && pend.d == d.dim, "bstream: pending residual mismatch");
             pend.on = false;
-            finalize_norm(pend.slab, pend.kparts, nullptr, pend.res, xb, L.an, xnb, d.dim, R);
+            finalize_norm(pend.slab, pend.kparts, nullptr, pend.res, xb, L.an, xnb, d.dim, R, pend.sc);
         } else {
             m->prof.run(s, "norm", 0, 0, [&] {
                 launch_rmsnorm<T>(s, (const T*)xb, d.dim, (const T*)L.an, d.dim, m->c.norm_eps, (T*)xnb, d.dim, R);
@@ -361,7 +381,7 @@ template <typename T> struct Run {
         }
         int kp = 0;
         if (bs && bs_linear(L.wo, nullptr, m->att, d.nq(), R, d.dim, d.nq(), nullptr, d.dim, m->bsA, EPI_SLAB, &kp)) {
-            finalize_norm(m->bsA, kp, L.bo, xb, hb, L.fn, xnb, d.dim, R);  // h = x + wo(att); xn = ffn_norm(h)
+            finalize_norm(m->bsA, kp, L.bo, xb, hb, L.fn, xnb, d.dim, R, wscale(L.wo));  // h = x + wo(att); xn = ffn_norm(h)
         } else {
             linear(L.wo, nullptr, L.bo, m->att, d.nq(), R, d.dim, d.nq(), hb, d.dim, xb, d.dim, nullptr,
                    EPI_RESID, "linear");
@@ -385,6 +405,7 @@ template <typename T> struct Run {
             pend.R = R;
             pend.res = hb;
             pend.out = xb;
+            pend.sc = wscale(L.w2);
         } else {
             linear(L.w2, nullptr, nullptr, m->act, d.inter, R, d.dim, d.inter, xb, d.dim, hb, d.dim, nullptr,
                    EPI_RESID, "linear");
@@ -398,7 +419,12 @@ template <typename T> struct Run {
         return a;
     }
     void gemv(GemvArgs<T> a, int pro, int epi, int ksb, const char* cls) {
-        const int64_t wbytes = (int64_t)a.N * a.K * E * (epi == EPI_SWIGLU ? 2 : 1);
+        if (const auto* q = m->qinfo(a.W)) {  // weight-only int8: the int8 stream, whole 64-k units per slice
+            a.Wq = q->q8;
+            a.wscale = (const T*)q->scale;
+            while (ksb > 1 && (a.K / ksb) % 64) ksb /= 2;
+        }
+        const int64_t wbytes = (int64_t)a.N * a.K * (a.Wq ? 1 : E) * (epi == EPI_SWIGLU ? 2 : 1);
         const int64_t bytes = wbytes + (int64_t)a.R * a.K * E;
         const double flops = 2.0 * a.R * a.N * a.K * (epi == EPI_SWIGLU ? 2 : 1);
         hipStream_t st = s;
@@ -435,7 +461,7 @@ template <typename T> struct Run {
         fa.dbg = fm_tuning().dbg;
         // fast model: attention recomputed by every block of the Wo GEMV (PRO_FATT, one row) --
         // no attention launch (fm_tune attn_wo; measured slower, kept under test)
-        const bool att_wo = is_fast && fm_tuning().attn_wo && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
+        const bool att_wo = is_fast && fm_tuning().attn_wo && !m->quant && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
                             d.hd <= 128 && d.nh % d.nkv == 0 && (d.nq() / kp.wo) % d.hd == 0 && d.nqkv() % 8 == 0;
         // QKV (+ attention_norm)
         {
@@ -810,6 +836,55 @@ static bool is_linear_weight(const std::string& n) {
            n == "fast_project_in.weight";
 }
 
+// every nn.Linear of the model (WeightOnlyInt8QuantHandler quantizes them all, quantize.py:190-206);
+// the tied head is F.linear on the embedding table, not a module, and stays in T
+static bool is_quant_linear(const std::string& n) { return is_linear_weight(n) || n == "output.weight"; }
+static std::string base_of(const std::string& n) { return n.substr(0, n.size() - strlen(".weight")); }
+
+// int8 row-major [rows][cols] (rows padded to 16) -> packed int8 decode-GEMV layout
+static void* pack_q8_dev(fm_llm* m, const void* q, int rows, int cols) {
+    FMCHECK(cols % 64 == 0, "int8 weights need in_features % 64 == 0");
+    void* dst = nullptr;
+    HIPCHK(hipMalloc(&dst, (size_t)(rows + 15) / 16 * 16 * cols));
+    launch_pack_q8(m->stream, (const int8_t*)q, rows, cols, (int8_t*)dst);
+    HIPCHK(hipGetLastError());
+    m->allocs.push_back(dst);
+    return dst;
+}
+
+// int8 mode, before packing: every quantized linear ends with t.p = T(q) row-major (what the
+// T-fragment kernels read), t.q = int8 row-major, t.s = row scales.  int8 checkpoints supply q and
+// "<name>.scales"; float weights are quantized here with quantize.py's per-channel rule.
+static void quantize_linears(fm_llm* m) {
+    for (auto& kv : m->w) {
+        if (!is_quant_linear(kv.first)) continue;
+        DTensor& t = kv.second;
+        const size_t rp = (size_t)(t.rows + 15) / 16 * 16;
+        DTensor& sc = m->w.at(base_of(kv.first) + ".scales");
+        if (t.q) {
+            FMCHECK(sc.set, "int8 weight without scales: " + kv.first);
+            FMCHECK(!t.p, "tensor set twice: " + kv.first);
+            HIPCHK(hipMalloc(&t.p, rp * t.cols * m->esz));
+            if (m->prec == FM_PREC_BF16)
+                launch_i8_to<bf16_t>(m->stream, (const int8_t*)t.q, (int64_t)rp * t.cols, (bf16_t*)t.p);
+            else
+                launch_i8_to<float>(m->stream, (const int8_t*)t.q, (int64_t)rp * t.cols, (float*)t.p);
+            t.s = sc.p;
+        } else {
+            FMCHECK(!sc.set, "scales given with a float weight: " + kv.first);
+            HIPCHK(hipMalloc(&t.q, rp * t.cols));
+            HIPCHK(hipMemsetAsync(t.q, 0, rp * t.cols, m->stream));
+            t.s = m->dalloc(rp * m->esz);
+            if (m->prec == FM_PREC_BF16)
+                launch_quant_rows<bf16_t>(m->stream, (bf16_t*)t.p, (int)t.rows, (int)t.cols, (int8_t*)t.q, (bf16_t*)t.s);
+            else
+                launch_quant_rows<float>(m->stream, (float*)t.p, (int)t.rows, (int)t.cols, (int8_t*)t.q, (float*)t.s);
+        }
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(m->stream));
+}
+
 // row-major [rows][cols] device tensor -> packed fragment layout (fm_kernels.h)
 static void* pack_dev(fm_llm* m, const void* src, int rows, int cols) {
     const size_t n = (size_t)(rows + 15) / 16 * 16 * cols;
@@ -846,6 +921,24 @@ static void* pack_w13(fm_llm* m, const std::string& p, int inter, int dim) {
     HIPCHK(hipMemcpy2DAsync((char*)tmp + 8 * rb, 16 * rb, t3.p, 8 * rb, 8 * rb, inter / 8, hipMemcpyDeviceToDevice,
                             m->stream));
     void* pk = pack_dev(m, tmp, 2 * inter, dim);
+    if (m->quant) {  // the same interleave of the int8 rows and of the row scales
+        void* qt = nullptr;
+        HIPCHK(hipMalloc(&qt, 2 * (size_t)inter * dim));
+        HIPCHK(hipMemcpy2DAsync(qt, 16 * (size_t)dim, t1.q, 8 * (size_t)dim, 8 * (size_t)dim, inter / 8,
+                                hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpy2DAsync((char*)qt + 8 * (size_t)dim, 16 * (size_t)dim, t3.q, 8 * (size_t)dim,
+                                8 * (size_t)dim, inter / 8, hipMemcpyDeviceToDevice, m->stream));
+        void* s13 = m->dalloc(2 * (size_t)inter * E);
+        HIPCHK(hipMemcpy2DAsync(s13, 16 * E, t1.s, 8 * E, 8 * E, inter / 8, hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpy2DAsync((char*)s13 + 8 * E, 16 * E, t3.s, 8 * E, 8 * E, inter / 8, hipMemcpyDeviceToDevice,
+                                m->stream));
+        m->qmap[pk] = fm_llm::QInfo{(const unsigned char*)pack_q8_dev(m, qt, 2 * inter, dim), s13};
+        HIPCHK(hipStreamSynchronize(m->stream));
+        HIPCHK(hipFree(qt));
+        HIPCHK(hipFree(t1.q));
+        HIPCHK(hipFree(t3.q));
+        t1.q = t3.q = nullptr;
+    }
     HIPCHK(hipStreamSynchronize(m->stream));
     HIPCHK(hipFree(tmp));
     HIPCHK(hipFree(t1.p));
@@ -858,11 +951,18 @@ static void* pack_w13(fm_llm* m, const std::string& p, int inter, int dim) {
 static void finalize(fm_llm* m) {
     if (m->finalized) return;
     const fm_model_config& c = m->c;
-    for (auto& kv : m->w) FMCHECK(kv.second.set, "tensor not set: " + kv.first);
+    for (auto& kv : m->w) FMCHECK(kv.second.set || kv.second.optional, "tensor not set: " + kv.first);
+    if (m->quant) quantize_linears(m);
     for (auto& kv : m->w) {
         if (!is_linear_weight(kv.first) || is_ffn_w13(kv.first)) continue;  // W1/W3: pack_w13 below
         DTensor& t = kv.second;
         void* pk = pack_dev(m, t.p, (int)t.rows, (int)t.cols);
+        if (m->quant) {
+            m->qmap[pk] = fm_llm::QInfo{(const unsigned char*)pack_q8_dev(m, t.q, (int)t.rows, (int)t.cols), t.s};
+            HIPCHK(hipStreamSynchronize(m->stream));
+            HIPCHK(hipFree(t.q));
+            t.q = nullptr;
+        }
         HIPCHK(hipStreamSynchronize(m->stream));
         HIPCHK(hipFree(t.p));
         t.p = pk;
@@ -886,11 +986,15 @@ static void finalize(fm_llm* m) {
     };
     stack("layers.", m->sd, m->slow);
     stack("fast_layers.", m->fdm, m->fast);
+    if (m->quant) {  // WeightOnlyInt8Linear has no bias (quantize.py:206-229): the checkpoint's are unused
+        for (auto* st : {&m->slow, &m->fast})
+            for (LayerW& L : *st) L.bqkv = L.bo = nullptr;
+    }
     m->emb = W(m, "embeddings.weight");
     m->cbemb = W(m, "codebook_embeddings.weight");
     m->norm = W(m, "norm.weight");
     m->fproj_w = Wopt(m, "fast_project_in.weight");
-    m->fproj_b = Wopt(m, "fast_project_in.bias");
+    m->fproj_b = m->quant ? nullptr : Wopt(m, "fast_project_in.bias");
     m->femb = W(m, "fast_embeddings.weight");
     m->fnorm = W(m, "fast_norm.weight");
     m->fout = W(m, "fast_output.weight");
@@ -909,6 +1013,23 @@ static void finalize(fm_llm* m) {
                           m->stream));
     m->head_c = pack_dev(m, head_rm, m->Nhead, c.dim);
     m->allocs.push_back(m->head_c);
+    if (m->quant && !c.tie_word_embeddings) {  // the same compact rows of the int8 head and its scales
+        DTensor& o = m->w.at("output.weight");
+        void* hq = m->dalloc((size_t)(m->Nhead + 15) / 16 * 16 * c.dim);
+        HIPCHK(hipMemcpyAsync(hq, (const char*)o.q + (size_t)c.semantic_begin_id * c.dim, (size_t)m->nsem * c.dim,
+                              hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpyAsync((char*)hq + (size_t)m->nsem * c.dim, (const char*)o.q + (size_t)c.im_end_id * c.dim,
+                              c.dim, hipMemcpyDeviceToDevice, m->stream));
+        void* hs = m->dalloc((size_t)(m->Nhead + 15) / 16 * 16 * m->esz);
+        HIPCHK(hipMemcpyAsync(hs, (const char*)o.s + (size_t)c.semantic_begin_id * m->esz, (size_t)m->nsem * m->esz,
+                              hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpyAsync((char*)hs + (size_t)m->nsem * m->esz, (const char*)o.s + (size_t)c.im_end_id * m->esz,
+                              m->esz, hipMemcpyDeviceToDevice, m->stream));
+        m->qmap[m->head_c] = fm_llm::QInfo{(const unsigned char*)pack_q8_dev(m, hq, m->Nhead, c.dim), hs};
+        HIPCHK(hipStreamSynchronize(m->stream));
+        HIPCHK(hipFree(o.q));
+        o.q = nullptr;
+    }
     // caches [slot][layer][kv][S][hd]
     const StackDims& d = m->sd;
     m->layer_stride = (size_t)d.nkv * m->S * d.hd;
@@ -1110,11 +1231,49 @@ int fm_llm_open(const fm_model_config* cfg, int device, int precision, int max_s
     });
 }
 
+int fm_llm_set_quant(fm_llm* m, int mode) {
+    return fm_guard([&] {
+        FMCHECK(m && (mode == FM_QUANT_NONE || mode == FM_QUANT_INT8), "bad arguments");
+        FMCHECK(!m->finalized, "weights are frozen after finalize");
+        for (auto& kv : m->w) FMCHECK(!kv.second.set, "set the quantization mode before any tensor");
+        if (mode == m->quant) return;
+        FMCHECK(m->quant == FM_QUANT_NONE, "quantization mode already set");
+        m->quant = mode;
+        std::vector<std::pair<std::string, int64_t>> add;
+        for (auto& kv : m->w) {
+            if (!is_quant_linear(kv.first)) continue;
+            FMCHECK(kv.second.cols % 64 == 0, "int8 weights need in_features % 64 == 0: " + kv.first);
+            add.emplace_back(base_of(kv.first) + ".scales", kv.second.rows);
+            auto b = m->w.find(base_of(kv.first) + ".bias");
+            if (b != m->w.end()) b->second.optional = true;
+        }
+        for (auto& a : add) {
+            add_t(m, a.first, 1, a.second);
+            m->w[a.first].optional = true;
+        }
+    });
+}
+
 int fm_llm_set_tensor(fm_llm* m, const char* name, const void* data, int dtype, int64_t numel) {
     return fm_guard([&] {
         FMCHECK(m && name && data, "null argument");
         FMCHECK(!m->finalized, "weights are frozen after finalize");
         HIPCHK(hipSetDevice(m->device));
+        if (dtype == FM_DT_I8) {  // an int8 checkpoint's weight (WeightOnlyInt8QuantHandler state_dict)
+            FMCHECK(m->quant == FM_QUANT_INT8 && is_quant_linear(name), std::string("int8 data for ") + name +
+                                                                             " needs fm_llm_set_quant(INT8) and a linear weight");
+            auto it = m->w.find(name);
+            FMCHECK(it != m->w.end() && it->second.numel == numel, std::string("unknown tensor or wrong numel: ") + name);
+            DTensor& t = it->second;
+            FMCHECK(!t.set, std::string("tensor set twice: ") + name);
+            const size_t bytes = (size_t)(t.rows + 15) / 16 * 16 * t.cols;
+            HIPCHK(hipMalloc(&t.q, bytes));
+            HIPCHK(hipMemsetAsync(t.q, 0, bytes, m->stream));
+            HIPCHK(hipMemcpyAsync(t.q, data, (size_t)numel, hipMemcpyHostToDevice, m->stream));
+            HIPCHK(hipStreamSynchronize(m->stream));
+            t.set = true;
+            return;
+        }
         DTensor& t = tensor_for(m, name, numel);
         const size_t sb = dtype == FM_DT_BF16 ? 2 : 4;
         void* tmp = nullptr;
@@ -1384,14 +1543,20 @@ int64_t fm_llm_frame_bytes(fm_llm* m, int n, int pos) {
     if (!m) return -1;
     const fm_model_config& c = m->c;
     const int64_t E = (int64_t)m->esz;
+    // weight-only int8: one byte per linear weight plus one T scale per output row
+    const int64_t WE = m->quant ? 1 : E, SE = m->quant ? E : 0;
+    const bool hq = m->quant && !c.tie_word_embeddings;
     auto stack_bytes = [&](const StackDims& d) {
-        int64_t per = (int64_t)d.nqkv() * d.dim + (int64_t)d.dim * d.nq() + 3LL * d.inter * d.dim + 2LL * d.dim;
-        if (d.qk_norm) per += 2LL * d.hd;
-        return per * d.n_layer * E;
+        const int64_t lin = (int64_t)d.nqkv() * d.dim + (int64_t)d.dim * d.nq() + 3LL * d.inter * d.dim;
+        const int64_t rows = (int64_t)d.nqkv() + d.dim + 3LL * d.inter;
+        int64_t per = lin * WE + rows * SE + 2LL * d.dim * E;
+        if (d.qk_norm) per += 2LL * d.hd * E;
+        return per * d.n_layer;
     };
-    int64_t b = stack_bytes(m->sd) + (int64_t)m->Nhead * c.dim * E + (int64_t)c.dim * E;  // slow + head + norm
-    b += (int64_t)m->C * stack_bytes(m->fdm) + (int64_t)(m->C - 1) * ((int64_t)m->cb * c.fast_dim + c.fast_dim) * E;
-    if (m->fproj_w) b += (int64_t)c.fast_dim * c.dim * E;
+    int64_t b = stack_bytes(m->sd) + (int64_t)m->Nhead * (c.dim * (hq ? 1 : E) + (hq ? E : 0)) + (int64_t)c.dim * E;
+    b += (int64_t)m->C * stack_bytes(m->fdm) +
+         (int64_t)(m->C - 1) * ((int64_t)m->cb * (c.fast_dim * WE + SE) + (int64_t)c.fast_dim * E);
+    if (m->fproj_w) b += (int64_t)c.fast_dim * (c.dim * WE + SE);
     // per-stream: KV reads (+ the row written), embeddings
     int64_t per_stream = 2LL * m->sd.n_layer * m->sd.nkv * m->sd.hd * E * (pos + 1);
     for (int cc = 0; cc < m->C; ++cc) per_stream += 2LL * m->fdm.n_layer * m->fdm.nkv * m->fdm.hd * E * (cc + 1);

@@ -170,6 +170,86 @@ template <typename T> void launch_pack(hipStream_t s, const T* src, int N, int K
 }
 template void launch_pack<bf16_t>(hipStream_t, const bf16_t*, int, int, bf16_t*);
 
+// ---- weight-only int8 (tools/llama/quantize.py) -----------------------------------------------
+// One block per row: dynamically_quantize_per_channel (quantize.py:22-52) with quant range
+// [-128, 127] on w.float(): the fp32 scale divides, the stored scale is bf16(s) (quantize.py:206 on
+// the bf16 model quantize.py loads), held in T.
+template <typename T>
+__global__ __launch_bounds__(256) void quant_rows_kernel(T* __restrict__ w, int K, int8_t* __restrict__ q,
+                                                         T* __restrict__ scale) {
+    __shared__ float rmn[8], rmx[8];
+    T* wr = w + (size_t)blockIdx.x * K;
+    float mn = INFINITY, mx = -INFINITY;
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+        const float v = ld(wr, k);
+        mn = fminf(mn, v);
+        mx = fmaxf(mx, v);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = fminf(mn, __shfl_xor(mn, o));
+        mx = fmaxf(mx, __shfl_xor(mx, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        rmn[threadIdx.x >> 6] = mn;
+        rmx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    mn = rmn[0];
+    mx = rmx[0];
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) {
+        mn = fminf(mn, rmn[i]);
+        mx = fmaxf(mx, rmx[i]);
+    }
+    const float m = fmaxf(-fminf(mn, 0.f), fmaxf(mx, 0.f));
+    const float sc = fmaxf(m / 127.5f, 1.1920928955078125e-07f);  // torch.finfo(float32).eps
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+        const float v = fminf(fmaxf(rintf(ld(wr, k) / sc), -128.f), 127.f);
+        q[(size_t)blockIdx.x * K + k] = (int8_t)v;
+        st(wr, k, v);
+    }
+    // quantize.py quantizes the bf16 model (quantize.py:441-446): scales are stored as bf16
+    if (threadIdx.x == 0) st(scale, blockIdx.x, rnd<bf16_t>(sc));
+}
+template <typename T> void launch_quant_rows(hipStream_t s, T* w, int N, int K, int8_t* q, T* scale) {
+    quant_rows_kernel<T><<<N, 256, 0, s>>>(w, K, q, scale);
+}
+
+template <typename T>
+__global__ void i8_to_kernel(const int8_t* __restrict__ q, int64_t n, T* __restrict__ dst) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        st(dst, i, (float)q[i]);
+}
+template <typename T> void launch_i8_to(hipStream_t s, const int8_t* q, int64_t n, T* dst) {
+    i8_to_kernel<T><<<(int)std::min<int64_t>(FM_CEIL(n, 256), 16384), 256, 0, s>>>(q, n, dst);
+}
+
+// one thread per (unit, lane): 16 bytes = k-steps 2u and 2u + 1 of row (l & 15), k-offset 8 * (l >> 4)
+__global__ void pack_q8_kernel(const int8_t* __restrict__ src, int N, int K, int8_t* __restrict__ dst) {
+    const int U = K >> 6;
+    const int64_t n = (int64_t)((N + 15) / 16) * U * 64;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t unit = i >> 6;
+        const int l = (int)(i & 63);
+        const int t = (int)(unit / U), u = (int)(unit - (int64_t)t * U);
+        const int row = 16 * t + (l & 15);
+        int8_t* d = dst + i * 16;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                d[8 * h + j] = row < N ? src[(size_t)row * K + 64 * u + 32 * h + 8 * (l >> 4) + j] : (int8_t)0;
+    }
+}
+void launch_pack_q8(hipStream_t s, const int8_t* src, int N, int K, int8_t* dst) {
+    const int64_t n = (int64_t)((N + 15) / 16) * (K / 64) * 64;
+    pack_q8_kernel<<<(int)std::min<int64_t>(FM_CEIL(n, 256), 16384), 256, 0, s>>>(src, N, K, dst);
+}
+template void launch_quant_rows<bf16_t>(hipStream_t, bf16_t*, int, int, int8_t*, bf16_t*);
+template void launch_quant_rows<float>(hipStream_t, float*, int, int, int8_t*, float*);
+template void launch_i8_to<bf16_t>(hipStream_t, const int8_t*, int64_t, bf16_t*);
+template void launch_i8_to<float>(hipStream_t, const int8_t*, int64_t, float*);
+
 template <typename T>
 __global__ void swiglu_i8_kernel(const T* __restrict__ t, int ldt, T* __restrict__ act, int lda, int inter, int R) {
     const int64_t n = (int64_t)R * inter;
@@ -194,6 +274,7 @@ __device__ __forceinline__ float silu_f(float a) { return a / (1.0f + expf(-a));
 template <typename T, int EPI>
 __device__ __forceinline__ void linear_epi(const LinearArgs<T>& a, int n, int col, float v0, float v1) {
     const size_t yi = (size_t)col * a.ldy + n;
+    if (a.wscale) v0 = rnd<T>(rnd<T>(v0) * ld(a.wscale, n));  // WeightOnlyInt8Linear (no bias)
     if (a.bias) v0 += ld(a.bias, n);
     if constexpr (EPI == EPI_STORE) {
         st(a.Y, yi, v0);

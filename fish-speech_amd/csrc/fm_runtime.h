@@ -87,6 +87,9 @@ struct DTensor {
     int64_t numel = 0;      // logical elements
     int64_t rows = 0, cols = 0;  // 2-D view (rows padded to 16 in the allocation)
     bool set = false;
+    bool optional = false;  // may stay unset (int8 mode: scales of float weights, dropped biases)
+    void* q = nullptr;      // int8 mode: row-major int8 values [rows padded to 16][cols]
+    void* s = nullptr;      //            per-row scales (storage type) [rows padded to 16]
 };
 
 // simple per-class profiler on HIP events (the stream the kernels run on)

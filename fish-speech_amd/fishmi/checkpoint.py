@@ -8,8 +8,8 @@
 * ``model.pth``: optional ``state_dict`` unwrap, ``model.`` prefix strip, ``audio_*`` keys
   dropped (llama.py:567-582) -- loaded with ``torch.load(weights_only=True)`` only.
 
-Tensors come back as numpy arrays: bf16 as uint16 bit patterns (``Tensor.bf16=True``),
-everything else as float32.  The safetensors reader is a plain header parse + mmap.
+Tensors come back as numpy arrays: bf16 as uint16 bit patterns (``Tensor.bf16=True``), int8
+(the weights of a tools/llama/quantize.py int8 checkpoint) as int8, everything else as float32.  The safetensors reader is a plain header parse + mmap.
 """
 from __future__ import annotations
 
@@ -29,13 +29,18 @@ from .synth import bf16_bits_to_f32, f32_to_bf16_bits
 _ST_DTYPES = {
     "F32": (np.float32, False), "F16": (np.float16, False), "BF16": (np.uint16, True),
     "F64": (np.float64, False), "I64": (np.int64, False), "I32": (np.int32, False),
+    "I8": (np.int8, False),
 }
 
 
 @dataclass
 class Tensor:
-    data: np.ndarray   # uint16 bits when bf16, else float32
+    data: np.ndarray   # uint16 bits when bf16, int8 for int8 weights, else float32
     bf16: bool
+
+    @property
+    def int8(self) -> bool:
+        return self.data.dtype == np.int8
 
     @property
     def shape(self):
@@ -63,7 +68,7 @@ def read_safetensors(path) -> "OrderedDict[str, Tensor]":
         dt, is_bf16 = _ST_DTYPES[meta["dtype"]]
         a, b = meta["data_offsets"]
         arr = np.frombuffer(mm[base + a: base + b], dtype=dt).reshape(meta["shape"])
-        if not is_bf16 and dt != np.float32:
+        if not is_bf16 and dt not in (np.float32, np.int8):
             arr = arr.astype(np.float32)
         out[name] = Tensor(arr, is_bf16)
     return out
@@ -92,7 +97,9 @@ def merge_qkv(weights: "OrderedDict[str, Tensor]"):
         p = k[: -len("wq.weight")]
         q, kk, v = weights.pop(p + "wq.weight"), weights.pop(p + "wk.weight"), weights.pop(p + "wv.weight")
         bf = q.bf16 and kk.bf16 and v.bf16
-        if bf:
+        if q.int8 and kk.int8 and v.int8:
+            data, bf = np.concatenate([q.data, kk.data, v.data], axis=0), False
+        elif bf:
             data = np.concatenate([q.data, kk.data, v.data], axis=0)
         else:
             data = np.concatenate([q.as_f32(), kk.as_f32(), v.as_f32()], axis=0)
@@ -101,8 +108,14 @@ def merge_qkv(weights: "OrderedDict[str, Tensor]"):
 
 
 def load_llm_weights(path) -> "OrderedDict[str, Tensor]":
+    """llama.py:545-584.  One deliberate difference: a directory named like a quantize.py int8 output
+    ("int8" in the path, llama.py:528) with a model.pth loads that file first.  quantize.py copies
+    the source checkpoint's files beside its model.pth (quantize.py:458-466), and the reference's
+    precedence would load the copied float shards into the int8 modules instead."""
     p = Path(path)
     index_json, single, pth = p / "model.safetensors.index.json", p / "model.safetensors", p / "model.pth"
+    if "int8" in str(p) and pth.exists():
+        index_json = single = p / "__none__"
     if index_json.exists():
         with open(index_json) as f:
             idx = json.load(f)
@@ -126,6 +139,8 @@ def load_llm_weights(path) -> "OrderedDict[str, Tensor]":
                 continue
             if v.dtype == torch.bfloat16:
                 weights[k] = Tensor(v.contiguous().view(torch.int16).numpy().view(np.uint16), True)
+            elif v.dtype == torch.int8:
+                weights[k] = Tensor(v.contiguous().numpy(), False)
             else:
                 weights[k] = Tensor(v.float().numpy(), False)
     else:

@@ -45,7 +45,7 @@ def resolve_im_end_id(path) -> Optional[int]:
 
 class DualARModel:
     def __init__(self, cfg: DualARConfig, device: int = 0, precision: str = "bf16",
-                 max_slots: int = 1):
+                 max_slots: int = 1, quant: Optional[str] = None):
         if cfg.im_end_id < 0:
             raise ValueError("config.im_end_id must be set (tokenizer's <|im_end|> id)")
         self.cfg = cfg
@@ -61,6 +61,11 @@ class DualARModel:
         prec = native.FM_PREC_BF16 if precision == "bf16" else native.FM_PREC_FP32
         native.check(L.fm_llm_open(ctypes.byref(self._c), device, prec, max_slots, ctypes.byref(h)))
         self.h = h
+        if quant not in (None, "int8"):
+            raise ValueError(f"quant must be None or 'int8', got {quant!r}")
+        self.quant = quant
+        if quant == "int8":  # WeightOnlyInt8QuantHandler.convert_for_runtime (llama.py:528-535)
+            native.check(L.fm_llm_set_quant(h, native.FM_QUANT_INT8))
         self._finalized = False
         self.tokenizer = None  # FishTokenizer when loaded from a checkpoint with tokenizer.json
 
@@ -83,16 +88,20 @@ class DualARModel:
         if im is None:
             raise ValueError(f"cannot resolve <|im_end|> id: no tokenizer.json in {path}; pass im_end_id")
         cfg.im_end_id = im
-        m = cls(cfg, device, precision, max_slots)
-        m.load_weights(load_llm_weights(path))
+        weights = load_llm_weights(path)
+        quant = "int8" if any(t.int8 for t in weights.values()) else None
+        m = cls(cfg, device, precision, max_slots, quant)
+        m.load_weights(weights)
         m.finalize()
         m.tokenizer = tok
         return m
 
     @classmethod
     def synthetic(cls, cfg: DualARConfig, seed: int, log2_half: int = 5, device: int = 0,
-                  precision: str = "bf16", max_slots: int = 1):
-        m = cls(cfg, device, precision, max_slots)
+                  precision: str = "bf16", max_slots: int = 1, quant: Optional[str] = None):
+        """Seeded weights at cfg's shapes; quant="int8" quantizes the linears at finalize with
+        quantize.py's per-channel rule."""
+        m = cls(cfg, device, precision, max_slots, quant)
         m.synth(seed, log2_half)
         m.finalize()
         return m
@@ -103,12 +112,20 @@ class DualARModel:
         missing = [k for k in shapes if k not in weights]
         if missing:
             raise KeyError(f"checkpoint lacks {len(missing)} tensors, e.g. {missing[:3]}")
-        for name in shapes:
+        names = list(shapes)
+        if self.quant == "int8":  # int8 checkpoints carry "<module>.scales" beside the int8 weights
+            names += [k for k in weights if k.endswith(".scales")]
+        elif any(weights[k].int8 for k in names):
+            raise ValueError("int8 weights need DualARModel(..., quant='int8')")
+        for name in names:
             t = weights[name]
             a = np.ascontiguousarray(t.data)
-            dt = native.FM_DT_BF16 if t.bf16 else native.FM_DT_F32
-            if not t.bf16:
-                a = np.ascontiguousarray(a, dtype=np.float32)
+            if t.int8:
+                dt = native.FM_DT_I8
+            else:
+                dt = native.FM_DT_BF16 if t.bf16 else native.FM_DT_F32
+                if not t.bf16:
+                    a = np.ascontiguousarray(a, dtype=np.float32)
             native.check(L.fm_llm_set_tensor(self.h, name.encode(), a.ctypes.data_as(ctypes.c_void_p),
                                              dt, a.size))
 

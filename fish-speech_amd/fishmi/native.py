@@ -14,13 +14,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfishmi.so")
 
 FM_PREC_BF16, FM_PREC_FP32 = 0, 1
-FM_DT_F32, FM_DT_BF16 = 0, 1
+FM_DT_F32, FM_DT_BF16, FM_DT_I8 = 0, 1, 2
+FM_QUANT_NONE, FM_QUANT_INT8 = 0, 1
 
 _lib = None
 
 # every symbol include/fishmi.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = [
-    "fm_device_count", "fm_last_error", "fm_llm_open", "fm_llm_set_tensor", "fm_llm_synth_tensor",
+    "fm_device_count", "fm_last_error", "fm_llm_open", "fm_llm_set_quant", "fm_llm_set_tensor", "fm_llm_synth_tensor",
     "fm_llm_finalize", "fm_llm_prefill", "fm_llm_decode", "fm_llm_decode_frames", "fm_llm_generate", "fm_llm_generate_at", "fm_llm_prefill_at", "fm_llm_slot_pos", "fm_llm_teacher_step",
     "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph", "fm_tune", "fm_debug_ts_read",
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
@@ -55,6 +56,7 @@ def lib():
     L.fm_last_error.restype = ctypes.c_char_p
     L.fm_device_count.restype = i32
     L.fm_llm_open.argtypes = [vp, i32, i32, i32, ctypes.POINTER(vp)]
+    L.fm_llm_set_quant.argtypes = [vp, i32]
     L.fm_llm_set_tensor.argtypes = [vp, ctypes.c_char_p, vp, i32, i64]
     L.fm_llm_synth_tensor.argtypes = [vp, ctypes.c_char_p, i64, u64, f32, i32]
     L.fm_llm_finalize.argtypes = [vp]

@@ -50,9 +50,14 @@ extern "C" {
 #define FM_PREC_BF16 0
 #define FM_PREC_FP32 1
 
-/* source dtype for fm_*_set_tensor */
+/* source dtype for fm_*_set_tensor (FM_DT_I8: int8 linear weights, fm_llm_set_quant INT8 only) */
 #define FM_DT_F32 0
 #define FM_DT_BF16 1
+#define FM_DT_I8 2
+
+/* weight-only quantization of the Dual-AR linears (fm_llm_set_quant) */
+#define FM_QUANT_NONE 0
+#define FM_QUANT_INT8 1
 
 /* == DualARModelArgs after from_pretrained (llama.py:27-193); im_end_id from the tokenizer. */
 typedef struct fm_model_config {
@@ -84,6 +89,16 @@ const char* fm_last_error(void);
 
 int fm_llm_open(const fm_model_config* cfg, int device, int precision, int max_slots,
                 fm_llm** out);
+/* Weight-only int8 linears, opt-in (replaces tools/llama/quantize.py WeightOnlyInt8QuantHandler
+   .convert_for_runtime + the int8 branch of from_pretrained, llama.py:528-535; quantize.py:190-232).
+   Call before any set_tensor.  Every nn.Linear (attention wqkv/wo, feed_forward w1/w2/w3 of both
+   stacks, output when untied, fast_project_in, fast_output) then takes either int8 data
+   (FM_DT_I8) plus "<module>.scales" [out_features], as quantize.py writes them, or float weights
+   that finalize quantizes per output channel with quantize.py's rule.  Outputs are
+   round(round(x . q) * scale) like WeightOnlyInt8Linear.forward; the linears' biases are unused
+   (that module has none).  Off the bf16 parity contract: parity is against the reference's own
+   int8 model. */
+int fm_llm_set_quant(fm_llm* h, int mode);
 /* name = reference state_dict key after remap (e.g. "layers.3.attention.wqkv.weight") */
 int fm_llm_set_tensor(fm_llm* h, const char* name, const void* host_data, int src_dtype,
                       int64_t numel);

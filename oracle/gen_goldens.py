@@ -628,6 +628,116 @@ def cmd_llm_wide():
 
 
 # --------------------------------------------------------------------------------------
+# Weight-only int8: tools/llama/quantize.py's WeightOnlyInt8QuantHandler
+# (create_quantized_state_dict on the bf16 model, as quantize.py:441-458 runs it, then
+# convert_for_runtime + load, llama.py:528-535) and the reference's generate / teacher forcing
+# on that int8 model.  llm_q: biases on qkv/o, an untied output head and fast_project_in (all
+# three nn.Linear -> WeightOnlyInt8Linear, biases dropped); every in_features a multiple of 64.
+# --------------------------------------------------------------------------------------
+LLM_Q_CONFIG = {
+    "model_type": "dual_ar",
+    "vocab_size": 400, "n_layer": 3, "n_head": 4, "n_local_heads": 2, "head_dim": 32,
+    "dim": 128, "intermediate_size": 256, "rope_base": 10000, "norm_eps": 1e-5,
+    "max_seq_len": 192, "tie_word_embeddings": False, "attention_qkv_bias": True,
+    "attention_o_bias": True, "attention_qk_norm": False, "codebook_size": 64,
+    "num_codebooks": 6, "semantic_begin_id": 300, "semantic_end_id": 363,
+    "n_fast_layer": 2, "fast_dim": 64, "fast_n_head": 2, "fast_n_local_heads": 1,
+    "fast_head_dim": 32, "fast_intermediate_size": 128, "scale_codebook_embeddings": False,
+    "norm_fastlayer_input": False,
+}
+
+
+def _quantize_module():
+    """tools/llama/quantize.py as shipped imports inference.load_model, which the reference's
+    inference.py no longer defines (it has init_model): the module fails to import.  Its quantization
+    classes do not use that name, so it is aliased before the import (test infrastructure only)."""
+    from fish_speech.models.text2semantic import inference
+
+    if not hasattr(inference, "load_model"):
+        inference.load_model = inference.init_model
+    from tools.llama import quantize
+
+    return quantize
+
+
+def int8_model(config, qsd, seed, log2_half, dtype):
+    """The reference's int8 model: modules converted, the quantized state_dict loaded."""
+    WeightOnlyInt8QuantHandler = _quantize_module().WeightOnlyInt8QuantHandler
+
+    model = build_llm(config, None, seed, log2_half)
+    model = WeightOnlyInt8QuantHandler(model).convert_for_runtime()
+    err = model.load_state_dict(qsd, strict=False, assign=True)
+    assert not err.missing_keys, err.missing_keys
+    assert all(k.endswith(".bias") for k in err.unexpected_keys), err.unexpected_keys
+    return model.to(dtype).eval()
+
+
+def quantized_state(config, seed, log2_half):
+    WeightOnlyInt8QuantHandler = _quantize_module().WeightOnlyInt8QuantHandler
+
+    model = build_llm(config, None, seed, log2_half).to(torch.bfloat16)
+    return WeightOnlyInt8QuantHandler(model).create_quantized_state_dict()
+
+
+def cmd_llm_int8():
+    from fish_speech.models.text2semantic import inference
+
+    qdir = os.path.join(GOLD, "llm_q_int8")
+    os.makedirs(qdir, exist_ok=True)
+    with open(os.path.join(qdir, "config.json"), "w") as f:
+        json.dump(LLM_Q_CONFIG, f, indent=1)
+    qsd = quantized_state(LLM_Q_CONFIG, 29, 3)
+    torch.save(OrderedDict((k, v.contiguous()) for k, v in qsd.items()), os.path.join(qdir, "model.pth"))
+    T, n_new = 19, 24
+    for dtype in (torch.float32, torch.bfloat16):
+        model = int8_model(LLM_Q_CONFIG, qsd, 29, 3, dtype)
+        prompt = make_prompt(model.config, T, 4)
+        seq = inference.generate(model=model, prompt=prompt.clone(), max_new_tokens=n_new,
+                                 audio_masks=None, audio_parts=None, temperature=0.7, top_p=0.9, top_k=1)
+        n = seq.shape[1] - T
+        slow, fast, hid = teacher_forced(model, seq, T, n, dtype)
+        tag = {torch.float32: "fp32", torch.bfloat16: "bf16"}[dtype]
+        extra = {}
+        if dtype == torch.bfloat16:
+            s32, f32, _ = teacher_forced(int8_model(LLM_Q_CONFIG, qsd, 29, 3, torch.float32), seq, T, n,
+                                         torch.float32)
+            extra = dict(slow_logits_f32=s32, fast_logits_f32=f32)
+        np.savez_compressed(os.path.join(GOLD, f"llm_q_int8_{tag}.npz"), prompt=prompt.numpy().astype(np.int32),
+                            seq=seq.numpy().astype(np.int32), slow_logits=slow, fast_logits=fast, hidden=hid,
+                            torch_version=torch.__version__, **extra)
+        print(f"llm_q_int8 {tag}: T={T} generated {n} frames; first columns", seq[:, T:T + 3].T.tolist())
+
+
+def cmd_llm_wide_int8():
+    """S2-Pro widths, int8: the same synthetic bf16 weights as llm_wide, quantized by the reference's
+    handler.  The build quantizes them on the device (quant_rows_kernel); only logits are stored."""
+    from fish_speech.models.text2semantic import inference
+
+    T = 64
+    qsd = quantized_state(LLM_WIDE_CONFIG, 41, 5)
+    model = int8_model(LLM_WIDE_CONFIG, qsd, 41, 5, torch.bfloat16)
+    cfg = model.config
+    prompt = make_prompt(cfg, T, 3)
+    t0 = time.time()
+    seq = inference.generate(model=model, prompt=prompt.clone(), max_new_tokens=9,
+                             audio_masks=None, audio_parts=None, temperature=0.7, top_p=0.9, top_k=1)
+    n = seq.shape[1] - T
+    slow, fast, hid = teacher_forced(model, seq, T, n, torch.bfloat16)
+    del model
+    s32, f32, _ = teacher_forced(int8_model(LLM_WIDE_CONFIG, qsd, 41, 5, torch.float32), seq, T, n, torch.float32)
+    keep = np.r_[IM_END_ID, cfg.semantic_begin_id:cfg.semantic_end_id + 1]
+    # per-tensor checksums of the reference's quantization (int8 sum, scale sum) for the device rule
+    sums = {k: (int(v.to(torch.int64).sum()), float(qsd[k[:-len("weight")] + "scales"].float().sum()))
+            for k, v in qsd.items() if v.dtype == torch.int8}
+    np.savez_compressed(os.path.join(GOLD, "llm_wide_int8_bf16.npz"),
+                        prompt=prompt.numpy().astype(np.int32), seq=seq.numpy().astype(np.int32),
+                        slow_rows=keep.astype(np.int32), slow_logits=slow[:, keep], fast_logits=fast,
+                        slow_logits_f32=s32[:, keep], fast_logits_f32=f32, synth_seed=41, log2_half=5,
+                        qsums=json.dumps(sums), torch_version=torch.__version__)
+    print(f"llm_wide_int8: {n} frames in {time.time() - t0:.1f}s; first cols", seq[:, T:T + 2].T.tolist())
+
+
+# --------------------------------------------------------------------------------------
 # Prompt side (SURVEY.md §8f row 2): the reference's own Conversation / ContentSequence
 # encode_for_inference and the speaker batching of generate_long (inference.py:454-651),
 # driven with a tiny local tokenizer (tests/golden/tok_tiny, written here) whose ids match the
@@ -792,6 +902,7 @@ if __name__ == "__main__":
     cmds = sys.argv[1:] or ["all"]
     if cmds == ["all"]:
         cmds = ["ops", "llm", "codec", "codec_full", "codec_long", "codec_enc", "codec_enc_full",
-                "codec_enc_long", "codec_keys", "llm_wide", "prompt", "engine", "engine_clone"]
+                "codec_enc_long", "codec_keys", "llm_wide", "llm_int8", "llm_wide_int8", "prompt", "engine",
+                "engine_clone"]
     for c in cmds:
         globals()[f"cmd_{c}"]()
