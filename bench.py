@@ -54,6 +54,8 @@ def parse():
                     help="config-5 leg: speaker turns (0: skip), each --longform-frames frames")
     ap.add_argument("--longform-frames", type=int, default=323, help="config-5 leg: frames per turn (15 s)")
     ap.add_argument("--no-int8", action="store_true", help="skip the opt-in weight-only int8 leg")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="fm_tune developer knob before the run (repeatable)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the in-run rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on the GEMV")
     ap.add_argument("--encode-seconds", type=float, default=30.0,
@@ -436,6 +438,11 @@ def main():
     from fishmi.config import S2_PRO_CONFIG, S2_PRO_IM_END_ID, CodecConfig, DualARConfig
     from fishmi.llm import DualARModel
 
+    from fishmi import native
+
+    for kv in args.tune:
+        k, v = kv.split("=")
+        native.tune(k, int(v))
     cfg = DualARConfig._from_fish_qwen3_omni(S2_PRO_CONFIG)
     cfg.im_end_id = S2_PRO_IM_END_ID
     cfg.max_seq_len = max(1024, args.prompt_len + args.frames + 8, 256 + args.batch_frames + 8)

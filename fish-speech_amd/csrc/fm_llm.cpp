@@ -98,6 +98,7 @@ struct fm_llm {
     int* attn_cnt = nullptr;
     float *ssX = nullptr, *ssH = nullptr;  // per-16-column tile sums of squares of the residual rows
     int* tickets = nullptr;               // EPI_SLABFIN / linear split-K arrival counters (zero between launches)
+    int* chain_done = nullptr;            // gemv_chain_kernel task counters [CHAIN_MAX] + error flag
     float* skpart = nullptr;              // linear_kernel split-K partial tiles
     long long skpart_cap = 0;             //   floats
     float *slabA = nullptr, *slabB = nullptr;  // split-K partials of wo / w2 (small-batch path)
@@ -251,7 +252,7 @@ template <typename T> struct Run {
         hipStream_t st = s;
         auto go = [st, a, epi] { launch_linear<T>(st, a, epi); };
         m->prof.record(cls, bytes, go);
-        m->prof.run(s, cls, bytes, flops, go);
+        run_(cls, bytes, flops, go);
     }
 
     // TransformerBlock.forward (llama.py:838-843) on R rows; x is updated in place.
@@ -292,7 +293,7 @@ template <typename T> struct Run {
         hipStream_t st = s;
         auto go = [st, a, epi, p] { FMCHECK(launch_bstream<T>(st, a, epi, p), "bstream: no kernel for the plan"); };
         m->prof.record("linear", bytes, go);
-        m->prof.run(s, "linear", bytes, flops, go);
+        run_("linear", bytes, flops, go);
         if (kparts_out) *kparts_out = p.kparts;
         return true;
     }
@@ -304,7 +305,7 @@ template <typename T> struct Run {
                        void* xn, int d, int R, const void* sc) {
         FinalizeArgs<T> f{slab, kparts, d, (const T*)bias, (const T*)res, d, (T*)out, d, (const T*)nw,
                           m->c.norm_eps, (T*)xn, d, d, R, (const T*)sc};
-        m->prof.run(s, "norm", 0, 0, [&] { launch_finalize_norm<T>(s, f); });
+        run_("norm", 0, 0, [&] { launch_finalize_norm<T>(s, f); });
     }
     // finalise a W2 left pending by the last block of a stack (no norm)
     void flush() {
@@ -319,7 +320,7 @@ template <typename T> struct Run {
             pend.on = false;
             finalize_norm(pend.slab, pend.kparts, nullptr, pend.res, xb, L.an, xnb, d.dim, R, pend.sc);
         } else {
-            m->prof.run(s, "norm", 0, 0, [&] {
+            run_("norm", 0, 0, [&] {
                 launch_rmsnorm<T>(s, (const T*)xb, d.dim, (const T*)L.an, d.dim, m->c.norm_eps, (T*)xnb, d.dim, R);
             });
         }
@@ -337,7 +338,7 @@ template <typename T> struct Run {
                        nullptr, EPI_STORE, "linear");
         } else {
             flush();
-            m->prof.run(s, "norm", 0, 0, [&] {
+            run_("norm", 0, 0, [&] {
                 launch_rmsnorm<T>(s, (const T*)xb, d.dim, (const T*)L.an, d.dim, eps, (T*)xnb, d.dim, R);
             });
             linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
@@ -358,25 +359,25 @@ template <typename T> struct Run {
             aa.cnt = m->attn_cnt;
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
-            m->prof.run(s, "attn", 0, 0, [&] { attn_slow(aa, R); });
+            run_("attn", 0, 0, [&] { attn_slow(aa, R); });
         } else if (is_fast && fm_tuning().batched_fused_attn && fixed_pos >= 0 && fixed_pos < 16 && d.hd <= 256) {
             FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), rslot, d.nh, d.nkv, d.hd, d.qk_norm, eps,
                                 (const T*)L.qn, (const T*)L.kn, rope, (T*)kc, (T*)vc, sstride, loff, Sc,
                                 fixed_pos, scale, (T*)m->att};
             fa.dbg = fm_tuning().dbg;
-            m->prof.run(s, "attn", 0, 0, [&] { launch_fast_attn2<T>(s, fa, R); });
+            run_("attn", 0, 0, [&] { launch_fast_attn2<T>(s, fa, R); });
         } else {
             QkArgs<T> qa{(const T*)m->qkv, d.nqkv(), rslot, rpos, fixed_pos, d.nh, d.nkv, d.hd, d.qk_norm,
                          eps, (const T*)L.qn, (const T*)L.kn, rope, (T*)m->q, (T*)kc, (T*)vc, sstride, loff, Sc};
-            m->prof.run(s, "rope", 0, 0, [&] { launch_qk_rope_cache<T>(s, qa, R); });
+            run_("rope", 0, 0, [&] { launch_qk_rope_cache<T>(s, qa, R); });
             if (!is_fast) {
                 AttnArgs<T> aa{(const T*)m->q, rslot, rpos, (const T*)kc, (const T*)vc, sstride, loff, Sc,
                                d.nh, d.nkv, d.hd, ATTN_SPLIT, m->maxsplit, scale, m->part};
-                m->prof.run(s, "attn", 0, 0, [&] { launch_attn<T>(s, aa, R, m->maxsplit, (T*)m->att); });
+                run_("attn", 0, 0, [&] { launch_attn<T>(s, aa, R, m->maxsplit, (T*)m->att); });
             } else {
                 FastAttnArgs<T> fa{(const T*)m->q, rslot, (const T*)kc, (const T*)vc, sstride, loff, Sc,
                                    d.nh, d.nkv, d.hd, fixed_pos, scale, (T*)m->att};
-                m->prof.run(s, "attn", 0, 0, [&] { launch_fast_attn<T>(s, fa, R); });
+                run_("attn", 0, 0, [&] { launch_fast_attn<T>(s, fa, R); });
             }
         }
         int kp = 0;
@@ -385,7 +386,7 @@ template <typename T> struct Run {
         } else {
             linear(L.wo, nullptr, L.bo, m->att, d.nq(), R, d.dim, d.nq(), hb, d.dim, xb, d.dim, nullptr,
                    EPI_RESID, "linear");
-            m->prof.run(s, "norm", 0, 0, [&] {
+            run_("norm", 0, 0, [&] {
                 launch_rmsnorm<T>(s, (const T*)hb, d.dim, (const T*)L.fn, d.dim, eps, (T*)xnb, d.dim, R);
             });
         }
@@ -393,7 +394,7 @@ template <typename T> struct Run {
                               EPI_SWIGLU8))) {
             linear(L.w13, nullptr, nullptr, xnb, d.dim, R, 2 * d.inter, d.dim, m->act2, 2 * d.inter, nullptr, 0,
                    nullptr, EPI_STORE, "linear");
-            m->prof.run(s, "other", 0, 0, [&] {
+            run_("other", 0, 0, [&] {
                 launch_swiglu_i8<T>(s, (const T*)m->act2, 2 * d.inter, (T*)m->act, d.inter, d.inter, R);
             });
         }
@@ -429,9 +430,78 @@ template <typename T> struct Run {
         const double flops = 2.0 * a.R * a.N * a.K * (epi == EPI_SWIGLU ? 2 : 1);
         hipStream_t st = s;
         if (!a.tickets) a.tickets = m->tickets;
+        if (chain_ok(a, pro, epi, ksb)) {
+            if (chn.n && (chn.q8 != (a.Wq != nullptr))) flush_chain();
+            chn.c.t[chn.n++] = GemvTask<T>{a, pro, epi, ksb};
+            chn.q8 = a.Wq != nullptr;
+            chn.bytes += bytes;
+            chn.flops += flops;
+            chn.lds = std::max(chn.lds, gemv_lds_bytes(a.R, a.K / ksb, E));
+            if (chn.n == CHAIN_MAX) flush_chain();
+            return;
+        }
+        flush_chain();
         auto go = [st, a, pro, epi, ksb] { launch_gemv<T>(st, a, pro, epi, ksb); };
         m->prof.record(cls, bytes, go);
         m->prof.run(s, cls, bytes, flops, go);
+    }
+    // ---- consecutive small-batch GEMVs as one persistent launch (gemv_chain_kernel) ----
+    struct ChainPend {
+        GemvChain<T> c{};
+        bool q8 = false;
+        int64_t bytes = 0;
+        double flops = 0;
+        size_t lds = 0;
+        int n = 0;
+    } chn;
+    bool chain_ok(const GemvArgs<T>& a, int pro, int epi, int ksb) const {
+        if (!fm_tuning().gemv_chain || fm_tuning().dbg || a.R > GEMV_MAX_ROWS || a.xidx || a.residx) return false;
+        if (!((pro == PRO_PLAIN && (epi == EPI_SLABFIN || epi == EPI_STORE)) ||
+              (pro == PRO_PRENORM && (epi == EPI_SWIGLU8 || epi == EPI_STORE || epi == EPI_F32))))
+            return false;
+        return a.K % (32 * ksb) == 0 && (pro != PRO_PRENORM || a.K <= 4096);
+    }
+    void flush_chain() {
+        if (!chn.n) return;
+        chn.c.n = chn.n;
+        chn.c.done = m->chain_done;
+        chn.c.next = m->chain_done + CHAIN_MAX;
+        chn.c.err = m->chain_done + 2 * CHAIN_MAX;
+        const int grid = gemv_chain_grid<T>(chn.lds, chn.q8);
+        const GemvChain<T> c = chn.c;
+        const bool q8 = chn.q8;
+        const size_t lds = chn.lds;
+        const int64_t bytes = chn.bytes;
+        const double flops = chn.flops;
+        chn = ChainPend{};
+        hipStream_t st = s;
+        if (grid == 0) {  // not enough resident blocks for a persistent launch: one kernel per task
+            for (int t = 0; t < c.n; ++t) {
+                const GemvTask<T> tk = c.t[t];
+                auto go = [st, tk] { launch_gemv<T>(st, tk.a, tk.pro, tk.epi, tk.ksb); };
+                m->prof.record("linear", 0, go);
+                m->prof.run(s, "linear", 0, 0, go);
+            }
+            return;
+        }
+        auto go = [st, c, q8, grid, lds] { launch_gemv_chain<T>(st, c, q8, grid, lds); };
+        if (m->prof.sync_debug > 0) {
+            go();
+            if (hipStreamSynchronize(s) != hipSuccess) {
+                for (int t = 0; t < c.n; ++t)
+                    fprintf(stderr, "faulting chain task %d/%d: pro %d epi %d R %d N %d K %d ksb %d grid %d lds %zu\n",
+                            t, c.n, c.t[t].pro, c.t[t].epi, c.t[t].a.R, c.t[t].a.N, c.t[t].a.K, c.t[t].ksb, grid, lds);
+                fflush(stderr);
+            }
+        }
+        m->prof.record("linear", bytes, go);
+        if (m->prof.sync_debug > 0) return;
+        m->prof.run(s, "linear", bytes, flops, go);
+    }
+    // every other launch of a Run goes through here, so a pending chain is issued before it
+    template <typename F> void run_(const char* cls, int64_t bytes, double flops, F&& f) {
+        flush_chain();
+        m->prof.run(s, cls, bytes, flops, std::forward<F>(f));
     }
     struct KsbPlan {
         int wo, w2;
@@ -481,6 +551,7 @@ template <typename T> struct Run {
                 a.xidx = xidx;
                 a.xidx_ld = C1;
                 a.xidx_col = xcol;
+                a.xidx_rows = xidx ? m->cb : 0;
                 gemv(a, PRO_NORM, epi, 1, "linear");
             } else {
                 a.X = (const T*)xb;
@@ -500,9 +571,9 @@ template <typename T> struct Run {
             aa.cnt = m->attn_cnt;
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
-            m->prof.run(s, "attn", 0, 0, [&] { attn_slow(aa, n); });
+            run_("attn", 0, 0, [&] { attn_slow(aa, n); });
         } else if (!att_wo) {
-            m->prof.run(s, "attn", 0, 0, [&] {
+            run_("attn", 0, 0, [&] {
                 if (cpos < 16 && d.hd <= 256)
                     launch_fast_attn2<T>(s, fa, n);
                 else
@@ -527,6 +598,7 @@ template <typename T> struct Run {
                 a.residx = xidx;
                 a.xidx_ld = C1;
                 a.xidx_col = xcol;
+                a.xidx_rows = xidx ? m->cb : 0;
             } else {
                 a.res = (const T*)xb;
                 a.ldr = d.dim;
@@ -654,20 +726,20 @@ template <typename T> struct Run {
     void frame_tail_small(int n, bool ras_enable, bool sample, const void* hidden) {
         if (sample) {
             SampleArgs a = sargs(true, ras_enable, 0);
-            m->prof.run(s, "sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
+            run_("sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
         }
         fast_small(n, 0, false, hidden);  // position 0 fills the fast KV cache; logits discarded
         for (int cc = 1; cc < m->C; ++cc) {
             fast_small(n, cc, true, hidden);
             if (sample) {
                 SampleArgs a = sargs(false, 0, cc);
-                m->prof.run(s, "sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
+                run_("sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
             }
         }
     }
 
     void decode_frame_small(int n) {
-        m->prof.run(s, "other", 0, 0, [&] {
+        run_("other", 0, 0, [&] {
             launch_embed<T>(s, m->tok_in, n, (const T*)m->emb, (const T*)m->cbemb, m->c.dim, m->C, m->cb,
                             m->c.semantic_begin_id, m->c.semantic_end_id, m->c.scale_codebook_embeddings,
                             (T*)m->x, m->frame_slot);
@@ -676,6 +748,7 @@ template <typename T> struct Run {
         const KsbPlan kp = plan(m->sd, n);
         const void* hid = head_small(nullptr, true, n, kp.w2);
         frame_tail_small(n, true, true, hid);
+        flush_chain();
         launch_finish(s, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10, m->C1,
                       1, m->sp);
     }
@@ -690,7 +763,7 @@ template <typename T> struct Run {
     // final norm -> constrained head logits; hidden for the fast model (llama.py:447-466, 826)
     void head_and_hidden(const void* xlast, int n) {
         const fm_model_config& c = m->c;
-        m->prof.run(s, "norm", 0, 0, [&] {
+        run_("norm", 0, 0, [&] {
             launch_rmsnorm<T>(s, (const T*)xlast, c.dim, (const T*)m->norm, c.dim, c.norm_eps, (T*)m->xnl,
                               c.dim, n);
         });
@@ -711,7 +784,7 @@ template <typename T> struct Run {
                   m->fslot_stride, (size_t)l * m->flayer_stride, m->C, m->frope, m->fx, m->fh, m->fxn);
         flush();
         if (with_head) {
-            m->prof.run(s, "norm", 0, 0, [&] {
+            run_("norm", 0, 0, [&] {
                 launch_rmsnorm<T>(s, (const T*)m->fx, c.fast_dim, (const T*)m->fnorm, c.fast_dim,
                                   c.norm_eps, (T*)m->fxn, c.fast_dim, n);
             });
@@ -751,17 +824,17 @@ template <typename T> struct Run {
     void frame_tail(int n, bool ras_enable, bool sample) {
         if (sample) {
             SampleArgs a = sargs(true, ras_enable, 0);
-            m->prof.run(s, "sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
+            run_("sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
         }
         fast_pass(n, 0, false);  // position 0: fills the fast KV cache, logits discarded
         for (int cc = 1; cc < m->C; ++cc) {
-            m->prof.run(s, "other", 0, 0, [&] {
-                launch_gather_rows<T>(s, m->cols, m->C1, cc, (const T*)m->femb, m->c.fast_dim, n, (T*)m->fx);
+            run_("other", 0, 0, [&] {
+                launch_gather_rows<T>(s, m->cols, m->C1, cc, (const T*)m->femb, m->c.fast_dim, m->cb, n, (T*)m->fx);
             });
             fast_pass(n, cc, true);
             if (sample) {
                 SampleArgs a = sargs(false, 0, cc);
-                m->prof.run(s, "sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
+                run_("sample", 0, 0, [&] { launch_sample_radix<T>(s, a, n); });
             }
         }
     }
@@ -771,7 +844,7 @@ template <typename T> struct Run {
             decode_frame_small(n);
             return;
         }
-        m->prof.run(s, "other", 0, 0, [&] {
+        run_("other", 0, 0, [&] {
             launch_embed<T>(s, m->tok_in, n, (const T*)m->emb, (const T*)m->cbemb, m->c.dim, m->C, m->cb,
                             m->c.semantic_begin_id, m->c.semantic_end_id, m->c.scale_codebook_embeddings,
                             (T*)m->x, m->frame_slot);
@@ -783,6 +856,7 @@ template <typename T> struct Run {
         head_and_hidden(m->x, n);
         frame_tail(n, true, true);
         bs_frame = false;
+        flush_chain();
         launch_finish(s, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10,
                       m->C1, 1, m->sp);
     }
@@ -1076,6 +1150,7 @@ static void finalize(fm_llm* m) {
         // arrival counters: one per 16-row tile of the largest decode GEMV (the slow head / W13)
         const int maxn = std::max({m->Nhead, 2 * c.intermediate_size, 2 * c.fast_intermediate_size, qkvmax, dmax, m->cb});  // W1||W3 is one 2*I-row linear on the batched path
         m->tickets = (int*)m->dalloc((size_t)(maxn / 16 + 16) * sizeof(int));
+        m->chain_done = (int*)m->dalloc(3 * CHAIN_MAX * sizeof(int));  // done[], next[], err
         m->skpart_cap = 8ll << 20;  // 32 MiB of partial tiles
         m->skpart = (float*)m->dalloc((size_t)m->skpart_cap * sizeof(float), false);
     }
@@ -1112,9 +1187,11 @@ template <typename F> static int with_prec(fm_llm* m, F&& f) {
     if (m->prec == FM_PREC_BF16) {
         Run<bf16_t> r(m);
         f(r);
+        r.flush_chain();
     } else {
         Run<float> r(m);
         f(r);
+        r.flush_chain();
     }
     return 0;
 }
@@ -1166,6 +1243,14 @@ static void upload_frame_rows(fm_llm* m, const int32_t* slots, int n) {
 }
 
 // one decode frame for the uploaded rows (graph replay when enabled), async
+// a gemv_chain_kernel wait that gave up (bounded spin) leaves its flag set: report, never hang
+static void check_chain(fm_llm* m) {
+    if (!m->chain_done) return;
+    int e = 0;
+    HIPCHK(hipMemcpy(&e, m->chain_done + 2 * CHAIN_MAX, sizeof(int), hipMemcpyDeviceToHost));
+    FMCHECK(e == 0, "gemv chain: a persistent wait timed out (results of the last frames are invalid)");
+}
+
 static void launch_frame(fm_llm* m, int n) {
     if (m->use_graph && !m->prof.on) {
         auto it = m->graphs.find(n);
@@ -1411,6 +1496,7 @@ int fm_llm_decode_frames(fm_llm* m, const int32_t* slots, int n, int nframes, in
             HIPCHK(hipMemcpyAsync(m->h_hist + per * k, m->cols, per * 4, hipMemcpyDeviceToHost, m->stream));
         }
         HIPCHK(hipStreamSynchronize(m->stream));
+        check_chain(m);
         m->prof.collect();
         for (int i = 0; i < n; ++i) {
             m->host_pos[slots[i]] += nframes;
@@ -1459,6 +1545,7 @@ static void do_generate(fm_llm* m, int slot, const int32_t* prompt, int T, int p
         m->prof.collect();
         (void)hipEventDestroy(ev[0]);
         (void)hipEventDestroy(ev[1]);
+        check_chain(m);
         m->host_pos[slot] = pos0 + T + issued;  // device advanced once per issued frame
         m->host_step[slot] = 1 + issued;
         m->uploaded_slots.clear();
@@ -1503,6 +1590,7 @@ int fm_llm_teacher_step(fm_llm* m, int slot, const int32_t* x, int S, int pos0, 
         with_prec(m, [&](auto& r) {
             const void* last = r.prefill_slow(slot, x, S, pos0);
             const void* hid = r.head_small(last, false, 1, 1);
+            r.flush_chain();
             HIPCHK(hipMemcpyAsync(lg.data(), m->logits, (size_t)m->Nhead * 4, hipMemcpyDeviceToHost, m->stream));
             if (hidden) {
                 std::vector<uint8_t> hb((size_t)c.fast_dim * m->esz);
@@ -1522,6 +1610,7 @@ int fm_llm_teacher_step(fm_llm* m, int slot, const int32_t* x, int S, int pos0, 
                 r.fast_small(1, 0, false, hid);
                 for (int cc = 1; cc < m->C; ++cc) {
                     r.fast_small(1, cc, true, hid);
+                    r.flush_chain();
                     if (fast_logits)
                         HIPCHK(hipMemcpyAsync(fast_logits + (size_t)(cc - 1) * m->cb, m->flogits, (size_t)m->cb * 4,
                                               hipMemcpyDeviceToHost, m->stream));
@@ -1598,6 +1687,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "attn_cap") {
             FMCHECK(value == 0 || (value >= 16 && value % 16 == 0), "attn_cap must be 0 or a multiple of 16");
             t.attn_cap = value;
+        } else if (k == "gemv_chain") {
+            t.gemv_chain = value != 0;
         } else if (k == "attn_wo") {
             t.attn_wo = value != 0;
         } else if (k == "gemv_wpb") {

@@ -64,9 +64,10 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
 template <typename T>
 __global__ __launch_bounds__(256) void gather_rows_kernel(const int32_t* __restrict__ codes,
                                                           int ldc, int col, const T* __restrict__ table,
-                                                          int d, T* __restrict__ x) {
+                                                          int d, int rows, T* __restrict__ x) {
     const int r = blockIdx.x;
-    const int c = codes[(size_t)r * ldc + col];
+    int c = codes[(size_t)r * ldc + col];
+    c = c < 0 ? 0 : (c >= rows ? rows - 1 : c);  // defence in depth: codes come from the sampler
     for (int i = threadIdx.x; i < d; i += blockDim.x) x[(size_t)r * d + i] = table[(size_t)c * d + i];
 }
 
@@ -808,8 +809,8 @@ void launch_embed(hipStream_t s, const int32_t* tok, int R, const T* emb, const 
 }
 template <typename T>
 void launch_gather_rows(hipStream_t s, const int32_t* codes, int ldc, int col, const T* table,
-                        int d, int R, T* x) {
-    gather_rows_kernel<T><<<R, 256, 0, s>>>(codes, ldc, col, table, d, x);
+                        int d, int rows, int R, T* x) {
+    gather_rows_kernel<T><<<R, 256, 0, s>>>(codes, ldc, col, table, d, rows, x);
 }
 template <typename T>
 void launch_rmsnorm(hipStream_t s, const T* x, int ldx, const T* w, int d, float eps, T* y,
@@ -904,7 +905,7 @@ void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* 
     template void launch_embed<T>(hipStream_t, const int32_t*, int, const T*, const T*, int, int, \
                                   int, int, int, int, T*, const int*);                           \
     template void launch_gather_rows<T>(hipStream_t, const int32_t*, int, int, const T*, int, int, \
-                                        T*);                                                     \
+                                        int, T*);                                                   \
     template void launch_rmsnorm<T>(hipStream_t, const T*, int, const T*, int, float, T*, int, int); \
     template void launch_linear<T>(hipStream_t, const LinearArgs<T>&, int);                      \
     template void launch_qk_rope_cache<T>(hipStream_t, const QkArgs<T>&, int);                   \

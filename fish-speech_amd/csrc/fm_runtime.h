@@ -1,5 +1,7 @@
 // fm_runtime.h -- host-side helpers shared by the LLM and codec runtimes of libfishmi.
 #pragma once
+#include <cstdio>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -129,7 +131,24 @@ struct Profiler {
         pool.pop_back();
         return e;
     }
+    // FISHMI_SYNC_DEBUG=1 (with FISHMI_GRAPH=0): synchronise after every launch and name the class
+    // of the first one that fails -- a developer aid for locating a device fault
+    int sync_debug = -1;
     template <typename F> void run(hipStream_t s, const char* cls, int64_t bytes, double flops, F&& f) {
+        if (sync_debug < 0) {
+            const char* e = getenv("FISHMI_SYNC_DEBUG");
+            sync_debug = e && e[0] == '1';
+        }
+        if (sync_debug) {
+            f();
+            const hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) {
+                fprintf(stderr, "FISHMI_SYNC_DEBUG: launch of class '%s' failed: %s\n", cls, hipGetErrorString(e));
+                fflush(stderr);
+                throw FmError{FM_ERR_HIP, std::string("device fault in class ") + cls};
+            }
+            return;
+        }
         if (!on) {
             f();
             return;
