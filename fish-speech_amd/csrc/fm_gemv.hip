@@ -22,8 +22,6 @@
 #include "fm_attn_dev.h"
 #include "fm_frag.h"
 
-#include <map>
-
 __device__ __forceinline__ float silu_g(float a) { return a / (1.0f + expf(-a)); }
 
 // 8 consecutive elements of T as raw 16-byte vectors (bf16: one, fp32: two)
@@ -52,51 +50,6 @@ template <typename T> __device__ __forceinline__ void c8_to_f(const C8<T>& c, fl
     }
 }
 
-// ---- hand-offs inside one launch (gemv_chain_kernel): another workgroup, possibly on another XCD,
-// wrote the operand, so it is read past the XCD's non-coherent L2 (sc1) and results are written
-// through (sc1); cdna_hip_programming.md §5, the write-through split-K form.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t coh_rsrc(const void* base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
-}
-template <typename T> __device__ __forceinline__ C8<T> load_c8_coh(const T* base, size_t elem) {
-    const __amdgpu_buffer_rsrc_t r = coh_rsrc(base);
-    const unsigned off = (unsigned)(elem * sizeof(T));
-    C8<T> c;
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 2); ++i)
-        c.v[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, off + 16 * i, 0, 16 /*sc1*/));
-    return c;
-}
-template <typename T> __device__ __forceinline__ float ld_coh(const T* p, size_t i) {
-    if constexpr (sizeof(T) == 2)
-        return __uint_as_float((uint32_t)__hip_atomic_load(reinterpret_cast<const unsigned short*>(p) + i,
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 16);
-    else
-        return __hip_atomic_load(reinterpret_cast<const float*>(p) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T> __device__ __forceinline__ void st_wt(T* p, size_t i, float v) {
-    if constexpr (sizeof(T) == 2)
-        __hip_atomic_store(reinterpret_cast<unsigned short*>(p) + i, (unsigned short)(__float_as_uint(rnd<T>(v)) >> 16),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        __hip_atomic_store(reinterpret_cast<float*>(p) + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// one thread polls the previous task's completion counter (bounded: a wedged chain reports through
-// err instead of hanging the device), then the block proceeds
-__device__ __forceinline__ void chain_wait(const int* cnt, int target, int* err) {
-    if (threadIdx.x == 0) {
-        int it = 0;
-        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++it > (1 << 23)) {
-                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-}
-
 constexpr int GEMV_RMAX = 8;  // rows (streams) of the small-batch path
 constexpr int GEMV_PRE = 8;   // (row, chunk) items of X preloaded per thread before the weight ring
 // occupancy target (waves per SIMD) of the tiled GEMV: the interleaved W1||W3 grid (1216 blocks of
@@ -107,14 +60,10 @@ constexpr int gemv_wpe(int pro, int epi) { return pro == PRO_PRENORM && epi == E
 // Q8 (weight-only int8): the weight stream is a.Wq, one ring slot = one 64-k unit (1 KiB per wave,
 // as a T fragment is), dequantised exactly to two T fragments in registers; each output is
 // round(round(acc) * wscale[row]) (WeightOnlyInt8Linear.forward, quantize.py:228-229).
-// PS (persistent, gemv_chain_kernel): the block runs tile bx / K slice ks of a task; the weight ring
-// is issued before it waits for the previous task (wait_cnt >= wait_target), operands written by
-// earlier tasks of the launch are read coherently and results written through.
-template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8, bool PS>
-__device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, const int ks, const int gy,
-                                          unsigned char* smem, const int* wait_cnt, int wait_target, int* err) {
+template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(gemv_wpe(PRO, EPI))))
+void gemv_kernel(GemvArgs<T> a) {
     static_assert(!(Q8 && (EPI == EPI_SWIGLU || EPI == EPI_SLAB || PRO == PRO_FATT)), "no int8 form");
-    static_assert(!PS || PRO == PRO_PLAIN || PRO == PRO_PRENORM, "chain tasks stage X from a previous task");
     // X items preloaded per thread ahead of the weight ring: PRO_PRENORM's operand is one dim-wide
     // row per stream (2 items per thread at R = 1), and its register budget is what lets the
     // 1216-block W1||W3 grid stay resident (5 waves per SIMD)
@@ -122,9 +71,11 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
     using G = Frag<T>;
     constexpr int NACC = (EPI == EPI_SWIGLU) ? 2 : 1;
     constexpr int NTH = WPB * 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int n0 = bx * 16;
-    const int Kb = a.K / gy;  // host guarantees a multiple of 32 (64 with Q8)
+    const int n0 = blockIdx.x * 16;
+    const int ks = blockIdx.y;
+    const int Kb = a.K / gridDim.y;  // host guarantees a multiple of 32 (64 with Q8)
     const int kbeg = ks * Kb;
     const int R = a.R;
     const int xstride = Kb + 8;  // +16 B per row: conflict-free ds_read_b128 across rows
@@ -146,7 +97,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
     // the compiler drain vmcnt(0) before every MFMA (no pipelining at all), so tail slots re-load
     // the run's last fragment (a cache hit) instead of being predicated off.
     const int ilast = nmy > 0 ? nmy - 1 : 0;
-    const size_t run0 = ((size_t)bx * S + sb0 + (nmy > 0 ? wa : 0)) * (Q8 ? 1024 : 512);
+    const size_t run0 = ((size_t)blockIdx.x * S + sb0 + (nmy > 0 ? wa : 0)) * (Q8 ? 1024 : 512);
     const T* wrun = Q8 ? nullptr : a.W + run0;
     const T* wrun2 = (EPI == EPI_SWIGLU) ? a.W2 + run0 : nullptr;
     const unsigned char* qrun = Q8 ? a.Wq + run0 : nullptr;
@@ -171,7 +122,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
         // weight ring starts after it (its block reductions would otherwise wait on weights)
         __shared__ float red_s[16];
         const int nch = a.K >> 3;
-        const bool writer = (bx == 0 && ks == 0);
+        const bool writer = (blockIdx.x == 0 && ks == 0);
         for (int rr = 0; rr < R; ++rr) {
             int xi = a.xidx ? a.xidx[(size_t)rr * a.xidx_ld + a.xidx_col] : rr;
             if (a.xidx_rows > 0) xi = xi < 0 ? 0 : (xi >= a.xidx_rows ? a.xidx_rows - 1 : xi);  // defence in depth
@@ -277,29 +228,18 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
         const int h0 = kbeg / hd, h1 = (kbeg + Kb) / hd;
         for (int hb = h0 + 8 * wave; hb < h1; hb += 8 * WPB)
             fast_attn_heads8_lds<T>(at, hb, h1, lane, raw_s, kv_s, qn_s, kn_s, tab_s, xs + (size_t)(hb - h0) * hd,
-                                    bx == 0, slot);
+                                    blockIdx.x == 0, slot);
     } else {
         // PRO_PLAIN / PRO_PRENORM: (row, 8-element chunk) items of the slice, up to PRE_N per
         // thread preloaded ahead of the weight ring (the rest, large R x Kb only, after it)
         const int nch = Kb >> 3, nitem = R * nch;
         C8<T> xc[PRE_N], wc[PRO == PRO_PRENORM ? PRE_N : 1];
-        // X of the slice: coherent in a chain (written by the previous task of the launch)
-        auto ldx8 = [&](int rr, int cc) {
-            const size_t e = (size_t)rr * a.ldx + kbeg + 8 * cc;
-            if constexpr (PS) return load_c8_coh(a.X, e);
-            else return load_c8(a.X + e);
-        };
-        if constexpr (PS) {  // the weight ring goes out before the wait on the producer task
-#pragma unroll
-            for (int u = 0; u < U; ++u) issue(u, u);
-            if (wait_cnt) chain_wait(wait_cnt, wait_target, err);
-        }
 #pragma unroll
         for (int q = 0; q < PRE_N; ++q) {
             const int it = threadIdx.x + NTH * q;
             if (it < nitem) {
                 const int rr = it / nch, cc = it - rr * nch;
-                xc[q] = ldx8(rr, cc);
+                xc[q] = load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc);
                 if constexpr (PRO == PRO_PRENORM) wc[q] = load_c8(a.nw + kbeg + 8 * cc);
             }
         }
@@ -314,14 +254,11 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
 #pragma unroll
             for (int q = 0; q < GEMV_SSQ; ++q) {
                 const int e = threadIdx.x + NTH * q;
-                if constexpr (PS) ssv[q] = ld_coh(a.ss_in, e < nss ? e : nss - 1);
-                else ssv[q] = a.ss_in[e < nss ? e : nss - 1];
+                ssv[q] = a.ss_in[e < nss ? e : nss - 1];
             }
         }
-        if constexpr (!PS) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) issue(u, u);
-        }
+        for (int u = 0; u < U; ++u) issue(u, u);
         if constexpr (PRO == PRO_PRENORM) {
             // stage the tile sums in `red` (free until the cross-wave reduction), then every wave
             // reduces each row's sums itself: per-row 1/rms in the wave's LDS slot (a register
@@ -331,8 +268,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
                 const int e = threadIdx.x + NTH * q;  // last sum (same value), and no branch lets
                 red[e < nss ? e : nss - 1] = ssv[q];  // the compiler sink a load past the ring
             }
-            for (int e = threadIdx.x + NTH * GEMV_SSQ; e < nss; e += NTH)  // R * K large
-                red[e] = PS ? ld_coh(a.ss_in, e) : a.ss_in[e];
+            for (int e = threadIdx.x + NTH * GEMV_SSQ; e < nss; e += NTH) red[e] = a.ss_in[e];  // R * K large
             __syncthreads();
             if (a.dbg) tsA = __builtin_amdgcn_s_memrealtime();
             const int nt = a.K >> 4;
@@ -346,7 +282,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
                 if (lane == 0) rsw[rr] = v;
             }
             __builtin_amdgcn_wave_barrier();
-            const bool writer = bx == 0 && ks == 0 && a.xn_out;
+            const bool writer = blockIdx.x == 0 && ks == 0 && a.xn_out;
             auto put = [&](int rr, int cc, const C8<T>& xq, const C8<T>& wq) {
                 float xv[8], wv[8];
                 c8_to_f(xq, xv);
@@ -357,14 +293,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
 #pragma unroll
                 for (int u = 0; u < 8; ++u) st(ov, u, rnd<T>(xv[u] * rs) * wv[u]);
                 *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) = o;  // one 16/32-B store
-                if (writer) {
-                    if constexpr (PS) {
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) st_wt(a.xn_out, (size_t)rr * a.ldxo + kbeg + 8 * cc + u, ld(ov, u));
-                    } else {
-                        *reinterpret_cast<C8<T>*>(a.xn_out + (size_t)rr * a.ldxo + kbeg + 8 * cc) = o;
-                    }
-                }
+                if (writer) *reinterpret_cast<C8<T>*>(a.xn_out + (size_t)rr * a.ldxo + kbeg + 8 * cc) = o;
             };
 #pragma unroll
             for (int q = 0; q < PRE_N; ++q) {
@@ -373,7 +302,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
             }
             for (int it = threadIdx.x + NTH * PRE_N; it < nitem; it += NTH) {
                 const int rr = it / nch, cc = it - rr * nch;
-                put(rr, cc, ldx8(rr, cc), load_c8(a.nw + kbeg + 8 * cc));
+                put(rr, cc, load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc), load_c8(a.nw + kbeg + 8 * cc));
             }
             if (a.dbg) tsB = __builtin_amdgcn_s_memrealtime();
         } else {
@@ -387,7 +316,8 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
             }
             for (int it = threadIdx.x + NTH * PRE_N; it < nitem; it += NTH) {  // large R x Kb
                 const int rr = it / nch, cc = it - rr * nch;
-                *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) = ldx8(rr, cc);
+                *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) =
+                    load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc);
             }
         }
     }
@@ -438,7 +368,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
             const unsigned long long slot = atomicAdd(a.dbg, 1ull);
             if (slot < (1ull << 20)) {
                 unsigned long long* q = a.dbg + 8 + slot * 8;
-                q[0] = ((unsigned long long)a.N << 32) | ((unsigned long long)ks << 16) | bx;
+                q[0] = ((unsigned long long)a.N << 32) | ((unsigned long long)blockIdx.y << 16) | blockIdx.x;
                 q[1] = ts0;
                 q[2] = ts1;
                 q[3] = ts2;
@@ -454,7 +384,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
     if constexpr (EPI == EPI_SWIGLU8) {  // rows 0-7 gate, 8-15 up of the same 8 outputs
         for (int o = threadIdx.x; o < 8 * R; o += NTH) {
             const int row = o / R, col = o - row * R;
-            const int n = bx * 8 + row;
+            const int n = blockIdx.x * 8 + row;
             if (n >= (a.N >> 1)) continue;
             float v0 = 0.f, v1 = 0.f;
 #pragma unroll
@@ -464,9 +394,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
             }
             v0 = wsc(v0, n0 + row);
             v1 = wsc(v1, n0 + row + 8);
-            const float yv = rnd<T>(silu_g(rnd<T>(v0))) * rnd<T>(v1);
-            if constexpr (PS) st_wt(a.Y, (size_t)col * a.ldy + n, yv);
-            else st(a.Y, (size_t)col * a.ldy + n, yv);
+            st(a.Y, (size_t)col * a.ldy + n, rnd<T>(silu_g(rnd<T>(v0))) * rnd<T>(v1));
         }
         stamp();
         return;
@@ -486,7 +414,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
             a.Yf[((size_t)ks * R + col) * a.ldy + n] = v0;
         } else if constexpr (EPI == EPI_SLABFIN) {
             if (a.bias && ks == 0) v0 += ld(a.bias, n);
-            if (gy == 1) {  // whole K in this block: finalise from LDS below
+            if (gridDim.y == 1) {  // whole K in this block: finalise from LDS below
                 fin[col * 16 + (n - n0)] = v0;
             } else {  // write-through (sc1) partial: visible to the tile's reducer without a fence
                 __hip_atomic_store(a.Yf + ((size_t)ks * R + col) * a.ldy + n, v0, __ATOMIC_RELAXED,
@@ -497,14 +425,12 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
             if (a.bias) v0 += ld(a.bias, n);
             const size_t yi = (size_t)col * a.ldy + n;
             if constexpr (EPI == EPI_STORE) {
-                if constexpr (PS) st_wt(a.Y, yi, v0);
-                else st(a.Y, yi, v0);
+                st(a.Y, yi, v0);
             } else if constexpr (EPI == EPI_SWIGLU) {
                 const float ga = rnd<T>(v0), ub = rnd<T>(v1);
                 st(a.Y, yi, rnd<T>(silu_g(ga)) * ub);
             } else {
-                if constexpr (PS) __hip_atomic_store(a.Yf + yi, rnd<T>(v0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else a.Yf[yi] = rnd<T>(v0);
+                a.Yf[yi] = rnd<T>(v0);
             }
         }
     }
@@ -514,15 +440,15 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
         // the consumer's RMSNorm.  Hand-off in its write-through form (cdna_hip_programming.md §5,
         // split-K recipe): sc1 partial stores drained by every wave, a relaxed agent ticket, sc1
         // loads in the reducer -- no release / acquire fence.  ksb == 1: straight from LDS.
-        const int ksb = gy;
+        const int ksb = gridDim.y;
         if (ksb > 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (ksb > 1) {
             if (threadIdx.x == 0) {
-                const int t = __hip_atomic_fetch_add(a.tickets + bx, 1, __ATOMIC_RELAXED,
+                const int t = __hip_atomic_fetch_add(a.tickets + blockIdx.x, 1, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
                 const int last = t == ksb - 1;
-                if (last) __hip_atomic_store(a.tickets + bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (last) __hip_atomic_store(a.tickets + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 flag[0] = last;
             }
             __syncthreads();
@@ -543,27 +469,15 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bx, co
                                            __HIP_MEMORY_SCOPE_AGENT);
             int ri = a.residx ? a.residx[(size_t)col * a.xidx_ld + a.xidx_col] : col;
             if (a.residx && a.xidx_rows > 0) ri = ri < 0 ? 0 : (ri >= a.xidx_rows ? a.xidx_rows - 1 : ri);
-            const float rv = PS ? ld_coh(a.res, (size_t)ri * a.ldr + n) : ld(a.res + (size_t)ri * a.ldr, n);
-            const float x = rnd<T>(rv + rnd<T>(wsc(y, n)));
-            if constexpr (PS) st_wt(a.res_out, (size_t)col * a.ldro + n, x);
-            else st(a.res_out, (size_t)col * a.ldro + n, x);
+            const float x = rnd<T>(ld(a.res + (size_t)ri * a.ldr, n) + rnd<T>(wsc(y, n)));
+            st(a.res_out, (size_t)col * a.ldro + n, x);
             float sq = x * x;
 #pragma unroll
             for (int m = 1; m < 16; m <<= 1) sq += __shfl_xor(sq, m);
-            if ((t & 15) == 0) {
-                if constexpr (PS) __hip_atomic_store(a.ss_out + (size_t)bx * R + col, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else a.ss_out[(size_t)bx * R + col] = sq;
-            }
+            if ((t & 15) == 0) a.ss_out[(size_t)blockIdx.x * R + col] = sq;
         }
     }
     stamp();
-}
-
-template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8>
-__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(gemv_wpe(PRO, EPI))))
-void gemv_kernel(GemvArgs<T> a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    gemv_body<T, PRO, EPI, NT, U, WPB, Q8, false>(a, blockIdx.x, blockIdx.y, gridDim.y, smem, nullptr, 0, nullptr);
 }
 
 template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8 = false>
@@ -654,87 +568,3 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
 
 template void launch_gemv<bf16_t>(hipStream_t, const GemvArgs<bf16_t>&, int, int, int);
 template void launch_gemv<float>(hipStream_t, const GemvArgs<float>&, int, int, int);
-
-// =============================================================================================
-// gemv_chain_kernel: consecutive decode GEMVs (fm_kernels.h GemvChain) in one persistent launch.
-// Every block is resident (grid from the occupancy query), tasks run in order, and each waits
-// only on its predecessor's counter, so no wait can block a producer.
-// =============================================================================================
-template <typename T, bool Q8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-void gemv_chain_kernel(GemvChain<T> c) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ int vb_s;
-    int wt = 0;  // virtual blocks of the previous task
-#pragma unroll 1
-    for (int t = 0; t < c.n; ++t) {
-        const GemvTask<T>& tk = c.t[t];
-        const int tiles = FM_CEIL(tk.a.N, 16), nvb = tiles * tk.ksb;
-        bool first = true;
-        // Virtual blocks are taken from a per-task counter, so only running blocks ever hold work
-        // and no resident block can wait on a block that was never scheduled.
-#pragma unroll 1
-        for (;;) {
-            if (threadIdx.x == 0) vb_s = __hip_atomic_fetch_add(c.next + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            const int vb = vb_s;
-            __syncthreads();  // vb_s is rewritten by the next take
-            if (vb >= nvb) break;
-            const int bx = vb % tiles, ks = vb / tiles;
-            const int* w = (t > 0 && first) ? c.done + (t - 1) : nullptr;
-            first = false;
-#define CB(P, E)                                                                                  \
-    if (tk.pro == P && tk.epi == E)                                                               \
-        gemv_body<T, P, E, true, 8, 4, Q8, true>(tk.a, bx, ks, tk.ksb, smem, w, wt, c.err);    \
-    else
-            CB(PRO_PLAIN, EPI_SLABFIN) CB(PRO_PRENORM, EPI_SWIGLU8) CB(PRO_PRENORM, EPI_STORE)
-            CB(PRO_PRENORM, EPI_F32) CB(PRO_PLAIN, EPI_STORE) {}
-#undef CB
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's write-through results landed
-            __syncthreads();
-            if (threadIdx.x == 0) __hip_atomic_fetch_add(c.done + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        wt = nvb;
-    }
-}
-
-template <typename T> int gemv_chain_grid(size_t lds, bool q8) {
-    static std::map<std::pair<size_t, bool>, int> memo;
-    auto it = memo.find({lds, q8});
-    if (it != memo.end()) return it->second;
-    int dev = 0, cus = 0, nb = 0;
-    HIPCHK(hipGetDevice(&dev));
-    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const void* k = q8 ? reinterpret_cast<const void*>(&gemv_chain_kernel<T, true>)
-                       : reinterpret_cast<const void*>(&gemv_chain_kernel<T, false>);
-    if (lds > 64 * 1024) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, lds) != hipSuccess) nb = 0;
-    const int g = nb >= 2 ? nb * cus : 0;
-    memo[{lds, q8}] = g;
-    return g;
-}
-
-template <typename T> void launch_gemv_chain(hipStream_t s, const GemvChain<T>& c, bool q8, int grid, size_t lds) {
-    FMCHECK(c.n >= 1 && c.n <= CHAIN_MAX && grid > 0 && c.done && c.next == c.done + CHAIN_MAX && c.err,
-            "gemv chain: bad plan");
-    for (int t = 0; t < c.n; ++t) {
-        const GemvArgs<T>& a = c.t[t].a;
-        FMCHECK(a.R >= 1 && a.R <= GEMV_RMAX && a.K % (32 * c.t[t].ksb) == 0 && (!q8 || (a.Wq && a.K % (64 * c.t[t].ksb) == 0)),
-                "gemv chain: task shape");
-        FMCHECK(c.t[t].pro != PRO_PRENORM || a.K <= 4096, "gemv chain: PRO_PRENORM needs K <= 4096");
-    }
-    HIPCHK(hipMemsetAsync(c.done, 0, 2 * CHAIN_MAX * sizeof(int), s));  // done[] and next[]
-    if (lds > 64 * 1024) {
-        const void* k = q8 ? reinterpret_cast<const void*>(&gemv_chain_kernel<T, true>)
-                           : reinterpret_cast<const void*>(&gemv_chain_kernel<T, false>);
-        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    }
-    if (q8)
-        gemv_chain_kernel<T, true><<<grid, 256, lds, s>>>(c);
-    else
-        gemv_chain_kernel<T, false><<<grid, 256, lds, s>>>(c);
-}
-template int gemv_chain_grid<bf16_t>(size_t, bool);
-template int gemv_chain_grid<float>(size_t, bool);
-template void launch_gemv_chain<bf16_t>(hipStream_t, const GemvChain<bf16_t>&, bool, int, size_t);
-template void launch_gemv_chain<float>(hipStream_t, const GemvChain<float>&, bool, int, size_t);

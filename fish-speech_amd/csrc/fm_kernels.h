@@ -211,7 +211,6 @@ struct FmTuning {
     int linear_u32 = 4;      // linear_kernel weight fragments in flight per wave at 16 < R <= 32 (4 or 8)
     int linear_fill = 0;     // batched linear_kernel: split K until this many blocks (0: never; measured slower)
     int attn3 = 1;           // 1: slow decode attention on attn_dec3_kernel, 0: attn_decode2_kernel
-    int gemv_chain = 0;      // 1: consecutive small-batch decode GEMVs run as one persistent launch (under validation)
     int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)
     int bstream_kparts = 0;  // bstream EPI_SLAB K parts (0: by K)
     int bstream_nw = 0;      // bstream waves per block (0: 16 whole-K, 8 split-K)
@@ -229,27 +228,6 @@ inline size_t gemv_lds_bytes(int R, int Kb, size_t esz) {
            8 * 8 * sizeof(float);
 }
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb);
-// A chain of decode GEMVs in ONE persistent launch (gemv_chain_kernel): grid = the resident
-// blocks; a block takes virtual blocks (tile, K slice) of each task in order from a per-task counter.
-// Before its first virtual block of task t a block issues that block's weight ring, then waits
-// until every virtual block of task t-1 has counted itself done (counters zeroed per launch), so
-// the weight stream runs across the producer->consumer seams that kernel boundaries stall on.
-// Tasks: PRO_PLAIN / PRO_PRENORM with EPI_SLABFIN / EPI_SWIGLU8 / EPI_STORE / EPI_F32.
-constexpr int CHAIN_MAX = 4;
-template <typename T> struct GemvTask {
-    GemvArgs<T> a;
-    int pro, epi, ksb;
-};
-template <typename T> struct GemvChain {
-    GemvTask<T> t[CHAIN_MAX];
-    int n;
-    int* done;  // [CHAIN_MAX] completion counters, zero at launch
-    int* next;  // [CHAIN_MAX] virtual-block take counters (= done + CHAIN_MAX), zero at launch
-    int* err;   // set when a wait gives up (bounded spin): the frame's results are invalid
-};
-// resident blocks for a chain needing `lds` bytes of LDS per block (0: cannot run persistent)
-template <typename T> int gemv_chain_grid(size_t lds, bool q8);
-template <typename T> void launch_gemv_chain(hipStream_t s, const GemvChain<T>& c, bool q8, int grid, size_t lds);
 
 // ---- batched decode weight streaming with register-resident X, 8 < R <= 32 (fm_bstream.hip) ---
 template <typename T> struct BstreamArgs {

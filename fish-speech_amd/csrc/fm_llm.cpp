@@ -98,7 +98,6 @@ struct fm_llm {
     int* attn_cnt = nullptr;
     float *ssX = nullptr, *ssH = nullptr;  // per-16-column tile sums of squares of the residual rows
     int* tickets = nullptr;               // EPI_SLABFIN / linear split-K arrival counters (zero between launches)
-    int* chain_done = nullptr;            // gemv_chain_kernel task counters [CHAIN_MAX] + error flag
     float* skpart = nullptr;              // linear_kernel split-K partial tiles
     long long skpart_cap = 0;             //   floats
     float *slabA = nullptr, *slabB = nullptr;  // split-K partials of wo / w2 (small-batch path)
@@ -430,77 +429,11 @@ template <typename T> struct Run {
         const double flops = 2.0 * a.R * a.N * a.K * (epi == EPI_SWIGLU ? 2 : 1);
         hipStream_t st = s;
         if (!a.tickets) a.tickets = m->tickets;
-        if (chain_ok(a, pro, epi, ksb)) {
-            if (chn.n && (chn.q8 != (a.Wq != nullptr))) flush_chain();
-            chn.c.t[chn.n++] = GemvTask<T>{a, pro, epi, ksb};
-            chn.q8 = a.Wq != nullptr;
-            chn.bytes += bytes;
-            chn.flops += flops;
-            chn.lds = std::max(chn.lds, gemv_lds_bytes(a.R, a.K / ksb, E));
-            if (chn.n == CHAIN_MAX) flush_chain();
-            return;
-        }
-        flush_chain();
         auto go = [st, a, pro, epi, ksb] { launch_gemv<T>(st, a, pro, epi, ksb); };
         m->prof.record(cls, bytes, go);
         m->prof.run(s, cls, bytes, flops, go);
     }
-    // ---- consecutive small-batch GEMVs as one persistent launch (gemv_chain_kernel) ----
-    struct ChainPend {
-        GemvChain<T> c{};
-        bool q8 = false;
-        int64_t bytes = 0;
-        double flops = 0;
-        size_t lds = 0;
-        int n = 0;
-    } chn;
-    bool chain_ok(const GemvArgs<T>& a, int pro, int epi, int ksb) const {
-        if (!fm_tuning().gemv_chain || fm_tuning().dbg || a.R > GEMV_MAX_ROWS || a.xidx || a.residx) return false;
-        if (!((pro == PRO_PLAIN && (epi == EPI_SLABFIN || epi == EPI_STORE)) ||
-              (pro == PRO_PRENORM && (epi == EPI_SWIGLU8 || epi == EPI_STORE || epi == EPI_F32))))
-            return false;
-        return a.K % (32 * ksb) == 0 && (pro != PRO_PRENORM || a.K <= 4096);
-    }
-    void flush_chain() {
-        if (!chn.n) return;
-        chn.c.n = chn.n;
-        chn.c.done = m->chain_done;
-        chn.c.next = m->chain_done + CHAIN_MAX;
-        chn.c.err = m->chain_done + 2 * CHAIN_MAX;
-        const int grid = gemv_chain_grid<T>(chn.lds, chn.q8);
-        const GemvChain<T> c = chn.c;
-        const bool q8 = chn.q8;
-        const size_t lds = chn.lds;
-        const int64_t bytes = chn.bytes;
-        const double flops = chn.flops;
-        chn = ChainPend{};
-        hipStream_t st = s;
-        if (grid == 0) {  // not enough resident blocks for a persistent launch: one kernel per task
-            for (int t = 0; t < c.n; ++t) {
-                const GemvTask<T> tk = c.t[t];
-                auto go = [st, tk] { launch_gemv<T>(st, tk.a, tk.pro, tk.epi, tk.ksb); };
-                m->prof.record("linear", 0, go);
-                m->prof.run(s, "linear", 0, 0, go);
-            }
-            return;
-        }
-        auto go = [st, c, q8, grid, lds] { launch_gemv_chain<T>(st, c, q8, grid, lds); };
-        if (m->prof.sync_debug > 0) {
-            go();
-            if (hipStreamSynchronize(s) != hipSuccess) {
-                for (int t = 0; t < c.n; ++t)
-                    fprintf(stderr, "faulting chain task %d/%d: pro %d epi %d R %d N %d K %d ksb %d grid %d lds %zu\n",
-                            t, c.n, c.t[t].pro, c.t[t].epi, c.t[t].a.R, c.t[t].a.N, c.t[t].a.K, c.t[t].ksb, grid, lds);
-                fflush(stderr);
-            }
-        }
-        m->prof.record("linear", bytes, go);
-        if (m->prof.sync_debug > 0) return;
-        m->prof.run(s, "linear", bytes, flops, go);
-    }
-    // every other launch of a Run goes through here, so a pending chain is issued before it
     template <typename F> void run_(const char* cls, int64_t bytes, double flops, F&& f) {
-        flush_chain();
         m->prof.run(s, cls, bytes, flops, std::forward<F>(f));
     }
     struct KsbPlan {
@@ -748,7 +681,6 @@ template <typename T> struct Run {
         const KsbPlan kp = plan(m->sd, n);
         const void* hid = head_small(nullptr, true, n, kp.w2);
         frame_tail_small(n, true, true, hid);
-        flush_chain();
         launch_finish(s, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10, m->C1,
                       1, m->sp);
     }
@@ -856,7 +788,6 @@ template <typename T> struct Run {
         head_and_hidden(m->x, n);
         frame_tail(n, true, true);
         bs_frame = false;
-        flush_chain();
         launch_finish(s, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10,
                       m->C1, 1, m->sp);
     }
@@ -1150,7 +1081,6 @@ static void finalize(fm_llm* m) {
         // arrival counters: one per 16-row tile of the largest decode GEMV (the slow head / W13)
         const int maxn = std::max({m->Nhead, 2 * c.intermediate_size, 2 * c.fast_intermediate_size, qkvmax, dmax, m->cb});  // W1||W3 is one 2*I-row linear on the batched path
         m->tickets = (int*)m->dalloc((size_t)(maxn / 16 + 16) * sizeof(int));
-        m->chain_done = (int*)m->dalloc(3 * CHAIN_MAX * sizeof(int));  // done[], next[], err
         m->skpart_cap = 8ll << 20;  // 32 MiB of partial tiles
         m->skpart = (float*)m->dalloc((size_t)m->skpart_cap * sizeof(float), false);
     }
@@ -1187,11 +1117,9 @@ template <typename F> static int with_prec(fm_llm* m, F&& f) {
     if (m->prec == FM_PREC_BF16) {
         Run<bf16_t> r(m);
         f(r);
-        r.flush_chain();
     } else {
         Run<float> r(m);
         f(r);
-        r.flush_chain();
     }
     return 0;
 }
@@ -1243,14 +1171,6 @@ static void upload_frame_rows(fm_llm* m, const int32_t* slots, int n) {
 }
 
 // one decode frame for the uploaded rows (graph replay when enabled), async
-// a gemv_chain_kernel wait that gave up (bounded spin) leaves its flag set: report, never hang
-static void check_chain(fm_llm* m) {
-    if (!m->chain_done) return;
-    int e = 0;
-    HIPCHK(hipMemcpy(&e, m->chain_done + 2 * CHAIN_MAX, sizeof(int), hipMemcpyDeviceToHost));
-    FMCHECK(e == 0, "gemv chain: a persistent wait timed out (results of the last frames are invalid)");
-}
-
 static void launch_frame(fm_llm* m, int n) {
     if (m->use_graph && !m->prof.on) {
         auto it = m->graphs.find(n);
@@ -1496,7 +1416,6 @@ int fm_llm_decode_frames(fm_llm* m, const int32_t* slots, int n, int nframes, in
             HIPCHK(hipMemcpyAsync(m->h_hist + per * k, m->cols, per * 4, hipMemcpyDeviceToHost, m->stream));
         }
         HIPCHK(hipStreamSynchronize(m->stream));
-        check_chain(m);
         m->prof.collect();
         for (int i = 0; i < n; ++i) {
             m->host_pos[slots[i]] += nframes;
@@ -1545,7 +1464,6 @@ static void do_generate(fm_llm* m, int slot, const int32_t* prompt, int T, int p
         m->prof.collect();
         (void)hipEventDestroy(ev[0]);
         (void)hipEventDestroy(ev[1]);
-        check_chain(m);
         m->host_pos[slot] = pos0 + T + issued;  // device advanced once per issued frame
         m->host_step[slot] = 1 + issued;
         m->uploaded_slots.clear();
@@ -1590,8 +1508,7 @@ int fm_llm_teacher_step(fm_llm* m, int slot, const int32_t* x, int S, int pos0, 
         with_prec(m, [&](auto& r) {
             const void* last = r.prefill_slow(slot, x, S, pos0);
             const void* hid = r.head_small(last, false, 1, 1);
-            r.flush_chain();
-            HIPCHK(hipMemcpyAsync(lg.data(), m->logits, (size_t)m->Nhead * 4, hipMemcpyDeviceToHost, m->stream));
+                HIPCHK(hipMemcpyAsync(lg.data(), m->logits, (size_t)m->Nhead * 4, hipMemcpyDeviceToHost, m->stream));
             if (hidden) {
                 std::vector<uint8_t> hb((size_t)c.fast_dim * m->esz);
                 HIPCHK(hipMemcpyAsync(hb.data(), hid, hb.size(), hipMemcpyDeviceToHost, m->stream));
@@ -1610,8 +1527,7 @@ int fm_llm_teacher_step(fm_llm* m, int slot, const int32_t* x, int S, int pos0, 
                 r.fast_small(1, 0, false, hid);
                 for (int cc = 1; cc < m->C; ++cc) {
                     r.fast_small(1, cc, true, hid);
-                    r.flush_chain();
-                    if (fast_logits)
+                                if (fast_logits)
                         HIPCHK(hipMemcpyAsync(fast_logits + (size_t)(cc - 1) * m->cb, m->flogits, (size_t)m->cb * 4,
                                               hipMemcpyDeviceToHost, m->stream));
                 }
@@ -1687,8 +1603,6 @@ int fm_tune(const char* key, int value) {
         } else if (k == "attn_cap") {
             FMCHECK(value == 0 || (value >= 16 && value % 16 == 0), "attn_cap must be 0 or a multiple of 16");
             t.attn_cap = value;
-        } else if (k == "gemv_chain") {
-            t.gemv_chain = value != 0;
         } else if (k == "attn_wo") {
             t.attn_wo = value != 0;
         } else if (k == "gemv_wpb") {

@@ -251,29 +251,6 @@ def test_wide_real_widths_production_decode_vs_reference(golden):
     m.close()
 
 
-@pytest.mark.parametrize("quant", [None, "int8"])
-def test_gemv_chain_bit_identical_to_per_kernel_launches(quant, golden, knob):
-    """S2-Pro widths, bf16, B=1: the persistent gemv_chain_kernel (Wo -> W13 -> W2 -> next QKV / head
-    in one launch, coherent operand reads, write-through results) computes exactly what one
-    gemv_kernel launch per GEMV computes: teacher-forced logits and free-running tokens identical."""
-    from fishmi.llm import DualARModel
-
-    g = golden("llm_wide_bf16.npz")
-    cfg = _cfg("llm_wide")
-    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 1, quant=quant)
-    T = g["prompt"].shape[1]
-    out = {}
-    for chain in (0, 1):
-        knob("gemv_chain", chain, 0)
-        slow, fast = m.teacher_decode(g["prompt"], g["seq"][:, T:])
-        toks = m.generate(g["prompt"], 12, top_k=30, seed=5, mask_im_end=True)
-        out[chain] = (slow, fast, toks)
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-    np.testing.assert_array_equal(out[0][1], out[1][1])
-    np.testing.assert_array_equal(out[0][2], out[1][2])
-    m.close()
-
-
 def test_wide_batched_32_slots_production_decode_vs_reference(golden):
     """BASELINE config 3's batched path at S2-Pro widths: 32 slots decoded together (batched MFMA
     linear_kernel, row RMSNorm, attn_decode2 one row per slot, hipGraph per frame), every slot
