@@ -386,12 +386,13 @@ __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
                 st(out, e2, o0 * il);
                 st(out, e2 + 1, o1 * il);
             } else {
+                // write-through (sc1): the combining block reads them back without a fence
                 float* pp = part + (size_t)hh * a.maxsplit * (hd + 2);
-                pp[2 + e2] = o0;
-                pp[3 + e2] = o1;
+                __hip_atomic_store(pp + 2 + e2, o0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(pp + 3 + e2, o1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (e2 == 0) {
-                    pp[0] = ml[2 * hh];
-                    pp[1] = ml[2 * hh + 1];
+                    __hip_atomic_store(pp, ml[2 * hh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(pp + 1, ml[2 * hh + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         }
@@ -402,34 +403,31 @@ __global__ __launch_bounds__(512) void attn_decode2_kernel(AttnDecArgs<T> a) {
         dbg_record(a.dbg, 0xFFFD, (unsigned)(nsp << 16 | nj), tz);
     }
     if (single) return;
-    // ---- split combine by the last-arriving block of (row, kv head)
+    // ---- split combine by the last-arriving block of (row, kv head): every wave drains its sc1
+    // partial stores, one lane takes a relaxed agent ticket, the last arriver reads the partials
+    // with sc1 loads (the write-through hand-off, MI355X_MICROARCH.md; no release / acquire fence)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int t = __hip_atomic_fetch_add(a.cnt + (size_t)r * a.nkv + kvh, 1, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
         flag[0] = t == nsp - 1;
-        if (t == nsp - 1) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(a.cnt + (size_t)r * a.nkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (t == nsp - 1) __hip_atomic_store(a.cnt + (size_t)r * a.nkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (!flag[0]) return;
+    auto ldp = [](const float* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     const float* p0 = a.part + (((size_t)r * a.nh + (size_t)kvh * g) * a.maxsplit) * (hd + 2);
     for (int idx = threadIdx.x; idx < g * hd; idx += 512) {
         const int hh = idx / hd, e = idx - hh * hd;
         const float* pp = p0 + (size_t)hh * a.maxsplit * (hd + 2);
         float M = -INFINITY;
-        for (int q = 0; q < nsp; ++q) M = fmaxf(M, pp[(size_t)q * (hd + 2)]);
+        for (int q = 0; q < nsp; ++q) M = fmaxf(M, ldp(pp + (size_t)q * (hd + 2)));
         float L = 0.f, O = 0.f;
         for (int q = 0; q < nsp; ++q) {
-            const float w = expf(pp[(size_t)q * (hd + 2)] - M);
-            L += w * pp[(size_t)q * (hd + 2) + 1];
-            O += w * pp[(size_t)q * (hd + 2) + 2 + e];
+            const float w = expf(ldp(pp + (size_t)q * (hd + 2)) - M);
+            L += w * ldp(pp + (size_t)q * (hd + 2) + 1);
+            O += w * ldp(pp + (size_t)q * (hd + 2) + 2 + e);
         }
         st(a.out + (size_t)r * a.nh * hd + (size_t)(kvh * g + hh) * hd, e, O / L);
     }

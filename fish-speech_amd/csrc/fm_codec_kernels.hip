@@ -15,6 +15,7 @@
 #include <algorithm>
 
 #include "fm_codec.h"
+#include "fm_kernels.h"
 #include "fm_runtime.h"
 #include "fm_frag.h"
 
@@ -374,7 +375,151 @@ __global__ void conv_weight_kernel(const float* __restrict__ w, int kind, int Ci
 }
 
 // ---------------------------------------------------------------------------------------
+// conv_gemm2_kernel: the same implicit GEMM (and epilogues) as conv_gemm_kernel with both operands
+// staged through LDS.  Block = 4 waves, tile 128 output times x 16*NCO channels; wave w owns times
+// [32w, 32w + 32) (two MFMA column tiles) against all NCO channel tiles, so per 32-wide k-step a
+// block reads its X rows (8 KB, one 16-B chunk of one row per thread per half) and the NCO packed
+// weight fragments once from L2 instead of once per wave.  Double-buffered: the next k-step's
+// global loads are in flight while the MFMAs of the current one read LDS; one barrier per step.
+// X rows are padded to 40 elements in LDS (80 B for bf16): the B-fragment reads of a wave (16 rows
+// x 16 B) spread over all banks.
+constexpr int CG2_BM = 128, CG2_XS = 40;
+template <typename T, int NCO>
+__global__ __launch_bounds__(256) void conv_gemm2_kernel(ConvArgs<T> a) {
+    using F = Frag<T>;
+    constexpr int XBUF = CG2_BM * CG2_XS, WBUF = NCO * 512;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_cg[];
+    T* lds = reinterpret_cast<T*>(smem_cg);  // [2][XBUF + WBUF]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t0 = blockIdx.x * CG2_BM;
+    const int co0 = blockIdx.y * 16 * NCO;
+    const int phase = blockIdx.z;
+    const int Kt = a.ntaps * a.Ci, S = (Kt + 31) >> 5;
+    const T* wb = a.w + (size_t)phase * a.wphase + (size_t)(co0 >> 4) * S * 512;
+    const int nct = min(NCO, (a.Co - co0 + 15) >> 4);  // channel tiles present in this block
+    constexpr int EC = 16 / (int)sizeof(T);             // elements per 16-B chunk
+    constexpr int XCH = CG2_BM * 32 / EC / 256;          // X chunks per thread per step (2 bf16, 4 fp32)
+    constexpr int WCH_T = NCO * 512 / EC;                // W chunks per step
+    constexpr int WCH = (WCH_T + 255) / 256;
+    u32x4_t xr[XCH], wr[WCH];
+    auto gload = [&](int s) {
+#pragma unroll
+        for (int j = 0; j < XCH; ++j) {
+            const int c = tid + 256 * j;
+            const int row = c / (32 / EC), kc = c - row * (32 / EC);
+            const int kl = s * 32 + kc * EC;
+            int tap = kl / a.Ci;
+            const bool kin = tap < a.ntaps;
+            tap = kin ? tap : a.ntaps - 1;
+            const int ci = kl - tap * a.Ci;
+            const int t = t0 + row, tin = t - a.shift[tap];
+            const bool ok = kin && t < a.Lq && tin >= a.lo && tin < a.Lx;
+            const int rc = tin < a.lo ? a.lo : (tin >= a.Lx ? a.Lx - 1 : tin);
+            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.x + (ptrdiff_t)rc * a.ldx + (ok ? ci : 0));
+            const uint32_t m = ok ? 0xffffffffu : 0u;
+            xr[j] = (u32x4_t){v[0] & m, v[1] & m, v[2] & m, v[3] & m};
+        }
+#pragma unroll
+        for (int j = 0; j < WCH; ++j) {
+            const int c = tid + 256 * j;
+            const int ct = c / (512 / EC);
+            if (c < WCH_T && ct < nct)
+                wr[j] = *reinterpret_cast<const u32x4_t*>(wb + ((size_t)ct * S + s) * 512 + (c - ct * (512 / EC)) * EC);
+            else
+                wr[j] = (u32x4_t){0u, 0u, 0u, 0u};
+        }
+    };
+    auto sstore = [&](int buf) {
+        T* xs = lds + (size_t)buf * (XBUF + WBUF);
+        T* ws = xs + XBUF;
+#pragma unroll
+        for (int j = 0; j < XCH; ++j) {
+            const int c = tid + 256 * j;
+            const int row = c / (32 / EC), kc = c - row * (32 / EC);
+            *reinterpret_cast<u32x4_t*>(xs + row * CG2_XS + kc * EC) = xr[j];
+        }
+#pragma unroll
+        for (int j = 0; j < WCH; ++j) {
+            const int c = tid + 256 * j;
+            if (c < WCH_T) *reinterpret_cast<u32x4_t*>(ws + (size_t)c * EC) = wr[j];
+        }
+    };
+    f32x4_t acc[NCO][2];
+#pragma unroll
+    for (int c = 0; c < NCO; ++c) acc[c][0] = acc[c][1] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    const int xrow0 = 32 * wave + (lane & 15), xk = 8 * (lane >> 4);
+    for (int s = 0; s < S; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < S) gload(s + 1);
+        const T* xs = lds + (size_t)buf * (XBUF + WBUF);
+        const T* ws = xs + XBUF;
+        const typename F::f xb0 = F::load(xs + xrow0 * CG2_XS + xk);
+        const typename F::f xb1 = F::load(xs + (xrow0 + 16) * CG2_XS + xk);
+#pragma unroll
+        for (int c = 0; c < NCO; ++c) {
+            if (c < nct) {
+                const typename F::f wf = F::load_w(ws + c * 512, lane);
+                acc[c][0] = F::mma(wf, xb0, acc[c][0]);
+                acc[c][1] = F::mma(wf, xb1, acc[c][1]);
+            }
+        }
+        if (s + 1 < S) sstore(buf ^ 1);
+        __syncthreads();
+    }
+    const int fl = a.flags;
+#pragma unroll
+    for (int c = 0; c < NCO; ++c) {
+        if (c >= nct) break;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int t = t0 + 32 * wave + 16 * u + (lane & 15);
+            if (t >= a.Lq) continue;
+            const int tout = t * a.stride + phase;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int co = co0 + 16 * c + 4 * (lane >> 4) + i;
+                if (co >= a.Co) continue;
+                float y = acc[c][u][i];
+                if (fl & CE_BIAS) y += ld(a.bias, co);
+                y = rnd<T>(y);
+                if (fl & CE_GELU) y = rnd<T>(0.5f * y * (1.0f + erff(y * 0.70710678118654752f)));
+                if (fl & CE_RES) {
+                    const float rv = ld(a.res, (size_t)tout * a.ldr + co);
+                    if (fl & CE_GAMMA) y = rnd<T>(rv + rnd<T>(ld(a.gamma, co) * y));
+                    else y = rnd<T>(rv + y);
+                }
+                if (fl & CE_TANH) y = tanhf(y);
+                if (fl & CE_STORE) {
+                    if (fl & CE_F32OUT) reinterpret_cast<float*>(a.out)[(size_t)tout * a.ldo + co] = y;
+                    else st(reinterpret_cast<T*>(a.out), (size_t)tout * a.ldo + co, y);
+                }
+                if (fl & CE_SNAKE) st(a.out2, (size_t)tout * a.ldo2 + co, snake_f(y, ld(a.alpha2, co)));
+            }
+        }
+    }
+}
+
+template <typename T, int NCO> static void conv2_go(hipStream_t s, const ConvArgs<T>& a) {
+    const size_t lds = 2 * ((size_t)CG2_BM * CG2_XS + NCO * 512) * sizeof(T);
+    dim3 g(FM_CEIL(a.Lq, CG2_BM), FM_CEIL(a.Co, 16 * NCO), a.nphase);
+    conv_gemm2_kernel<T, NCO><<<g, 256, lds, s>>>(a);
+}
+
 template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a) {
+    // LDS-staged tiles where the channels fill them (every decoder / transformer / upsample GEMM);
+    // the few narrow ones (encoder stem, 1-channel output conv) keep the register-only kernel
+    // (measured per shape, 10 s decode: 442k x 96 k7 282 vs 292 us, 221k x 192 371 vs 452, 55k x 384
+    // 348 vs 370, 6.9k x 768 192 vs 202; at 216-864 rows the LDS tile leaves too few blocks and loses)
+    if (fm_tuning().conv2 && a.Ci % 8 == 0 && a.Co % 16 == 0 && a.Co >= 96 && a.Lq >= 4096) {
+        if (a.Co % 128 == 0 || a.Co >= 384)
+            conv2_go<T, 8>(s, a);
+        else
+            conv2_go<T, 6>(s, a);
+        return;
+    }
     dim3 g(FM_CEIL(a.Lq, 64), FM_CEIL(a.Co, 64), a.nphase);
     conv_gemm_kernel<T><<<g, 256, 0, s>>>(a);
 }

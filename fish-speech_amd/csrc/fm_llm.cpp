@@ -443,8 +443,9 @@ template <typename T> struct Run {
     // cross-block hand-off) whenever the x slice fits the LDS budget, else split K
     KsbPlan plan(const StackDims& d, int n) {
         auto fin_ksb = [&](int N, int K) {
-            if (gemv_lds_bytes(n, K, E) <= 120 * 1024) return 1;
-            return pick_ksb(N, K, n, E);
+            // (splitting K further to fill more CUs measured slower at B = 1: 4.37 -> 4.74 ms per
+            // frame at 320 blocks, the split-K hand-off costs more than the idle CUs)
+            return gemv_lds_bytes(n, K, E) <= 120 * 1024 ? 1 : pick_ksb(N, K, n, E);
         };
         return KsbPlan{fin_ksb(d.dim, d.nq()), fin_ksb(d.dim, d.inter)};
     }
@@ -1603,6 +1604,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "attn_cap") {
             FMCHECK(value == 0 || (value >= 16 && value % 16 == 0), "attn_cap must be 0 or a multiple of 16");
             t.attn_cap = value;
+        } else if (k == "conv2") {
+            t.conv2 = value != 0;
         } else if (k == "attn_wo") {
             t.attn_wo = value != 0;
         } else if (k == "gemv_wpb") {
