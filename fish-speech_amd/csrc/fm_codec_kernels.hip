@@ -385,7 +385,7 @@ __global__ void conv_weight_kernel(const float* __restrict__ w, int kind, int Ci
 // x 16 B) spread over all banks.
 constexpr int CG2_BM = 128, CG2_XS = 40;
 template <typename T, int NCO>
-__global__ __launch_bounds__(256) void conv_gemm2_kernel(ConvArgs<T> a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv_gemm2_kernel(ConvArgs<T> a) {
     using F = Frag<T>;
     constexpr int XBUF = CG2_BM * CG2_XS, WBUF = NCO * 512;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_cg[];
