@@ -86,6 +86,16 @@ void gemv_kernel(GemvArgs<T> a) {
     float* rsl = fin + 16 * R;                        // [8 waves][GEMV_RMAX] PRO_PRENORM 1/rms
 
     const unsigned long long ts0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    // EPI_SLABFIN: the residual element this thread will finalise, loaded in the first round trip
+    // (unconditional, clamped index: a load under a branch drains vmcnt before the MFMAs)
+    float res_pre = 0.f;
+    if constexpr (EPI == EPI_SLABFIN) {
+        const int tt = min((int)threadIdx.x, 16 * a.R - 1);
+        const int col = tt >> 4, nn = min(blockIdx.x * 16 + (tt & 15), a.N - 1);
+        int ri = a.residx ? a.residx[(size_t)col * a.xidx_ld + a.xidx_col] : col;
+        if (a.residx && a.xidx_rows > 0) ri = ri < 0 ? 0 : (ri >= a.xidx_rows ? a.xidx_rows - 1 : ri);
+        res_pre = ld(a.res + (size_t)ri * a.ldr, nn);
+    }
     unsigned long long tsA = 0, tsB = 0;  // PRO_PRENORM: tile sums staged / X' written
     const int r = lane & 15, g = lane >> 4;
     constexpr int KU = Q8 ? 64 : 32;  // k per ring slot
@@ -467,9 +477,7 @@ void gemv_kernel(GemvArgs<T> a) {
                 for (int q = 0; q < ksb; ++q)
                     y += __hip_atomic_load(a.Yf + ((size_t)q * R + col) * a.ldy + n, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-            int ri = a.residx ? a.residx[(size_t)col * a.xidx_ld + a.xidx_col] : col;
-            if (a.residx && a.xidx_rows > 0) ri = ri < 0 ? 0 : (ri >= a.xidx_rows ? a.xidx_rows - 1 : ri);
-            const float x = rnd<T>(ld(a.res + (size_t)ri * a.ldr, n) + rnd<T>(wsc(y, n)));
+            const float x = rnd<T>(res_pre + rnd<T>(wsc(y, n)));
             st(a.res_out, (size_t)col * a.ldro + n, x);
             float sq = x * x;
 #pragma unroll
