@@ -1,13 +1,14 @@
 // fm_attn.hip -- decode attention with the qk-norm / RoPE / KV-cache write fused in, and the
 // radix-select sampler.
 //
-//   attn_decode_kernel  slow model, one row per stream: grid (R, nkv, splits of 64 positions).
-//                       The block of the split holding `pos` normalises+ropes k and v of the new
-//                       position (llama.py:894-910), writes them to the cache (llama.py:205-214)
-//                       and uses them from LDS; every block ropes its GQA group's q heads.  K/V
-//                       tiles are staged once per block in LDS (padded rows) and shared by the
-//                       group's q heads (no repeat_interleave, llama.py:912-913).  Output: split
-//                       partials (m, l, o) combined by attn_combine_kernel (fm_llm_kernels.hip).
+//   attn_fd_kernel      slow model, every batch size (the default): flash-decode splits of the
+//                       context, online softmax per wave, last-arriving split combines.  The split
+//                       holding `pos` normalises + ropes k (llama.py:894-910), writes k / v to the
+//                       cache (llama.py:205-214) and uses them from LDS; K/V rows are read once
+//                       per (row, kv head) and shared by the GQA group (no repeat_interleave,
+//                       llama.py:912-913).
+//   attn_decode2 / attn_dec3  the same attention for shapes attn_fd does not take (more than 4 q
+//                       heads per kv head, head_dim outside {32, 64, 128}).
 //   fast_attn_fused     fast model (llama.py:947-975) at codebook position cpos: same fusion,
 //                       every rounding of the matmul-softmax-matmul reproduced.
 //   sample_radix_kernel top-k via 4-pass radix select on order-preserving keys + rank-by-count
@@ -51,111 +52,6 @@ __device__ __forceinline__ void head_prep(const T* src, int hd, bool norm, const
         }
     }
 }
-
-template <typename T>
-__global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecArgs<T> a) {
-    constexpr int TILE = 64;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int r = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
-    const int pos = a.row_pos[r];
-    const int j0 = sp * TILE;
-    if (j0 > pos) return;
-    const int nj = min(TILE, pos + 1 - j0);
-    const bool owner = (pos - j0) < TILE;  // this split holds the new position
-    const int slot = a.row_slot[r];
-    const int hd = a.hd, g = a.nh / a.nkv, ks = hd + 8;
-    T* Ks = reinterpret_cast<T*>(smem);
-    T* Vs = Ks + (size_t)TILE * ks;
-    float* qs = reinterpret_cast<float*>(Vs + (size_t)TILE * hd);  // [4][hd]
-    float* ps = qs + 4 * hd;                                        // [4][TILE]
-    const size_t base = (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * hd;
-    T* kc = a.kc + base;
-    T* vc = a.vc + base;
-    const T* raw = a.qkv + (size_t)r * a.ldqkv;
-    const float* tab = a.rope + (size_t)pos * hd;
-
-    // new k / v (owner block): waves 0 and 1
-    if (owner && wave < 2) {
-        float x0[2], x1[2];
-        int np;
-        const int hk = wave == 0 ? a.nh + kvh : a.nh + a.nkv + kvh;
-        head_prep<T>(raw + (size_t)hk * hd, hd, wave == 0 && a.qk_norm, a.kn, a.eps, tab, wave == 0,
-                     x0, x1, np, lane);
-        T* dst = (wave == 0 ? kc : vc) + (size_t)pos * hd;
-        T* tile = wave == 0 ? Ks + (size_t)(pos - j0) * ks : Vs + (size_t)(pos - j0) * hd;
-        for (int i = 0; i < np; ++i) {
-            const int p = lane + 64 * i;
-            st(dst, 2 * p, x0[i]);
-            st(dst, 2 * p + 1, x1[i]);
-            st(tile, 2 * p, x0[i]);
-            st(tile, 2 * p + 1, x1[i]);
-        }
-    }
-    // cached rows [j0, j0+nj) except the new one: 16-byte chunks
-    {
-        const int cpr = hd * (int)sizeof(T) / 16;  // chunks per row
-        const int nrows = owner ? nj - 1 : nj;
-        for (int idx = threadIdx.x; idx < nrows * cpr * 2; idx += 256) {
-            const int which = idx / (nrows * cpr);
-            const int rem = idx - which * nrows * cpr;
-            const int j = rem / cpr, c = rem - j * cpr;
-            const T* src = (which == 0 ? kc : vc) + (size_t)(j0 + j) * hd;
-            T* dst = which == 0 ? Ks + (size_t)j * ks : Vs + (size_t)j * hd;
-            *reinterpret_cast<u32x4_t*>(reinterpret_cast<char*>(dst) + 16 * c) =
-                *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const char*>(src) + 16 * c);
-        }
-    }
-    const float scale = a.scale;
-    for (int hb = 0; hb < g; hb += 4) {
-        const int ql = hb + wave;  // q head within the group
-        if (ql < g) {
-            float x0[2], x1[2];
-            int np;
-            const int h = kvh * g + ql;
-            head_prep<T>(raw + (size_t)h * hd, hd, a.qk_norm, a.qn, a.eps, tab, true, x0, x1, np, lane);
-            for (int i = 0; i < np; ++i) {
-                const int p = lane + 64 * i;
-                qs[wave * hd + 2 * p] = x0[i];
-                qs[wave * hd + 2 * p + 1] = x1[i];
-            }
-        }
-        __syncthreads();
-        if (ql < g) {
-            // scores: lane j of wave `wave`
-            float sc = -INFINITY;
-            if (lane < nj) {
-                const T* kr = Ks + (size_t)lane * ks;
-                float dot = 0.f;
-                for (int e = 0; e < hd; e += 8) {
-                    float kv[8];
-                    load8(kr + e, kv);
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) dot += qs[wave * hd + e + u] * kv[u];
-                }
-                sc = dot * scale;
-            }
-            const float m = wave_max(sc);
-            const float p = lane < nj ? expf(sc - m) : 0.f;
-            const float l = wave_sum(p);
-            ps[wave * TILE + lane] = p;
-            __builtin_amdgcn_wave_barrier();
-            const int h = kvh * g + ql;
-            float* out = a.part + (((size_t)r * a.nh + h) * a.maxsplit + sp) * (hd + 2);
-            for (int e = lane; e < hd; e += 64) {
-                float o = 0.f;
-                for (int j = 0; j < nj; ++j) o += ps[wave * TILE + j] * ld(Vs + (size_t)j * hd, e);
-                out[2 + e] = o;
-            }
-            if (lane == 0) {
-                out[0] = m;
-                out[1] = l;
-            }
-        }
-        __syncthreads();
-    }
-}
-
 
 // Slow-model decode attention for the small-batch path.  grid (R, nkv, maxs), 512 threads.
 // One block normally covers ALL of a row's cached positions for one kv head (up to `cap` rows,
@@ -651,6 +547,301 @@ __global__ __launch_bounds__(256) void attn_dec3_kernel(AttnDecArgs<T> a) {
             O += w * ldp(pp + (size_t)q * (hd + 2) + 2 + e);
         }
         st(a.out + (size_t)r * a.nh * hd + (size_t)(kvh * g + h) * hd, e, O / L);
+    }
+}
+
+// Slow-model decode attention, flash-decode form (every batch size): grid (R, nkv, maxsplit),
+// 256 threads.  A (row, kv head) is cut into nsp <= maxsplit contiguous splits of at least a.cap
+// positions, computed on the device from pos (one captured graph serves every frame).  A block
+// walks its split in passes of 64 positions (16 per wave, lane layout of attn_dec3: K slice =
+// position 16w + (lane & 15), quarter lane >> 4 of hd; V slices = positions 16w + 4it + (lane >> 4),
+// dims 8 (lane & 15) .. +8), the next pass's K / V loads in flight while the current one is scored.
+// Every wave keeps its own running (max, sum, o) per q head (online softmax: no block barrier in
+// the loop); the block folds its waves through LDS and writes the output (nsp == 1) or a
+// write-through (m, l, o) partial.  The last-arriving split (relaxed agent ticket) combines the
+// partials with every load issued up front: 16 lanes per group = 16 splits, shuffles reduce
+// across them (the loop-carried combine of attn_decode2 / attn_dec3 issued its loads one by one).
+// The split holding `pos` normalises + ropes the new k (llama.py:894-910), writes k / v to the
+// cache (llama.py:205-214) and uses them in place of the cache rows it loaded.
+// 16 bytes of T as floats (bf16: 8, fp32: 4)
+template <typename T> __device__ __forceinline__ void cvt16(const u32x4_t v, float (&o)[16 / sizeof(T)]) {
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            o[2 * i] = __uint_as_float(v[i] << 16);
+            o[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = __uint_as_float(v[i]);
+    }
+}
+
+constexpr int FD_TILE = 64, FD_GM = 4;
+template <typename T, int HD>
+__global__ __launch_bounds__(256) void attn_fd_kernel(AttnDecArgs<T> a) {
+    static_assert(HD % 32 == 0 && HD <= 128, "head_dim a multiple of 32 up to 128");
+    constexpr int QD = HD / 4;                      // K dims per lane
+    constexpr int KL = QD * (int)sizeof(T) / 16;    // 16-B loads per K slice
+    constexpr int VL = 8 * (int)sizeof(T) / 16;     // 16-B loads per V slice
+    constexpr int half = HD / 2;
+    __shared__ __attribute__((aligned(16))) float q_s[FD_GM][HD];
+    __shared__ __attribute__((aligned(16))) float kv_new[2][HD];
+    __shared__ __attribute__((aligned(16))) float wml[4][FD_GM][2];
+    __shared__ __attribute__((aligned(16))) float ored[4][4][FD_GM][HD];  // [wave][V position group][head][dim] PV partials
+    __shared__ int flag;
+    unsigned long long tz[7] = {0, 0, 0, 0, 0, 0, 0};
+    DBG_TS(tz, 0)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int l16 = lane & 15, qq = lane >> 4;
+    const int r = blockIdx.x, kvh = blockIdx.y, sp = blockIdx.z;
+    const int g = a.nh / a.nkv, nitem = g + 2;
+    // ---- round trip 1: slot, pos and this wave's raw rows (q heads, then new k, new v); the raw
+    // loads do not depend on pos and go out with it (clamped, unconditional)
+    const int slot = a.row_slot[r];
+    const int pos = a.row_pos[r];
+    const T* raw = a.qkv + (size_t)r * a.ldqkv;
+    float x0[2], x1[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int it = wave + 4 * i;
+        const int row = it < g ? kvh * g + it : (it == g ? a.nh + kvh : a.nh + a.nkv + kvh);
+        const bool ok = it < nitem && lane < half;
+        const T* src = raw + (size_t)(it < nitem ? row : 0) * HD + 2 * (lane < half ? lane : 0);
+        const float v0 = ld(src, 0), v1 = ld(src, 1);
+        x0[i] = ok ? v0 : 0.f;
+        x1[i] = ok ? v1 : 0.f;
+    }
+    const int npos = pos + 1;
+    int nsp = min((int)gridDim.z, (npos + a.cap - 1) / a.cap);
+    const int chunk = ((npos + nsp - 1) / nsp + 15) & ~15;
+    nsp = (npos + chunk - 1) / chunk;
+    if (sp >= nsp) return;
+    const int j0 = sp * chunk, jend = min(j0 + chunk, npos);
+    const bool owner = jend == npos;
+    // ---- round trip 2 (pass 0's K / V), issued before the q-side arithmetic
+    const size_t base = (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * HD;
+    T* kc = a.kc + base;
+    T* vc = a.vc + base;
+    const int vd = 8 * l16 < HD ? 8 * l16 : HD - 8;
+    u32x4_t kb[KL], vb[4][VL];
+    auto issue = [&](int jb) {
+        const int jk = min(jb + 16 * wave + l16, jend - 1);
+        const u32x4_t* pk = reinterpret_cast<const u32x4_t*>(kc + (size_t)jk * HD + qq * QD);
+#pragma unroll
+        for (int c = 0; c < KL; ++c) kb[c] = pk[c];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int jv = min(jb + 16 * wave + 4 * it + qq, jend - 1);
+            const u32x4_t* pv = reinterpret_cast<const u32x4_t*>(vc + (size_t)jv * HD + vd);
+#pragma unroll
+            for (int c = 0; c < VL; ++c) vb[it][c] = pv[c];
+        }
+    };
+    issue(j0);
+    // ---- q heads (+ new k / v in the owner): qk-norm (fp32 incl. weight, one rounding), RoPE
+    const float* tab = a.rope + (size_t)pos * HD;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int it = wave + 4 * i;
+        if (it >= nitem || (it >= g && !owner)) continue;
+        const bool isq = it < g, isk = it == g;
+        if (a.qk_norm && (isq || isk)) {
+            const float ss = wave_sum(x0[i] * x0[i] + x1[i] * x1[i]);
+            const float rs = 1.0f / sqrtf(ss / (float)HD + a.eps);
+            const T* nw = isq ? a.qn : a.kn;
+            if (lane < half) {
+                x0[i] = rnd<T>((x0[i] * rs) * ld(nw, 2 * lane));
+                x1[i] = rnd<T>((x1[i] * rs) * ld(nw, 2 * lane + 1));
+            }
+        }
+        if (lane < half) {
+            float y0 = x0[i], y1 = x1[i];
+            if (isq || isk) {
+                const float c = tab[2 * lane], sn = tab[2 * lane + 1];
+                y0 = rnd<T>(x0[i] * c - x1[i] * sn);
+                y1 = rnd<T>(x1[i] * c + x0[i] * sn);
+            }
+            if (isq) {
+                q_s[it][2 * lane] = y0;
+                q_s[it][2 * lane + 1] = y1;
+                if (a.qdbg && sp == 0) {  // per-op test hook only
+                    float* qdp = a.qdbg + ((size_t)r * a.nh + kvh * g + it) * HD;
+                    qdp[2 * lane] = y0;
+                    qdp[2 * lane + 1] = y1;
+                }
+            } else {
+                kv_new[isk ? 0 : 1][2 * lane] = y0;
+                kv_new[isk ? 0 : 1][2 * lane + 1] = y1;
+                T* dst = (isk ? kc : vc) + (size_t)pos * HD;
+                st(dst, 2 * lane, y0);
+                st(dst, 2 * lane + 1, y1);
+            }
+        }
+    }
+    __syncthreads();
+    DBG_TS(tz, 1)
+    // ---- passes: per wave online softmax over its 16 positions of each pass
+    float m_run[FD_GM], l_run[FD_GM], o[FD_GM][8];
+#pragma unroll
+    for (int h = 0; h < FD_GM; ++h) {
+        m_run[h] = -INFINITY;
+        l_run[h] = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[h][e] = 0.f;
+    }
+    const int npass = (jend - j0 + FD_TILE - 1) / FD_TILE;
+    for (int pa = 0; pa < npass; ++pa) {
+        const int jb = j0 + pa * FD_TILE;
+        float kf[QD], vf[4][8];
+#pragma unroll
+        for (int c = 0; c < KL; ++c) {
+            float t[16 / sizeof(T)];
+            cvt16<T>(kb[c], t);
+#pragma unroll
+            for (int u = 0; u < (int)(16 / sizeof(T)); ++u) kf[c * (16 / sizeof(T)) + u] = t[u];
+        }
+#pragma unroll
+        for (int it = 0; it < 4; ++it)
+#pragma unroll
+            for (int c = 0; c < VL; ++c) {
+                float t[16 / sizeof(T)];
+                cvt16<T>(vb[it][c], t);
+#pragma unroll
+                for (int u = 0; u < (int)(16 / sizeof(T)); ++u) vf[it][c * (16 / sizeof(T)) + u] = t[u];
+            }
+        issue(jb + FD_TILE);  // next pass (clamped: the last pass re-loads rows it already has)
+        const int jk = jb + 16 * wave + l16;
+        const bool kval = jk < jend;
+        if (owner) {  // the new row from LDS, not the cache row loaded before it was written
+            if (min(jk, jend - 1) == pos)
+#pragma unroll
+                for (int c = 0; c < QD; ++c) kf[c] = kv_new[0][qq * QD + c];
+#pragma unroll
+            for (int it = 0; it < 4; ++it)
+                if (min(jb + 16 * wave + 4 * it + qq, jend - 1) == pos)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) vf[it][e] = kv_new[1][vd + e];
+        }
+#pragma unroll
+        for (int h = 0; h < FD_GM; ++h) {
+            if (h >= g) break;
+            float d = 0.f;
+#pragma unroll
+            for (int c = 0; c < QD; ++c) d += q_s[h][qq * QD + c] * kf[c];
+            d += __shfl_xor(d, 16);
+            d += __shfl_xor(d, 32);
+            const float s = kval ? d * a.scale : -INFINITY;
+            const float mx = row_max16(s);
+            const float mnew = fmaxf(m_run[h], mx);
+            const float alpha = mnew == -INFINITY ? 1.f : expf(m_run[h] - mnew);
+            const float p = kval ? expf(s - mnew) : 0.f;
+            m_run[h] = mnew;
+            l_run[h] = l_run[h] * alpha + p;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[h][e] *= alpha;
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const float pv = __shfl(p, 4 * it + qq);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[h][e] += pv * vf[it][e];
+            }
+        }
+    }
+    DBG_TS(tz, 2)
+    // ---- fold the block's waves: PV partials of the 4 V position groups through LDS (no
+    // cross-row shuffles), (max, sum) per wave and head
+#pragma unroll
+    for (int h = 0; h < FD_GM; ++h) {
+        if (h >= g) break;
+        const float l = row_sum16(l_run[h]);
+        if (8 * l16 < HD) {
+            f32x4_t* dst = reinterpret_cast<f32x4_t*>(&ored[wave][qq][h][8 * l16]);
+            dst[0] = (f32x4_t){o[h][0], o[h][1], o[h][2], o[h][3]};
+            dst[1] = (f32x4_t){o[h][4], o[h][5], o[h][6], o[h][7]};
+        }
+        if (lane == 0) {
+            wml[wave][h][0] = m_run[h];
+            wml[wave][h][1] = l;
+        }
+    }
+    __syncthreads();
+    DBG_TS(tz, 3)
+    const bool single = nsp == 1;
+    for (int idx = threadIdx.x; idx < g * HD; idx += 256) {
+        const int h = idx / HD, e = idx - h * HD;
+        const float M = fmaxf(fmaxf(wml[0][h][0], wml[1][h][0]), fmaxf(wml[2][h][0], wml[3][h][0]));
+        float L = 0.f, O = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const float sc = expf(wml[w][h][0] - M);  // a wave with no position: exp(-inf) = 0
+            L += sc * wml[w][h][1];
+            O += sc * ((ored[w][0][h][e] + ored[w][1][h][e]) + (ored[w][2][h][e] + ored[w][3][h][e]));
+        }
+        if (single) {
+            st(a.out + (size_t)r * a.nh * HD + (size_t)(kvh * g + h) * HD, e, O / L);
+        } else {  // write-through (sc1): read back by the combining block without a fence
+            float* pp = a.part + (((size_t)r * a.nh + (size_t)kvh * g + h) * a.maxsplit + sp) * (HD + 2);
+            __hip_atomic_store(pp + 2 + e, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (e == 0) {
+                __hip_atomic_store(pp, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(pp + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if (a.dbg && threadIdx.x == 0) {
+        tz[4] = __builtin_amdgcn_s_memrealtime();
+        dbg_record(a.dbg, 0xFFFC, (unsigned)(nsp << 16 | (jend - j0)), tz);
+    }
+    if (single) return;
+    // ---- split combine by the last-arriving block of (row, kv head): sc1 partial stores drained by
+    // every wave, a relaxed agent ticket, sc1 loads in the combiner (MI355X_MICROARCH.md hand-off
+    // table, first row; no release / acquire fence)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int t = __hip_atomic_fetch_add(a.cnt + (size_t)r * a.nkv + kvh, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        flag = t == nsp - 1;
+        if (t == nsp - 1) __hip_atomic_store(a.cnt + (size_t)r * a.nkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!flag) return;
+    // lane q of a 16-lane group holds split q; group grp owns PP consecutive (dim pair) items of one
+    // head.  Every load is unconditional (split index clamped) and issued before any is used.
+    constexpr int PP = FD_GM * HD / 32;
+    const int q = l16, grp = threadIdx.x >> 4;
+    const int k0 = grp * PP, h = k0 / half, e0 = 2 * (k0 - h * half);
+    if (h >= g) return;  // whole 16-lane groups
+    const int qc = q < nsp ? q : nsp - 1;
+    const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(
+        a.part + (((size_t)r * a.nh + (size_t)kvh * g + h) * a.maxsplit + qc) * (HD + 2));
+    const unsigned long long ml = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long ov[PP];
+#pragma unroll
+    for (int j = 0; j < PP; ++j) ov[j] = __hip_atomic_load(pp + 1 + e0 / 2 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float mq = q < nsp ? __uint_as_float((unsigned)ml) : -INFINITY;
+    const float lq = __uint_as_float((unsigned)(ml >> 32));
+    float M = mq;
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) M = fmaxf(M, __shfl_xor(M, m));
+    const float w = q < nsp ? expf(mq - M) : 0.f;
+    float L = w * lq;
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) L += __shfl_xor(L, m);
+    T* out = a.out + (size_t)r * a.nh * HD + (size_t)(kvh * g + h) * HD + e0;
+#pragma unroll
+    for (int j = 0; j < PP; ++j) {
+        float o0 = w * __uint_as_float((unsigned)ov[j]), o1 = w * __uint_as_float((unsigned)(ov[j] >> 32));
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {
+            o0 += __shfl_xor(o0, m);
+            o1 += __shfl_xor(o1, m);
+        }
+        if (q == (j & 15)) {
+            st(out, 2 * j, o0 / L);
+            st(out, 2 * j + 1, o1 / L);
+        }
     }
 }
 
@@ -1262,12 +1453,6 @@ __global__ __launch_bounds__(256) void sample_fast_kernel(SampleArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-template <typename T> void launch_attn_decode(hipStream_t s, const AttnDecArgs<T>& a, int R) {
-    dim3 g1(R, a.nkv, a.maxsplit);
-    const size_t lds = (size_t)64 * (a.hd + 8) * sizeof(T) + (size_t)64 * a.hd * sizeof(T) +
-                       (size_t)4 * a.hd * 4 + 4 * 64 * 4;
-    attn_decode_kernel<T><<<g1, 256, lds, s>>>(a);
-}
 template <typename T> void launch_attn_decode2(hipStream_t s, const AttnDecArgs<T>& a, int R) {
     dim3 g1(R, a.nkv, a.maxsplit);
     static bool attr = false;  // > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
@@ -1277,6 +1462,18 @@ template <typename T> void launch_attn_decode2(hipStream_t s, const AttnDecArgs<
         attr = true;
     }
     attn_decode2_kernel<T><<<g1, 512, attn2_lds_bytes(a.hd, a.nh / a.nkv, a.cap, sizeof(T)), s>>>(a);
+}
+template <typename T> void launch_attn_fd(hipStream_t s, const AttnDecArgs<T>& a0, int R) {
+    FMCHECK(attn_fd_ok(a0.hd, a0.nh / a0.nkv), "attn_fd: head_dim 32, 64 or 128 and at most 4 q heads per kv head");
+    FMCHECK(a0.cap >= 16 && a0.cnt && a0.part && a0.out, "attn_fd: min split >= 16, tickets, partials and output set");
+    AttnDecArgs<T> a = a0;
+    a.maxsplit = std::min(FD_NSP, FM_CEIL(a.S, a.cap));
+    const dim3 grid(R, a.nkv, a.maxsplit);
+    switch (a.hd) {
+        case 32: attn_fd_kernel<T, 32><<<grid, 256, 0, s>>>(a); break;
+        case 64: attn_fd_kernel<T, 64><<<grid, 256, 0, s>>>(a); break;
+        default: attn_fd_kernel<T, 128><<<grid, 256, 0, s>>>(a); break;
+    }
 }
 template <typename T> void launch_attn_decode3(hipStream_t s, const AttnDecArgs<T>& a0, int R) {
     FMCHECK(a0.hd % 32 == 0 && a0.hd <= 128 && a0.nh % a0.nkv == 0 && a0.nh / a0.nkv <= 6,
@@ -1299,10 +1496,10 @@ template <typename T> void launch_sample_radix(hipStream_t s, const SampleArgs& 
     else
         sample_radix_kernel<T><<<R, 256, sizeof(float) * a.Nl, s>>>(a);
 }
-template void launch_attn_decode<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
-template void launch_attn_decode<float>(hipStream_t, const AttnDecArgs<float>&, int);
 template void launch_attn_decode2<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
 template void launch_attn_decode2<float>(hipStream_t, const AttnDecArgs<float>&, int);
+template void launch_attn_fd<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
+template void launch_attn_fd<float>(hipStream_t, const AttnDecArgs<float>&, int);
 template void launch_attn_decode3<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
 template void launch_attn_decode3<float>(hipStream_t, const AttnDecArgs<float>&, int);
 template void launch_fast_attn2<bf16_t>(hipStream_t, const FastFusedArgs<bf16_t>&, int);

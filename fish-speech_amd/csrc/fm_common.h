@@ -85,6 +85,19 @@ __device__ __forceinline__ float wave_sum(float v) {
     const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
     return (r0 + r1) + (r2 + r3);
 }
+// every lane of a 16-lane row gets the row's total / maximum (DPP only, no LDS)
+__device__ __forceinline__ float row_sum16(float v) {
+    v += dpp_f<0xB1>(v);
+    v += dpp_f<0x4E>(v);
+    v += dpp_f<0x141>(v);
+    return v + dpp_f<0x140>(v);
+}
+__device__ __forceinline__ float row_max16(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v));
+    v = fmaxf(v, dpp_f<0x4E>(v));
+    v = fmaxf(v, dpp_f<0x141>(v));
+    return fmaxf(v, dpp_f<0x140>(v));
+}
 __device__ __forceinline__ float wave_max(float v) {
     v = fmaxf(v, dpp_f<0xB1>(v));
     v = fmaxf(v, dpp_f<0x4E>(v));

@@ -211,6 +211,9 @@ struct FmTuning {
     int linear_u32 = 4;      // linear_kernel weight fragments in flight per wave at 16 < R <= 32 (4 or 8)
     int linear_fill = 0;     // batched linear_kernel: split K until this many blocks (0: never; measured slower)
     int attn3 = 1;           // 1: slow decode attention on attn_dec3_kernel, 0: attn_decode2_kernel
+    int attn_fd = 1;         // 1: slow decode attention on attn_fd_kernel (flash-decode splits) where eligible
+    int fd_min = 32;         // attn_fd: minimum positions per split at R <= 8
+    int fd_min_batched = 512;  // attn_fd: minimum positions per split at R > 8 (B=32: one split below 512)
     int conv2 = 1;           // 1: codec GEMMs on the LDS-staged conv_gemm2_kernel, 0: conv_gemm_kernel
     int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)
     int bstream_kparts = 0;  // bstream EPI_SLAB K parts (0: by K)
@@ -289,7 +292,6 @@ template <typename T> struct AttnDecArgs {
     unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
     float* qdbg = nullptr;    // per-op test hook (fm_op_qk_rope): q after qk-norm + RoPE [R][nh][hd]
 };
-template <typename T> void launch_attn_decode(hipStream_t s, const AttnDecArgs<T>& a, int R);
 // decode attention for the small-batch path (see fm_attn.hip): a.cap rows per block, a.maxsplit =
 // ceil(S / cap) blocks per (row, kv head), output straight to a.out (bf16 / T)
 template <typename T> void launch_attn_decode2(hipStream_t s, const AttnDecArgs<T>& a, int R);
@@ -307,6 +309,12 @@ inline int attn2_cap(int hd, int g, size_t esz) {
 }
 // decode attention v3 (fm_attn.hip attn_dec3_kernel): 64 positions per block in registers,
 // maxsplit set by the launcher (ceil(S / 64)); a.part must hold [R][nh][ceil(S / 64)][hd + 2]
+// flash-decode attention (fm_attn.hip attn_fd_kernel), every batch size: splits of at least a.cap
+// (>= 16) positions, at most FD_NSP per (row, kv head); maxsplit set by the launcher; a.part must
+// hold [R][nh][min(FD_NSP, ceil(S / cap))][hd + 2], a.cnt [R][nkv] zeroed tickets
+constexpr int FD_NSP = 16;
+inline bool attn_fd_ok(int hd, int g) { return (hd == 32 || hd == 64 || hd == 128) && g >= 1 && g <= 4; }
+template <typename T> void launch_attn_fd(hipStream_t s, const AttnDecArgs<T>& a, int R);
 template <typename T> void launch_attn_decode3(hipStream_t s, const AttnDecArgs<T>& a, int R);
 template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFusedArgs<T>& a, int R);
 // fast-model attention, one wave per q head (cpos < 16 cached rows, hd <= 256)

@@ -269,8 +269,13 @@ template <typename T> struct Run {
     // slow-model decode attention: attn_dec3 (registers, 64 positions per block) for the batched
     // frame (B=32: 35.7 vs 38.1 us per layer), attn_decode2 (LDS tiles, 32-row blocks) at B <= 8,
     // where it is the faster of the two (B=1 frame 4.28 vs 4.52 ms)
-    void attn_slow(const AttnDecArgs<T>& aa, int R) {
-        if (fm_tuning().attn3 && R > GEMV_MAX_ROWS && aa.hd % 32 == 0 && aa.hd <= 128 && aa.nh / aa.nkv <= 6)
+    void attn_slow(const AttnDecArgs<T>& aa, int R) { attn_slow_on(s, aa, R); }
+    static void attn_slow_on(hipStream_t s, const AttnDecArgs<T>& aa, int R) {
+        if (fm_tuning().attn_fd && attn_fd_ok(aa.hd, aa.nh / aa.nkv)) {
+            AttnDecArgs<T> b = aa;
+            b.cap = std::max(16, R > GEMV_MAX_ROWS ? fm_tuning().fd_min_batched : fm_tuning().fd_min);
+            launch_attn_fd<T>(s, b, R);
+        } else if (fm_tuning().attn3 && R > GEMV_MAX_ROWS && aa.hd % 32 == 0 && aa.hd <= 128 && aa.nh / aa.nkv <= 6)
             launch_attn_decode3<T>(s, aa, R);
         else
             launch_attn_decode2<T>(s, aa, R);
@@ -358,13 +363,15 @@ template <typename T> struct Run {
             aa.cnt = m->attn_cnt;
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
-            run_("attn", 0, 0, [&] { attn_slow(aa, R); });
+            hipStream_t st = s;
+            run_rec("attn", [st, aa, R] { attn_slow_on(st, aa, R); });
         } else if (is_fast && fm_tuning().batched_fused_attn && fixed_pos >= 0 && fixed_pos < 16 && d.hd <= 256) {
             FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), rslot, d.nh, d.nkv, d.hd, d.qk_norm, eps,
                                 (const T*)L.qn, (const T*)L.kn, rope, (T*)kc, (T*)vc, sstride, loff, Sc,
                                 fixed_pos, scale, (T*)m->att};
             fa.dbg = fm_tuning().dbg;
-            run_("attn", 0, 0, [&] { launch_fast_attn2<T>(s, fa, R); });
+            hipStream_t st = s;
+            run_rec("attn", [st, fa, R] { launch_fast_attn2<T>(st, fa, R); });
         } else {
             QkArgs<T> qa{(const T*)m->qkv, d.nqkv(), rslot, rpos, fixed_pos, d.nh, d.nkv, d.hd, d.qk_norm,
                          eps, (const T*)L.qn, (const T*)L.kn, rope, (T*)m->q, (T*)kc, (T*)vc, sstride, loff, Sc};
@@ -436,6 +443,11 @@ template <typename T> struct Run {
     template <typename F> void run_(const char* cls, int64_t bytes, double flops, F&& f) {
         m->prof.run(s, cls, bytes, flops, std::forward<F>(f));
     }
+    // run + record for fm_llm_kernel_bench: `go` must capture by value (it is replayed later)
+    template <typename F> void run_rec(const char* cls, F go) {
+        m->prof.record(cls, 0, go);
+        m->prof.run(s, cls, 0, 0, go);
+    }
     struct KsbPlan {
         int wo, w2;
     };
@@ -505,13 +517,16 @@ template <typename T> struct Run {
             aa.cnt = m->attn_cnt;
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
-            run_("attn", 0, 0, [&] { attn_slow(aa, n); });
+            hipStream_t st = s;
+            run_rec("attn", [st, aa, n] { attn_slow_on(st, aa, n); });
         } else if (!att_wo) {
-            run_("attn", 0, 0, [&] {
-                if (cpos < 16 && d.hd <= 256)
-                    launch_fast_attn2<T>(s, fa, n);
+            hipStream_t st = s;
+            const bool f2 = cpos < 16 && d.hd <= 256;
+            run_rec("attn", [st, fa, n, f2] {
+                if (f2)
+                    launch_fast_attn2<T>(st, fa, n);
                 else
-                    launch_fast_attn_fused<T>(s, fa, n);
+                    launch_fast_attn_fused<T>(st, fa, n);
             });
         }
         // wo, split-K; the last block of each tile finalises h = x + wo(att) and its sums of squares
@@ -1629,6 +1644,14 @@ int fm_tune(const char* key, int value) {
             t.ksb_balance = value != 0;
         } else if (k == "attn3") {
             t.attn3 = value != 0;
+        } else if (k == "attn_fd") {
+            t.attn_fd = value != 0;
+        } else if (k == "fd_min") {
+            FMCHECK(value >= 16 && value % 16 == 0, "fd_min must be a multiple of 16");
+            t.fd_min = value;
+        } else if (k == "fd_min_batched") {
+            FMCHECK(value >= 16 && value % 16 == 0, "fd_min_batched must be a multiple of 16");
+            t.fd_min_batched = value;
         } else if (k == "bstream") {
             t.bstream = value != 0;
         } else if (k == "bstream_kparts") {

@@ -8,6 +8,8 @@
 //                   standalone row kernel of the batched / prefill path
 //   fm_op_qk_rope   QK-norm (llama.py:861-863) + RoPE with the bf16 table (llama.py:1003-1037)
 //                   inside the fused decode attention kernels (slow attn_decode2, fast attn2)
+//   fm_op_decode_attn  the whole slow decode attention (QK-norm, RoPE, KV write, scaled dot-product
+//                   attention over the cache, llama.py:883-945) on R rows with caller K/V caches
 //   fm_op_embed     the Dual-AR input embedding (llama.py:399-420)
 //   fm_rope_table   the host-built bf16 cos/sin table (no device needed)
 // Operands are fp32 host arrays, converted to the precision's storage type (bf16 rounding is the
@@ -198,6 +200,56 @@ void qk_rope_t(hipStream_t s, int kernel, const float* qkv, int nh, int nkv, int
     HIPCHK(hipStreamSynchronize(s));
 }
 
+// one decode attention launch over R rows (slot r = row r) with caller K/V caches [R][nkv][S][hd]
+// holding rows < pos[r]; the kernel writes row pos[r] (normed + roped k, raw v) itself
+template <typename T>
+void decode_attn_t(hipStream_t s, int kernel, const float* qkv, int R, int nh, int nkv, int hd, const float* qn,
+                   const float* kn, int qk_norm, float eps, float base, const int* pos, const float* kcache,
+                   const float* vcache, int S, int min_split, float* out, float* kc_out, float* vc_out) {
+    DevBufs b(s);
+    const int ld = (nh + 2 * nkv) * hd;
+    T* raw = b.upload<T>(qkv, (size_t)R * ld);
+    T* qnd = qk_norm ? b.upload<T>(qn, (size_t)hd) : (T*)b.alloc((size_t)hd * sizeof(T));
+    T* knd = qk_norm ? b.upload<T>(kn, (size_t)hd) : (T*)b.alloc((size_t)hd * sizeof(T));
+    auto tab = rope_table_host(S, hd, base);
+    float* rope = (float*)b.alloc(tab.size() * 4);
+    b.put(rope, tab.data(), tab.size() * 4);
+    const size_t stride = (size_t)nkv * S * hd;
+    T* kc = b.upload<T>(kcache, (size_t)R * stride);
+    T* vc = b.upload<T>(vcache, (size_t)R * stride);
+    T* o = (T*)b.alloc((size_t)R * nh * hd * sizeof(T));
+    int* rows = (int*)b.alloc((size_t)2 * R * 4);
+    std::vector<int> rs(2 * R);
+    for (int r = 0; r < R; ++r) {
+        rs[r] = r;
+        rs[R + r] = pos[r];
+    }
+    b.put(rows, rs.data(), rs.size() * 4);
+    AttnDecArgs<T> a{raw, ld, rows, rows + R, nh, nkv, hd, qk_norm, eps, qnd, knd, rope, kc, vc, stride, 0, S,
+                     1, 1.0f / sqrtf((float)hd), nullptr};
+    const int g = nh / nkv;
+    a.maxsplit = FM_CEIL(S, 16);
+    a.part = (float*)b.alloc((size_t)R * nh * a.maxsplit * (hd + 2) * 4);
+    a.cnt = (int*)b.alloc((size_t)R * nkv * 4);
+    a.out = o;
+    if (kernel == 3) {
+        FMCHECK(attn_fd_ok(hd, g), "attn_fd: head_dim 32, 64 or 128 and at most 4 q heads per kv head");
+        a.cap = min_split;
+        launch_attn_fd<T>(s, a, R);
+    } else if (kernel == 2) {
+        FMCHECK(hd % 32 == 0 && hd <= 128 && g <= 6, "attn_dec3: hd a multiple of 32 up to 128, g <= 6");
+        launch_attn_decode3<T>(s, a, R);
+    } else {
+        a.cap = std::min(min_split, attn2_cap(hd, g, sizeof(T)));
+        a.maxsplit = FM_CEIL(S, a.cap);
+        launch_attn_decode2<T>(s, a, R);
+    }
+    HIPCHK(hipGetLastError());
+    download<T>(o, (size_t)R * nh * hd, out, s);
+    download<T>(kc, (size_t)R * stride, kc_out, s);
+    download<T>(vc, (size_t)R * stride, vc_out, s);
+}
+
 template <typename T>
 void embed_t(hipStream_t s, const int32_t* tok, int R, const float* emb, int V, const float* cbemb, int d, int C,
              int cb, int sb, int se, int scale, float* x) {
@@ -228,6 +280,28 @@ int fm_op_rmsnorm(int device, int precision, int mode, const float* x, const flo
             rmsnorm_t<bf16_t>(g.s, mode, x, w, R, d, eps, y);
         else
             rmsnorm_t<float>(g.s, mode, x, w, R, d, eps, y);
+    });
+}
+
+int fm_op_decode_attn(int device, int precision, int kernel, const float* qkv, int R, int nh, int nkv, int hd,
+                      const float* qn, const float* kn, int qk_norm, float eps, float rope_base, const int* pos,
+                      const float* kcache, const float* vcache, int S, int min_split, float* out, float* kc_out,
+                      float* vc_out) {
+    return fm_guard([&] {
+        FMCHECK(qkv && pos && kcache && vcache && out && kc_out && vc_out, "null argument");
+        FMCHECK(!qk_norm || (qn && kn), "qk_norm needs both norm weights");
+        FMCHECK(kernel == 0 || kernel == 2 || kernel == 3, "kernel must be 0 (attn_decode2), 2 (attn_dec3) or 3 (attn_fd)");
+        FMCHECK(R >= 1 && R <= 64 && nh >= 1 && nkv >= 1 && nh % nkv == 0, "bad rows / head counts");
+        FMCHECK(hd >= 32 && hd <= 128 && hd % 32 == 0, "head_dim a multiple of 32 up to 128");
+        FMCHECK(S >= 16 && S <= 65536 && min_split >= 16 && min_split % 16 == 0, "bad S / min_split");
+        for (int r = 0; r < R; ++r) FMCHECK(pos[r] >= 0 && pos[r] < S, "position outside the cache");
+        StreamGuard g(device);
+        if (precision == FM_PREC_BF16)
+            decode_attn_t<bf16_t>(g.s, kernel, qkv, R, nh, nkv, hd, qn, kn, qk_norm, eps, rope_base, pos, kcache, vcache,
+                                  S, min_split, out, kc_out, vc_out);
+        else
+            decode_attn_t<float>(g.s, kernel, qkv, R, nh, nkv, hd, qn, kn, qk_norm, eps, rope_base, pos, kcache, vcache,
+                                 S, min_split, out, kc_out, vc_out);
     });
 }
 

@@ -51,6 +51,35 @@ def qk_rope(qkv_row, nh, nkv, hd, pos, rope_base, qn=None, kn=None, eps=1e-6, pr
     return q.reshape(nh, hd), k.reshape(nkv, hd)
 
 
+ATTN_KERNELS = {"slow": 0, "slow3": 2, "fd": 3}  # attn_decode2 / attn_dec3 / attn_fd
+
+
+def decode_attn(qkv, nh, nkv, hd, pos, kcache, vcache, rope_base, qn=None, kn=None, eps=1e-6,
+                precision="bf16", kernel="fd", min_split=32, device=0):
+    """The slow decode attention (llama.py:883-945) on R rows: qkv (R, (nh+2nkv)*hd) raw projections,
+    pos (R,), kcache / vcache (R, nkv, S, hd) holding rows < pos[r].  Returns (out (R, nh, hd),
+    kcache, vcache after the kernel's write of row pos[r])."""
+    raw = np.ascontiguousarray(qkv, np.float32)
+    R = raw.shape[0]
+    assert raw.shape[1] == (nh + 2 * nkv) * hd
+    kc = np.ascontiguousarray(kcache, np.float32)
+    vc = np.ascontiguousarray(vcache, np.float32)
+    S = kc.shape[2]
+    assert kc.shape == (R, nkv, S, hd) and vc.shape == kc.shape
+    p = np.ascontiguousarray(pos, np.int32)
+    qk = qn is not None
+    qn_ = np.ascontiguousarray(qn if qk else np.ones(hd), np.float32)
+    kn_ = np.ascontiguousarray(kn if qk else np.ones(hd), np.float32)
+    out = np.zeros((R, nh, hd), np.float32)
+    kco = np.zeros_like(kc)
+    vco = np.zeros_like(vc)
+    native.check(native.lib().fm_op_decode_attn(device, _prec(precision), ATTN_KERNELS[kernel], native.f32p(raw), R,
+                                                nh, nkv, hd, native.f32p(qn_), native.f32p(kn_), int(qk), float(eps),
+                                                float(rope_base), native.i32p(p), native.f32p(kc), native.f32p(vc), S,
+                                                int(min_split), native.f32p(out), native.f32p(kco), native.f32p(vco)))
+    return out, kco, vco
+
+
 def embed(tok, emb, cbemb, num_codebooks, codebook_size, semantic_begin_id, semantic_end_id, scale,
           precision="bf16", device=0):
     """tok: (R, C+1) rows (row r = one position's [text/semantic token, codes...])."""

@@ -188,6 +188,15 @@ int fm_op_rmsnorm(int device, int precision, int mode, const float* x, const flo
 int fm_op_qk_rope(int device, int precision, int kernel, const float* qkv, int nh, int nkv, int hd,
                   const float* qn, const float* kn, int qk_norm, float eps, float rope_base, int pos,
                   float* q_out, float* k_out);
+/* The whole slow-model decode attention as the decode path runs it (llama.py:883-945: QK-norm, RoPE,
+   KV-cache write, scaled dot-product attention with the GQA group sharing its kv head) on R rows;
+   row r uses slot r of caller caches kcache / vcache [R][nkv][S][hd] holding rows < pos[r].
+   kernel 0 = attn_decode2, 2 = attn_dec3, 3 = attn_fd (flash-decode splits of >= min_split
+   positions).  out [R][nh * hd]; kc_out / vc_out receive the caches after the kernel's write. */
+int fm_op_decode_attn(int device, int precision, int kernel, const float* qkv, int R, int nh, int nkv, int hd,
+                      const float* qn, const float* kn, int qk_norm, float eps, float rope_base, const int* pos,
+                      const float* kcache, const float* vcache, int S, int min_split, float* out, float* kc_out,
+                      float* vc_out);
 /* Dual-AR input embedding (llama.py:399-420): tok R x (C+1) row-major, x R x dim. */
 int fm_op_embed(int device, int precision, const int32_t* tok, int R, const float* emb, int vocab,
                 const float* cbemb, int dim, int num_codebooks, int codebook_size, int semantic_begin_id,

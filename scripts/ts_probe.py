@@ -39,7 +39,7 @@ if len(smp):
     lo = (smp[:, 0].astype(np.int64) & 0xFFFF)
     print("sampler candidates: mean", round(lo.mean(), 1), "max", lo.max(), "overflow", int(((smp[:, 0].astype(np.int64) >> 16) & 1).sum()))
 for tag, name, labels in ((0xFFFE, "fast_attn2", ("load", "prep", "scores", "pv+store")),
-                          (0xFFFC, "qkv tail attn", ("load", "prep", "scores", "pv+store")),
+                          (0xFFFC, "attn_fd", ("rt1+qprep", "passes", "fold", "store")),
                           (0xFFFD, "attn_decode2", ("kv load", "q prep", "scores", "softmax", "pv", "rec"))):
     a = rec[(rec[:, 0] >> 32) == tag].astype(np.float64)
     if len(a):

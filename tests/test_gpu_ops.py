@@ -111,3 +111,60 @@ def test_embedding(precision, golden):
     x = ops.embed(tok, emb, cbe, C, cb, 200, 327, True, precision)
     assert ((tok[:, 0] >= 200) & (tok[:, 0] <= 327)).any() and ((tok[:, 0] < 200)).any()
     _check(x, ref, precision)
+
+
+def _attn_ref(q, kc, vc, pos, nkv):
+    """float64 softmax(q K^T / sqrt(hd)) V over cache rows 0..pos of each row (GQA: q head h uses kv
+    head h // (nh / nkv)), from the q the qk_rope hook returns and the caches the kernel wrote."""
+    R, nh, hd = q.shape
+    g = nh // nkv
+    out = np.zeros((R, nh, hd))
+    for r in range(R):
+        for h in range(nh):
+            K = kc[r, h // g, : pos[r] + 1].astype(np.float64)
+            V = vc[r, h // g, : pos[r] + 1].astype(np.float64)
+            s = K @ q[r, h].astype(np.float64) / np.sqrt(hd)
+            p = np.exp(s - s.max())
+            out[r, h] = p @ V / p.sum()
+    return out
+
+
+@pytest.mark.parametrize("kernel", ["fd", "slow", "slow3"])
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+@pytest.mark.parametrize("shape", [(32, 8, 128), (4, 2, 32)])
+def test_decode_attention(kernel, precision, shape):
+    """The whole slow decode attention (llama.py:883-945) against a float64 softmax over the cache
+    the kernel wrote, at positions that cross every split / pass boundary of the flash-decode
+    kernel (single split, several splits, 16 splits of several 64-position passes), one row and
+    three rows in different slots.  The new row's k equals the qk_rope hook's (pinned to ops.npz),
+    its v the raw input; rows below pos are untouched.  Bound: fp32 2e-5 relative to the row's
+    max |o|; bf16 one rounding of the output (2^-8 relative) plus the reference's bf16 q error."""
+    nh, nkv, hd = shape
+    S = 2304
+    rng = np.random.default_rng(7 + hd)
+    rb = round_bf16 if precision == "bf16" else (lambda a: a.astype(np.float32))
+    qn = rb(1.0 + 0.1 * rng.standard_normal(hd))
+    kn = rb(1.0 + 0.1 * rng.standard_normal(hd))
+    for R, positions in ((1, [0, 5, 31, 32, 170, 700, 2250]), (3, [[17, 300, 1], [2200, 64, 999]])):
+        for pos in positions:
+            pos = np.atleast_1d(np.array(pos, np.int32))
+            qkv = rb(rng.standard_normal((R, (nh + 2 * nkv) * hd)).astype(np.float32))
+            kc = rb(rng.standard_normal((R, nkv, S, hd)).astype(np.float32))
+            vc = rb(rng.standard_normal((R, nkv, S, hd)).astype(np.float32))
+            min_split = 64 if R > 1 else 32
+            out, kco, vco = ops.decode_attn(qkv, nh, nkv, hd, pos, kc, vc, 10000, qn=qn, kn=kn, eps=1e-6,
+                                            precision=precision, kernel=kernel, min_split=min_split)
+            q = np.zeros((R, nh, hd), np.float32)
+            for r in range(R):
+                qr, kr = ops.qk_rope(qkv[r], nh, nkv, hd, int(pos[r]), 10000, qn=qn, kn=kn, eps=1e-6,
+                                     precision=precision, kernel="slow")
+                q[r] = qr
+                np.testing.assert_array_equal(kco[r, :, pos[r]], kr)
+                np.testing.assert_array_equal(vco[r, :, pos[r]], qkv[r, (nh + nkv) * hd:].reshape(nkv, hd))
+                np.testing.assert_array_equal(kco[r, :, : pos[r]], kc[r, :, : pos[r]])
+                np.testing.assert_array_equal(vco[r, :, : pos[r]], vc[r, :, : pos[r]])
+            ref = _attn_ref(q, kco, vco, pos, nkv)
+            scale = np.abs(ref).max(axis=-1, keepdims=True)
+            err = np.abs(out - ref) / scale
+            tol = 2e-5 if precision == "fp32" else 2.0 ** -8 + 2e-3
+            assert err.max() <= tol, (kernel, precision, shape, R, pos.tolist(), float(err.max()))
