@@ -19,7 +19,16 @@ struct PackedW {
     int Co = 0, Ci = 0, ntaps = 1, nphase = 1, stride = 1;
     int shift[8] = {0};
     void* bias = nullptr;
+    int ks = 1;  // split-K factor (small-M layers; a property of the layer, so every chunking of a
+                 // streamed decode sums in the same order as the one-shot decode)
 };
+// split-K factor of a layer that runs at a few hundred rows: K steps of 32 per slice >= 8, <= 8 slices
+static void small_m(PackedW& W) {
+    const int S = (W.ntaps * W.Ci + 31) / 32;
+    int ks = 1;
+    while (ks < 8 && S / (2 * ks) >= 8) ks *= 2;
+    W.ks = W.Co % 8 == 0 ? ks : 1;
+}
 
 struct TLayer {
     void *an, *fn, *ag, *fg;
@@ -74,6 +83,8 @@ struct fm_codec {
     void *xb = nullptr, *A = nullptr, *B = nullptr, *Cb = nullptr;
     float* wave = nullptr;
     // stream state: carried rows per causal site (zeros at a stream start == causal padding)
+    float* ksp = nullptr;                   // split-K workspace (conv_gemm_kernel slabs)
+    size_t ksp_cap = 0;                     // floats
     void* st_kv[16] = {};                   // per transformer layer: window-1 qkv rows
     void *st_dw[2] = {}, *st_c0 = nullptr, *st_cf = nullptr;
     void *st_ct[4] = {}, *st_c7[4][3] = {};
@@ -499,6 +510,7 @@ static void finalize(fm_codec* m) {
         L.w1 = prep(m, raw(m, p + "feed_forward.w1.weight"), 3, D, I, 1, 1, 1, nullptr);
         L.w3 = prep(m, raw(m, p + "feed_forward.w3.weight"), 3, D, I, 1, 1, 1, nullptr);
         L.w2 = prep(m, raw(m, p + "feed_forward.w2.weight"), 3, I, D, 1, 1, 1, nullptr);
+        for (PackedW* W : {&L.wqkv, &L.wo, &L.w1, &L.w3, &L.w2}) small_m(*W);
     }
     m->tnorm = as_T(m, raw(m, "quantizer.post_module.norm.weight"), D);
     for (int u = 0; u < 2; ++u) {
@@ -511,9 +523,11 @@ static void finalize(fm_codec* m) {
         m->up_pw1[u] = prep(m, raw(m, p + "1.pwconv1.weight"), 3, D, 4 * D, 1, 1, 1, raw(m, p + "1.pwconv1.bias"));
         m->up_pw2[u] = prep(m, raw(m, p + "1.pwconv2.weight"), 3, 4 * D, D, 1, 1, 1, raw(m, p + "1.pwconv2.bias"));
         m->up_gm[u] = as_T(m, raw(m, p + "1.gamma"), D);
+        for (PackedW* W : {&m->up_ct[u], &m->up_pw1[u], &m->up_pw2[u]}) small_m(*W);
     }
     const int ch = c.decoder_dim;
     m->conv0 = prep_wn_conv(m, "decoder.model.0.", D, ch, 7, 1);
+    small_m(m->conv0);
     int cin = ch;
     const int rates[4] = {8, 8, 4, 2};
     for (int b = 0; b < 4; ++b) {
@@ -581,6 +595,8 @@ static void finalize(fm_codec* m) {
         m->st_cf = m->dstate((size_t)6 * cc * E);
     }
     m->Cb = m->dalloc(Tm * maxact * E);
+    m->ksp_cap = (size_t)4 << 20;  // split-K partial slabs of the small-grid codec GEMMs (16 MB)
+    m->ksp = (float*)m->dalloc(m->ksp_cap * 4);
     m->wave = (float*)m->dalloc(Tm * 2048 * 4);
     if (m->enc_dim) finalize_encoder(m);
     HIPCHK(hipEventCreate(&m->e0));
@@ -621,6 +637,9 @@ template <typename T> struct CRun {
         a.ldo2 = ldo2;
         a.flags = flags | (W.bias ? CE_BIAS : 0) | (out2 ? CE_SNAKE : 0);
         a.lo = lo;
+        a.slab = m->ksp;
+        a.slab_cap = m->ksp_cap;
+        a.ksplit = fm_tuning().conv_splitk ? W.ks : 1;
         launch_conv_gemm<T>(s, a);
         m->flops += 2.0 * Lq * W.nphase * (double)W.Co * W.ntaps * W.Ci;
         m->launches++;

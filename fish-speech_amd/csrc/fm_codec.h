@@ -36,6 +36,9 @@ template <typename T> struct ConvArgs {
     int flags;
     int lo;                    // lowest input row read (<= 0): rows [lo, 0) are the carried causal
                                // context of a streamed chunk (buffer prefix), 0 = causal zeros
+    float* slab;               // split-K workspace (launcher): fp32 partials [ksplit][nphase][Lq][Co]
+    size_t slab_cap;           // its capacity in floats (0: no split-K)
+    int ksplit;                // set by the launcher
 };
 
 struct RvqPtrs {

@@ -31,10 +31,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int tq0 = blockIdx.x * 64 + (wave & 1) * 32;
     const int co0 = blockIdx.y * 64 + (wave >> 1) * 32;
-    const int phase = blockIdx.z;
+    const int ks = a.ksplit > 1 ? a.ksplit : 1;
+    const int phase = blockIdx.z % a.nphase, kz = blockIdx.z / a.nphase;
     if (co0 >= a.Co) return;
     const int r = lane & 15, g = lane >> 4;
     const int Kt = a.ntaps * a.Ci, S = (Kt + 31) >> 5;  // weights zero-padded to 32-multiples
+    const int sb = (int)((long long)S * kz / ks), se = (int)((long long)S * (kz + 1) / ks);
     const T* wb = a.w + (size_t)phase * a.wphase;
     const bool c1 = co0 + 16 < a.Co;
     const int ct0 = co0 >> 4;
@@ -45,7 +47,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
         for (int u = 0; u < 2; ++u) acc[c][u] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     const int tq[2] = {tq0 + r, tq0 + 16 + r};
 #pragma unroll 4
-    for (int s = 0; s < S; ++s) {
+    for (int s = sb; s < se; ++s) {
         // this lane's 8-element chunk lies inside one tap (Ci % 8 == 0)
         const int kl = s * 32 + 8 * g;
         int tap = kl / a.Ci;
@@ -68,6 +70,20 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
             acc[0][u] = F::mma(fa0, fb[u], acc[0][u]);
             acc[1][u] = F::mma(fa1, fb[u], acc[1][u]);
         }
+    }
+    if (ks > 1) {  // split K: raw fp32 partials, the epilogue runs in conv_splitk_epi_kernel
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (c == 1 && !c1) break;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int t = tq0 + 16 * u + (lane & 15);
+                if (t >= a.Lq) continue;
+                float* dst = a.slab + ((size_t)(kz * a.nphase + phase) * a.Lq + t) * a.Co + co0 + 16 * c + 4 * (lane >> 4);
+                *reinterpret_cast<f32x4_t*>(dst) = acc[c][u];
+            }
+        }
+        return;
     }
     const int fl = a.flags;
 #pragma unroll
@@ -98,6 +114,60 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
                 }
                 if (fl & CE_SNAKE) st(a.out2, (size_t)tout * a.ldo2 + co, snake_f(y, ld(a.alpha2, co)));
             }
+        }
+    }
+}
+
+// split-K reduction + the conv epilogue on 8 consecutive channels per thread (16-B accesses):
+// y = round(sum_kz partial + bias) -> GELU -> residual / LayerScale -> tanh -> store / Snake
+template <typename T>
+__global__ __launch_bounds__(256) void conv_splitk_epi_kernel(ConvArgs<T> a) {
+    const int cpr = a.Co >> 3;
+    const size_t n = (size_t)a.nphase * a.Lq * cpr;
+    const int fl = a.flags;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const int cc = (int)(i % cpr);
+        const size_t pt = i / cpr;  // phase * Lq + t
+        const int t = (int)(pt % a.Lq), phase = (int)(pt / a.Lq);
+        const int co = 8 * cc;
+        float y[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int kz = 0; kz < a.ksplit; ++kz) {
+            const float* p = a.slab + ((size_t)kz * a.nphase * a.Lq + pt) * a.Co + co;
+            const f32x4_t p0 = *reinterpret_cast<const f32x4_t*>(p), p1 = *reinterpret_cast<const f32x4_t*>(p + 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                y[j] += p0[j];
+                y[4 + j] += p1[j];
+            }
+        }
+        float b[8];
+        if (fl & CE_BIAS) load8(a.bias + co, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float v = y[j];
+            if (fl & CE_BIAS) v += b[j];
+            v = rnd<T>(v);
+            if (fl & CE_GELU) v = rnd<T>(0.5f * v * (1.0f + erff(v * 0.70710678118654752f)));
+            y[j] = v;
+        }
+        const size_t tout = (size_t)t * a.stride + phase;
+        if (fl & CE_RES) {
+            float rv[8], gm[8];
+            load8(a.res + tout * a.ldr + co, rv);
+            if (fl & CE_GAMMA) load8(a.gamma + co, gm);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[j] = (fl & CE_GAMMA) ? rnd<T>(rv[j] + rnd<T>(gm[j] * y[j])) : rnd<T>(rv[j] + y[j]);
+        }
+        if (fl & CE_TANH)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[j] = tanhf(y[j]);
+        if (fl & CE_STORE) store8(reinterpret_cast<T*>(a.out) + tout * a.ldo + co, y);
+        if (fl & CE_SNAKE) {
+            float al[8], sn[8];
+            load8(a.alpha2 + co, al);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sn[j] = rnd<T>(snake_f(y[j], al[j]));
+            store8(a.out2 + tout * a.ldo2 + co, sn);
         }
     }
 }
@@ -469,43 +539,87 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
         if (s + 1 < S) sstore(buf ^ 1);
         __syncthreads();
     }
+    // ---- epilogue through LDS (coalesced): each wave parks its 32 x 16*NCO accumulator tile as T
+    // (bias, first rounding, GELU applied) in the staging buffer -- every wave passed the loop's last
+    // barrier, and a wave reads back only its own rows -- then handles 16-B chunks of 8 consecutive
+    // channels of one row per lane: residual / LayerScale, tanh, the store and the next stage's Snake
+    // with 16-B loads and stores (the fragment layout would store 2 B per lane, 64 rows per instruction)
     const int fl = a.flags;
+    constexpr int EW = 16 * NCO + 8;  // LDS row stride (elements)
+    T* et = lds;
 #pragma unroll
     for (int c = 0; c < NCO; ++c) {
         if (c >= nct) break;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int t = t0 + 32 * wave + 16 * u + (lane & 15);
-            if (t >= a.Lq) continue;
-            const int tout = t * a.stride + phase;
+            const int tl = 32 * wave + 16 * u + (lane & 15), cl = 16 * c + 4 * (lane >> 4);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int co = co0 + 16 * c + 4 * (lane >> 4) + i;
-                if (co >= a.Co) continue;
                 float y = acc[c][u][i];
-                if (fl & CE_BIAS) y += ld(a.bias, co);
+                if (fl & CE_BIAS) y += ld(a.bias, co0 + cl + i);
                 y = rnd<T>(y);
                 if (fl & CE_GELU) y = rnd<T>(0.5f * y * (1.0f + erff(y * 0.70710678118654752f)));
-                if (fl & CE_RES) {
-                    const float rv = ld(a.res, (size_t)tout * a.ldr + co);
-                    if (fl & CE_GAMMA) y = rnd<T>(rv + rnd<T>(ld(a.gamma, co) * y));
-                    else y = rnd<T>(rv + y);
-                }
-                if (fl & CE_TANH) y = tanhf(y);
-                if (fl & CE_STORE) {
-                    if (fl & CE_F32OUT) reinterpret_cast<float*>(a.out)[(size_t)tout * a.ldo + co] = y;
-                    else st(reinterpret_cast<T*>(a.out), (size_t)tout * a.ldo + co, y);
-                }
-                if (fl & CE_SNAKE) st(a.out2, (size_t)tout * a.ldo2 + co, snake_f(y, ld(a.alpha2, co)));
+                st(et, (size_t)tl * EW + cl + i, y);
             }
+        }
+    }
+    constexpr int CPR = 2 * NCO;  // chunks of 8 channels per row
+    for (int q = lane; q < 32 * CPR; q += 64) {
+        const int tl = 32 * wave + q / CPR, cc = q - (q / CPR) * CPR;
+        const int t = t0 + tl;
+        if (t >= a.Lq || cc >= 2 * nct) continue;
+        const int co = co0 + 8 * cc;
+        const size_t tout = (size_t)t * a.stride + phase;
+        float y[8];
+        load8(et + (size_t)tl * EW + 8 * cc, y);
+        if (fl & CE_RES) {
+            float rv[8], gm[8];
+            load8(a.res + tout * a.ldr + co, rv);
+            if (fl & CE_GAMMA) load8(a.gamma + co, gm);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[j] = (fl & CE_GAMMA) ? rnd<T>(rv[j] + rnd<T>(gm[j] * y[j])) : rnd<T>(rv[j] + y[j]);
+        }
+        if (fl & CE_TANH)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[j] = tanhf(y[j]);
+        if (fl & CE_STORE) store8(reinterpret_cast<T*>(a.out) + tout * a.ldo + co, y);
+        if (fl & CE_SNAKE) {
+            float al[8], sn[8];
+            load8(a.alpha2 + co, al);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sn[j] = rnd<T>(snake_f(y[j], al[j]));
+            store8(a.out2 + tout * a.ldo2 + co, sn);
         }
     }
 }
 
 template <typename T, int NCO> static void conv2_go(hipStream_t s, const ConvArgs<T>& a) {
-    const size_t lds = 2 * ((size_t)CG2_BM * CG2_XS + NCO * 512) * sizeof(T);
+    const size_t lds = std::max(2 * ((size_t)CG2_BM * CG2_XS + NCO * 512), (size_t)CG2_BM * (16 * NCO + 8)) * sizeof(T);
     dim3 g(FM_CEIL(a.Lq, CG2_BM), FM_CEIL(a.Co, 16 * NCO), a.nphase);
     conv_gemm2_kernel<T, NCO><<<g, 256, lds, s>>>(a);
+}
+
+// A split-K layer (PackedW::ks > 1): K slices into fp32 slabs, then conv_splitk_epi_kernel; rows in
+// segments that fit the workspace (pointers offset, the carried-context bound lo moved with them)
+template <typename T> static void conv_splitk_go(hipStream_t s, const ConvArgs<T>& a) {
+    const size_t per_row = (size_t)a.ksplit * a.nphase * a.Co;
+    const int seg = (int)std::min<size_t>((size_t)a.Lq, a.slab_cap / per_row / 64 * 64);
+    FMCHECK(seg >= 64 || seg == a.Lq, "conv split-K: workspace too small");
+    for (int r0 = 0; r0 < a.Lq; r0 += seg) {
+        ConvArgs<T> b = a;
+        b.Lq = std::min(seg, a.Lq - r0);
+        b.x = a.x + (ptrdiff_t)r0 * a.ldx;
+        b.Lx = a.Lx - r0;
+        b.lo = a.lo - r0;
+        const size_t o = (size_t)r0 * a.stride;
+        if (a.out) b.out = (char*)a.out + o * a.ldo * sizeof(T);
+        if (a.res) b.res = a.res + o * a.ldr;
+        if (a.out2) b.out2 = a.out2 + o * a.ldo2;
+        dim3 g(FM_CEIL(b.Lq, 64), FM_CEIL(b.Co, 64), b.nphase * b.ksplit);
+        conv_gemm_kernel<T><<<g, 256, 0, s>>>(b);
+        const size_t n = (size_t)b.nphase * b.Lq * (b.Co / 8);
+        conv_splitk_epi_kernel<T><<<(int)std::min<size_t>(FM_CEIL(n, 256), 4096), 256, 0, s>>>(b);
+    }
 }
 
 template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a) {
@@ -513,16 +627,26 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a)
     // the few narrow ones (encoder stem, 1-channel output conv) keep the register-only kernel
     // (measured per shape, 10 s decode: 442k x 96 k7 282 vs 292 us, 221k x 192 371 vs 452, 55k x 384
     // 348 vs 370, 6.9k x 768 192 vs 202; at 216-864 rows the LDS tile leaves too few blocks and loses)
-    if (fm_tuning().conv2 && a.Ci % 8 == 0 && a.Co % 16 == 0 && a.Co >= 96 && a.Lq >= 4096) {
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const bool vec_ok = !(a.flags & CE_F32OUT) && al16(a.out) && al16(a.out2) && al16(a.res) && a.ldo % 8 == 0 &&
+                        a.ldo2 % 8 == 0 && a.ldr % 8 == 0;  // the coalesced epilogue's 16-B accesses
+    if (a.ksplit > 1 && a.slab && vec_ok && a.Co % 8 == 0) {
+        conv_splitk_go<T>(s, a);
+        return;
+    }
+    if (fm_tuning().conv2 && vec_ok && a.Ci % 8 == 0 && a.Co % 16 == 0 && a.Co >= 96 && a.Lq >= 4096) {
         if (a.Co % 128 == 0 || a.Co >= 384)
             conv2_go<T, 8>(s, a);
         else
             conv2_go<T, 6>(s, a);
         return;
     }
+    ConvArgs<T> b = a;
+    b.ksplit = 1;
     dim3 g(FM_CEIL(a.Lq, 64), FM_CEIL(a.Co, 64), a.nphase);
-    conv_gemm_kernel<T><<<g, 256, 0, s>>>(a);
+    conv_gemm_kernel<T><<<g, 256, 0, s>>>(b);
 }
+
 template <typename T> void launch_silu_mul(hipStream_t s, const T* g, T* y, size_t n) {
     silu_mul_kernel<T><<<(int)std::min<size_t>(FM_CEIL(n, 256), 16384), 256, 0, s>>>(g, y, n);
 }

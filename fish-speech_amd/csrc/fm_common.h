@@ -53,6 +53,20 @@ template <typename T> __device__ __forceinline__ void load8(const T* p, float (&
     }
 }
 
+// 8 floats -> 8 consecutive elements of T (values already T-representable for bf16: rounded here
+// by the hardware conversion, which is exact on them)
+template <typename T> __device__ __forceinline__ void store8(T* p, const float (&v)[8]) {
+    if constexpr (is_bf16<T>::value) {
+        u32x4_t o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (uint32_t)f2bf(v[2 * j]) | ((uint32_t)f2bf(v[2 * j + 1]) << 16);
+        *reinterpret_cast<u32x4_t*>(p) = o;
+    } else {
+        *reinterpret_cast<f32x4_t*>(p) = (f32x4_t){v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4_t*>(p + 4) = (f32x4_t){v[4], v[5], v[6], v[7]};
+    }
+}
+
 // developer phase timestamps: one 8-word record {tag << 32 | aux, t0..t6} per call
 __device__ __forceinline__ void dbg_record(unsigned long long* dbg, unsigned tag, unsigned aux,
                                            const unsigned long long (&t)[7]) {

@@ -1621,6 +1621,8 @@ int fm_tune(const char* key, int value) {
             t.attn_cap = value;
         } else if (k == "conv2") {
             t.conv2 = value != 0;
+        } else if (k == "conv_splitk") {
+            t.conv_splitk = value != 0;
         } else if (k == "attn_wo") {
             t.attn_wo = value != 0;
         } else if (k == "gemv_wpb") {
