@@ -123,19 +123,29 @@ def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world):
         llm.prefill(s, make_prompt(cfg, 16, 77 + s), DualARModel.sampling(mask_im_end=True))
     llm.decode_frames(warm, 2)
 
+    phase = {"prefill": 0.0, "decode": 0.0, "codec": 0.0}  # host wall per phase (each call syncs)
+
+    def timed(name, f):
+        t = time.perf_counter()
+        r = f()
+        phase[name] += time.perf_counter() - t
+        return r
+
     def start(slot, req):
-        return llm.prefill(slot, req.prompt, DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30,
-                                                                  seed=req.seed, mask_im_end=True))
+        return timed("prefill", lambda: llm.prefill(
+            slot, req.prompt, DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30, seed=req.seed,
+                                                   mask_im_end=True)))
 
     def step(slots, n):
-        return llm.decode_frames(slots, n)
+        return timed("decode", lambda: llm.decode_frames(slots, n))
 
     def finish(slot, req, cols):
-        codec.stream_reset()
-        mx = codec.max_frames
-        pcm = np.concatenate([codec.decode_chunk(np.ascontiguousarray(cols[1:, t:t + mx]))
-                              for t in range(0, cols.shape[1], mx)])
-        return dp.pcm_to_int16(pcm)
+        def vocode():
+            codec.stream_reset()
+            mx = codec.max_frames
+            return dp.pcm_to_int16(np.concatenate([codec.decode_chunk(np.ascontiguousarray(cols[1:, t:t + mx]))
+                                                   for t in range(0, cols.shape[1], mx)]))
+        return timed("codec", vocode)
 
     sync()
     t0 = time.perf_counter()
@@ -165,6 +175,7 @@ def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world):
             "requests": len(q.results), "batch_per_gpu": batch, "frames": frames,
             "value": round(audio_s / dt, 2), "unit": "audio-sec/wall-sec", "wall_s": round(dt, 3),
             "decode_frames_rank0": stats["frames"], "ticks": stats["ticks"],
+            "phase_s_rank0": {k: round(v, 3) for k, v in phase.items()},
             "per_stream_rtf": round(audio_s / len(q.results) / dt, 3)}
 
 

@@ -142,8 +142,14 @@ template <typename T>
 __global__ __launch_bounds__(FN_THREADS) void finalize_norm_kernel(FinalizeArgs<T> a) {
     __shared__ float red_s[FN_THREADS / 64];
     const int r = blockIdx.x;
-    float v[FN_CPT][8];
+    float v[FN_CPT][8], wn[FN_CPT][8];
     float ss = 0.f;
+    // the norm weights go out with the slab / residual loads (one round trip, not one per phase)
+#pragma unroll
+    for (int c = 0; c < FN_CPT; ++c) {
+        const int i = 8 * (threadIdx.x + FN_THREADS * c);
+        if (a.nw && i < a.d) load8(a.nw + i, wn[c]);
+    }
 #pragma unroll
     for (int c = 0; c < FN_CPT; ++c) {
         const int i = 8 * (threadIdx.x + FN_THREADS * c);
@@ -194,11 +200,9 @@ __global__ __launch_bounds__(FN_THREADS) void finalize_norm_kernel(FinalizeArgs<
     for (int c = 0; c < FN_CPT; ++c) {
         const int i = 8 * (threadIdx.x + FN_THREADS * c);
         if (i < a.d) {
-            float w[8];
-            load8(a.nw + i, w);
             T* xn = a.xn_out + (size_t)r * a.ldxn + i;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) st(xn, j, rnd<T>(rnd<T>(v[c][j] * rs) * w[j]));
+            for (int j = 0; j < 8; ++j) st(xn, j, rnd<T>(rnd<T>(v[c][j] * rs) * wn[c][j]));
         }
     }
 }

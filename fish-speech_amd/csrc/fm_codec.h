@@ -24,6 +24,7 @@ template <typename T> struct ConvArgs {
     size_t wphase;             // elements per phase
     int Co, ntaps, stride, nphase;
     int shift[8];              // per tap
+    int shift0, shiftd;        // shift[tap] = shift0 + tap * shiftd (set and checked by the launcher)
     const T* bias;
     const T* gamma;
     const T* res;              // residual [t_out][co], ldr

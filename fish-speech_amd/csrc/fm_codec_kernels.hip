@@ -24,6 +24,14 @@ __device__ __forceinline__ float snake_f(float y, float al) {
     return y + (1.0f / (al + 1e-9f)) * (s * s);
 }
 
+// a.shift[tap] for a per-lane tap as arithmetic on two kernel-argument scalars: every conv here has
+// shifts linear in the tap ((k-1-j)*dil causal, j transposed).  Indexing the argument array with a
+// lane value makes the compiler fetch it with a vector memory load (and drain vmcnt before it),
+// one dependent round trip in front of every X address.
+template <typename T> __device__ __forceinline__ int conv_shift(const ConvArgs<T>& a, int tap) {
+    return a.shift0 + tap * a.shiftd;
+}
+
 // block = 4 waves, block tile 64 time x 64 channels, wave tile 32 x 32 (2x2 MFMA 16x16x32)
 template <typename T>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
@@ -54,7 +62,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
         const bool kin = tap < a.ntaps;
         tap = kin ? tap : a.ntaps - 1;
         const int ci0 = kin ? kl - tap * a.Ci : 0;
-        const int sh = a.shift[tap];
+        const int sh = conv_shift(a, tap);
         typename F::f fa0 = F::load_w(wb + ((size_t)ct0 * S + s) * 512, lane);
         typename F::f fa1 = F::load_w(wb + ((size_t)(c1 ? ct0 + 1 : ct0) * S + s) * 512, lane);
         typename F::f fb[2];
@@ -453,9 +461,18 @@ __global__ void conv_weight_kernel(const float* __restrict__ w, int kind, int Ci
 // global loads are in flight while the MFMAs of the current one read LDS; one barrier per step.
 // X rows are padded to 40 elements in LDS (80 B for bf16): the B-fragment reads of a wave (16 rows
 // x 16 B) spread over all banks.
+// Three-stage pipeline: the global loads of k-step s+2 go out before the MFMAs of step s (two
+// register staging sets, used alternately), step s+1's set is written to the other LDS buffer after
+// them, one barrier per step -- an L2 round trip is hidden behind two steps of MFMAs instead of
+// one.  Every staging load is unconditional (clamped step / tile indices): a load under a branch
+// makes the compiler drain vmcnt(0), which would serialise the stages again.
+// (Measured and dropped: 256-row tiles, 4 row fragments per wave at 2 waves per SIMD -- 20-25 %
+// slower on every decoder shape: this loop is latency-bound, not LDS- or L2-bandwidth-bound.)
 constexpr int CG2_BM = 128, CG2_XS = 40;
+// waves per SIMD the register budget targets: the second staging set costs 8 * (XCH + WCH) VGPRs
+constexpr int cg2_wpe(int esz, int nco) { return esz == 4 ? 2 : (nco == 8 ? 3 : 4); }
 template <typename T, int NCO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv_gemm2_kernel(ConvArgs<T> a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(cg2_wpe(sizeof(T), NCO)))) void conv_gemm2_kernel(ConvArgs<T> a) {
     using F = Frag<T>;
     constexpr int XBUF = CG2_BM * CG2_XS, WBUF = NCO * 512;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_cg[];
@@ -471,42 +488,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     constexpr int XCH = CG2_BM * 32 / EC / 256;          // X chunks per thread per step (2 bf16, 4 fp32)
     constexpr int WCH_T = NCO * 512 / EC;                // W chunks per step
     constexpr int WCH = (WCH_T + 255) / 256;
-    u32x4_t xr[XCH], wr[WCH];
-    auto gload = [&](int s) {
+    using XR = u32x4_t[XCH];
+    using WR = u32x4_t[WCH];
+    using XM = uint32_t[XCH];
+    // raw X chunks and their validity masks: the mask is applied when the chunk is written to LDS,
+    // so no ALU op consumes a load before the step that stores it (that would drain vmcnt early)
+    u32x4_t xr0[XCH], wr0[WCH], xr1[XCH], wr1[WCH];
+    uint32_t xm0[XCH], xm1[XCH];
+    auto gload = [&](int s, XR& xr, XM& xm, WR& wr) {
+        s = s < S ? s : S - 1;
+        // the step's first tap once per wave (uniform), then at most one boundary inside the
+        // 32-wide step (host: Ci >= 32) -- no per-lane integer division
+        const int kb = s * 32, tap0 = kb / a.Ci, ci0 = kb - tap0 * a.Ci;
 #pragma unroll
         for (int j = 0; j < XCH; ++j) {
             const int c = tid + 256 * j;
             const int row = c / (32 / EC), kc = c - row * (32 / EC);
-            const int kl = s * 32 + kc * EC;
-            int tap = kl / a.Ci;
+            int ci = ci0 + kc * EC, tap = tap0;
+            if (ci >= a.Ci) {
+                ci -= a.Ci;
+                ++tap;
+            }
             const bool kin = tap < a.ntaps;
             tap = kin ? tap : a.ntaps - 1;
-            const int ci = kl - tap * a.Ci;
-            const int t = t0 + row, tin = t - a.shift[tap];
+            const int t = t0 + row, tin = t - conv_shift(a, tap);
             const bool ok = kin && t < a.Lq && tin >= a.lo && tin < a.Lx;
             const int rc = tin < a.lo ? a.lo : (tin >= a.Lx ? a.Lx - 1 : tin);
-            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.x + (ptrdiff_t)rc * a.ldx + (ok ? ci : 0));
-            const uint32_t m = ok ? 0xffffffffu : 0u;
-            xr[j] = (u32x4_t){v[0] & m, v[1] & m, v[2] & m, v[3] & m};
+            xr[j] = *reinterpret_cast<const u32x4_t*>(a.x + (ptrdiff_t)rc * a.ldx + (ok ? ci : 0));
+            xm[j] = ok ? 0xffffffffu : 0u;
         }
 #pragma unroll
         for (int j = 0; j < WCH; ++j) {
-            const int c = tid + 256 * j;
-            const int ct = c / (512 / EC);
-            if (c < WCH_T && ct < nct)
-                wr[j] = *reinterpret_cast<const u32x4_t*>(wb + ((size_t)ct * S + s) * 512 + (c - ct * (512 / EC)) * EC);
-            else
-                wr[j] = (u32x4_t){0u, 0u, 0u, 0u};
+            // tiles past nct are never read by the MFMA loop: clamped re-reads, no branch
+            int c = tid + 256 * j;
+            c = c < WCH_T ? c : WCH_T - 1;
+            int ct = c / (512 / EC);
+            const int e = c - ct * (512 / EC);
+            ct = ct < nct ? ct : nct - 1;
+            wr[j] = *reinterpret_cast<const u32x4_t*>(wb + ((size_t)ct * S + s) * 512 + e * EC);
         }
     };
-    auto sstore = [&](int buf) {
+    auto sstore = [&](int buf, const XR& xr, const XM& xm, const WR& wr) {
         T* xs = lds + (size_t)buf * (XBUF + WBUF);
         T* ws = xs + XBUF;
 #pragma unroll
         for (int j = 0; j < XCH; ++j) {
             const int c = tid + 256 * j;
             const int row = c / (32 / EC), kc = c - row * (32 / EC);
-            *reinterpret_cast<u32x4_t*>(xs + row * CG2_XS + kc * EC) = xr[j];
+            const uint32_t m = xm[j];
+            *reinterpret_cast<u32x4_t*>(xs + row * CG2_XS + kc * EC) = (u32x4_t){xr[j][0] & m, xr[j][1] & m, xr[j][2] & m, xr[j][3] & m};
         }
 #pragma unroll
         for (int j = 0; j < WCH; ++j) {
@@ -517,13 +547,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     f32x4_t acc[NCO][2];
 #pragma unroll
     for (int c = 0; c < NCO; ++c) acc[c][0] = acc[c][1] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    gload(0);
-    sstore(0);
-    __syncthreads();
     const int xrow0 = 32 * wave + (lane & 15), xk = 8 * (lane >> 4);
-    for (int s = 0; s < S; ++s) {
-        const int buf = s & 1;
-        if (s + 1 < S) gload(s + 1);
+    auto mma_step = [&](int buf) {
         const T* xs = lds + (size_t)buf * (XBUF + WBUF);
         const T* ws = xs + XBUF;
         const typename F::f xb0 = F::load(xs + xrow0 * CG2_XS + xk);
@@ -536,8 +561,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
                 acc[c][1] = F::mma(wf, xb1, acc[c][1]);
             }
         }
-        if (s + 1 < S) sstore(buf ^ 1);
+    };
+    // step s: loads of s+2 into `nx`, MFMAs on LDS buffer s&1, step s+1 (held in `cur`) -> LDS
+    auto step = [&](int s, XR& nx, XM& nm, WR& nw, const XR& cur, const XM& cm, const WR& cw) {
+        gload(s + 2, nx, nm, nw);
+        mma_step(s & 1);
+        if (s + 1 < S) sstore((s + 1) & 1, cur, cm, cw);
         __syncthreads();
+    };
+    gload(0, xr0, xm0, wr0);
+    gload(1, xr1, xm1, wr1);
+    sstore(0, xr0, xm0, wr0);
+    __syncthreads();
+    for (int s = 0; s < S; s += 2) {
+        step(s, xr0, xm0, wr0, xr1, xm1, wr1);
+        if (s + 1 < S) step(s + 1, xr1, xm1, wr1, xr0, xm0, wr0);
     }
     // ---- epilogue through LDS (coalesced): each wave parks its 32 x 16*NCO accumulator tile as T
     // (bias, first rounding, GELU applied) in the staging buffer -- every wave passed the loop's last
@@ -547,6 +585,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     const int fl = a.flags;
     constexpr int EW = 16 * NCO + 8;  // LDS row stride (elements)
     T* et = lds;
+    // this lane's bias values, all loads in flight together (clamped channel, no branch)
+    float bsv[NCO][4];
+    {
+        const T* bp = (fl & CE_BIAS) ? a.bias : a.w;
+#pragma unroll
+        for (int c = 0; c < NCO; ++c)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bsv[c][i] = ld(bp, min(co0 + 16 * c + 4 * (lane >> 4) + i, a.Co - 1));
+    }
 #pragma unroll
     for (int c = 0; c < NCO; ++c) {
         if (c >= nct) break;
@@ -556,7 +603,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 float y = acc[c][u][i];
-                if (fl & CE_BIAS) y += ld(a.bias, co0 + cl + i);
+                if (fl & CE_BIAS) y += bsv[c][i];
                 y = rnd<T>(y);
                 if (fl & CE_GELU) y = rnd<T>(0.5f * y * (1.0f + erff(y * 0.70710678118654752f)));
                 st(et, (size_t)tl * EW + cl + i, y);
@@ -622,7 +669,11 @@ template <typename T> static void conv_splitk_go(hipStream_t s, const ConvArgs<T
     }
 }
 
-template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a) {
+template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0) {
+    ConvArgs<T> a = a0;
+    a.shift0 = a.shift[0];
+    a.shiftd = a.ntaps > 1 ? a.shift[1] - a.shift[0] : 0;
+    for (int j = 0; j < a.ntaps; ++j) FMCHECK(a.shift[j] == a.shift0 + j * a.shiftd, "conv: tap shifts must be linear in the tap");
     // LDS-staged tiles where the channels fill them (every decoder / transformer / upsample GEMM);
     // the few narrow ones (encoder stem, 1-channel output conv) keep the register-only kernel
     // (measured per shape, 10 s decode: 442k x 96 k7 282 vs 292 us, 221k x 192 371 vs 452, 55k x 384
@@ -634,7 +685,7 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a)
         conv_splitk_go<T>(s, a);
         return;
     }
-    if (fm_tuning().conv2 && vec_ok && a.Ci % 8 == 0 && a.Co % 16 == 0 && a.Co >= 96 && a.Lq >= 4096) {
+    if (fm_tuning().conv2 && vec_ok && a.Ci % 8 == 0 && a.Ci >= 32 && a.Co % 16 == 0 && a.Co >= 96 && a.Lq >= 4096) {
         if (a.Co % 128 == 0 || a.Co >= 384)
             conv2_go<T, 8>(s, a);
         else
