@@ -19,9 +19,22 @@
 #include "fm_runtime.h"
 #include "fm_frag.h"
 
+// sin^2(x) without the library sinf's wide-range machinery (the epilogues apply it to every output
+// element): Cody-Waite reduction by pi/2 in three fmas (x = n pi/2 + r, |r| <= pi/4, good to
+// |x| ~ 1e4), the Cephes sin polynomial on r, and sin^2(x) = sin^2(r) for even n, 1 - sin^2(r) for
+// odd n (sin^2(r) <= 1/2 there, so no cancellation).  Within a few fp32 ulp of sinf(x)^2.
+__device__ __forceinline__ float sin2_f(float x) {
+    const float n = rintf(x * 0.636619772367581343f);
+    float r = fmaf(-n, 1.5703125f, x);
+    r = fmaf(-n, 4.837512969970703125e-4f, r);
+    r = fmaf(-n, 7.54978995489188216e-8f, r);
+    const float z = r * r;
+    const float sr = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+    const float s2 = sr * sr;
+    return (((int)n) & 1) ? 1.0f - s2 : s2;
+}
 __device__ __forceinline__ float snake_f(float y, float al) {
-    const float s = sinf(al * y);
-    return y + (1.0f / (al + 1e-9f)) * (s * s);
+    return y + (1.0f / (al + 1e-9f)) * sin2_f(al * y);
 }
 
 // a.shift[tap] for a per-lane tap as arithmetic on two kernel-argument scalars: every conv here has
@@ -466,8 +479,82 @@ __global__ void conv_weight_kernel(const float* __restrict__ w, int kind, int Ci
 // them, one barrier per step -- an L2 round trip is hidden behind two steps of MFMAs instead of
 // one.  Every staging load is unconditional (clamped step / tile indices): a load under a branch
 // makes the compiler drain vmcnt(0), which would serialise the stages again.
-// (Measured and dropped: 256-row tiles, 4 row fragments per wave at 2 waves per SIMD -- 20-25 %
-// slower on every decoder shape: this loop is latency-bound, not LDS- or L2-bandwidth-bound.)
+// (Measured and dropped: 256-row tiles, 4 row fragments per wave at 2 waves per SIMD, 20-25 % slower
+// on every decoder shape; LDS-DMA (global_load_lds) staging of 64-deep k stages, 2 blocks per CU,
+// 7-18 % slower on three of the four decoder shapes.  Occupancy, not LDS or L2 bandwidth, decides.)
+// Shared epilogue of the LDS-tiled conv GEMMs (128 output times x 16*NCO channels, wave w owning
+// times [32w, 32w + 32)), run after the k-loop's last barrier.  Phase 1: each wave parks its
+// accumulator tile as T (bias, first rounding, GELU applied) in LDS -- a wave reads back only its own
+// rows.  Phase 2: 16-B chunks of 8 consecutive channels of one row per lane: residual / LayerScale,
+// tanh, the store and the next stage's Snake with 16-B accesses.
+template <typename T, int NCO>
+__device__ __forceinline__ void cg_epilogue(const ConvArgs<T>& a, const f32x4_t (&acc)[NCO][2], T* et, int t0,
+                                            int co0, int phase, int nct, int wave, int lane) {
+    const int fl = a.flags;
+    constexpr int EW = 16 * NCO + 8;  // LDS row stride (elements)
+    float bsv[NCO][4];
+    {
+        const T* bp = (fl & CE_BIAS) ? a.bias : a.w;
+#pragma unroll
+        for (int c = 0; c < NCO; ++c)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bsv[c][i] = ld(bp, min(co0 + 16 * c + 4 * (lane >> 4) + i, a.Co - 1));
+    }
+#pragma unroll
+    for (int c = 0; c < NCO; ++c) {
+        if (c >= nct) break;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int tl = 32 * wave + 16 * u + (lane & 15), cl = 16 * c + 4 * (lane >> 4);
+            float y4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float y = acc[c][u][i];
+                if (fl & CE_BIAS) y += bsv[c][i];
+                y = rnd<T>(y);
+                if (fl & CE_GELU) y = rnd<T>(0.5f * y * (1.0f + erff(y * 0.70710678118654752f)));
+                y4[i] = y;
+            }
+            if constexpr (is_bf16<T>::value) {  // 4 consecutive channels: one 8-byte LDS store
+                uint32_t w0 = (__float_as_uint(y4[0]) >> 16) | (__float_as_uint(y4[1]) & 0xffff0000u);
+                uint32_t w1 = (__float_as_uint(y4[2]) >> 16) | (__float_as_uint(y4[3]) & 0xffff0000u);
+                *reinterpret_cast<uint2*>(et + (size_t)tl * EW + cl) = make_uint2(w0, w1);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) st(et, (size_t)tl * EW + cl + i, y4[i]);
+            }
+        }
+    }
+    constexpr int CPR = 2 * NCO;  // chunks of 8 channels per row
+    for (int q = lane; q < 32 * CPR; q += 64) {
+        const int tl = 32 * wave + q / CPR, cc = q - (q / CPR) * CPR;
+        const int t = t0 + tl;
+        if (t >= a.Lq || cc >= 2 * nct) continue;
+        const int co = co0 + 8 * cc;
+        const size_t tout = (size_t)t * a.stride + phase;
+        float y[8];
+        load8(et + (size_t)tl * EW + 8 * cc, y);
+        if (fl & CE_RES) {
+            float rv[8], gm[8];
+            load8(a.res + tout * a.ldr + co, rv);
+            if (fl & CE_GAMMA) load8(a.gamma + co, gm);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[j] = (fl & CE_GAMMA) ? rnd<T>(rv[j] + rnd<T>(gm[j] * y[j])) : rnd<T>(rv[j] + y[j]);
+        }
+        if (fl & CE_TANH)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[j] = tanhf(y[j]);
+        if (fl & CE_STORE) store8(reinterpret_cast<T*>(a.out) + tout * a.ldo + co, y);
+        if (fl & CE_SNAKE) {
+            float al[8], sn[8];
+            load8(a.alpha2 + co, al);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sn[j] = rnd<T>(snake_f(y[j], al[j]));
+            store8(a.out2 + tout * a.ldo2 + co, sn);
+        }
+    }
+}
+
 constexpr int CG2_BM = 128, CG2_XS = 40;
 // waves per SIMD the register budget targets: the second staging set costs 8 * (XCH + WCH) VGPRs
 constexpr int cg2_wpe(int esz, int nco) { return esz == 4 ? 2 : (nco == 8 ? 3 : 4); }
@@ -573,71 +660,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(cg2_wpe(siz
     gload(1, xr1, xm1, wr1);
     sstore(0, xr0, xm0, wr0);
     __syncthreads();
-    for (int s = 0; s < S; s += 2) {
+    for (int s = 0; s < S; s += 4) {  // 4 steps per trip: the loop-header vmcnt drain every 4 steps
         step(s, xr0, xm0, wr0, xr1, xm1, wr1);
         if (s + 1 < S) step(s + 1, xr1, xm1, wr1, xr0, xm0, wr0);
+        if (s + 2 < S) step(s + 2, xr0, xm0, wr0, xr1, xm1, wr1);
+        if (s + 3 < S) step(s + 3, xr1, xm1, wr1, xr0, xm0, wr0);
     }
-    // ---- epilogue through LDS (coalesced): each wave parks its 32 x 16*NCO accumulator tile as T
-    // (bias, first rounding, GELU applied) in the staging buffer -- every wave passed the loop's last
-    // barrier, and a wave reads back only its own rows -- then handles 16-B chunks of 8 consecutive
-    // channels of one row per lane: residual / LayerScale, tanh, the store and the next stage's Snake
-    // with 16-B loads and stores (the fragment layout would store 2 B per lane, 64 rows per instruction)
-    const int fl = a.flags;
-    constexpr int EW = 16 * NCO + 8;  // LDS row stride (elements)
-    T* et = lds;
-    // this lane's bias values, all loads in flight together (clamped channel, no branch)
-    float bsv[NCO][4];
-    {
-        const T* bp = (fl & CE_BIAS) ? a.bias : a.w;
-#pragma unroll
-        for (int c = 0; c < NCO; ++c)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) bsv[c][i] = ld(bp, min(co0 + 16 * c + 4 * (lane >> 4) + i, a.Co - 1));
-    }
-#pragma unroll
-    for (int c = 0; c < NCO; ++c) {
-        if (c >= nct) break;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int tl = 32 * wave + 16 * u + (lane & 15), cl = 16 * c + 4 * (lane >> 4);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float y = acc[c][u][i];
-                if (fl & CE_BIAS) y += bsv[c][i];
-                y = rnd<T>(y);
-                if (fl & CE_GELU) y = rnd<T>(0.5f * y * (1.0f + erff(y * 0.70710678118654752f)));
-                st(et, (size_t)tl * EW + cl + i, y);
-            }
-        }
-    }
-    constexpr int CPR = 2 * NCO;  // chunks of 8 channels per row
-    for (int q = lane; q < 32 * CPR; q += 64) {
-        const int tl = 32 * wave + q / CPR, cc = q - (q / CPR) * CPR;
-        const int t = t0 + tl;
-        if (t >= a.Lq || cc >= 2 * nct) continue;
-        const int co = co0 + 8 * cc;
-        const size_t tout = (size_t)t * a.stride + phase;
-        float y[8];
-        load8(et + (size_t)tl * EW + 8 * cc, y);
-        if (fl & CE_RES) {
-            float rv[8], gm[8];
-            load8(a.res + tout * a.ldr + co, rv);
-            if (fl & CE_GAMMA) load8(a.gamma + co, gm);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) y[j] = (fl & CE_GAMMA) ? rnd<T>(rv[j] + rnd<T>(gm[j] * y[j])) : rnd<T>(rv[j] + y[j]);
-        }
-        if (fl & CE_TANH)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) y[j] = tanhf(y[j]);
-        if (fl & CE_STORE) store8(reinterpret_cast<T*>(a.out) + tout * a.ldo + co, y);
-        if (fl & CE_SNAKE) {
-            float al[8], sn[8];
-            load8(a.alpha2 + co, al);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) sn[j] = rnd<T>(snake_f(y[j], al[j]));
-            store8(a.out2 + tout * a.ldo2 + co, sn);
-        }
-    }
+    cg_epilogue<T, NCO>(a, acc, lds, t0, co0, phase, nct, wave, lane);
 }
 
 template <typename T, int NCO> static void conv2_go(hipStream_t s, const ConvArgs<T>& a) {
@@ -645,6 +674,8 @@ template <typename T, int NCO> static void conv2_go(hipStream_t s, const ConvArg
     dim3 g(FM_CEIL(a.Lq, CG2_BM), FM_CEIL(a.Co, 16 * NCO), a.nphase);
     conv_gemm2_kernel<T, NCO><<<g, 256, lds, s>>>(a);
 }
+
+
 
 // A split-K layer (PackedW::ks > 1): K slices into fp32 slabs, then conv_splitk_epi_kernel; rows in
 // segments that fit the workspace (pointers offset, the carried-context bound lo moved with them)
