@@ -64,6 +64,7 @@ struct fm_codec {
     size_t esz = 2;
     hipStream_t stream = nullptr;
     std::map<std::string, DTensor> w;  // raw fp32 tensors
+    std::map<const void*, const float*> ialpha;  // Snake alpha (device, T) -> its fp32 reciprocals
     bool finalized = false;
     std::vector<void*> allocs;
     // prepared
@@ -294,6 +295,20 @@ static void* as_T(fm_codec* m, const float* src, int64_t n) {
     return d;
 }
 
+// a Snake alpha vector as T plus its fp32 reciprocals 1 / (alpha + 1e-9) (descript Snake1d, restated
+// in oracle/ref_stubs.py), computed once from the T-rounded values so every epilogue multiplies
+// by the same fp32 number the per-element division gave
+static void* as_snake(fm_codec* m, const float* src, int64_t n) {
+    void* d = as_T(m, src, n);
+    float* ia = (float*)m->dalloc((size_t)n * sizeof(float));
+    if (m->prec == FM_PREC_BF16)
+        launch_snake_inv<bf16_t>(m->stream, (const bf16_t*)d, n, ia);
+    else
+        launch_snake_inv<float>(m->stream, (const float*)d, n, ia);
+    m->ialpha[d] = ia;
+    return d;
+}
+
 // prepare a GEMM weight: kind per conv_weight_kernel; returns phases packed
 static PackedW prep(fm_codec* m, const float* w, int kind, int Ci, int Co, int k, int s, int dil,
                     const float* bias) {
@@ -411,12 +426,12 @@ static void finalize_encoder(fm_codec* m) {
         const int dils[3] = {1, 3, 9};
         for (int r = 0; r < 3; ++r) {
             std::string rp = p + std::to_string(r) + ".block.";
-            B.ru[r].a0 = as_T(m, raw(m, rp + "0.alpha"), h);
-            B.ru[r].a2 = as_T(m, raw(m, rp + "2.alpha"), h);
+            B.ru[r].a0 = as_snake(m, raw(m, rp + "0.alpha"), h);
+            B.ru[r].a2 = as_snake(m, raw(m, rp + "2.alpha"), h);
             B.ru[r].c7 = prep_wn_conv(m, rp + "1.", h, h, 7, dils[r]);
             B.ru[r].c1 = prep_wn_conv(m, rp + "3.", h, h, 1, 1);
         }
-        B.a3 = as_T(m, raw(m, p + "3.alpha"), h);
+        B.a3 = as_snake(m, raw(m, p + "3.alpha"), h);
         const float* w = fold(m, p + "4.conv.parametrizations.weight.original0",
                               p + "4.conv.parametrizations.weight.original1", d, h * 2 * st);
         B.down = prep_strided(m, w, h, d, st, raw(m, p + "4.conv.bias"));
@@ -426,7 +441,7 @@ static void finalize_encoder(fm_codec* m) {
             m->etnorm = as_T(m, raw(m, p + "5.norm.weight"), d);
         }
     }
-    m->e_a5 = as_T(m, raw(m, "encoder.block.5.alpha"), d);
+    m->e_a5 = as_snake(m, raw(m, "encoder.block.5.alpha"), d);
     m->e_cf = prep_wn_conv(m, "encoder.block.6.", d, D, 3, 1);
     for (int i = 0; i < 2; ++i) {
         std::string p = "quantizer.downsample." + std::to_string(i) + ".";
@@ -534,7 +549,7 @@ static void finalize(fm_codec* m) {
         const int cout = cin / 2, s = rates[b];
         std::string p = "decoder.model." + std::to_string(b + 1) + ".block.";
         DBlock& B = m->blk[b];
-        B.alpha = as_T(m, raw(m, p + "0.alpha"), cin);
+        B.alpha = as_snake(m, raw(m, p + "0.alpha"), cin);
         // ConvTranspose1d weight norm: dim 0 is the INPUT channel (norm over (out, k))
         const float* wt = fold(m, p + "1.conv.parametrizations.weight.original0",
                                p + "1.conv.parametrizations.weight.original1", cin, cout * 2 * s);
@@ -542,14 +557,14 @@ static void finalize(fm_codec* m) {
         const int dils[3] = {1, 3, 9};
         for (int r = 0; r < 3; ++r) {
             std::string rp = p + std::to_string(r + 2) + ".block.";
-            B.ru[r].a0 = as_T(m, raw(m, rp + "0.alpha"), cout);
-            B.ru[r].a2 = as_T(m, raw(m, rp + "2.alpha"), cout);
+            B.ru[r].a0 = as_snake(m, raw(m, rp + "0.alpha"), cout);
+            B.ru[r].a2 = as_snake(m, raw(m, rp + "2.alpha"), cout);
             B.ru[r].c7 = prep_wn_conv(m, rp + "1.", cout, cout, 7, dils[r]);
             B.ru[r].c1 = prep_wn_conv(m, rp + "3.", cout, cout, 1, 1);
         }
         cin = cout;
     }
-    m->falpha = as_T(m, raw(m, "decoder.model.5.alpha"), cin);
+    m->falpha = as_snake(m, raw(m, "decoder.model.5.alpha"), cin);
     m->convf = prep_wn_conv(m, "decoder.model.6.", cin, 1, 7, 1);
     // rope table for the transformer (positions 0..Tmax-1, bf16-valued)
     auto rt = rope_table_host(std::max(m->max_frames, CODEC_STREAM_MAX), c.t_head_dim, c.rope_base);
@@ -631,6 +646,11 @@ template <typename T> struct CRun {
         a.res = (const T*)res;
         a.ldr = ldr;
         a.alpha2 = (const T*)alpha2;
+        if (alpha2) {
+            auto it = m->ialpha.find(alpha2);
+            FMCHECK(it != m->ialpha.end(), "codec: Snake alpha without reciprocals");
+            a.ialpha2 = it->second;
+        }
         a.out = out;
         a.ldo = ldo;
         a.out2 = (T*)out2;

@@ -30,6 +30,7 @@ template <typename T> struct ConvArgs {
     const T* res;              // residual [t_out][co], ldr
     int ldr;
     const T* alpha2;           // snake alpha for out2
+    const float* ialpha2;      // 1 / (alpha2 + 1e-9) per channel (fp32, computed once at load)
     void* out;
     int ldo;
     T* out2;
@@ -49,6 +50,7 @@ struct RvqPtrs {
 };
 
 template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a);
+template <typename T> void launch_snake_inv(hipStream_t s, const T* alpha, int64_t n, float* ialpha);
 // encode side (fm_codec_encode)
 struct VqEncPtrs {
     const float* wi[16];  // folded in_proj [cd][D]

@@ -36,6 +36,14 @@ __device__ __forceinline__ float sin2_f(float x) {
 __device__ __forceinline__ float snake_f(float y, float al) {
     return y + (1.0f / (al + 1e-9f)) * sin2_f(al * y);
 }
+// the same with the channel's reciprocal precomputed (ia = 1.0f / (al + 1e-9f), bit-identical)
+__device__ __forceinline__ float snake_fi(float y, float al, float ia) { return y + ia * sin2_f(al * y); }
+
+template <typename T>
+__global__ void snake_inv_kernel(const T* __restrict__ alpha, int64_t n, float* __restrict__ ia) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) ia[i] = 1.0f / (ld(alpha, i) + 1e-9f);
+}
 
 // a.shift[tap] for a per-lane tap as arithmetic on two kernel-argument scalars: every conv here has
 // shifts linear in the tap ((k-1-j)*dil causal, j transposed).  Indexing the argument array with a
@@ -133,7 +141,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
                     if (fl & CE_F32OUT) reinterpret_cast<float*>(a.out)[(size_t)tout * a.ldo + co] = y;
                     else st(reinterpret_cast<T*>(a.out), (size_t)tout * a.ldo + co, y);
                 }
-                if (fl & CE_SNAKE) st(a.out2, (size_t)tout * a.ldo2 + co, snake_f(y, ld(a.alpha2, co)));
+                if (fl & CE_SNAKE) st(a.out2, (size_t)tout * a.ldo2 + co, snake_fi(y, ld(a.alpha2, co), a.ialpha2[co]));
             }
         }
     }
@@ -184,10 +192,11 @@ __global__ __launch_bounds__(256) void conv_splitk_epi_kernel(ConvArgs<T> a) {
             for (int j = 0; j < 8; ++j) y[j] = tanhf(y[j]);
         if (fl & CE_STORE) store8(reinterpret_cast<T*>(a.out) + tout * a.ldo + co, y);
         if (fl & CE_SNAKE) {
-            float al[8], sn[8];
+            float al[8], ia[8], sn[8];
             load8(a.alpha2 + co, al);
+            load8(a.ialpha2 + co, ia);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) sn[j] = rnd<T>(snake_f(y[j], al[j]));
+            for (int j = 0; j < 8; ++j) sn[j] = rnd<T>(snake_fi(y[j], al[j], ia[j]));
             store8(a.out2 + tout * a.ldo2 + co, sn);
         }
     }
@@ -546,10 +555,11 @@ __device__ __forceinline__ void cg_epilogue(const ConvArgs<T>& a, const f32x4_t 
             for (int j = 0; j < 8; ++j) y[j] = tanhf(y[j]);
         if (fl & CE_STORE) store8(reinterpret_cast<T*>(a.out) + tout * a.ldo + co, y);
         if (fl & CE_SNAKE) {
-            float al[8], sn[8];
+            float al[8], ia[8], sn[8];
             load8(a.alpha2 + co, al);
+            load8(a.ialpha2 + co, ia);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) sn[j] = rnd<T>(snake_f(y[j], al[j]));
+            for (int j = 0; j < 8; ++j) sn[j] = rnd<T>(snake_fi(y[j], al[j], ia[j]));
             store8(a.out2 + tout * a.ldo2 + co, sn);
         }
     }
@@ -716,7 +726,10 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0
         conv_splitk_go<T>(s, a);
         return;
     }
-    if (fm_tuning().conv2 && vec_ok && a.Ci % 8 == 0 && a.Ci >= 32 && a.Co % 16 == 0 && a.Co >= 96 && a.Lq >= 4096) {
+    // LDS tiles once they give the chip >= 256 blocks (the 128-row tile, 96-128 channels)
+    const long long cg2_blocks = (long long)FM_CEIL(a.Lq, CG2_BM) * FM_CEIL(a.Co, 128) * a.nphase;
+    if (fm_tuning().conv2 && vec_ok && a.Ci % 8 == 0 && a.Ci >= 32 && a.Co % 16 == 0 && a.Co >= 96 &&
+        (a.Lq >= 4096 || cg2_blocks >= 256)) {
         if (a.Co % 128 == 0 || a.Co >= 384)
             conv2_go<T, 8>(s, a);
         else
@@ -729,6 +742,9 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0
     conv_gemm_kernel<T><<<g, 256, 0, s>>>(b);
 }
 
+template <typename T> void launch_snake_inv(hipStream_t s, const T* alpha, int64_t n, float* ialpha) {
+    snake_inv_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(alpha, n, ialpha);
+}
 template <typename T> void launch_silu_mul(hipStream_t s, const T* g, T* y, size_t n) {
     silu_mul_kernel<T><<<(int)std::min<size_t>(FM_CEIL(n, 256), 16384), 256, 0, s>>>(g, y, n);
 }
@@ -784,6 +800,7 @@ void launch_conv_weight(hipStream_t s, const float* w, int kind, int Ci, int Co,
     template void launch_rope_qk<T>(hipStream_t, T*, int, int, int, const float*, int);              \
     template void launch_window_attn<T>(hipStream_t, const T*, int, int, int, int, T*, int);         \
     template void launch_snake<T>(hipStream_t, const T*, int, size_t, const T*, T*);                 \
+    template void launch_snake_inv<T>(hipStream_t, const T*, int64_t, float*);                       \
     template void launch_audio8<T>(hipStream_t, const float*, int64_t, int64_t, T*);                 \
     template void launch_conv_weight<T>(hipStream_t, const float*, int, int, int, int, int, T*);
 CINST(bf16_t)
