@@ -214,6 +214,7 @@ struct FmTuning {
     int attn_fd = 1;         // 1: slow decode attention on attn_fd_kernel (flash-decode splits) where eligible
     int fd_min = 32;         // attn_fd: minimum positions per split at R <= 8
     int fd_min_batched = 512;  // attn_fd: minimum positions per split at R > 8 (B=32: one split below 512)
+    int prompt_gemm = 1;     // 1: prompt-chunk linears (R > 32) on the codec's LDS-tiled GEMM kernels
     int conv2 = 1;           // 1: codec GEMMs on the LDS-staged conv_gemm2_kernel, 0: conv_gemm_kernel
     int conv_splitk = 1;     // 1: small-grid codec GEMMs split K into fp32 slabs + a reduce/epilogue kernel
     int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)

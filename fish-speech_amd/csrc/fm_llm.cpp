@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <memory>
 
+#include "fm_codec.h"
 #include "fm_kernels.h"
 #include "fm_runtime.h"
 
@@ -232,11 +233,52 @@ template <typename T> struct Run {
     bool rows_distinct_slots = false;  // slow_layers rows are one per slot (batched decode frame)
     explicit Run(fm_llm* mm) : m(mm), s(mm->stream), E(sizeof(T)) {}
 
+    // Prompt chunks (R > 32 rows): a linear is a GEMM, not a weight stream, so it runs on the codec's
+    // LDS-tiled implicit-GEMM kernels as a one-tap conv (conv_gemm2_kernel: 128-row x 96-128-column
+    // tiles, or the 64 x 64 register tiles with split-K when the grid would not fill the chip).
+    // The packed weight layout is the same; epilogues: round(acc + bias) and round(res + round(acc)).
+    bool prompt_gemm(const void* W, const void* W2, const void* bias, const void* X, int ldx, int R, int N, int K,
+                     void* Y, int ldy, const void* res, int ldr, int epi, const char* cls) {
+        if (R <= 32 || W2 || m->qinfo(W) || !fm_tuning().prompt_gemm || (epi != EPI_STORE && epi != EPI_RESID) ||
+            N % 16 || K % 32 || N < 96)
+            return false;
+        ConvArgs<T> c{};
+        c.x = (const T*)X;
+        c.ldx = ldx;
+        c.Ci = K;
+        c.Lq = R;
+        c.Lx = R;
+        c.w = (const T*)W;
+        c.Co = N;
+        c.ntaps = 1;
+        c.stride = 1;
+        c.nphase = 1;
+        c.bias = (const T*)bias;
+        c.res = epi == EPI_RESID ? (const T*)res : nullptr;
+        c.ldr = ldr;
+        c.out = Y;
+        c.ldo = ldy;
+        c.flags = CE_STORE | (bias ? CE_BIAS : 0) | (epi == EPI_RESID ? CE_RES : 0);
+        const long long tiles64 = (long long)FM_CEIL(R, 64) * FM_CEIL(N, 64);
+        int ks = 1;
+        while (tiles64 * ks < 256 && ks < 8 && K / 32 >= 16 * ks * 2) ks *= 2;
+        c.ksplit = ks;
+        c.slab = m->skpart;
+        c.slab_cap = (size_t)m->skpart_cap;
+        const int64_t bytes = (int64_t)N * K * E + (int64_t)R * K * E + (int64_t)R * N * E;
+        const double flops = 2.0 * R * N * K;
+        hipStream_t st = s;
+        auto go = [st, c] { launch_conv_gemm<T>(st, c); };
+        m->prof.record(cls, bytes, go);
+        run_(cls, bytes, flops, go);
+        return true;
+    }
     void linear(const void* W, const void* W2, const void* bias, const void* X, int ldx, int R, int N,
                 int K, void* Y, int ldy, const void* res, int ldr, float* Yf, int epi, const char* cls) {
         if (bs_use(R, false) && !W2 && !res && (epi == EPI_F32 || epi == EPI_STORE) &&
             bs_linear(W, bias, X, ldx, R, N, K, Y, ldy, Yf, epi))
             return;  // heads / fast_project_in of a batched frame
+        if (prompt_gemm(W, W2, bias, X, ldx, R, N, K, Y, ldy, res, ldr, epi, cls)) return;
         LinearArgs<T> a{(const T*)W, (const T*)W2, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y,
                         ldy, (const T*)res, ldr, Yf};
         if (const auto* q = m->qinfo(W)) a.wscale = (const T*)q->scale;
@@ -1619,6 +1661,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "attn_cap") {
             FMCHECK(value == 0 || (value >= 16 && value % 16 == 0), "attn_cap must be 0 or a multiple of 16");
             t.attn_cap = value;
+        } else if (k == "prompt_gemm") {
+            t.prompt_gemm = value != 0;
         } else if (k == "conv2") {
             t.conv2 = value != 0;
         } else if (k == "conv_splitk") {
