@@ -125,7 +125,7 @@ constexpr size_t LINEAR_PART_CAP = (size_t)8 << 20;     // floats of split-K par
 int linear_ksb(int N, int K, int R, int nacc, bool can_split);
 template <typename T> void launch_qk_rope_cache(hipStream_t s, const QkArgs<T>& a, int R);
 template <typename T>
-void launch_attn(hipStream_t s, const AttnArgs<T>& a, int R, int nsplit, T* out);
+void launch_attn(hipStream_t s, const AttnArgs<T>& a, int R, int nsplit, T* out, bool one_slot);  // one_slot: rows of one prompt
 template <typename T> void launch_fast_attn(hipStream_t s, const FastAttnArgs<T>& a, int R);
 template <typename T> void launch_sample(hipStream_t s, const SampleArgs& a, int R);
 void launch_finish(hipStream_t s, int R, const int* row_slot, int* row_pos, const int32_t* cols,
@@ -214,6 +214,7 @@ struct FmTuning {
     int attn_fd = 1;         // 1: slow decode attention on attn_fd_kernel (flash-decode splits) where eligible
     int fd_min = 32;         // attn_fd: minimum positions per split at R <= 8
     int fd_min_batched = 512;  // attn_fd: minimum positions per split at R > 8 (B=32: one split below 512)
+    int prefill_attn = 1;    // 1: prompt-chunk attention on attn_prefill_kernel (bf16, head_dim 128, flash form)
     int prompt_gemm = 1;     // 1: prompt-chunk linears (R > 32) on the codec's LDS-tiled GEMM kernels
     int conv2 = 1;           // 1: codec GEMMs on the LDS-staged conv_gemm2_kernel, 0: conv_gemm_kernel
     int conv_splitk = 1;     // 1: small-grid codec GEMMs split K into fp32 slabs + a reduce/epilogue kernel

@@ -421,7 +421,7 @@ template <typename T> struct Run {
             if (!is_fast) {
                 AttnArgs<T> aa{(const T*)m->q, rslot, rpos, (const T*)kc, (const T*)vc, sstride, loff, Sc,
                                d.nh, d.nkv, d.hd, ATTN_SPLIT, m->maxsplit, scale, m->part};
-                run_("attn", 0, 0, [&] { launch_attn<T>(s, aa, R, m->maxsplit, (T*)m->att); });
+                run_("attn", 0, 0, [&] { launch_attn<T>(s, aa, R, m->maxsplit, (T*)m->att, !rows_are_slots); });
             } else {
                 FastAttnArgs<T> fa{(const T*)m->q, rslot, (const T*)kc, (const T*)vc, sstride, loff, Sc,
                                    d.nh, d.nkv, d.hd, fixed_pos, scale, (T*)m->att};
@@ -1661,6 +1661,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "attn_cap") {
             FMCHECK(value == 0 || (value >= 16 && value % 16 == 0), "attn_cap must be 0 or a multiple of 16");
             t.attn_cap = value;
+        } else if (k == "prefill_attn") {
+            t.prefill_attn = value != 0;
         } else if (k == "prompt_gemm") {
             t.prompt_gemm = value != 0;
         } else if (k == "conv2") {

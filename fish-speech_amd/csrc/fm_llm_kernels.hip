@@ -539,6 +539,127 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs<T> a) {
     }
 }
 
+
+// =========================================================================================
+// prompt attention (causal SDPA of a prefill chunk, llama.py:883-946), bf16, head_dim HD:
+// flash form on MFMA.  Block = one kv head x 16 consecutive rows; wave w = q head kvh*g + w of the
+// GQA group (g <= 4), so every K/V tile staged in LDS serves the whole group.  Per 32-key tile:
+// S = Q K^T (16 x 32, fp32), scale + causal mask, online softmax in fp32 (running max / sum per
+// row), P rounded to bf16 for the P V MFMA (as a bf16 SDPA does), O in fp32; out = round(O / l).
+// =========================================================================================
+template <int HD>
+__global__ __launch_bounds__(256) void attn_prefill_kernel(AttnArgs<bf16_t> a, int R, bf16_t* __restrict__ out) {
+    using F = Frag<bf16_t>;
+    constexpr int KT = 32, KP = HD + 8, VP = KT + 8;
+    __shared__ __attribute__((aligned(16))) bf16_t ks[KT][KP];     // K tile [key][dim]
+    __shared__ __attribute__((aligned(16))) bf16_t vt[HD][VP];     // V tile transposed [dim][key]
+    __shared__ __attribute__((aligned(16))) bf16_t ps[4][16][VP];  // per-wave P [row][key]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kvh = blockIdx.y, r0 = blockIdx.x * 16;
+    const int g = a.nh / a.nkv;
+    const bool active = wave < g;
+    const int h = kvh * g + (active ? wave : 0);
+    const int slot = a.row_slot[r0];
+    int maxpos = 0;
+    for (int i = 0; i < 16; ++i) maxpos = max(maxpos, a.row_pos[min(r0 + i, R - 1)]);
+    const bf16_t* kc = a.kc + (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * HD;
+    const bf16_t* vc = a.vc + (size_t)slot * a.slot_stride + a.layer_off + (size_t)kvh * a.S * HD;
+    // Q as A fragments: lane l -> row r0 + (l & 15), dims 32c + 8 (l >> 4) .. + 8
+    const int qa_row = min(r0 + (lane & 15), R - 1);
+    F::f qf[HD / 32];
+#pragma unroll
+    for (int c = 0; c < HD / 32; ++c)
+        qf[c] = F::load(a.q + (size_t)qa_row * a.nh * HD + (size_t)h * HD + 32 * c + 8 * (lane >> 4));
+    // this lane's S / O rows: 4 (l >> 4) + i
+    int prow[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) prow[i] = a.row_pos[min(r0 + 4 * (lane >> 4) + i, R - 1)];
+    f32x4_t o[HD / 16];
+#pragma unroll
+    for (int t = 0; t < HD / 16; ++t) o[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    float mrow[4], lrow[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        mrow[i] = -INFINITY;
+        lrow[i] = 0.f;
+    }
+    constexpr int CPK = HD / 8;  // 16-B chunks per key row
+    for (int j0 = 0; j0 <= maxpos; j0 += KT) {
+        __syncthreads();  // the previous tile's LDS reads are done
+        for (int c = tid; c < KT * CPK; c += 256) {
+            const int key = c / CPK, ch = c - key * CPK, jj = j0 + key;
+            const bool ok = jj <= maxpos;
+            const size_t off = (size_t)(ok ? jj : 0) * HD + 8 * ch;
+            u32x4_t kv = *reinterpret_cast<const u32x4_t*>(kc + off);
+            u32x4_t vv = *reinterpret_cast<const u32x4_t*>(vc + off);
+            if (!ok) kv = vv = (u32x4_t){0u, 0u, 0u, 0u};
+            *reinterpret_cast<u32x4_t*>(&ks[key][8 * ch]) = kv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                reinterpret_cast<uint16_t*>(&vt[8 * ch + 2 * e][key])[0] = (uint16_t)(vv[e] & 0xffffu);
+                reinterpret_cast<uint16_t*>(&vt[8 * ch + 2 * e + 1][key])[0] = (uint16_t)(vv[e] >> 16);
+            }
+        }
+        __syncthreads();
+        if (!active) continue;
+        f32x4_t sc[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            sc[hf] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < HD / 32; ++c) {
+                const F::f kb = *reinterpret_cast<const u32x4_t*>(&ks[16 * hf + (lane & 15)][32 * c + 8 * (lane >> 4)]);
+                sc[hf] = F::mma(qf[c], kb, sc[hf]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float sv[2];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int key = j0 + 16 * hf + (lane & 15);
+                sv[hf] = key <= prow[i] ? sc[hf][i] * a.scale : -INFINITY;
+            }
+            float mx = fmaxf(sv[0], sv[1]);
+#pragma unroll
+            for (int d = 1; d < 16; d <<= 1) mx = fmaxf(mx, __shfl_xor(mx, d, 64));
+            const float mn = fmaxf(mrow[i], mx);
+            const float al = mn == -INFINITY ? 1.f : expf(mrow[i] - mn);
+            const float p0 = sv[0] == -INFINITY ? 0.f : expf(sv[0] - mn);
+            const float p1 = sv[1] == -INFINITY ? 0.f : expf(sv[1] - mn);
+            float sum = p0 + p1;
+#pragma unroll
+            for (int d = 1; d < 16; d <<= 1) sum += __shfl_xor(sum, d, 64);
+            lrow[i] = lrow[i] * al + sum;
+            mrow[i] = mn;
+#pragma unroll
+            for (int t = 0; t < HD / 16; ++t) o[t][i] *= al;
+            const int prr = 4 * (lane >> 4) + i;
+            ps[wave][prr][lane & 15] = f2bf(p0);
+            ps[wave][prr][16 + (lane & 15)] = f2bf(p1);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const F::f pf = *reinterpret_cast<const u32x4_t*>(&ps[wave][lane & 15][8 * (lane >> 4)]);
+#pragma unroll
+        for (int t = 0; t < HD / 16; ++t) {
+            const F::f vf = *reinterpret_cast<const u32x4_t*>(&vt[16 * t + (lane & 15)][8 * (lane >> 4)]);
+            o[t] = F::mma(pf, vf, o[t]);
+        }
+        __builtin_amdgcn_wave_barrier();  // ps is rewritten by the next tile
+    }
+    if (!active) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = r0 + 4 * (lane >> 4) + i;
+        if (row >= R) continue;
+        const float inv = 1.0f / lrow[i];
+        bf16_t* orow = out + (size_t)row * a.nh * HD + (size_t)h * HD;
+#pragma unroll
+        for (int t = 0; t < HD / 16; ++t) st(orow, 16 * t + (lane & 15), o[t][i] * inv);
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void attn_combine_kernel(const float* __restrict__ part,
                                                           const int* __restrict__ row_pos, int nh,
@@ -863,7 +984,13 @@ template <typename T> void launch_qk_rope_cache(hipStream_t s, const QkArgs<T>& 
     dim3 grid(R, FM_CEIL(a.nh + 2 * a.nkv, 4));
     qk_rope_cache_kernel<T><<<grid, 256, 0, s>>>(a);
 }
-template <typename T> void launch_attn(hipStream_t s, const AttnArgs<T>& a, int R, int nsplit, T* out) {
+template <typename T> void launch_attn(hipStream_t s, const AttnArgs<T>& a, int R, int nsplit, T* out, bool one_slot) {
+    if constexpr (is_bf16<T>::value) {
+        if (one_slot && fm_tuning().prefill_attn && a.hd == 128 && a.nh % a.nkv == 0 && a.nh / a.nkv <= 4) {
+            attn_prefill_kernel<128><<<dim3(FM_CEIL(R, 16), a.nkv), 256, 0, s>>>(a, R, out);
+            return;
+        }
+    }
     dim3 g1(R, a.nkv, nsplit);
     attn_split_kernel<T><<<g1, 256, 0, s>>>(a);
     dim3 g2(R, a.nh);
@@ -909,7 +1036,7 @@ void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* 
     template void launch_rmsnorm<T>(hipStream_t, const T*, int, const T*, int, float, T*, int, int); \
     template void launch_linear<T>(hipStream_t, const LinearArgs<T>&, int);                      \
     template void launch_qk_rope_cache<T>(hipStream_t, const QkArgs<T>&, int);                   \
-    template void launch_attn<T>(hipStream_t, const AttnArgs<T>&, int, int, T*);                 \
+    template void launch_attn<T>(hipStream_t, const AttnArgs<T>&, int, int, T*, bool);           \
     template void launch_fast_attn<T>(hipStream_t, const FastAttnArgs<T>&, int);                 \
     template void launch_attn_combine<T>(hipStream_t, const float*, const int*, int, int, int, int, \
                                          int, T*);                                               \

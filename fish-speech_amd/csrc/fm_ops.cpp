@@ -10,6 +10,8 @@
 //                   inside the fused decode attention kernels (slow attn_decode2, fast attn2)
 //   fm_op_decode_attn  the whole slow decode attention (QK-norm, RoPE, KV write, scaled dot-product
 //                   attention over the cache, llama.py:883-945) on R rows with caller K/V caches
+//   fm_op_prompt_attn  the prompt-chunk causal attention (llama.py:883-946) over a cache prefix,
+//                   on the split kernel or the flash-form attn_prefill_kernel
 //   fm_op_embed     the Dual-AR input embedding (llama.py:399-420)
 //   fm_rope_table   the host-built bf16 cos/sin table (no device needed)
 // Operands are fp32 host arrays, converted to the precision's storage type (bf16 rounding is the
@@ -200,6 +202,34 @@ void qk_rope_t(hipStream_t s, int kernel, const float* qkv, int nh, int nkv, int
     HIPCHK(hipStreamSynchronize(s));
 }
 
+// R prompt rows of one slot at positions pos0 .. pos0 + R - 1 over caller caches [nkv][S][hd]
+// (keys / values of every position <= pos0 + R - 1 already written, as qk_rope_cache leaves them)
+template <typename T>
+void prompt_attn_t(hipStream_t s, int kernel, const float* q, int R, int nh, int nkv, int hd, int pos0,
+                   const float* kcache, const float* vcache, int S, float* out) {
+    DevBufs b(s);
+    T* qd = b.upload<T>(q, (size_t)R * nh * hd);
+    T* kc = b.upload<T>(kcache, (size_t)nkv * S * hd);
+    T* vc = b.upload<T>(vcache, (size_t)nkv * S * hd);
+    T* o = (T*)b.alloc((size_t)R * nh * hd * sizeof(T));
+    int* rows = (int*)b.alloc((size_t)2 * R * 4);
+    std::vector<int> rs(2 * R);
+    for (int r = 0; r < R; ++r) {
+        rs[r] = 0;
+        rs[R + r] = pos0 + r;
+    }
+    b.put(rows, rs.data(), rs.size() * 4);
+    const int split = 64, maxsplit = FM_CEIL(S, split);
+    AttnArgs<T> a{qd, rows, rows + R, kc, vc, (size_t)nkv * S * hd, 0, S, nh, nkv, hd, split, maxsplit,
+                  1.0f / sqrtf((float)hd), (float*)b.alloc((size_t)R * nh * maxsplit * (hd + 2) * 4)};
+    FmTuning& tu = fm_tuning();
+    const int keep = tu.prefill_attn;
+    tu.prefill_attn = kernel;
+    launch_attn<T>(s, a, R, maxsplit, o, true);
+    tu.prefill_attn = keep;
+    download<T>(o, (size_t)R * nh * hd, out, s);
+}
+
 // one decode attention launch over R rows (slot r = row r) with caller K/V caches [R][nkv][S][hd]
 // holding rows < pos[r]; the kernel writes row pos[r] (normed + roped k, raw v) itself
 template <typename T>
@@ -280,6 +310,22 @@ int fm_op_rmsnorm(int device, int precision, int mode, const float* x, const flo
             rmsnorm_t<bf16_t>(g.s, mode, x, w, R, d, eps, y);
         else
             rmsnorm_t<float>(g.s, mode, x, w, R, d, eps, y);
+    });
+}
+
+int fm_op_prompt_attn(int device, int precision, int kernel, const float* q, int R, int nh, int nkv, int hd, int pos0,
+                      const float* kcache, const float* vcache, int S, float* out) {
+    return fm_guard([&] {
+        FMCHECK(q && kcache && vcache && out, "null argument");
+        FMCHECK(kernel == 0 || kernel == 1, "kernel must be 0 (split + combine) or 1 (attn_prefill_kernel)");
+        FMCHECK(R >= 1 && R <= 1024 && nh % nkv == 0 && pos0 >= 0 && pos0 + R <= S, "bad rows / positions");
+        FMCHECK(kernel == 0 || (precision == FM_PREC_BF16 && hd == 128 && nh / nkv <= 4),
+                "attn_prefill_kernel: bf16, head_dim 128, at most 4 q heads per kv head");
+        StreamGuard g(device);
+        if (precision == FM_PREC_BF16)
+            prompt_attn_t<bf16_t>(g.s, kernel, q, R, nh, nkv, hd, pos0, kcache, vcache, S, out);
+        else
+            prompt_attn_t<float>(g.s, kernel, q, R, nh, nkv, hd, pos0, kcache, vcache, S, out);
     });
 }
 

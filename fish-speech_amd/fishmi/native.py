@@ -27,7 +27,7 @@ ABI_SYMBOLS = [
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
     "fm_codec_finalize", "fm_codec_decode", "fm_codec_stream_reset", "fm_codec_decode_chunk",
     "fm_codec_profile_read", "fm_codec_debug_read", "fm_codec_enable_encoder", "fm_codec_encode",
-    "fm_codec_close", "fm_llm_force", "fm_llm_read_logits", "fm_op_rmsnorm", "fm_op_qk_rope", "fm_op_decode_attn",
+    "fm_codec_close", "fm_llm_force", "fm_llm_read_logits", "fm_op_rmsnorm", "fm_op_qk_rope", "fm_op_decode_attn", "fm_op_prompt_attn",
     "fm_op_embed", "fm_rope_table",
 ]
 
@@ -85,6 +85,7 @@ def lib():
     L.fm_llm_read_logits.argtypes = [vp, i32, pf32, pf32]
     L.fm_op_rmsnorm.argtypes = [i32, i32, i32, pf32, pf32, i32, i32, f32, pf32]
     L.fm_op_qk_rope.argtypes = [i32, i32, i32, pf32, i32, i32, i32, pf32, pf32, i32, f32, f32, i32, pf32, pf32]
+    L.fm_op_prompt_attn.argtypes = [i32, i32, i32, pf32, i32, i32, i32, i32, i32, pf32, pf32, i32, pf32]
     L.fm_op_decode_attn.argtypes = [i32, i32, i32, pf32, i32, i32, i32, i32, pf32, pf32, i32, f32, f32, pi32, pf32,
                                     pf32, i32, i32, pf32, pf32, pf32]
     L.fm_op_embed.argtypes = [i32, i32, pi32, i32, pf32, i32, pf32, i32, i32, i32, i32, i32, i32, pf32]

@@ -80,6 +80,22 @@ def decode_attn(qkv, nh, nkv, hd, pos, kcache, vcache, rope_base, qn=None, kn=No
     return out, kco, vco
 
 
+def prompt_attn(q, nh, nkv, hd, pos0, kcache, vcache, precision="bf16", kernel="flash", device=0):
+    """Causal attention of R prompt rows (positions pos0 .. pos0+R-1, one slot) over caches
+    kcache / vcache (nkv, S, hd): q (R, nh*hd).  kernel "flash" (attn_prefill_kernel) or "split"."""
+    qq = np.ascontiguousarray(q, np.float32)
+    R = qq.shape[0]
+    kc = np.ascontiguousarray(kcache, np.float32)
+    vc = np.ascontiguousarray(vcache, np.float32)
+    S = kc.shape[1]
+    assert qq.shape[1] == nh * hd and kc.shape == (nkv, S, hd) and vc.shape == kc.shape
+    out = np.zeros((R, nh, hd), np.float32)
+    native.check(native.lib().fm_op_prompt_attn(device, _prec(precision), {"split": 0, "flash": 1}[kernel],
+                                                native.f32p(qq), R, nh, nkv, hd, int(pos0), native.f32p(kc),
+                                                native.f32p(vc), S, native.f32p(out)))
+    return out
+
+
 def embed(tok, emb, cbemb, num_codebooks, codebook_size, semantic_begin_id, semantic_end_id, scale,
           precision="bf16", device=0):
     """tok: (R, C+1) rows (row r = one position's [text/semantic token, codes...])."""

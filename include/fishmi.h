@@ -197,6 +197,13 @@ int fm_op_decode_attn(int device, int precision, int kernel, const float* qkv, i
                       const float* qn, const float* kn, int qk_norm, float eps, float rope_base, const int* pos,
                       const float* kcache, const float* vcache, int S, int min_split, float* out, float* kc_out,
                       float* vc_out);
+/* prompt-chunk causal attention (llama.py:883-946, the prefill path after QK-norm / RoPE / KV
+   write): q [R][nh * hd] of rows at positions pos0 .. pos0 + R - 1 of one slot, caches
+   kcache / vcache [nkv][S][hd] holding every position <= pos0 + R - 1.  kernel 0 = split +
+   combine kernels, 1 = attn_prefill_kernel (flash form on MFMA; bf16, head_dim 128, <= 4 q heads
+   per kv head).  out [R][nh * hd]. */
+int fm_op_prompt_attn(int device, int precision, int kernel, const float* q, int R, int nh, int nkv, int hd, int pos0,
+                      const float* kcache, const float* vcache, int S, float* out);
 /* Dual-AR input embedding (llama.py:399-420): tok R x (C+1) row-major, x R x dim. */
 int fm_op_embed(int device, int precision, const int32_t* tok, int R, const float* emb, int vocab,
                 const float* cbemb, int dim, int num_codebooks, int codebook_size, int semantic_begin_id,

@@ -168,3 +168,27 @@ def test_decode_attention(kernel, precision, shape):
             err = np.abs(out - ref) / scale
             tol = 2e-5 if precision == "fp32" else 2.0 ** -8 + 2e-3
             assert err.max() <= tol, (kernel, precision, shape, R, pos.tolist(), float(err.max()))
+
+
+@pytest.mark.parametrize("kernel", ["flash", "split"])
+@pytest.mark.parametrize("R, pos0", [(1, 0), (16, 0), (37, 0), (256, 0), (100, 450), (256, 1100)])
+def test_prompt_attention(kernel, R, pos0):
+    """The prompt-chunk causal attention (llama.py:883-946) at S2-Pro head shapes (32 q heads, 8 kv
+    heads, head_dim 128), bf16, against a float64 causal softmax over the cache: single rows, ragged
+    16-row blocks (37 rows), a full 256-row chunk, and chunks after a cached prefix (prefix reuse,
+    later prefill chunks) that cross many 32-key tiles.  Bound: one bf16 rounding of the output
+    (2^-8 of the row's max |o|) plus the bf16 rounding of the probabilities the flash form feeds
+    its P V product (as a bf16 SDPA does): 2^-8 + 4e-3."""
+    nh, nkv, hd = 32, 8, 128
+    S = 1536
+    rng = np.random.default_rng(11 + R + pos0)
+    q = round_bf16(rng.standard_normal((R, nh * hd)).astype(np.float32))
+    kc = round_bf16(rng.standard_normal((nkv, S, hd)).astype(np.float32))
+    vc = round_bf16(rng.standard_normal((nkv, S, hd)).astype(np.float32))
+    out = ops.prompt_attn(q, nh, nkv, hd, pos0, kc, vc, precision="bf16", kernel=kernel)
+    pos = pos0 + np.arange(R)
+    ref = _attn_ref(q.reshape(R, nh, hd), np.broadcast_to(kc, (R,) + kc.shape), np.broadcast_to(vc, (R,) + vc.shape),
+                    pos, nkv)
+    scale = np.abs(ref).max(axis=-1, keepdims=True)
+    err = np.abs(out - ref) / scale
+    assert err.max() <= 2.0 ** -8 + 4e-3, (kernel, R, pos0, float(err.max()))
