@@ -577,8 +577,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(cg2_wpe(siz
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t0 = blockIdx.x * CG2_BM;
     const int co0 = blockIdx.y * 16 * NCO;
-    const int phase = blockIdx.z;
+    // grid z = phase + nphase * k-slice (ksplit > 1: fp32 partial slabs, conv_splitk_epi_kernel runs
+    // the epilogue); this block's k-steps are [sb, sb + NS)
+    const int ks = a.ksplit > 1 ? a.ksplit : 1;
+    const int phase = blockIdx.z % a.nphase, kz = blockIdx.z / a.nphase;
     const int Kt = a.ntaps * a.Ci, S = (Kt + 31) >> 5;
+    const int sb = (int)((long long)S * kz / ks), NS = (int)((long long)S * (kz + 1) / ks) - sb;
     const T* wb = a.w + (size_t)phase * a.wphase + (size_t)(co0 >> 4) * S * 512;
     const int nct = min(NCO, (a.Co - co0 + 15) >> 4);  // channel tiles present in this block
     constexpr int EC = 16 / (int)sizeof(T);             // elements per 16-B chunk
@@ -593,7 +597,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(cg2_wpe(siz
     u32x4_t xr0[XCH], wr0[WCH], xr1[XCH], wr1[WCH];
     uint32_t xm0[XCH], xm1[XCH];
     auto gload = [&](int s, XR& xr, XM& xm, WR& wr) {
-        s = s < S ? s : S - 1;
+        s = sb + (s < NS ? s : NS - 1);
         // the step's first tap once per wave (uniform), then at most one boundary inside the
         // 32-wide step (host: Ci >= 32) -- no per-lane integer division
         const int kb = s * 32, tap0 = kb / a.Ci, ci0 = kb - tap0 * a.Ci;
@@ -663,25 +667,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(cg2_wpe(siz
     auto step = [&](int s, XR& nx, XM& nm, WR& nw, const XR& cur, const XM& cm, const WR& cw) {
         gload(s + 2, nx, nm, nw);
         mma_step(s & 1);
-        if (s + 1 < S) sstore((s + 1) & 1, cur, cm, cw);
+        if (s + 1 < NS) sstore((s + 1) & 1, cur, cm, cw);
         __syncthreads();
     };
     gload(0, xr0, xm0, wr0);
     gload(1, xr1, xm1, wr1);
     sstore(0, xr0, xm0, wr0);
     __syncthreads();
-    for (int s = 0; s < S; s += 4) {  // 4 steps per trip: the loop-header vmcnt drain every 4 steps
+    for (int s = 0; s < NS; s += 4) {  // 4 steps per trip: the loop-header vmcnt drain every 4 steps
         step(s, xr0, xm0, wr0, xr1, xm1, wr1);
-        if (s + 1 < S) step(s + 1, xr1, xm1, wr1, xr0, xm0, wr0);
-        if (s + 2 < S) step(s + 2, xr0, xm0, wr0, xr1, xm1, wr1);
-        if (s + 3 < S) step(s + 3, xr1, xm1, wr1, xr0, xm0, wr0);
+        if (s + 1 < NS) step(s + 1, xr1, xm1, wr1, xr0, xm0, wr0);
+        if (s + 2 < NS) step(s + 2, xr0, xm0, wr0, xr1, xm1, wr1);
+        if (s + 3 < NS) step(s + 3, xr1, xm1, wr1, xr0, xm0, wr0);
+    }
+    if (ks > 1) {  // raw fp32 partials [kz][phase][Lq][Co]: 4 consecutive channels per lane
+#pragma unroll
+        for (int c = 0; c < NCO; ++c) {
+            if (c >= nct) break;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int t = t0 + 32 * wave + 16 * u + (lane & 15);
+                if (t >= a.Lq) continue;
+                float* dst = a.slab + ((size_t)(kz * a.nphase + phase) * a.Lq + t) * a.Co + co0 + 16 * c + 4 * (lane >> 4);
+                *reinterpret_cast<f32x4_t*>(dst) = acc[c][u];
+            }
+        }
+        return;
     }
     cg_epilogue<T, NCO>(a, acc, lds, t0, co0, phase, nct, wave, lane);
 }
 
 template <typename T, int NCO> static void conv2_go(hipStream_t s, const ConvArgs<T>& a) {
     const size_t lds = std::max(2 * ((size_t)CG2_BM * CG2_XS + NCO * 512), (size_t)CG2_BM * (16 * NCO + 8)) * sizeof(T);
-    dim3 g(FM_CEIL(a.Lq, CG2_BM), FM_CEIL(a.Co, 16 * NCO), a.nphase);
+    dim3 g(FM_CEIL(a.Lq, CG2_BM), FM_CEIL(a.Co, 16 * NCO), a.nphase * (a.ksplit > 1 ? a.ksplit : 1));
     conv_gemm2_kernel<T, NCO><<<g, 256, lds, s>>>(a);
 }
 
@@ -703,8 +721,16 @@ template <typename T> static void conv_splitk_go(hipStream_t s, const ConvArgs<T
         if (a.out) b.out = (char*)a.out + o * a.ldo * sizeof(T);
         if (a.res) b.res = a.res + o * a.ldr;
         if (a.out2) b.out2 = a.out2 + o * a.ldo2;
-        dim3 g(FM_CEIL(b.Lq, 64), FM_CEIL(b.Co, 64), b.nphase * b.ksplit);
-        conv_gemm_kernel<T><<<g, 256, 0, s>>>(b);
+        const long long t128 = (long long)FM_CEIL(b.Lq, CG2_BM) * FM_CEIL(b.Co, 128) * b.nphase * b.ksplit;
+        if (fm_tuning().conv2 && b.Ci % 8 == 0 && b.Ci >= 32 && b.Co % 16 == 0 && b.Co >= 96 && t128 >= 256) {
+            if (b.Co % 128 == 0 || b.Co >= 384)
+                conv2_go<T, 8>(s, b);
+            else
+                conv2_go<T, 6>(s, b);
+        } else {
+            dim3 g(FM_CEIL(b.Lq, 64), FM_CEIL(b.Co, 64), b.nphase * b.ksplit);
+            conv_gemm_kernel<T><<<g, 256, 0, s>>>(b);
+        }
         const size_t n = (size_t)b.nphase * b.Lq * (b.Co / 8);
         conv_splitk_epi_kernel<T><<<(int)std::min<size_t>(FM_CEIL(n, 256), 4096), 256, 0, s>>>(b);
     }
@@ -730,10 +756,12 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0
     const long long cg2_blocks = (long long)FM_CEIL(a.Lq, CG2_BM) * FM_CEIL(a.Co, 128) * a.nphase;
     if (fm_tuning().conv2 && vec_ok && a.Ci % 8 == 0 && a.Ci >= 32 && a.Co % 16 == 0 && a.Co >= 96 &&
         (a.Lq >= 4096 || cg2_blocks >= 256)) {
-        if (a.Co % 128 == 0 || a.Co >= 384)
-            conv2_go<T, 8>(s, a);
+        ConvArgs<T> b = a;
+        b.ksplit = 1;
+        if (b.Co % 128 == 0 || b.Co >= 384)
+            conv2_go<T, 8>(s, b);
         else
-            conv2_go<T, 6>(s, a);
+            conv2_go<T, 6>(s, b);
         return;
     }
     ConvArgs<T> b = a;

@@ -259,9 +259,10 @@ template <typename T> struct Run {
         c.out = Y;
         c.ldo = ldy;
         c.flags = CE_STORE | (bias ? CE_BIAS : 0) | (epi == EPI_RESID ? CE_RES : 0);
-        const long long tiles64 = (long long)FM_CEIL(R, 64) * FM_CEIL(N, 64);
+        // split K (fp32 slabs + the conv split-K epilogue) until the 128 x 128 tiles number >= 384
+        const long long t128 = (long long)FM_CEIL(R, 128) * FM_CEIL(N, 128);
         int ks = 1;
-        while (tiles64 * ks < 256 && ks < 8 && K / 32 >= 16 * ks * 2) ks *= 2;
+        while (t128 * ks < 384 && ks < 8 && K / 32 >= 8 * ks * 2) ks *= 2;
         c.ksplit = ks;
         c.slab = m->skpart;
         c.slab_cap = (size_t)m->skpart_cap;
@@ -1139,7 +1140,7 @@ static void finalize(fm_llm* m) {
         // arrival counters: one per 16-row tile of the largest decode GEMV (the slow head / W13)
         const int maxn = std::max({m->Nhead, 2 * c.intermediate_size, 2 * c.fast_intermediate_size, qkvmax, dmax, m->cb});  // W1||W3 is one 2*I-row linear on the batched path
         m->tickets = (int*)m->dalloc((size_t)(maxn / 16 + 16) * sizeof(int));
-        m->skpart_cap = 8ll << 20;  // 32 MiB of partial tiles
+        m->skpart_cap = 16ll << 20;  // 64 MiB of partial tiles (prompt GEMM slabs: 256 rows x 2 x 19456)
         m->skpart = (float*)m->dalloc((size_t)m->skpart_cap * sizeof(float), false);
     }
     HIPCHK(hipMemsetAsync(m->attn_cnt, 0, (size_t)R * d.nkv * sizeof(int), m->stream));
