@@ -562,6 +562,13 @@ static void finalize(fm_codec* m) {
             B.ru[r].c7 = prep_wn_conv(m, rp + "1.", cout, cout, 7, dils[r]);
             B.ru[r].c1 = prep_wn_conv(m, rp + "3.", cout, cout, 1, 1);
         }
+        if (b == 0) {
+            // the first stage runs on ~32 x T rows at 768 channels (1.3 LDS tiles per CU): its
+            // transposed conv and k7 convs split K in two (a fixed property of the layer, so every
+            // chunking of a streamed decode sums in the same order)
+            B.ct.ks = 2;
+            for (int r = 0; r < 3; ++r) B.ru[r].c7.ks = 2;
+        }
         cin = cout;
     }
     m->falpha = as_snake(m, raw(m, "decoder.model.5.alpha"), cin);
@@ -610,7 +617,7 @@ static void finalize(fm_codec* m) {
         m->st_cf = m->dstate((size_t)6 * cc * E);
     }
     m->Cb = m->dalloc(Tm * maxact * E);
-    m->ksp_cap = (size_t)4 << 20;  // split-K partial slabs of the small-grid codec GEMMs (16 MB)
+    m->ksp_cap = (size_t)16 << 20;  // split-K partial slabs of the small-grid codec GEMMs (64 MB)
     m->ksp = (float*)m->dalloc(m->ksp_cap * 4);
     m->wave = (float*)m->dalloc(Tm * 2048 * 4);
     if (m->enc_dim) finalize_encoder(m);

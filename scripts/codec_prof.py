@@ -29,6 +29,17 @@ def run():
         print(f"conv2={conv2}: {ms1 - ms0:.2f} ms, {(f1 - f0) / ((ms1 - ms0) * 1e-3) / 1e12:.1f} TFLOP/s", flush=True)
 
 
+def sequence(db, n_decodes):
+    """the last decode's kernels in launch order (name, grid, us): maps times to layers"""
+    import sqlite3
+
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, start, end, grid_x, grid_y, grid_z, workgroup_x from kernels order by start").fetchall()
+    per = len(rows) // n_decodes
+    for r in rows[-per:]:
+        print(f"{(r[2] - r[1]) / 1e3:9.2f} us  {r[0].split('(')[0].replace('void ', '')[:44]:44s} grid=({r[3] // r[6]},{r[4]},{r[5]})")
+
+
 def summarise(db):
     import sqlite3
     from collections import defaultdict
@@ -47,7 +58,9 @@ def summarise(db):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1:
+    if len(sys.argv) > 2:
+        sequence(sys.argv[1], int(sys.argv[2]))
+    elif len(sys.argv) > 1:
         summarise(sys.argv[1])
     else:
         run()
