@@ -214,20 +214,28 @@ __global__ void silu_mul_kernel(const T* __restrict__ g, T* __restrict__ y, size
 
 // z[t][c] = (semantic out_proj(cb[code])) + (sum of residual out_proj(cb_q[code_q]))
 template <typename T>
-__global__ __launch_bounds__(256) void rvq_decode_kernel(const int32_t* __restrict__ codes, int Tn, int nq1,
+__global__ __launch_bounds__(1024) void rvq_decode_kernel(const int32_t* __restrict__ codes, int Tn, int nq1,
                                                          int sem_size, int cb_size, int cd, RvqPtrs p,
                                                          int D, T* __restrict__ z) {
+    // the frame's codebook rows are staged in LDS first (codes, then rows: two round trips for the
+    // block instead of two per stage per thread); sums in the reference's order
+    __shared__ float erow[16][8];
     const int t = blockIdx.x;
+    if (threadIdx.x < nq1 * cd) {
+        const int q = threadIdx.x / cd, j = threadIdx.x - q * cd;
+        int code = codes[(size_t)q * Tn + t];
+        const int mx = (q == 0 ? sem_size : cb_size) - 1;
+        code = code > mx ? mx : code;  // rvq.py:354-359 clamps the max only
+        erow[q][j] = p.cb[q][(size_t)code * cd + j];
+    }
+    __syncthreads();
     for (int c = threadIdx.x; c < D; c += blockDim.x) {
         float zs = 0.f, zr = 0.f;
+#pragma unroll 5
         for (int q = 0; q < nq1; ++q) {
-            int code = codes[(size_t)q * Tn + t];
-            const int mx = (q == 0 ? sem_size : cb_size) - 1;
-            code = code > mx ? mx : code;  // rvq.py:354-359 clamps the max only
-            const float* e = p.cb[q] + (size_t)code * cd;
             const float* w = p.w[q] + (size_t)c * cd;
             float acc = 0.f;
-            for (int j = 0; j < cd; ++j) acc += w[j] * e[j];
+            for (int j = 0; j < cd; ++j) acc += w[j] * erow[q][j];
             acc += p.b[q][c];
             if (q == 0) zs += acc;
             else zr += acc;
@@ -779,7 +787,8 @@ template <typename T> void launch_silu_mul(hipStream_t s, const T* g, T* y, size
 template <typename T>
 void launch_rvq_decode(hipStream_t s, const int32_t* codes, int Tn, int nq1, int sem, int cbs, int cd,
                        const RvqPtrs& p, int D, T* z) {
-    rvq_decode_kernel<T><<<Tn, 256, 0, s>>>(codes, Tn, nq1, sem, cbs, cd, p, D, z);
+    FMCHECK(nq1 >= 1 && nq1 <= 16 && cd >= 1 && cd <= 8, "rvq decode: at most 16 stages of codebook dim <= 8");
+    rvq_decode_kernel<T><<<Tn, 1024, 0, s>>>(codes, Tn, nq1, sem, cbs, cd, p, D, z);
 }
 template <typename T>
 void launch_dwconv_ln(hipStream_t s, const T* x, int L, int D, const T* dw, const T* db, const T* lw,
