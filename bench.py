@@ -460,7 +460,9 @@ def main():
     ccfg = CodecConfig()
     llm = DualARModel.synthetic(cfg, seed=args.seed, log2_half=5, device=local, precision="bf16",
                                 max_slots=max(1, args.batch))
-    codec = FishMICodec.synthetic(ccfg, args.seed + 1, local, "bf16", max_frames=args.frames)
+    # one codec handle for the utterance leg and the config-3 streams: sized so a 512-frame request
+    # vocodes in one pass (the reference decodes a request's codes in one decode_vq_tokens call)
+    codec = FishMICodec.synthetic(ccfg, args.seed + 1, local, "bf16", max_frames=max(args.frames, args.batch_frames))
 
     def sync():
         torch.cuda.synchronize()
