@@ -136,6 +136,12 @@ def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world):
             slot, req.prompt, DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30, seed=req.seed,
                                                    mask_im_end=True)))
 
+    def start_batch(pairs):  # a tick's new requests prefilled together (one GEMM pass over all prompts)
+        return timed("prefill", lambda: llm.prefill_batch(
+            [sl for sl, _ in pairs], [r.prompt for _, r in pairs],
+            [DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30, seed=r.seed, mask_im_end=True)
+             for _, r in pairs]))
+
     def step(slots, n):
         return timed("decode", lambda: llm.decode_frames(slots, n))
 
@@ -150,7 +156,7 @@ def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world):
     sync()
     t0 = time.perf_counter()
     q = S.TickQueue(reqs, C1)
-    stats = S.serve(q, batch, start, step, finish, tick_frames=32)
+    stats = S.serve(q, batch, start, step, finish, tick_frames=32, start_batch=start_batch)
     sync()
     dt = time.perf_counter() - t0
     if dist is not None:

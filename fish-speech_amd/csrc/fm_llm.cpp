@@ -9,6 +9,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <array>
 #include <memory>
 
 #include "fm_codec.h"
@@ -94,6 +95,7 @@ struct fm_llm {
     void *x = nullptr, *h = nullptr, *xn = nullptr, *qkv = nullptr, *q = nullptr, *att = nullptr,
          *act = nullptr;
     void *xl = nullptr, *xnl = nullptr, *fx = nullptr, *fh = nullptr, *fxn = nullptr;
+    void* plast = nullptr;  // batched prefill: the last prompt row of each request [max_slots][dim]
     float *part = nullptr, *logits = nullptr, *flogits = nullptr;
     void* act2 = nullptr;  // batched path: [R][2 * inter] output of the interleaved W1||W3
     int* attn_cnt = nullptr;
@@ -419,7 +421,14 @@ template <typename T> struct Run {
             QkArgs<T> qa{(const T*)m->qkv, d.nqkv(), rslot, rpos, fixed_pos, d.nh, d.nkv, d.hd, d.qk_norm,
                          eps, (const T*)L.qn, (const T*)L.kn, rope, (T*)m->q, (T*)kc, (T*)vc, sstride, loff, Sc};
             run_("rope", 0, 0, [&] { launch_qk_rope_cache<T>(s, qa, R); });
-            if (!is_fast) {
+            if (!is_fast && !segs.empty()) {  // a batched prefill chunk: one attention per prompt
+                for (const auto& sg : segs) {
+                    const size_t o = (size_t)sg[0] * d.nh * d.hd;
+                    AttnArgs<T> aa{(const T*)m->q + o, rslot + sg[0], rpos + sg[0], (const T*)kc, (const T*)vc,
+                                   sstride, loff, Sc, d.nh, d.nkv, d.hd, ATTN_SPLIT, m->maxsplit, scale, m->part};
+                    run_("attn", 0, 0, [&] { launch_attn<T>(s, aa, sg[1], m->maxsplit, (T*)m->att + o, true); });
+                }
+            } else if (!is_fast) {
                 AttnArgs<T> aa{(const T*)m->q, rslot, rpos, (const T*)kc, (const T*)vc, sstride, loff, Sc,
                                d.nh, d.nkv, d.hd, ATTN_SPLIT, m->maxsplit, scale, m->part};
                 run_("attn", 0, 0, [&] { launch_attn<T>(s, aa, R, m->maxsplit, (T*)m->att, !rows_are_slots); });
@@ -875,6 +884,51 @@ template <typename T> struct Run {
         }
         return (const char*)m->x + (size_t)last * m->c.dim * E;
     }
+
+    // Several prompts (one slot each, positions from 0) through the slow stack together: their rows
+    // packed into PREFILL_CHUNK-row chunks, so every linear is one GEMM over all of them (a prompt
+    // may span chunks: its earlier rows are in the KV cache by then); the attention runs per prompt
+    // segment (segs); the last row of prompt i is copied to plast row i.
+    std::vector<std::array<int, 2>> segs;  // (first row, rows) of each prompt inside the current chunk
+    void prefill_multi(int n, const int32_t* slots, const int32_t* const* toks, const int* Ts) {
+        const int C1 = m->C1, dim = m->c.dim;
+        std::vector<int32_t> rows((size_t)PREFILL_CHUNK * C1);
+        std::vector<int> rs(PREFILL_CHUNK), rp(PREFILL_CHUNK);
+        int i = 0, t = 0;  // next (prompt, position) to place
+        while (i < n) {
+            int R = 0;
+            segs.clear();
+            std::vector<std::array<int, 2>> lasts;  // (prompt, row) of prompts ending in this chunk
+            while (R < PREFILL_CHUNK && i < n) {
+                const int take = std::min(PREFILL_CHUNK - R, Ts[i] - t);
+                segs.push_back({R, take});
+                for (int r = 0; r < take; ++r) {
+                    for (int q = 0; q < C1; ++q) rows[(size_t)(R + r) * C1 + q] = toks[i][(size_t)q * Ts[i] + t + r];
+                    rs[R + r] = slots[i];
+                    rp[R + r] = t + r;
+                }
+                R += take;
+                t += take;
+                if (t == Ts[i]) {
+                    lasts.push_back({i, R - 1});
+                    ++i;
+                    t = 0;
+                }
+            }
+            HIPCHK(hipMemcpyAsync(m->ptok, rows.data(), (size_t)R * C1 * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(m->prow_slot, rs.data(), (size_t)R * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(m->prow_pos, rp.data(), (size_t)R * 4, hipMemcpyHostToDevice, s));
+            launch_embed<T>(s, m->ptok, R, (const T*)m->emb, (const T*)m->cbemb, dim, m->C, m->cb,
+                            m->c.semantic_begin_id, m->c.semantic_end_id, m->c.scale_codebook_embeddings,
+                            (T*)m->x, nullptr);
+            slow_layers(R, m->prow_slot, m->prow_pos);
+            for (const auto& l : lasts)
+                HIPCHK(hipMemcpyAsync((char*)m->plast + (size_t)l[0] * dim * E, (const char*)m->x + (size_t)l[1] * dim * E,
+                                      (size_t)dim * E, hipMemcpyDeviceToDevice, s));
+            segs.clear();
+            HIPCHK(hipStreamSynchronize(s));  // host vectors reused by the next chunk
+        }
+    }
 };
 
 // ------------------------------------------------------------------------------------------
@@ -1127,6 +1181,7 @@ static void finalize(fm_llm* m) {
     m->act2 = m->dalloc((size_t)R * 2 * imax * E);
     const int n = m->max_slots;
     m->xl = m->dalloc((size_t)n * dmax * E);
+    m->plast = m->dalloc((size_t)n * dmax * E);
     m->xnl = m->dalloc((size_t)n * dmax * E);
     m->fx = m->dalloc((size_t)n * dmax * E);
     m->fh = m->dalloc((size_t)n * dmax * E);
@@ -1405,6 +1460,63 @@ static void do_prefill(fm_llm* m, int slot, const int32_t* tokens, int T, const 
     m->host_step[slot] = 1;
     m->uploaded_slots.clear();
     if (first_col) memcpy(first_col, m->h_cols, (size_t)m->C1 * 4);
+}
+
+// Several requests prefilled together (each from position 0 of its own slot): one pass of the slow
+// stack over all their prompt rows, then one batched first frame (head + fast model + samplers) for
+// their last rows -- the same columns as n separate do_prefill calls.
+static void do_prefill_batch(fm_llm* m, int n, const int32_t* slots, const int32_t* tokens, const int32_t* T,
+                             const fm_sampling* sps, int32_t* first_cols) {
+    FMCHECK(n >= 1 && n <= m->max_slots, "bad request count");
+    std::vector<const int32_t*> tk(n);
+    size_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        FMCHECK(slots[i] >= 0 && slots[i] < m->max_slots, "bad slot");
+        for (int j = 0; j < i; ++j) FMCHECK(slots[j] != slots[i], "duplicate slot");
+        FMCHECK(T[i] >= 1 && T[i] < m->c.max_seq_len, "prompt must end before max_seq_len");
+        tk[i] = tokens + off;
+        check_tokens(m, tk[i], T[i]);
+        off += (size_t)m->C1 * T[i];
+    }
+    for (int i = 0; i < n; ++i) reset_slot(m, slots[i], sps ? sps + i : nullptr);
+    m->uploaded_slots.clear();
+    HIPCHK(hipMemcpyAsync(m->frame_slot, slots, (size_t)n * 4, hipMemcpyHostToDevice, m->stream));
+    with_prec(m, [&](auto& r) {
+        r.prefill_multi(n, slots, tk.data(), T);
+        if (n <= GEMV_MAX_ROWS) {
+            const void* hid = r.head_small(m->plast, false, n, 1);
+            r.frame_tail_small(n, false, true, hid);
+        } else {
+            r.bs_frame = true;
+            r.head_and_hidden(m->plast, n);
+            r.frame_tail(n, false, true);
+            r.bs_frame = false;
+        }
+    });
+    std::vector<int> pos(n);
+    for (int i = 0; i < n; ++i) pos[i] = T[i] - 1;  // finish() advances it
+    HIPCHK(hipMemcpyAsync(m->frame_pos, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice, m->stream));
+    launch_finish(m->stream, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10,
+                  m->C1, 0, m->sp);
+    HIPCHK(hipMemcpyAsync(m->h_cols, m->cols, (size_t)n * m->C1 * 4, hipMemcpyDeviceToHost, m->stream));
+    HIPCHK(hipStreamSynchronize(m->stream));
+    m->prof.collect();
+    for (int i = 0; i < n; ++i) {
+        m->host_pos[slots[i]] = T[i];
+        m->host_step[slots[i]] = 1;
+    }
+    m->uploaded_slots.clear();
+    if (first_cols) memcpy(first_cols, m->h_cols, (size_t)n * m->C1 * 4);
+}
+
+int fm_llm_prefill_batch(fm_llm* m, int n, const int32_t* slots, const int32_t* tokens, const int32_t* T,
+                         const fm_sampling* sp, int32_t* first_cols) {
+    return fm_guard([&] {
+        FMCHECK(m && slots && tokens && T, "null argument");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        do_prefill_batch(m, n, slots, tokens, T, sp, first_cols);
+    });
 }
 
 int fm_llm_prefill(fm_llm* m, int slot, const int32_t* tokens, int T, const fm_sampling* sp,

@@ -170,6 +170,22 @@ class DualARModel:
                                                      ctypes.byref(sampling), native.i32p(col)))
         return col
 
+    def prefill_batch(self, slots, prompts, samplings) -> np.ndarray:
+        """Prefill several requests together (fm_llm_prefill_batch): slots distinct, prompts (C+1, T_i),
+        one sampling record each; returns the first columns (n, C+1), as n prefill() calls would."""
+        n = len(slots)
+        assert n == len(prompts) == len(samplings) and n >= 1
+        s = np.ascontiguousarray(slots, dtype=np.int32)
+        ps = [np.ascontiguousarray(p, dtype=np.int32) for p in prompts]
+        assert all(p.shape[0] == self.C1 for p in ps)
+        T = np.array([p.shape[1] for p in ps], np.int32)
+        tok = np.ascontiguousarray(np.concatenate([p.ravel() for p in ps]))
+        sp = (native.SamplingC * n)(*samplings)
+        out = np.zeros((n, self.C1), np.int32)
+        native.check(native.lib().fm_llm_prefill_batch(self.h, n, native.i32p(s), native.i32p(tok), native.i32p(T),
+                                                       sp, native.i32p(out)))
+        return out
+
     def decode(self, slots) -> np.ndarray:
         s = np.ascontiguousarray(slots, dtype=np.int32)
         out = np.zeros((s.size, self.C1), np.int32)

@@ -22,7 +22,7 @@ _lib = None
 # every symbol include/fishmi.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = [
     "fm_device_count", "fm_last_error", "fm_llm_open", "fm_llm_set_quant", "fm_llm_set_tensor", "fm_llm_synth_tensor",
-    "fm_llm_finalize", "fm_llm_prefill", "fm_llm_decode", "fm_llm_decode_frames", "fm_llm_generate", "fm_llm_generate_at", "fm_llm_prefill_at", "fm_llm_slot_pos", "fm_llm_teacher_step",
+    "fm_llm_finalize", "fm_llm_prefill", "fm_llm_prefill_batch", "fm_llm_decode", "fm_llm_decode_frames", "fm_llm_generate", "fm_llm_generate_at", "fm_llm_prefill_at", "fm_llm_slot_pos", "fm_llm_teacher_step",
     "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph", "fm_tune", "fm_debug_ts_read",
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
     "fm_codec_finalize", "fm_codec_decode", "fm_codec_stream_reset", "fm_codec_decode_chunk",
@@ -61,6 +61,7 @@ def lib():
     L.fm_llm_synth_tensor.argtypes = [vp, ctypes.c_char_p, i64, u64, f32, i32]
     L.fm_llm_finalize.argtypes = [vp]
     L.fm_llm_prefill.argtypes = [vp, i32, pi32, i32, ctypes.POINTER(SamplingC), pi32]
+    L.fm_llm_prefill_batch.argtypes = [vp, i32, pi32, pi32, pi32, ctypes.POINTER(SamplingC), pi32]
     L.fm_llm_decode.argtypes = [vp, pi32, i32, pi32]
     L.fm_llm_decode_frames.argtypes = [vp, pi32, i32, i32, pi32]
     L.fm_llm_generate.argtypes = [vp, i32, pi32, i32, i32, ctypes.POINTER(SamplingC), pi32,

@@ -205,10 +205,13 @@ class _Stream:
 
 def serve(queue: TickQueue, max_concurrent: int, start: Callable[[int, Request], np.ndarray],
           step: Callable[[List[int], int], np.ndarray], finish: Callable[[int, Request, np.ndarray], np.ndarray],
-          tick_frames: int = 16, im_end: Optional[int] = None) -> Dict[str, int]:
+          tick_frames: int = 16, im_end: Optional[int] = None,
+          start_batch: Optional[Callable[[List[tuple]], np.ndarray]] = None) -> Dict[str, int]:
     """Per-rank serving loop over the tick queue.
 
-    start(slot, req) prefills the request into its KV slot and returns the first column (C+1,).
+    start(slot, req) prefills the request into its KV slot and returns the first column (C+1,);
+    start_batch([(slot, req), ...]), when given, prefills a tick's new requests together and returns
+    their first columns (n, C+1) (fm_llm_prefill_batch).
     step(slots, n) decodes n batched frames for the slots and returns (n, len(slots), C+1).
     finish(slot, req, cols (C+1, N)) turns the stream into its result payload (PCM or codes).
     A stream ends after req.frames columns, or at the column whose main token is `im_end`. The
@@ -224,9 +227,15 @@ def serve(queue: TickQueue, max_concurrent: int, start: Callable[[int, Request],
         finished = []
         if new is None:
             break
-        for req in new:
-            slot = free_slots.pop()
-            active[slot] = _Stream(req, [start(slot, req)], 1)
+        if start_batch is not None and new:
+            pairs = [(free_slots.pop(), req) for req in new]
+            firsts = start_batch(pairs)
+            for (slot, req), col in zip(pairs, firsts):
+                active[slot] = _Stream(req, [col], 1)
+        else:
+            for req in new:
+                slot = free_slots.pop()
+                active[slot] = _Stream(req, [start(slot, req)], 1)
         done_now = []
         for slot, s in active.items():  # a stream can end on its first column
             if s.done >= s.req.frames or (im_end is not None and s.cols[-1][0] == im_end):

@@ -106,6 +106,13 @@ int fm_llm_set_tensor(fm_llm* h, const char* name, const void* host_data, int sr
 int fm_llm_synth_tensor(fm_llm* h, const char* name, int64_t numel, uint64_t seed, float center,
                         int log2_half);
 int fm_llm_finalize(fm_llm* h);
+/* n requests prefilled together (each from position 0 of its own slot, slots distinct): tokens
+   holds each request's (C+1) x T[i] prompt block back to back, sp one sampling record per request;
+   one pass of the slow stack over all prompt rows, one batched first frame; writes n first columns
+   (n x (C+1)), the same as n fm_llm_prefill calls (the reference prefills requests one by one:
+   inference.py:620-724; this is the serving side's batched form of it). */
+int fm_llm_prefill_batch(fm_llm* h, int n, const int32_t* slots, const int32_t* tokens, const int32_t* T,
+                         const fm_sampling* sp, int32_t* first_cols);
 /* resets slot's caches and runs the prompt; writes the first emitted column (C+1). */
 int fm_llm_prefill(fm_llm* h, int slot, const int32_t* tokens, int T, const fm_sampling* sp,
                    int32_t* first_col);

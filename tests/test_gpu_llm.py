@@ -508,3 +508,32 @@ def test_fast_attention_in_wo_prologue(name, golden):
         np.testing.assert_array_equal(out, ref)
     finally:
         native.tune("attn_wo", 0)
+
+
+@pytest.mark.parametrize("n", [3, 10])
+def test_prefill_batch_matches_single(n, golden):
+    """fm_llm_prefill_batch (config 3's tick of new requests prefilled together: one slow-stack pass
+    over all prompt rows packed into 256-row chunks, prompts spanning chunks, attention per prompt
+    segment, one batched first frame) gives every request the same first column and the same
+    greedy continuation as its own fm_llm_prefill (fp32 mode); n = 3 takes the batch-1 GEMV tail,
+    n = 10 the batched one."""
+    from fishmi.llm import DualARModel
+
+    m, g, cfg = _model("llm_b", "fp32", golden, max_slots=n)
+    rng = np.random.default_rng(31 + n)
+    lens = rng.integers(5, 150, n)
+    prompts = []
+    for T in lens:
+        p = np.zeros((cfg.num_codebooks + 1, int(T)), np.int32)
+        p[0] = rng.integers(16, cfg.semantic_begin_id, int(T))
+        p[1:] = rng.integers(0, cfg.codebook_size, (cfg.num_codebooks, int(T)))
+        prompts.append(p)
+    sps = [DualARModel.sampling(top_k=1, seed=s, mask_im_end=True) for s in range(n)]
+    slots = list(range(n))
+    single = [m.prefill(s, p, sp) for s, p, sp in zip(slots, prompts, sps)]
+    single_fr = m.decode_frames(slots, 6)
+    batch = m.prefill_batch(slots[::-1], prompts[::-1], sps[::-1])[::-1]
+    batch_fr = m.decode_frames(slots, 6)
+    np.testing.assert_array_equal(np.stack(single), batch)
+    np.testing.assert_array_equal(single_fr, batch_fr)
+    m.close()
