@@ -25,7 +25,8 @@ extern "C" int fm_device_count(void) {
     return n;
 }
 
-static constexpr int PREFILL_CHUNK = 256;
+static constexpr int PREFILL_CHUNK = 1024;  // prompt rows per slow-stack pass (GEMM M)
+static constexpr int ATTN_PIECE = 256;      // prompt rows per attention launch (bounds the split partials)
 static constexpr int ATTN_SPLIT = 64;
 static constexpr int GEMV_MAX_ROWS = 8;  // frames with <= 8 streams take the fused GEMV path
 static constexpr int KSB_MAX = 8;
@@ -421,17 +422,21 @@ template <typename T> struct Run {
             QkArgs<T> qa{(const T*)m->qkv, d.nqkv(), rslot, rpos, fixed_pos, d.nh, d.nkv, d.hd, d.qk_norm,
                          eps, (const T*)L.qn, (const T*)L.kn, rope, (T*)m->q, (T*)kc, (T*)vc, sstride, loff, Sc};
             run_("rope", 0, 0, [&] { launch_qk_rope_cache<T>(s, qa, R); });
-            if (!is_fast && !segs.empty()) {  // a batched prefill chunk: one attention per prompt
-                for (const auto& sg : segs) {
-                    const size_t o = (size_t)sg[0] * d.nh * d.hd;
-                    AttnArgs<T> aa{(const T*)m->q + o, rslot + sg[0], rpos + sg[0], (const T*)kc, (const T*)vc,
-                                   sstride, loff, Sc, d.nh, d.nkv, d.hd, ATTN_SPLIT, m->maxsplit, scale, m->part};
-                    run_("attn", 0, 0, [&] { launch_attn<T>(s, aa, sg[1], m->maxsplit, (T*)m->att + o, true); });
-                }
-            } else if (!is_fast) {
-                AttnArgs<T> aa{(const T*)m->q, rslot, rpos, (const T*)kc, (const T*)vc, sstride, loff, Sc,
-                               d.nh, d.nkv, d.hd, ATTN_SPLIT, m->maxsplit, scale, m->part};
-                run_("attn", 0, 0, [&] { launch_attn<T>(s, aa, R, m->maxsplit, (T*)m->att, !rows_are_slots); });
+            if (!is_fast) {
+                // rows [r0, r0 + len) in pieces of <= ATTN_PIECE rows (rows are independent given the cache)
+                auto attn_rows = [&](int r0, int len, bool one_slot) {
+                    for (int p0 = r0; p0 < r0 + len; p0 += ATTN_PIECE) {
+                        const int pn = std::min(ATTN_PIECE, r0 + len - p0);
+                        const size_t o = (size_t)p0 * d.nh * d.hd;
+                        AttnArgs<T> aa{(const T*)m->q + o, rslot + p0, rpos + p0, (const T*)kc, (const T*)vc, sstride,
+                                       loff, Sc, d.nh, d.nkv, d.hd, ATTN_SPLIT, m->maxsplit, scale, m->part};
+                        run_("attn", 0, 0, [&] { launch_attn<T>(s, aa, pn, m->maxsplit, (T*)m->att + o, one_slot); });
+                    }
+                };
+                if (!segs.empty())  // a batched prefill chunk: attention per prompt segment
+                    for (const auto& sg : segs) attn_rows(sg[0], sg[1], true);
+                else
+                    attn_rows(0, R, !rows_are_slots);
             } else {
                 FastAttnArgs<T> fa{(const T*)m->q, rslot, (const T*)kc, (const T*)vc, sstride, loff, Sc,
                                    d.nh, d.nkv, d.hd, fixed_pos, scale, (T*)m->att};
@@ -1187,7 +1192,8 @@ static void finalize(fm_llm* m) {
     m->fh = m->dalloc((size_t)n * dmax * E);
     m->fxn = m->dalloc((size_t)n * dmax * E);
     m->maxsplit = FM_CEIL(m->S, ATTN_SPLIT);
-    m->part = (float*)m->dalloc((size_t)R * d.nh * std::max(m->maxsplit, FM_CEIL(m->S, 16)) * (d.hd + 2) * 4, false);
+    const int Rpart = std::max(m->max_slots, ATTN_PIECE);  // decode rows, or one prompt attention piece
+    m->part = (float*)m->dalloc((size_t)Rpart * d.nh * std::max(m->maxsplit, FM_CEIL(m->S, 16)) * (d.hd + 2) * 4, false);
     m->attn_cnt = (int*)m->dalloc((size_t)R * d.nkv * sizeof(int));  // tickets: zeroed
     m->ssX = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
     m->ssH = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
