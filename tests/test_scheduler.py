@@ -49,7 +49,7 @@ def expected_codes(req):
     return np.array(cols, np.int32).T[1:, :-1]
 
 
-def _worker(rank, world, port, q, n_req, conc):
+def _worker(rank, world, port, q, n_req, conc, batched=False):
     import torch.distributed as dist
 
     from fishmi import scheduler as S
@@ -80,21 +80,25 @@ def _worker(rank, world, port, q, n_req, conc):
             del slots[slot]
             return np.ascontiguousarray(cols[1:]).reshape(-1).astype(np.int32)
 
-        stats = S.serve(queue, conc, start, step, finish, tick_frames=6, im_end=IM_END)
+        def start_batch(pairs):  # a tick's new requests at once (fm_llm_prefill_batch's seam)
+            return np.stack([start(slot, req) for slot, req in pairs])
+
+        stats = S.serve(queue, conc, start, step, finish, tick_frames=6, im_end=IM_END,
+                        start_batch=start_batch if batched else None)
         res = [(r.id, r.rank, r.data.tolist()) for r in queue.results] if rank == 0 else None
         q.put((rank, stats, peak[0], res))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_req,conc", [(11, 3), (2, 4), (0, 2)])
-def test_tick_queue_world2(n_req, conc):
+@pytest.mark.parametrize("n_req,conc,batched", [(11, 3, False), (2, 4, False), (0, 2, False), (11, 3, True)])
+def test_tick_queue_world2(n_req, conc, batched):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, n_req, conc)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, n_req, conc, batched)) for r in range(2)]
     for p in procs:
         p.start()
     out = {}
