@@ -260,7 +260,8 @@ def longform_leg(ccfg, device, turns, frames_per_turn, seed):
         firsts, samples, turn_t0 = [], 0, t0
         for o in E.generate_long(model=llm, text=text, max_new_tokens=frames_per_turn, top_p=0.8, top_k=30,
                                  temperature=0.8, chunk_length=200, prompt_text=["a thirty second reference"],
-                                 prompt_tokens=[ptok], seed=seed, stream_frames=22, mask_im_end=True):
+                                 prompt_tokens=[ptok], seed=seed, stream_frames=22, mask_im_end=True,
+                                 reuse_prefix=True):
             if o.action != "sample":
                 continue
             if o.stream == 0:

@@ -984,9 +984,154 @@ __device__ int sample_top(const float* cv, const int* cid, int K, float M, float
     return bid;
 }
 
+// ---- top_k > 64 (the reference's logits_to_probs takes any top_k, inference.py:54-77) ----------
+// The row's (key << 32 | ~id) words are sorted descending in LDS by a block bitonic sort (P, a power
+// of two >= Nl; padding 0 never ranks), so rank r is the reference's r-th entry of the stable
+// descending sort.  Thread 0 runs the reference's cumsum in rank order and finds the kept prefix
+// (rank 0, then ranks < top_k whose rounded cumulative probability stays <= top_p); the draw
+// argmax(prob / q) over it is a block reduction.  One sort serves both RAS draws.
+__device__ __forceinline__ float sw_val(uint64_t k) {
+    const uint32_t u = (uint32_t)(k >> 32);
+    return __uint_as_float(u & 0x80000000u ? (u & 0x7fffffffu) : ~u);
+}
+__device__ __forceinline__ int sw_id(uint64_t k) { return (int)~(uint32_t)k; }
+__host__ __device__ __forceinline__ int sw_pow2(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+// keys[0, P): filled by the caller (all threads), this sorts them, better first
+__device__ void sw_sort(uint64_t* keys, int P) {
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t x = keys[i], y = keys[ixj];
+                    const bool desc = (i & k) == 0;
+                    if (desc ? (x < y) : (x > y)) {
+                        keys[i] = y;
+                        keys[ixj] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// one draw over the sorted keys; every thread of the block calls it, every thread gets the token
+template <typename T>
+__device__ int sw_draw(const uint64_t* keys, int Nl, float M, float den, float temperature, float top_p,
+                       int top_k, uint64_t seed, uint64_t step, uint32_t draw, int* sh_i, float* sh_f) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (threadIdx.x == 0) {
+        const float tp = rnd<T>(top_p);
+        const int lim = top_k < Nl ? top_k : Nl;
+        float cum = 0.f;
+        int nk = 1;
+        for (int r = 0; r < lim; ++r) {
+            const float v = sw_val(keys[r]);
+            if (v == -INFINITY) break;  // zero probability: never drawn (sample_top's keep)
+            cum += rnd<T>(expf(v - M) / den);
+            if (r > 0 && rnd<T>(cum) > tp) break;
+            nk = r + 1;
+        }
+        sh_i[0] = nk;
+    }
+    __syncthreads();
+    const int nk = sh_i[0];
+    const float tt = fmaxf(rnd<T>(temperature), 1e-5f);
+    const float m2 = rnd<T>(sw_val(keys[0]) / tt);  // rank 0 holds the largest scaled logit
+    float e = 0.f;
+    for (int r = threadIdx.x; r < nk; r += blockDim.x) e += expf(rnd<T>(sw_val(keys[r]) / tt) - m2);
+    e = wave_sum(e);
+    __syncthreads();
+    if (lane == 0) sh_f[wave] = e;
+    __syncthreads();
+    float d2 = 0.f;
+    for (int w = 0; w < nw; ++w) d2 += sh_f[w];
+    float best = -1.f;
+    int bid = 0x7fffffff;
+    for (int r = threadIdx.x; r < nk; r += blockDim.x) {
+        const float v = sw_val(keys[r]);
+        const int id = sw_id(keys[r]);
+        const float prob = rnd<T>(expf(rnd<T>(v / tt) - m2) / d2);
+        const float u = rng_uniform_bf16(seed, step, draw, (uint32_t)id);
+        const float score = rnd<T>(prob / rnd<T>(-logf(u)));
+        if (cbetter(score, id, best, bid)) {
+            best = score;
+            bid = id;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float os = __shfl_xor(best, o, 64);
+        const int oid = __shfl_xor(bid, o, 64);
+        if (cbetter(os, oid, best, bid)) {
+            best = os;
+            bid = oid;
+        }
+    }
+    __syncthreads();
+    if (lane == 0) {
+        sh_f[wave] = best;
+        sh_i[1 + wave] = bid;
+    }
+    __syncthreads();
+    float bb = sh_f[0];
+    int bi = sh_i[1];
+    for (int w = 1; w < nw; ++w)
+        if (cbetter(sh_f[w], sh_i[1 + w], bb, bi)) {
+            bb = sh_f[w];
+            bi = sh_i[1 + w];
+        }
+    __syncthreads();
+    return bi;
+}
+
+// the wide path of both samplers: sort, draw (twice with RAS on the slow head), emit the column
+template <typename T>
+__device__ void sample_wide(const SampleArgs& a, const SlotParams& sp, int r, int slot, uint64_t* keys, int P,
+                            float M, float den) {
+    __shared__ int sh_i[1 + 16];
+    __shared__ float sh_f[16];
+    sw_sort(keys, P);
+    const uint64_t step = (uint64_t)sp.step;
+    int32_t* col = a.cols + (size_t)r * a.ldc;
+    if (a.slow) {
+        int tok = sw_draw<T>(keys, a.Nl, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed, step, 0, sh_i, sh_f);
+        const int hi = sw_draw<T>(keys, a.Nl, M, den, 1.0f, 0.9f, sp.top_k, sp.seed, step, 1, sh_i, sh_f);
+        if (threadIdx.x != 0) return;
+        if (a.ras_enable) {
+            const int32_t* prev = a.ras + (size_t)slot * a.ras_stride;
+            bool inwin = false;
+            for (int j = 0; j < 10; ++j) inwin |= prev[j] == tok;
+            if (inwin && tok >= a.sb && tok <= a.se) tok = hi;
+        }
+        if (!((tok >= a.sb && tok <= a.se) || tok == a.im_end)) tok = a.im_end;
+        int c = tok - a.sb;
+        c = c < 0 ? 0 : (c > a.cb - 1 ? a.cb - 1 : c);
+        if (sp.force) {
+            tok = a.force_cols[(size_t)slot * a.ldc];
+            c = a.force_cols[(size_t)slot * a.ldc + 1];
+        }
+        col[0] = tok;
+        col[1] = c;
+    } else {
+        const int code = sw_draw<T>(keys, a.Nl, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed, step,
+                                    (uint32_t)a.draw, sh_i, sh_f);
+        if (threadIdx.x == 0)
+            col[a.col_idx] = sp.force ? a.force_cols[(size_t)slot * a.ldc + a.col_idx]
+                                      : ((code >= 0 && code < a.cb) ? code : 0);
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void sample_radix_kernel(SampleArgs a) {
-    extern __shared__ float vals[];  // [Nl]
+    extern __shared__ __attribute__((aligned(16))) float vals[];  // [Nl]; [P] u64 keys (top_k > 64)
     __shared__ float scratch[16];
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh_prefix, sh_rem, sh_nstrict, sh_ntie;
@@ -1016,6 +1161,18 @@ __global__ __launch_bounds__(256) void sample_radix_kernel(SampleArgs a) {
     float sloc = 0.f;
     for (int i = threadIdx.x; i < Nl; i += 256) sloc += (vals[i] == -INFINITY) ? 0.f : expf(vals[i] - M);
     const float den = block_sum(sloc, scratch);
+    if (sp.top_k > 64) {  // block-uniform
+        const int P = sw_pow2(Nl);
+        uint64_t* keys = reinterpret_cast<uint64_t*>(vals);  // vals are re-read from the row
+        __syncthreads();
+        for (int i = threadIdx.x; i < P; i += 256) {
+            float v = i < Nl ? lg[i] : -INFINITY;
+            if (a.slow && sp.mask_im_end && i == Nl - 1) v = -INFINITY;
+            keys[i] = i < Nl ? (((uint64_t)fkey(v) << 32) | (uint32_t)~(uint32_t)tok_of(i)) : 0ull;
+        }
+        sample_wide<T>(a, sp, r, slot, keys, P, M, den);
+        return;
+    }
     int K = sp.top_k < 1 ? 1 : (sp.top_k > 64 ? 64 : sp.top_k);
     if (K > Nl) K = Nl;
 
@@ -1235,7 +1392,7 @@ __global__ __launch_bounds__(256) void sample_fast_kernel(SampleArgs a) {
     unsigned long long tsx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define SFTS(n) if (a.dbg) tsx[n] = __builtin_amdgcn_s_memrealtime();
     SFTS(0)
-    extern __shared__ float vals[];  // [Nl] (fallback path only)
+    extern __shared__ __attribute__((aligned(16))) float vals[];  // [Nl] fallback; [P] u64 keys (top_k > 64)
     __shared__ float redm[4], reds[4];
     __shared__ uint32_t wthr[4];
     __shared__ uint32_t ncand[4];
@@ -1315,6 +1472,18 @@ __global__ __launch_bounds__(256) void sample_fast_kernel(SampleArgs a) {
     __syncthreads();
     SFTS(4)
     const float den = reds[0] + reds[1] + reds[2] + reds[3];
+    if (sp.top_k > 64) {  // block-uniform: the wide path over the whole row (sorted in LDS)
+        const int P = sw_pow2(Nl);
+        uint64_t* keys = reinterpret_cast<uint64_t*>(vals);
+#pragma unroll
+        for (int i = 0; i < SF_PER; ++i) {
+            const int idx = threadIdx.x + 256 * i;
+            if (idx < Nl) keys[idx] = ((uint64_t)fkey(v[i]) << 32) | (uint32_t)~(uint32_t)tok_of(idx);
+        }
+        for (int i = Nl + threadIdx.x; i < P; i += 256) keys[i] = 0ull;
+        sample_wide<T>(a, sp, r, slot, keys, P, M, den);
+        return;
+    }
     if (overflow) {  // degenerate ties: park everything in LDS for the exact scan below
 #pragma unroll
         for (int i = 0; i < SF_PER; ++i) {
@@ -1491,10 +1660,21 @@ template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFused
     fast_attn_fused_kernel<T><<<g, 256, lds, s>>>(a);
 }
 template <typename T> void launch_sample_radix(hipStream_t s, const SampleArgs& a, int R) {
+    // dynamic LDS: the row's values, or the sorted keys of the top_k > 64 path (top_k lives on the
+    // device, per slot, so every launch reserves the larger)
+    const size_t lds = std::max(sizeof(float) * a.Nl, sizeof(uint64_t) * (size_t)sw_pow2(a.Nl));
+    static bool big = false;
+    if (lds > 64 * 1024 && !big) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sample_fast_kernel<T>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sample_radix_kernel<T>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        big = true;
+    }
     if (a.Nl <= 256 * SF_PER && fm_tuning().sampler_fast)
-        sample_fast_kernel<T><<<R, 256, sizeof(float) * a.Nl, s>>>(a);
+        sample_fast_kernel<T><<<R, 256, lds, s>>>(a);
     else
-        sample_radix_kernel<T><<<R, 256, sizeof(float) * a.Nl, s>>>(a);
+        sample_radix_kernel<T><<<R, 256, lds, s>>>(a);
 }
 template void launch_attn_decode2<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
 template void launch_attn_decode2<float>(hipStream_t, const AttnDecArgs<float>&, int);

@@ -90,7 +90,16 @@ struct fm_codec {
     void *st_dw[2] = {}, *st_c0 = nullptr, *st_cf = nullptr;
     void *st_ct[4] = {}, *st_c7[4][3] = {};
     std::vector<std::pair<void*, size_t>> st_all;
-    int spos = 0;                           // frames already streamed
+    std::vector<void**> st_slots;           // the st_* field each st_all buffer is bound to
+    int spos = 0;                           // frames already streamed (active stream)
+    // stream contexts (fm_codec_stream_open): each holds its own carried rows + position, so
+    // concurrent streamed requests on one handle never share state; id 0 is the handle's own
+    struct StreamCtx {
+        std::vector<void*> bufs;
+        int spos = 0;
+    };
+    std::map<int, StreamCtx> sctx;
+    int active_sid = 0, next_sid = 1;
     // encode side (fm_codec_enable_encoder / fm_codec_encode)
     int enc_dim = 0, enc_layers = 0;        // enc_dim 0: encoder not enabled
     EBlock eblk[4];
@@ -111,6 +120,9 @@ struct fm_codec {
 
     ~fm_codec() {
         if (device >= 0) (void)hipSetDevice(device);
+        for (auto& kv : sctx)
+            if (kv.first != 0)
+                for (void* p : kv.second.bufs) (void)hipFree(p);
         for (auto& kv : w)
             if (kv.second.p) (void)hipFree(kv.second.p);
         for (void* p : allocs) (void)hipFree(p);
@@ -121,10 +133,21 @@ struct fm_codec {
     void* dalloc_prefixed(size_t body, size_t prefix) {  // prefix bytes in front of the base
         return (char*)dalloc(prefix + body) + prefix;
     }
-    void* dstate(size_t bytes) {
+    void dstate(void** slot, size_t bytes) {
         void* p = dalloc(bytes);
         st_all.emplace_back(p, bytes);
-        return p;
+        st_slots.push_back(slot);
+        *slot = p;
+    }
+    // bind the st_* fields to stream `sid`'s buffers (the active stream's position saved first)
+    void activate(int sid) {
+        if (sid == active_sid) return;
+        auto it = sctx.find(sid);
+        FMCHECK(it != sctx.end(), "unknown codec stream id " + std::to_string(sid));
+        sctx[active_sid].spos = spos;
+        for (size_t i = 0; i < st_slots.size(); ++i) *st_slots[i] = it->second.bufs[i];
+        spos = it->second.spos;
+        active_sid = sid;
     }
     void* dalloc(size_t bytes) {
         void* p = nullptr;
@@ -603,18 +626,22 @@ static void finalize(fm_codec* m) {
     m->A = m->dalloc_prefixed(Tm * maxact * E, (size_t)CODEC_HALO * std::max(ch, D) * E);
     m->B = m->dalloc_prefixed(Tm * maxact * E, (size_t)CODEC_HALO * std::max(ch, D) * E);
     FMCHECK(c.t_layers <= 16 && c.window - 1 <= CODEC_HALO, "codec stream state: t_layers <= 16, window <= 129");
-    for (int l = 0; l < c.t_layers; ++l) m->st_kv[l] = m->dstate((size_t)(c.window - 1) * 3 * HD * E);
-    for (int u = 0; u < 2; ++u) m->st_dw[u] = m->dstate((size_t)6 * D * E);
-    m->st_c0 = m->dstate((size_t)6 * D * E);
+    for (int l = 0; l < c.t_layers; ++l) m->dstate(&m->st_kv[l], (size_t)(c.window - 1) * 3 * HD * E);
+    for (int u = 0; u < 2; ++u) m->dstate(&m->st_dw[u], (size_t)6 * D * E);
+    m->dstate(&m->st_c0, (size_t)6 * D * E);
     {
         int cc = ch;
         const int dl[3] = {1, 3, 9};
         for (int b = 0; b < 4; ++b) {
-            m->st_ct[b] = m->dstate((size_t)cc * E);
-            for (int r = 0; r < 3; ++r) m->st_c7[b][r] = m->dstate((size_t)6 * dl[r] * (cc / 2) * E);
+            m->dstate(&m->st_ct[b], (size_t)cc * E);
+            for (int r = 0; r < 3; ++r) m->dstate(&m->st_c7[b][r], (size_t)6 * dl[r] * (cc / 2) * E);
             cc /= 2;
         }
-        m->st_cf = m->dstate((size_t)6 * cc * E);
+        m->dstate(&m->st_cf, (size_t)6 * cc * E);
+    }
+    {
+        auto& c0 = m->sctx[0];
+        for (auto& pb : m->st_all) c0.bufs.push_back(pb.first);
     }
     m->Cb = m->dalloc(Tm * maxact * E);
     m->ksp_cap = (size_t)16 << 20;  // split-K partial slabs of the small-grid codec GEMMs (64 MB)
@@ -963,20 +990,69 @@ int fm_codec_decode(fm_codec* m, const int32_t* codes, int T, float* pcm) {
     return fm_guard([&] { codec_decode(m, codes, T, pcm, false); });
 }
 
+static void stream_zero(fm_codec* m) {
+    for (size_t i = 0; i < m->st_slots.size(); ++i)
+        HIPCHK(hipMemsetAsync(*m->st_slots[i], 0, m->st_all[i].second, m->stream));
+    HIPCHK(hipStreamSynchronize(m->stream));
+    m->spos = 0;
+}
+
 int fm_codec_stream_reset(fm_codec* m) {
     return fm_guard([&] {
         FMCHECK(m, "null handle");
         HIPCHK(hipSetDevice(m->device));
         finalize(m);
-        for (auto& pb : m->st_all) HIPCHK(hipMemsetAsync(pb.first, 0, pb.second, m->stream));
-        HIPCHK(hipStreamSynchronize(m->stream));
-        m->spos = 0;
+        m->activate(0);
+        stream_zero(m);
     });
 }
 
 int fm_codec_decode_chunk(fm_codec* m, const int32_t* codes, int T, float* pcm) {
+    return fm_codec_stream_decode(m, 0, codes, T, pcm);
+}
+
+int fm_codec_stream_open(fm_codec* m, int* sid) {
+    return fm_guard([&] {
+        FMCHECK(m && sid, "null argument");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        const int id = m->next_sid++;
+        fm_codec::StreamCtx ctx;
+        for (auto& pb : m->st_all) {
+            void* p = nullptr;
+            hipError_t e = hipMalloc(&p, pb.second);
+            if (e != hipSuccess) {
+                for (void* q : ctx.bufs) (void)hipFree(q);
+                throw FmError{FM_ERR_OOM, "codec stream state: hipMalloc failed"};
+            }
+            ctx.bufs.push_back(p);
+            HIPCHK(hipMemsetAsync(p, 0, pb.second, m->stream));
+        }
+        HIPCHK(hipStreamSynchronize(m->stream));
+        m->sctx.emplace(id, std::move(ctx));
+        *sid = id;
+    });
+}
+
+int fm_codec_stream_close(fm_codec* m, int sid) {
+    return fm_guard([&] {
+        FMCHECK(m && sid > 0, "bad stream id (0 is the handle's own stream)");
+        auto it = m->sctx.find(sid);
+        FMCHECK(it != m->sctx.end(), "unknown codec stream id " + std::to_string(sid));
+        HIPCHK(hipSetDevice(m->device));
+        if (m->active_sid == sid) m->activate(0);
+        HIPCHK(hipStreamSynchronize(m->stream));
+        for (void* p : it->second.bufs) (void)hipFree(p);
+        m->sctx.erase(it);
+    });
+}
+
+int fm_codec_stream_decode(fm_codec* m, int sid, const int32_t* codes, int T, float* pcm) {
     return fm_guard([&] {
         FMCHECK(m, "null handle");
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        m->activate(sid);
         FMCHECK(m->spos + (int64_t)T <= CODEC_STREAM_MAX, "stream longer than the RoPE table: reset it");
         codec_decode(m, codes, T, pcm, true);
         m->spos += T;

@@ -127,7 +127,6 @@ template <typename T> void launch_qk_rope_cache(hipStream_t s, const QkArgs<T>& 
 template <typename T>
 void launch_attn(hipStream_t s, const AttnArgs<T>& a, int R, int nsplit, T* out, bool one_slot);  // one_slot: rows of one prompt
 template <typename T> void launch_fast_attn(hipStream_t s, const FastAttnArgs<T>& a, int R);
-template <typename T> void launch_sample(hipStream_t s, const SampleArgs& a, int R);
 void launch_finish(hipStream_t s, int R, const int* row_slot, int* row_pos, const int32_t* cols,
                    int ldc, int32_t* tok_in, int32_t* ras, int ras_stride, int C1, int update_ras,
                    SlotParams* sp);

@@ -713,166 +713,6 @@ __global__ __launch_bounds__(64) void fast_attn_kernel(FastAttnArgs<T> a) {
 }
 
 // =========================================================================================
-// sampling (inference.py:43-93) + RAS (117-144).  One block (4 waves) per row.
-// Candidates are (value desc, token id asc): the order of a stable sort (CUDA radix sort).
-// =========================================================================================
-struct Cand {
-    float v;
-    int id;
-};
-__device__ __forceinline__ bool better(float v, int id, float bv, int bid) {
-    return v > bv || (v == bv && id < bid);
-}
-__device__ __forceinline__ void wave_argmax(float& v, int& id) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        float ov = __shfl_xor(v, o, 64);
-        int oid = __shfl_xor(id, o, 64);
-        if (better(ov, oid, v, id)) {
-            v = ov;
-            id = oid;
-        }
-    }
-}
-
-template <typename T>
-__device__ int sample_from(const Cand* cand, int K, float M, float den, float temperature,
-                           float top_p, int top_k, uint64_t seed, uint64_t step, uint32_t draw,
-                           int lane) {
-    // lane k < K holds rank k
-    const float v = lane < K ? cand[lane].v : -INFINITY;
-    const int id = lane < K ? cand[lane].id : 0x7fffffff;
-    const float p = (v == -INFINITY) ? 0.f : rnd<T>(expf(v - M) / den);
-    float cum = 0.f, mycum = 0.f;
-    for (int k = 0; k < K; ++k) {
-        cum += __shfl(p, k, 64);
-        if (lane == k) mycum = rnd<T>(cum);
-    }
-    const float t = rnd<T>(temperature), tp = rnd<T>(top_p);
-    const bool keep = lane < K && v != -INFINITY && (lane == 0 || (!(mycum > tp) && lane < top_k));
-    const float tt = fmaxf(t, 1e-5f);
-    const float lt = keep ? rnd<T>(v / tt) : -INFINITY;
-    const float m2 = wave_max(lt);
-    const float e = keep ? expf(lt - m2) : 0.f;
-    const float d2 = wave_sum(e);
-    const float prob = rnd<T>(e / d2);
-    float score = -1.f;
-    if (keep) {
-        const float u = rng_uniform_bf16(seed, step, draw, (uint32_t)id);
-        const float qv = rnd<T>(-logf(u));
-        score = rnd<T>(prob / qv);
-    }
-    int bid = keep ? id : 0x7fffffff;
-    wave_argmax(score, bid);
-    return bid;
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void sample_kernel(SampleArgs a) {
-    extern __shared__ float vals[];  // [Nl]
-    __shared__ float scratch[16];
-    __shared__ Cand wl[4][64];
-    __shared__ Cand cand[64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int r = blockIdx.x;
-    const int slot = a.row_slot[r];
-    const SlotParams sp = a.sp[slot];
-    const float* lg = a.logits + (size_t)r * a.ldl;
-    const int Nl = a.Nl;
-    for (int i = threadIdx.x; i < Nl; i += 256) {
-        float v = lg[i];
-        if (a.slow && sp.mask_im_end && i == Nl - 1) v = -INFINITY;
-        vals[i] = v;
-    }
-    __syncthreads();
-    // token id of row i: slow head rows = [sb..se] + im_end; fast head: identity
-    auto tok_of = [&](int i) { return a.slow ? (i < Nl - 1 ? a.sb + i : a.im_end) : i; };
-    float mloc = -INFINITY;
-    for (int i = threadIdx.x; i < Nl; i += 256) mloc = fmaxf(mloc, vals[i]);
-    const float M = block_max(mloc, scratch);
-    float sloc = 0.f;
-    for (int i = threadIdx.x; i < Nl; i += 256)
-        sloc += (vals[i] == -INFINITY) ? 0.f : expf(vals[i] - M);
-    const float den = block_sum(sloc, scratch);
-    int K = sp.top_k < 1 ? 1 : sp.top_k;
-    if (K > 64) K = 64;
-    if (K > Nl) K = Nl;
-    // ---- per-wave top-K by repeated wave argmax (each lane owns i = wave*64+lane + 256*j)
-    uint32_t taken = 0;
-    const int per = (Nl + 255) / 256;  // <= 32
-    for (int k = 0; k < K; ++k) {
-        float bv = -INFINITY;
-        int bid = 0x7fffffff, bj = -1;
-        for (int j = 0; j < per; ++j) {
-            const int i = wave * 64 + lane + 256 * j;
-            if (i < Nl && !((taken >> j) & 1u)) {
-                const float v = vals[i];
-                const int id = tok_of(i);
-                if (better(v, id, bv, bid)) {
-                    bv = v;
-                    bid = id;
-                    bj = j;
-                }
-            }
-        }
-        float wv = bv;
-        int wid = bid;
-        wave_argmax(wv, wid);
-        if (bj >= 0 && wid == bid && wv == bv) taken |= 1u << bj;
-        if (lane == 0) wl[wave][k] = Cand{wv, wid};
-    }
-    __syncthreads();
-    if (wave == 0) {
-        // merge 4 sorted lists: lane holds entries lane, lane+64, lane+128, lane+192 of wl
-        uint32_t tk = 0;
-        for (int k = 0; k < K; ++k) {
-            float bv = -INFINITY;
-            int bid = 0x7fffffff, bj = -1;
-            for (int j = 0; j < 4; ++j) {
-                const int e = lane + 64 * j;
-                const int w = e / K, kk = e % K;
-                if (e < 4 * K && !((tk >> j) & 1u) && better(wl[w][kk].v, wl[w][kk].id, bv, bid)) {
-                    bv = wl[w][kk].v;
-                    bid = wl[w][kk].id;
-                    bj = j;
-                }
-            }
-            float wv = bv;
-            int wid = bid;
-            wave_argmax(wv, wid);
-            if (bj >= 0 && wid == bid && wv == bv) tk |= 1u << bj;
-            if (lane == 0) cand[k] = Cand{wv, wid};
-        }
-        __builtin_amdgcn_wave_barrier();
-        const uint64_t step = (uint64_t)sp.step;
-        int32_t* col = a.cols + (size_t)r * a.ldc;
-        if (a.slow) {
-            int tok = sample_from<T>(cand, K, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed,
-                                     step, 0, lane);
-            const int hi = sample_from<T>(cand, K, M, den, 1.0f, 0.9f, sp.top_k, sp.seed, step, 1,
-                                          lane);
-            if (a.ras_enable) {
-                const int32_t* prev = a.ras + (size_t)slot * a.ras_stride;  // row 0, 10 entries
-                bool inwin = false;
-                for (int j = 0; j < 10; ++j) inwin |= prev[j] == tok;
-                const bool sem = tok >= a.sb && tok <= a.se;
-                if (inwin && sem) tok = hi;
-            }
-            if (lane == 0) {
-                col[0] = tok;
-                int c = tok - a.sb;
-                c = c < 0 ? 0 : (c > a.cb - 1 ? a.cb - 1 : c);
-                col[1] = c;
-            }
-        } else {
-            const int code = sample_from<T>(cand, K, M, den, sp.temperature, sp.top_p, sp.top_k,
-                                            sp.seed, step, (uint32_t)a.draw, lane);
-            if (lane == 0) col[a.col_idx] = code;
-        }
-    }
-}
-
-// =========================================================================================
 // frame bookkeeping: RAS window roll (inference.py:227-230), next input column, pos/step++
 // =========================================================================================
 __global__ void finish_kernel(int R, const int* __restrict__ row_slot, int* __restrict__ row_pos,
@@ -1005,9 +845,6 @@ template <typename T> void launch_fast_attn(hipStream_t s, const FastAttnArgs<T>
     dim3 g(R, a.nh);
     fast_attn_kernel<T><<<g, 64, 0, s>>>(a);
 }
-template <typename T> void launch_sample(hipStream_t s, const SampleArgs& a, int R) {
-    sample_kernel<T><<<R, 256, sizeof(float) * a.Nl, s>>>(a);
-}
 void launch_finish(hipStream_t s, int R, const int* row_slot, int* row_pos, const int32_t* cols,
                    int ldc, int32_t* tok_in, int32_t* ras, int ras_stride, int C1, int update_ras,
                    SlotParams* sp) {
@@ -1040,7 +877,6 @@ void launch_convert(hipStream_t s, const void* src, int src_bf16, int64_t n, T* 
     template void launch_fast_attn<T>(hipStream_t, const FastAttnArgs<T>&, int);                 \
     template void launch_attn_combine<T>(hipStream_t, const float*, const int*, int, int, int, int, \
                                          int, T*);                                               \
-    template void launch_sample<T>(hipStream_t, const SampleArgs&, int);                         \
     template void launch_synth<T>(hipStream_t, T*, int64_t, uint64_t, uint32_t, float, int);    \
     template void launch_convert<T>(hipStream_t, const void*, int, int64_t, T*);
 INST(bf16_t)

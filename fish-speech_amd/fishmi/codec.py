@@ -154,6 +154,14 @@ class FishMICodec:
         native.check(native.lib().fm_codec_decode_chunk(self.h, native.i32p(cd), cd.shape[1], native.f32p(out)))
         return out
 
+    def open_stream(self) -> "CodecStream":
+        """A stream context of its own (fm_codec_stream_open): its carried causal rows and RoPE
+        position are independent of the handle's stream and of every other context, so several
+        streamed requests can share one handle (calls still serialised by the caller)."""
+        sid = ctypes.c_int(0)
+        native.check(native.lib().fm_codec_stream_open(self.h, ctypes.byref(sid)))
+        return CodecStream(self, sid.value)
+
     def from_indices(self, indices) -> np.ndarray:
         idx = np.asarray(indices)
         if idx.ndim == 2:
@@ -186,6 +194,27 @@ class FishMICodec:
             self.close()
         except Exception:
             pass
+
+
+class CodecStream:
+    """One streamed vocoding context on a FishMICodec (open_stream); starts at zero state."""
+
+    def __init__(self, codec: FishMICodec, sid: int):
+        self.codec, self.sid = codec, sid
+
+    def decode_chunk(self, codes: np.ndarray) -> np.ndarray:
+        """As FishMICodec.decode_chunk, on this context's carried state."""
+        cd = np.ascontiguousarray(codes, dtype=np.int32)
+        assert cd.ndim == 2 and cd.shape[0] == self.codec.cfg.n_codebooks + 1
+        out = np.zeros(cd.shape[1] * self.codec.frame_length, np.float32)
+        native.check(native.lib().fm_codec_stream_decode(self.codec.h, self.sid, native.i32p(cd), cd.shape[1],
+                                                          native.f32p(out)))
+        return out
+
+    def close(self):
+        if self.sid and getattr(self.codec, "h", None):
+            native.check(native.lib().fm_codec_stream_close(self.codec.h, self.sid))
+        self.sid = 0
 
 
 def smoke_codec(golden_dir: str):

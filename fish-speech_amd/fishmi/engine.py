@@ -71,7 +71,7 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
                   temperature: float = 1.0, compile: bool = False, iterative_prompt: bool = True,
                   chunk_length: int = 512, prompt_text: Optional[Union[str, List[str]]] = None,
                   prompt_tokens=None, seed: Optional[int] = None,
-                  reuse_prefix: bool = True, stream_frames: int = 0,
+                  reuse_prefix: bool = False, stream_frames: int = 0,
                   mask_im_end: bool = False) -> Iterator[GenerateResponse]:
     """inference.py:523-733 on the native model.  `device`, `decode_one_token`, `compile`,
     `iterative_prompt` and `repetition_penalty` are accepted for signature compatibility; like
@@ -82,7 +82,8 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
     the longest prefix its new prompt shares with what the slot already ran (the previous prompt
     plus the columns fed back while generating), and prefills only the rest (fm_llm_generate_at).
     The prompt tokens are the same, so the codes are the same up to the fp32 accumulation order of
-    the reused positions (decode-path vs prefill-path kernels; tests/test_gpu_engine.py).
+    the reused positions (decode-path vs prefill-path kernels; tests/test_gpu_engine.py).  It is
+    opt-in: the default is the reference's own re-prefill flow.
 
     stream_frames > 0 (BASELINE config 5's streamed vocoder): each batch's codes are yielded as they
     are decoded, `stream_frames` columns at a time (GenerateResponse.stream = chunk index), instead of

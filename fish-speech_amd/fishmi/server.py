@@ -100,10 +100,14 @@ def create_app(engine: "TTS.TTSInferenceEngine", max_text_length: int = 0, api_k
         if req.streaming and req.format != "wav":
             raise HTTPException(400, detail="Streaming only supports WAV format")
         headers = {"Content-Disposition": f"attachment; filename=audio.{req.format}"}
+        if req.reference_id is not None and not TTS.valid_reference_id(req.reference_id):
+            raise HTTPException(400, detail="Invalid reference_id")
         if req.streaming:
+            from starlette.concurrency import run_in_threadpool
+
             gen = TTS.inference_wrapper(req, engine)
             try:  # the header (and any immediate engine error) before the response starts
-                first = next(gen)
+                first = await run_in_threadpool(next, gen)
             except TTS.EngineError as e:
                 raise HTTPException(500, detail=str(e))
 
@@ -121,11 +125,17 @@ def create_app(engine: "TTS.TTSInferenceEngine", max_text_length: int = 0, api_k
             return StreamingResponse(stream(), media_type=_content_type("wav"), headers=headers)
         if req.format not in ("wav", "pcm"):
             raise HTTPException(400, detail=f"format {req.format!r} needs an encoder absent from this build")
-        audio = None
-        try:
+        def run():  # blocking engine work off the event loop: concurrent requests reach the worker
+            out = None
             for chunk in TTS.inference_wrapper(req, engine):
                 if isinstance(chunk, np.ndarray):
-                    audio = chunk
+                    out = chunk
+            return out
+
+        from starlette.concurrency import run_in_threadpool
+
+        try:
+            audio = await run_in_threadpool(run)
         except TTS.EngineError as e:
             raise HTTPException(500, detail=str(e))
         data = TTS.wav_bytes(audio, sr) if req.format == "wav" else \
@@ -189,6 +199,17 @@ def main(argv=None):
 
     from .engine import _device_index
 
+    # flags of tools/server/api_utils.py:21-43 that this build cannot honour as given are refused or
+    # mapped explicitly (an operator must not get a different precision or worker count silently)
+    if a.decoder_config_name != "modded_dac_vq":
+        ap.error(f"--decoder-config-name {a.decoder_config_name!r}: only modded_dac_vq (the S2-Pro codec) is built")
+    if a.workers != 1:
+        ap.error("--workers > 1: one process drives one GPU here; run one server per GPU (or use --slots for "
+                 "concurrent requests on one GPU)")
+    if a.half:
+        log.warning("--half: fp16 is not built; the HIP path runs bf16 (the reference's default precision)")
+    if a.compile:
+        log.info("--compile: decode frames are always hipGraph-captured; the flag changes nothing")
     engine = build_engine(a.llama_checkpoint_path, a.decoder_checkpoint_path, _device_index(a.device), "bf16")
     host, port = a.listen.rsplit(":", 1)
     uvicorn.run(create_app(engine, a.max_text_length, a.api_key), host=host, port=int(port), workers=1)

@@ -38,14 +38,36 @@ def _splitmix64(z: np.ndarray) -> np.ndarray:
     return z
 
 
-def synth_f32(seed: int, name: str, n: int, center: float, log2_half: int) -> np.ndarray:
-    """fp32 values in [center - 2**-log2_half, center + 2**-log2_half)."""
-    idx = np.arange(n, dtype=np.uint64)
+def _synth_range(out: np.ndarray, base: np.uint64, lo: int, hi: int, center: float, log2_half: int) -> None:
+    idx = np.arange(lo, hi, dtype=np.uint64)
     with np.errstate(over="ignore"):
-        key = np.uint64(seed) * K1 + np.uint64(fnv1a32(name)) * K2 + idx
+        key = base + idx
     m = (_splitmix64(key) >> np.uint64(40)).astype(np.int64)
     r = ((2 * m - (1 << 24)).astype(np.float32)) * np.float32(2.0 ** (-24 - log2_half))
-    return (np.float32(center) + r).astype(np.float32)
+    out[lo:hi] = np.float32(center) + r
+
+
+_CHUNK = 1 << 23
+
+
+def synth_f32(seed: int, name: str, n: int, center: float, log2_half: int) -> np.ndarray:
+    """fp32 values in [center - 2**-log2_half, center + 2**-log2_half).  Large tensors are made in
+    8M-element chunks on a thread pool (numpy ufuncs release the GIL); every element is the same
+    pure function of (seed, name, index) either way."""
+    with np.errstate(over="ignore"):
+        base = np.uint64(seed) * K1 + np.uint64(fnv1a32(name)) * K2
+    out = np.empty(n, dtype=np.float32)
+    spans = [(lo, min(n, lo + _CHUNK)) for lo in range(0, n, _CHUNK)]
+    if len(spans) <= 1:
+        for lo, hi in spans:
+            _synth_range(out, base, lo, hi, center, log2_half)
+        return out
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        list(ex.map(lambda s: _synth_range(out, base, s[0], s[1], center, log2_half), spans))
+    return out
 
 
 def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:

@@ -153,7 +153,7 @@ class TTSInferenceEngine:
     decoder_model: a FishMICodec (its encoder enabled for voice-clone references)."""
 
     def __init__(self, llama_queue: "queue.Queue", decoder_model, precision="bf16", compile: bool = False,
-                 references_dir: str = "references", stream_frames: int = 22):
+                 references_dir: str = "references", stream_frames: int = 22, reuse_prefix: bool = False):
         self.llama_queue = llama_queue
         self.decoder_model = decoder_model
         self.precision = precision
@@ -165,6 +165,9 @@ class TTSInferenceEngine:
         # streaming requests with latency="balanced": codes arrive `stream_frames` columns at a time
         # (generate_long(stream_frames=...)) and are vocoded as one causal stream per text batch
         self.stream_frames = stream_frames
+        # prefix-KV reuse across a request's text batches (generate_long reuse_prefix): opt-in, the
+        # default is the reference's whole-conversation re-prefill
+        self.reuse_prefix = reuse_prefix
 
     # ---- references (reference_loader.py) -------------------------------------------------
     def encode_reference(self, reference_audio: bytes, enable_reference_audio: bool = True):
@@ -191,7 +194,12 @@ class TTSInferenceEngine:
         return tokens, texts
 
     def load_by_id(self, ref_id: str, use_cache: str):
+        if not valid_reference_id(ref_id):
+            raise ValueError(f"invalid reference_id {ref_id!r}")
         folder = self.references_dir / ref_id
+        root = self.references_dir.resolve()
+        if root not in folder.resolve().parents:
+            raise ValueError(f"reference_id {ref_id!r} leaves the references directory")
         if use_cache == "off" or ref_id not in self.ref_by_id:
             audios = sorted(p for p in folder.rglob("*") if p.suffix.lower() in AUDIO_EXTENSIONS) \
                 if folder.exists() else []
@@ -219,6 +227,8 @@ class TTSInferenceEngine:
                        chunk_length=req.chunk_length, prompt_tokens=prompt_tokens, prompt_text=prompt_texts)
         if req.seed is not None:
             request["seed"] = int(req.seed)
+        if self.reuse_prefix:
+            request["reuse_prefix"] = True
         if req.streaming and req.latency == "balanced" and self.stream_frames > 0:
             request["stream_frames"] = self.stream_frames
         rq: "queue.Queue" = queue.Queue()
@@ -232,13 +242,30 @@ class TTSInferenceEngine:
         with self._codec_lock:
             return self.decoder_model.decode_codes(c)
 
-    def get_audio_segment(self, result: GenerateResponse) -> np.ndarray:
+    def get_audio_segment(self, result: GenerateResponse, streams: Optional[dict] = None) -> np.ndarray:
+        """One "sample" response -> PCM.  A streamed chunk (result.stream set) continues its text
+        batch's causal stream, whose carried codec state belongs to the calling request alone:
+        `streams` is that request's holder ({"ctx": CodecStream}); chunk 0 replaces its context
+        with a fresh one.  Without a holder the handle's own stream is used (one caller only)."""
         if result.stream is not None:  # a chunk of one batch's causal stream: carried codec state
+            codes = np.asarray(result.codes)
             with self._codec_lock:
-                if result.stream == 0:
-                    self.decoder_model.stream_reset()
-                return np.asarray(self.decoder_model.decode_chunk(np.asarray(result.codes)), np.float32)
+                if streams is None or not hasattr(self.decoder_model, "open_stream"):
+                    if result.stream == 0:
+                        self.decoder_model.stream_reset()
+                    return np.asarray(self.decoder_model.decode_chunk(codes), np.float32)
+                if result.stream == 0 or streams.get("ctx") is None:
+                    if streams.get("ctx") is not None:
+                        streams["ctx"].close()
+                    streams["ctx"] = self.decoder_model.open_stream()
+                return np.asarray(streams["ctx"].decode_chunk(codes), np.float32)
         return np.asarray(self.decode_vq_tokens(result.codes), np.float32)
+
+    def _close_streams(self, streams: dict):
+        if streams.get("ctx") is not None:
+            with self._codec_lock:
+                streams["ctx"].close()
+            streams["ctx"] = None
 
     # ---- main entry (inference_engine/__init__.py:41-131) -----------------------------------
     def inference(self, req) -> Generator[InferenceResult, None, None]:
@@ -252,21 +279,25 @@ class TTSInferenceEngine:
         if req.streaming:
             yield InferenceResult(code="header", audio=(sr, np.frombuffer(wav_chunk_header(sr), np.uint8)), error=None)
         segments = []
-        while True:
-            wrapped: WrappedGenerateResponse = rq.get()
-            if wrapped.status == "error":
-                err = wrapped.response if isinstance(wrapped.response, Exception) else Exception("Unknown error")
-                yield InferenceResult(code="error", audio=None, error=err)
-                break
-            result = wrapped.response
-            if not isinstance(result, GenerateResponse):
-                raise TypeError(f"Expected GenerateResponse, got {type(result).__name__}")
-            if result.action == "next":
-                break
-            seg = self.get_audio_segment(result)
-            if req.streaming:
-                yield InferenceResult(code="segment", audio=(sr, seg), error=None)
-            segments.append(seg)
+        streams: dict = {}  # this request's codec stream context (latency="balanced" chunks)
+        try:
+            while True:
+                wrapped: WrappedGenerateResponse = rq.get()
+                if wrapped.status == "error":
+                    err = wrapped.response if isinstance(wrapped.response, Exception) else Exception("Unknown error")
+                    yield InferenceResult(code="error", audio=None, error=err)
+                    break
+                result = wrapped.response
+                if not isinstance(result, GenerateResponse):
+                    raise TypeError(f"Expected GenerateResponse, got {type(result).__name__}")
+                if result.action == "next":
+                    break
+                seg = self.get_audio_segment(result, streams)
+                if req.streaming:
+                    yield InferenceResult(code="segment", audio=(sr, seg), error=None)
+                segments.append(seg)
+        finally:
+            self._close_streams(streams)
         if not segments:
             yield InferenceResult(code="error", audio=None,
                                   error=RuntimeError("No audio generated, please check the input text."))

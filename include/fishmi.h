@@ -170,8 +170,14 @@ int fm_llm_use_graph(fm_llm* h, int enable);
    <|im_end|>, bias NOT applied) and fast logits ((C-1) x codebook_size, codebooks 1..C-1). */
 int fm_llm_force(fm_llm* h, int slot, const int32_t* col);
 int fm_llm_read_logits(fm_llm* h, int slot, float* slow_logits, float* fast_logits);
-/* process-wide developer knobs of the decode GEMV ("gemv_nt" 0|1, "gemv_u" 2|4|8, "gemv_wpb" 4|8, "gemv_sk" 0|1, "gemv_sk_bpc" 1..4, "ksb_blocks" n, "ksb_balance"
-   0|1, "rmsnorm_block" 0|1); they apply to launches recorded after the call (graphs captured earlier keep theirs). */
+/* process-wide developer knobs selecting kernel variants (every variant stays under the default
+   path's parity bar, tests/test_gpu_knobs.py): decode GEMV "gemv_nt" 0|1, "gemv_u" 2|4|8,
+   "gemv_wpb" 4|8, "ksb_blocks" n, "ksb_balance" 0|1; attention "attn_fd" 0|1, "attn3" 0|1,
+   "attn_cap" n, "attn_cap_batched" n, "fd_min" n, "fd_min_batched" n, "attn_wo" 0|1,
+   "batched_fused_attn" 0|1; batched linears "bstream" 0|1, "bstream_kparts" n, "bstream_nw" n,
+   "linear_u32" n, "linear_fill" n; prompt "prefill_attn", "prompt_gemm"; codec "conv2",
+   "conv_splitk"; "sampler_fast" 0|1, "rmsnorm_block" 0|1, "debug_ts" n.  They apply to launches
+   recorded after the call (graphs captured earlier keep theirs). */
 int fm_tune(const char* key, int value);
 /* developer hook ("debug_ts" armed): per-block records of 8 words {tag = N<<32 | blockIdx.y<<16 |
    blockIdx.x, start, staged, streamed, end, 3 kernel-specific} of the decode GEMVs,
@@ -243,10 +249,17 @@ int fm_codec_decode(fm_codec* h, const int32_t* codes, int T, float* pcm);
    inference_engine/vq_manager.py:16-21).  The codec is causal end to end, so a stream of chunks
    that carries each causal reader's previous rows (conv inputs, the transformer's window of
    keys/values, the RoPE position) reproduces the one-shot fm_codec_decode of the concatenated
-   codes exactly.  One stream per handle: stream_reset starts it, each decode_chunk appends T
-   frames (T <= max_frames) and returns their 2048*T samples. */
+   codes exactly.  The handle's own stream: stream_reset starts it, each decode_chunk appends T
+   frames (T <= max_frames) and returns their 2048*T samples.  Concurrent streams (one per
+   streamed request, several requests on one handle): stream_open gives a new context with its own
+   carried rows and position (starting at zero, like a reset), stream_decode appends to it,
+   stream_close frees it.  Calls on one handle are serialised by the caller (one host thread at a
+   time); a context switch rebinds pointers only. */
 int fm_codec_stream_reset(fm_codec* h);
 int fm_codec_decode_chunk(fm_codec* h, const int32_t* codes, int T, float* pcm);
+int fm_codec_stream_open(fm_codec* h, int* stream_id);
+int fm_codec_stream_decode(fm_codec* h, int stream_id, const int32_t* codes, int T, float* pcm);
+int fm_codec_stream_close(fm_codec* h, int stream_id);
 int fm_codec_profile_read(fm_codec* h, double* total_ms, int64_t* launches, double* flops);
 /* test hook: intermediate of the last decode as fp32, time-major (1 transformer out [T][latent],
    2 first upsample [2T][latent], 3 decoder input [4T][latent]); other stages' buffers are

@@ -628,6 +628,139 @@ def cmd_llm_wide():
 
 
 # --------------------------------------------------------------------------------------
+# The configurations the bench times (round 3): BASELINE config 2 at FULL S2-Pro depth (36 slow
+# + 4 fast layers), a >= 3000-token context at S2-Pro widths (config 5's flash-decode regime),
+# and config 3's ragged batch (32 prompts of uniform 16..256 tokens, seed 2).  Weights are the
+# synthetic rule of fishmi.synth (regenerated on the device from the seed), so only prompts,
+# the reference's columns and its teacher-forced logits are stored: slow logits for the 4097
+# rows the semantic bias leaves finite, the bf16 ones as exact bf16 bit patterns.
+# --------------------------------------------------------------------------------------
+def _wide_config(n_layer, n_fast_layer, max_seq_len):
+    import copy as _copy
+
+    c = _copy.deepcopy(LLM_WIDE_CONFIG)
+    c["text_config"]["n_layer"] = n_layer
+    c["text_config"]["max_seq_len"] = max_seq_len
+    c["audio_decoder_config"]["n_layer"] = n_fast_layer
+    return c
+
+
+def _llm_state(config, seed, log2_half):
+    """The synthetic bf16 state dict of a config (built once, shared by the bf16 and fp32 models)."""
+    from fish_speech.models.text2semantic import llama
+
+    cfg_path = os.path.join("/tmp/fishmi_cfg", "config.json")
+    os.makedirs(os.path.dirname(cfg_path), exist_ok=True)
+    with open(cfg_path, "w") as f:
+        json.dump(config, f, indent=1)
+    cfg = llama.BaseModelArgs.from_pretrained(cfg_path)
+    with torch.device("meta"):
+        keys = [(k, tuple(v.shape)) for k, v in llama.DualARTransformer(cfg).state_dict().items()]
+    return cfg, synth_state(keys, seed, functools.partial(synth.llm_rule, log2_half_linear=log2_half))
+
+
+def _llm_from_state(cfg, state, dtype):
+    """bf16: the state's tensors assigned (no copy); fp32: copied into fp32 parameters (the same as
+    build_llm(...).to(torch.float32), without a second full-size bf16 copy)."""
+    from fish_speech.models.text2semantic import llama
+
+    torch.manual_seed(0)
+    model = llama.DualARTransformer(cfg)
+    err = model.load_state_dict(state, strict=False, assign=(dtype == torch.bfloat16))
+    assert not err.missing_keys and not err.unexpected_keys, err
+    model.tokenizer = StubTokenizer()
+    return model.to(dtype).eval()
+
+
+def _bf16_bits(x: np.ndarray) -> np.ndarray:
+    b = synth.f32_to_bf16_bits(x)
+    assert np.array_equal(synth.bf16_bits_to_f32(b), x)  # the reference's bf16 logits are bf16-exact
+    return b
+
+
+def _timed_case(out_name, config, T, n_new, prompt_seed):
+    from fish_speech.models.text2semantic import inference
+
+    t0 = time.time()
+    cfg, state = _llm_state(config, 41, 5)
+    print(f"{out_name}: synthetic state in {time.time() - t0:.0f}s")
+    model = _llm_from_state(cfg, state, torch.bfloat16)
+    prompt = make_prompt(cfg, T, prompt_seed)
+    seq = inference.generate(model=model, prompt=prompt.clone(), max_new_tokens=n_new, audio_masks=None,
+                             audio_parts=None, temperature=0.7, top_p=0.9, top_k=1)
+    n = seq.shape[1] - T
+    slow, fast, _ = teacher_forced(model, seq, T, n, torch.bfloat16)
+    del model
+    print(f"{out_name}: bf16 generate + teacher forcing done at {time.time() - t0:.0f}s")
+    m32 = _llm_from_state(cfg, state, torch.float32)
+    del state
+    s32, f32, _ = teacher_forced(m32, seq, T, n, torch.float32)
+    del m32
+    keep = np.r_[IM_END_ID, cfg.semantic_begin_id:cfg.semantic_end_id + 1]
+    np.savez_compressed(os.path.join(GOLD, f"{out_name}.npz"), config=np.array(json.dumps(config)),
+                        prompt=prompt.numpy().astype(np.int32), seq=seq.numpy().astype(np.int32),
+                        slow_rows=keep.astype(np.int32), slow_logits_bits=_bf16_bits(slow[:, keep]),
+                        fast_logits_bits=_bf16_bits(fast), slow_logits_f32=s32[:, keep], fast_logits_f32=f32,
+                        synth_seed=41, log2_half=5, torch_version=torch.__version__,
+                        threads=torch.get_num_threads())
+    e_s = np.abs(slow[:, keep] - s32[:, keep])
+    print(f"{out_name}: T={T}, {n} frames in {time.time() - t0:.0f}s; reference bf16-vs-fp32 slow logits max "
+          f"{e_s.max():.4g} rms {np.sqrt((e_s ** 2).mean()):.4g}; first cols", seq[:, T:T + 2].T.tolist())
+
+
+def cmd_llm_full():
+    """Config 2 at full depth: 36 slow + 4 fast layers, 64-token prompt, prefill + 8 frames."""
+    _timed_case("llm_full_bf16", _wide_config(36, 4, 128), T=64, n_new=9, prompt_seed=3)
+
+
+def cmd_llm_long():
+    """A 3000-token context at S2-Pro widths (2 slow + 1 fast layers): every decode frame's slow
+    attention spans many flash-decode splits."""
+    _timed_case("llm_long_bf16", _wide_config(2, 1, 3072), T=3000, n_new=7, prompt_seed=5)
+
+
+def cmd_llm_ragged():
+    """Config 3's ragged batch at S2-Pro widths (2 slow + 1 fast layers): 32 prompts with lengths
+    uniform over 16..256 (seed 2), each run by the reference at batch 1 (its only
+    mode): greedy columns + teacher-forced logits for the prefill frame and 2 decode frames.  Fast
+    logits are kept for the last codebook only (its pass reads every fast cache position)."""
+    from fish_speech.models.text2semantic import inference
+
+    B, n_new = 32, 3
+    config = _wide_config(2, 1, 272)
+    lens = np.random.default_rng(2).integers(16, 257, B)
+    t0 = time.time()
+    cfg, state = _llm_state(config, 41, 5)
+    model = _llm_from_state(cfg, state, torch.bfloat16)
+    m32 = _llm_from_state(cfg, state, torch.float32)
+    del state
+    keep = np.r_[IM_END_ID, cfg.semantic_begin_id:cfg.semantic_end_id + 1]
+    res = {k: [] for k in ("seq", "slow_bits", "fast_bits", "slow_f32", "fast_f32")}
+    prompts = {}
+    for i, T in enumerate(lens):
+        T = int(T)
+        prompt = make_prompt(cfg, T, 100 + i)
+        prompts[f"prompt_{i}"] = prompt.numpy().astype(np.int32)
+        seq = inference.generate(model=model, prompt=prompt.clone(), max_new_tokens=n_new, audio_masks=None,
+                                 audio_parts=None, temperature=0.7, top_p=0.9, top_k=1)
+        assert seq.shape[1] - T == n_new
+        slow, fast, _ = teacher_forced(model, seq, T, n_new, torch.bfloat16)
+        s32, f32, _ = teacher_forced(m32, seq, T, n_new, torch.float32)
+        res["seq"].append(seq[:, T:].numpy().astype(np.int32))
+        res["slow_bits"].append(_bf16_bits(slow[:, keep]))
+        res["fast_bits"].append(_bf16_bits(fast[:, -1]))
+        res["slow_f32"].append(s32[:, keep])
+        res["fast_f32"].append(f32[:, -1])
+    np.savez_compressed(os.path.join(GOLD, "llm_ragged_bf16.npz"), config=np.array(json.dumps(config)),
+                        lens=lens.astype(np.int32), cols=np.stack(res["seq"]), slow_rows=keep.astype(np.int32),
+                        slow_logits_bits=np.stack(res["slow_bits"]), fast_last_bits=np.stack(res["fast_bits"]),
+                        slow_logits_f32=np.stack(res["slow_f32"]), fast_last_f32=np.stack(res["fast_f32"]),
+                        synth_seed=41, log2_half=5, torch_version=torch.__version__,
+                        threads=torch.get_num_threads(), **prompts)
+    print(f"llm_ragged: {B} prompts (lens {lens.min()}..{lens.max()}) x {n_new} frames in {time.time() - t0:.0f}s")
+
+
+# --------------------------------------------------------------------------------------
 # Weight-only int8 (SURVEY.md §8f row 4): tools/llama/quantize.py's WeightOnlyInt8QuantHandler
 # (create_quantized_state_dict on the bf16 model, as quantize.py:441-458 runs it, then
 # convert_for_runtime + load, llama.py:528-535) and the reference's generate / teacher forcing

@@ -1,0 +1,168 @@
+"""Parity at the configurations bench.py times.  This module sorts first among the GPU tests, so
+under `pytest -x -m gpu` nothing else can hide a failure here.
+
+* Config 2 at FULL S2-Pro depth (36 slow + 4 fast layers, 64-token prompt, prefill + 8 frames),
+  bf16, through the production decode graph (teacher forcing with the reference's columns).
+* A 3000-token context at S2-Pro widths (config 5's regime): every frame's slow attention spans
+  many flash-decode splits.
+* Config 3's ragged batch: 32 slots holding 32 different prompts of uniform 16..256 tokens (the
+  BASELINE distribution, seed 2), so every slot sits at its own position; decoded together on the
+  batched path, each slot's logits against the reference's batch-1 run of its own prompt (bf16),
+  and each slot's greedy stream against its own batch-1 stream (fp32 validation mode).
+
+Goldens: oracle/gen_goldens.py llm_full / llm_long / llm_ragged (the reference run on CPU in the
+dev container; weights regenerate from the seed on the device).  Bound: tests/parity_util.py."""
+import json
+
+import numpy as np
+import pytest
+
+from parity_util import bf16_vs_golden, bf16_vs_reference, bits_to_f32
+
+pytestmark = pytest.mark.gpu
+
+IM_END = 4
+
+
+def _cfg(g):
+    from fishmi.config import DualARConfig
+
+    cfg = DualARConfig._from_fish_qwen3_omni(json.loads(str(g["config"])))
+    cfg.im_end_id = IM_END
+    return cfg
+
+
+def _teacher_case(name, golden):
+    from fishmi.llm import DualARModel
+
+    g = golden(name)
+    cfg = _cfg(g)
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 1)
+    try:
+        T = g["prompt"].shape[1]
+        slow, fast = m.teacher_decode(g["prompt"], g["seq"][:, T:])
+    finally:
+        m.close()
+    return bf16_vs_golden(slow, fast, g, rows=g["slow_rows"])
+
+
+def test_config2_full_depth_bf16_vs_reference(golden):
+    """36 + 4 layers: bf16 error growth over the whole depth against the reference's own."""
+    st = _teacher_case("llm_full_bf16.npz", golden)
+    assert st["top1_checked"] >= 9
+
+
+def test_long_context_bf16_vs_reference(golden):
+    """3000-token prompt (prefill in chunks, flash-decode over >= 3000 positions per frame)."""
+    g = golden("llm_long_bf16.npz")
+    assert g["prompt"].shape[1] >= 3000
+    _teacher_case("llm_long_bf16.npz", golden)
+
+
+@pytest.mark.parametrize("prefill", ["batch", "single"])
+def test_config3_ragged_32_slots_bf16_vs_reference(prefill, golden):
+    """32 distinct prompts (16..256 tokens) in permuted slots: first frame from prefill_batch (the
+    serving tick's path) or per-slot prefill, then batched decode frames (bstream linears,
+    finalize_norm, attn_fd at 32 different positions), every slot teacher-forced with its own
+    reference columns.  Pooled over slots, the error is within BF16_RATIO x the reference's."""
+    from fishmi.llm import DualARModel
+
+    g = golden("llm_ragged_bf16.npz")
+    cfg = _cfg(g)
+    B = int(g["lens"].size)
+    assert B == 32 and g["lens"].min() >= 16 and g["lens"].max() <= 256 and len(set(g["lens"].tolist())) > 16
+    cols = g["cols"]  # (B, C+1, n)
+    n = cols.shape[2]
+    prompts = [g[f"prompt_{i}"] for i in range(B)]
+    slot_of = np.random.default_rng(4).permutation(B)  # prompt i lives in slot slot_of[i]
+    order = [int(slot_of[i]) for i in np.random.default_rng(5).permutation(B)]  # frame row order
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", B)
+    slow = np.zeros((B, n, cfg.vocab_size), np.float32)
+    fast = np.zeros((B, n, cfg.num_codebooks - 1, cfg.codebook_size), np.float32)
+    sp = DualARModel.sampling(top_k=1)
+    try:
+        for k in range(n):
+            for i in range(B):
+                m.force(int(slot_of[i]), cols[i, :, k])
+            if k == 0:
+                if prefill == "batch":
+                    m.prefill_batch([int(s) for s in slot_of], prompts, [sp] * B)
+                else:
+                    for i in range(B):
+                        m.prefill(int(slot_of[i]), prompts[i], sp)
+            else:
+                m.decode(order)
+            for i in range(B):
+                slow[i, k], fast[i, k] = m.read_logits(int(slot_of[i]))
+    finally:
+        for s in range(B):
+            m.force(s, None)
+        m.close()
+    rows = g["slow_rows"]
+    st = bf16_vs_reference(slow.reshape(B * n, -1)[:, rows], fast[:, :, -1:].reshape(B * n, 1, -1),
+                           bits_to_f32(g["slow_logits_bits"]).reshape(B * n, -1),
+                           bits_to_f32(g["fast_last_bits"]).reshape(B * n, 1, -1),
+                           g["slow_logits_f32"].reshape(B * n, -1), g["fast_last_f32"].reshape(B * n, 1, -1))
+    assert st["top1_checked"] >= B
+
+
+def _ragged_prompts(cfg, B, seed):
+    """Config 3's prompt-length distribution (uniform 16..256), random text / semantic tokens."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(16, 257, B)
+    prompts = []
+    for T in lens:
+        p = np.zeros((cfg.num_codebooks + 1, int(T)), np.int32)
+        p[0] = rng.integers(16, cfg.semantic_begin_id, int(T))
+        sem = rng.random(int(T)) < 0.4
+        p[0, sem] = rng.integers(cfg.semantic_begin_id, cfg.semantic_end_id + 1, int(sem.sum()))
+        p[1:, sem] = rng.integers(0, cfg.codebook_size, (cfg.num_codebooks, int(sem.sum())))
+        prompts.append(p)
+    return lens, prompts
+
+
+def _ragged_fp32(m, cfg, B, n_new, seed):
+    lens, prompts = _ragged_prompts(cfg, B, seed)
+    from fishmi.llm import DualARModel
+
+    slot_of = [int(s) for s in np.random.default_rng(seed + 1).permutation(B)]
+    single = [m.generate(p, n_new, top_k=1, slot=slot_of[i], mask_im_end=True) for i, p in enumerate(prompts)]
+    sp = DualARModel.sampling(top_k=1, mask_im_end=True)
+    firsts = m.prefill_batch(slot_of, prompts, [sp] * B)
+    fr = m.decode_frames(slot_of[::-1], n_new - 1)[:, ::-1]  # rows in reversed slot order
+    for i in range(B):
+        got = np.concatenate([firsts[i][:, None], fr[:, i, :].T], axis=1)
+        np.testing.assert_array_equal(got, single[i], err_msg=f"prompt {i} (T={lens[i]}) in slot {slot_of[i]}")
+
+
+def test_config3_ragged_32_slots_fp32_match_single(golden):
+    """fp32 validation mode, tiny model: 32 ragged prompts batched == each one's batch-1 stream."""
+    from fishmi.config import DualARConfig
+    from fishmi.llm import DualARModel
+    import os
+    from conftest import GOLDEN
+
+    cfg = DualARConfig.from_pretrained(os.path.join(GOLDEN, "llm_b"))
+    cfg.im_end_id = IM_END
+    cfg.max_seq_len = 320
+    g = golden("llm_b_fp32.npz")
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "fp32", 32)
+    try:
+        _ragged_fp32(m, cfg, 32, 12, seed=2)
+    finally:
+        m.close()
+
+
+def test_config3_ragged_32_slots_fp32_wide_match_single(golden):
+    """fp32 validation mode at S2-Pro widths (2 + 1 layers): the same property on the batched
+    bstream / finalize_norm / attn_fd path with the real head counts and widths."""
+    from fishmi.llm import DualARModel
+
+    g = golden("llm_ragged_bf16.npz")
+    cfg = _cfg(g)
+    cfg.max_seq_len = 272
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "fp32", 32)
+    try:
+        _ragged_fp32(m, cfg, 32, 5, seed=12)
+    finally:
+        m.close()

@@ -52,3 +52,38 @@ def test_stream_rejects_oversized_chunk(golden):
     with pytest.raises(FishMIError):
         m.decode_chunk(np.zeros((m.cfg.n_codebooks + 1, 17), np.int32))
     m.close()
+
+
+def test_interleaved_stream_contexts_equal_one_shot(golden):
+    """Two stream contexts (fm_codec_stream_open) plus the handle's own stream, their chunks
+    interleaved on one handle: each reproduces the one-shot decode of its own codes bit for bit
+    (one context per streamed request in the TTS engine)."""
+    m = _codec(golden, "bf16", 64)
+    rng = np.random.default_rng(21)
+    C1, T = m.cfg.n_codebooks + 1, 150
+    streams = []
+    for _ in range(3):
+        c = np.zeros((C1, T), np.int32)
+        c[0] = rng.integers(0, m.cfg.semantic_codebook_size, T)
+        c[1:] = rng.integers(0, m.cfg.codebook_size, (C1 - 1, T))
+        streams.append(c)
+    full = [m.decode_codes(c) for c in streams]
+    ctx = [m.open_stream(), m.open_stream(), None]
+    m.stream_reset()
+    pcm = [[], [], []]
+    sizes = [(22,) * 6 + (18,), (7, 30, 50, 63), (1, 49, 50, 50)]
+    pos = [0, 0, 0]
+    step = 0
+    while any(p < T for p in pos):
+        for i in range(3):
+            if step < len(sizes[i]):
+                n = sizes[i][step]
+                chunk = np.ascontiguousarray(streams[i][:, pos[i]:pos[i] + n])
+                pcm[i].append(ctx[i].decode_chunk(chunk) if ctx[i] is not None else m.decode_chunk(chunk))
+                pos[i] += n
+        step += 1
+    for i in range(3):
+        np.testing.assert_array_equal(np.concatenate(pcm[i]), full[i])
+    ctx[0].close()
+    ctx[1].close()
+    m.close()

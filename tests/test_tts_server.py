@@ -193,3 +193,79 @@ def test_http_vqgan_routes():
                headers={"Content-Type": "application/msgpack"})
     a = np.frombuffer(msgpack.unpackb(r.content, raw=False)["audios"][0], np.float16)
     assert a.size == 4 * 2048
+
+
+class FakeStreamCodec(FakeCodec):
+    """A codec whose streamed chunks continue a carried position, like the HIP codec's causal state:
+    a chunk decoded on the wrong context comes out shifted."""
+
+    def decode_codes(self, codes):
+        c = np.asarray(codes)
+        t = np.arange(c.shape[1] * self.frame_length, dtype=np.float32)
+        return (0.5 * np.sin(t * 0.01 + np.repeat(c[0].astype(np.float32), self.frame_length))).astype(np.float32)
+
+    def open_stream(self):
+        codec = self
+
+        class S:
+            pos = 0
+            closed = False
+
+            def decode_chunk(self, codes):
+                assert not self.closed
+                c = np.asarray(codes)
+                t = np.arange(self.pos, self.pos + c.shape[1] * codec.frame_length, dtype=np.float32)
+                self.pos += c.shape[1] * codec.frame_length
+                return (0.5 * np.sin(t * 0.01 + np.repeat(c[0].astype(np.float32), codec.frame_length))).astype(np.float32)
+
+            def close(self):
+                self.closed = True
+
+        return S()
+
+    def stream_reset(self):  # the handle's single stream must not be used by concurrent requests
+        raise AssertionError("shared codec stream used")
+
+    decode_chunk = stream_reset
+
+
+def test_interleaved_streaming_requests_keep_their_own_codec_state():
+    """Two latency=balanced streaming requests consumed alternately: each one's audio equals the
+    one-shot decode of its own codes (one shared carried state corrupted the other)."""
+    from fishmi.engine import GenerateResponse, WrappedGenerateResponse
+    from fishmi.tts import ServeTTSRequest, TTSInferenceEngine
+
+    q = queue.Queue()
+    codes_of = {}
+
+    def run():
+        while True:
+            item = q.get()
+            if item is None:
+                return
+            base = 3 if item.request["text"] == "a" else 40
+            chunks = [np.full((10, n), base + i, np.int32) for i, n in enumerate((2, 3, 1))]
+            codes_of[item.request["text"]] = np.concatenate(chunks, axis=1)
+            for i, c in enumerate(chunks):
+                item.response_queue.put(WrappedGenerateResponse("success", GenerateResponse("sample", c, "t", stream=i)))
+            item.response_queue.put(WrappedGenerateResponse("success", GenerateResponse("next")))
+
+    threading.Thread(target=run, daemon=True).start()
+    codec = FakeStreamCodec()
+    eng = TTSInferenceEngine(q, codec)
+    ga = eng.inference(ServeTTSRequest(text="a", streaming=True, latency="balanced"))
+    gb = eng.inference(ServeTTSRequest(text="b", streaming=True, latency="balanced"))
+    outs = {"a": [], "b": []}
+    live = {"a": ga, "b": gb}
+    while live:
+        for k in list(live):
+            try:
+                r = next(live[k])
+            except StopIteration:
+                del live[k]
+                continue
+            if r.code == "segment":
+                outs[k].append(r.audio[1])
+    q.put(None)
+    for k in ("a", "b"):
+        np.testing.assert_allclose(np.concatenate(outs[k]), codec.decode_codes(codes_of[k]), atol=1e-6)
