@@ -65,6 +65,108 @@ def _codes(x) -> np.ndarray:
     return np.asarray(x)
 
 
+@dataclass
+class BatchPlan:
+    """One generate() of generate_long: the full prompt, how much of it the slot already holds."""
+    enc: np.ndarray      # (C+1, T) int32: the whole conversation prompt of this batch
+    L: int               # positions [0, L) reused from the slot's KV (prefill enc[:, L:] at pos0 = L)
+    sp: object           # the slot's sampling record (model.sampling(...))
+    max_new: int         # most columns to emit, the prefill's included (inference.py:262-271)
+    text: str
+
+
+class ConversationJob:
+    """generate_long's host side (inference.py:523-733) as a state machine, so that one request's
+    text batches can be driven by the serial worker (generate_long) or interleaved with other
+    requests' on batched KV slots (fishmi.batching.BatchedWorker) with the same prompts, seeds and
+    prefix-reuse decisions.  next_batch() -> BatchPlan | "next" (a sample's batches are done) |
+    None (the request is done); finish_batch(y, fed_cols) -> the batch's codes."""
+
+    def __init__(self, model, *, text: str, tokenizer=None, device=None, decode_one_token=None, num_samples: int = 1,
+                 max_new_tokens: int = 0, top_p: float = 0.9, top_k: int = 30, repetition_penalty: float = 1.1,
+                 temperature: float = 1.0, compile: bool = False, iterative_prompt: bool = True,
+                 chunk_length: int = 512, prompt_text=None, prompt_tokens=None, seed: Optional[int] = None,
+                 reuse_prefix: bool = False, stream_frames: int = 0, mask_im_end: bool = False):
+        if not (0 < top_p <= 1):
+            raise AssertionError("top_p must be in (0, 1]")
+        if not (0 < temperature < 2):
+            raise AssertionError("temperature must be in (0, 2)")
+        self.tok = tokenizer if tokenizer is not None else getattr(model, "tokenizer", None)
+        if self.tok is None:
+            raise ValueError("generate_long needs the checkpoint tokenizer (tokenizer.json)")
+        self.model = model
+        self.C = model.cfg.num_codebooks
+        if isinstance(prompt_tokens, (list, tuple)):
+            ptoks = [_codes(t) for t in prompt_tokens]
+        elif prompt_tokens is not None:
+            # one (C, T) array: base_conversation wraps it together with a str prompt_text, as the
+            # reference does (inference.py:544-547)
+            ptoks = _codes(prompt_tokens)
+        else:
+            ptoks = None
+        self.base = P.base_conversation(prompt_text, ptoks)
+        turns = P.split_text_by_speaker(text)
+        self.batches = P.group_turns_into_batches(turns, max_speakers=5, max_bytes=chunk_length) if turns else [text]
+        log.info("Split into %d turns, grouped into %d batches", len(turns), len(self.batches))
+        self.num_samples, self.max_new_tokens = num_samples, max_new_tokens
+        self.top_p, self.top_k, self.temperature = top_p, top_k, temperature
+        self.seed, self.reuse_prefix, self.stream_frames = seed, reuse_prefix, stream_frames
+        self.mask_im_end = mask_im_end
+        self.rng = np.random.default_rng(seed)
+        self.sample_idx, self.batch_idx = 0, 0
+        self.conv = copy.deepcopy(self.base)
+        self.cached = None  # (C+1, P) tokens whose KV the slot holds at positions [0, P)
+        self.plan: Optional[BatchPlan] = None
+        self.t0 = time.perf_counter()
+
+    def next_batch(self):
+        if self.sample_idx >= self.num_samples:
+            return None
+        if self.batch_idx >= len(self.batches):
+            self.sample_idx += 1
+            self.batch_idx = 0
+            self.conv = copy.deepcopy(self.base)
+            self.cached = None
+            self.t0 = time.perf_counter()
+            return "next"
+        batch_text = self.batches[self.batch_idx]
+        self.conv.append(P.Message(role="user", parts=[P.TextPart(text=batch_text)]))
+        gen = copy.deepcopy(self.conv)
+        gen.append(P.Message(role="assistant", parts=[], modality="voice", add_im_end=False))
+        encoded, _, _ = gen.encode_for_inference(self.tok, num_codebooks=self.C)
+        max_len = self.model.cfg.max_seq_len
+        if encoded.shape[1] > max_len - 2048:
+            raise ValueError(f"Prompt is too long: {encoded.shape[1]} > {max_len - 2048}")
+        s = int(self.rng.integers(0, 2**63 - 1)) if self.seed is None \
+            else self.seed + 1000003 * self.sample_idx + self.batch_idx
+        enc = encoded.astype(np.int32)
+        L = 0
+        if self.reuse_prefix and self.cached is not None:
+            n = min(self.cached.shape[1], enc.shape[1] - 1)  # at least one new position to prefill
+            same = np.all(self.cached[:, :n] == enc[:, :n], axis=0)
+            L = int(n if same.all() else np.argmin(same))
+        T = enc.shape[1]
+        mx = self.max_new_tokens if (self.max_new_tokens and T + self.max_new_tokens <= max_len) else max_len - T
+        self.plan = BatchPlan(enc, L, self.model.sampling(self.temperature, self.top_p, self.top_k, s,
+                                                          self.mask_im_end), mx, batch_text)
+        return self.plan
+
+    def finish_batch(self, y: np.ndarray, fed_cols: np.ndarray) -> np.ndarray:
+        """y: (C+1, n) the emitted columns (generate()'s seq[:, T:]); fed_cols: the columns the slot
+        consumed while decoding (its KV past the prompt)."""
+        plan = self.plan
+        if self.reuse_prefix:
+            self.cached = np.concatenate([plan.enc, fed_cols], axis=1)
+        codes = np.ascontiguousarray(y[1:, :-1])  # y[1:, prompt_length:-1] of the reference
+        if (codes < 0).any():
+            raise AssertionError(f"Negative code found: {codes}")
+        log.info("Batch %d: generated %d frames in %.2fs", self.batch_idx, y.shape[1], time.perf_counter() - self.t0)
+        self.conv.append(P.Message(role="assistant", parts=[P.VQPart(codes=codes)], modality="voice"))
+        self.batch_idx += 1
+        self.plan = None
+        return codes
+
+
 def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = None, device=None,
                   decode_one_token=None, num_samples: int = 1, max_new_tokens: int = 0,
                   top_p: float = 0.9, top_k: int = 30, repetition_penalty: float = 1.1,
@@ -73,7 +175,7 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
                   prompt_tokens=None, seed: Optional[int] = None,
                   reuse_prefix: bool = False, stream_frames: int = 0,
                   mask_im_end: bool = False) -> Iterator[GenerateResponse]:
-    """inference.py:523-733 on the native model.  `device`, `decode_one_token`, `compile`,
+    """inference.py:523-733 on the native model (slot 0).  `device`, `decode_one_token`, `compile`,
     `iterative_prompt` and `repetition_penalty` are accepted for signature compatibility; like
     the reference, repetition_penalty is not applied (RAS is, inside the sampler).
 
@@ -89,67 +191,33 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
     are decoded, `stream_frames` columns at a time (GenerateResponse.stream = chunk index), instead of
     once per batch; their concatenation equals the batch's codes.  mask_im_end: fixed-length
     generation for benchmarks (the semantic bias keeps <|im_end|> at -inf)."""
-    if not (0 < top_p <= 1):
-        raise AssertionError("top_p must be in (0, 1]")
-    if not (0 < temperature < 2):
-        raise AssertionError("temperature must be in (0, 2)")
-    tok = tokenizer if tokenizer is not None else getattr(model, "tokenizer", None)
-    if tok is None:
-        raise ValueError("generate_long needs the checkpoint tokenizer (tokenizer.json)")
-    C = model.cfg.num_codebooks
-    if isinstance(prompt_tokens, (list, tuple)):
-        ptoks = [_codes(t) for t in prompt_tokens]
-    elif prompt_tokens is not None:
-        # one (C, T) array: base_conversation wraps it together with a str prompt_text, as the
-        # reference does (inference.py:544-547)
-        ptoks = _codes(prompt_tokens)
-    else:
-        ptoks = None
-    base = P.base_conversation(prompt_text, ptoks)
-    turns = P.split_text_by_speaker(text)
-    batches = P.group_turns_into_batches(turns, max_speakers=5, max_bytes=chunk_length) if turns else [text]
-    log.info("Split into %d turns, grouped into %d batches", len(turns), len(batches))
-    max_len = model.cfg.max_seq_len
-    rng = np.random.default_rng(seed)
-    for sample_idx in range(num_samples):
-        conv = copy.deepcopy(base)
-        t0 = time.perf_counter()
-        cached = None  # (C+1, P) tokens whose KV the slot holds at positions [0, P)
-        for batch_idx, batch_text in enumerate(batches):
-            conv.append(P.Message(role="user", parts=[P.TextPart(text=batch_text)]))
-            gen = copy.deepcopy(conv)
-            gen.append(P.Message(role="assistant", parts=[], modality="voice", add_im_end=False))
-            encoded, _, _ = gen.encode_for_inference(tok, num_codebooks=C)
-            if encoded.shape[1] > max_len - 2048:
-                raise ValueError(f"Prompt is too long: {encoded.shape[1]} > {max_len - 2048}")
-            s = int(rng.integers(0, 2**63 - 1)) if seed is None else seed + 1000003 * sample_idx + batch_idx
-            enc = encoded.astype(np.int32)
-            L = 0
-            if reuse_prefix and cached is not None:
-                n = min(cached.shape[1], enc.shape[1] - 1)  # at least one new position to prefill
-                same = np.all(cached[:, :n] == enc[:, :n], axis=0)
-                L = int(n if same.all() else np.argmin(same))
-            if stream_frames > 0:
-                y, fed_cols = yield from _stream_batch(model, enc, L, max_new_tokens, stream_frames, batch_text,
-                                                       model.sampling(temperature, top_p, top_k, s, mask_im_end))
-            elif L > 0:
+    job = ConversationJob(model, text=text, tokenizer=tokenizer, num_samples=num_samples,
+                          max_new_tokens=max_new_tokens, top_p=top_p, top_k=top_k, temperature=temperature,
+                          chunk_length=chunk_length, prompt_text=prompt_text, prompt_tokens=prompt_tokens,
+                          seed=seed, reuse_prefix=reuse_prefix, stream_frames=stream_frames,
+                          mask_im_end=mask_im_end)
+    while True:
+        plan = job.next_batch()
+        if plan is None:
+            return
+        if plan == "next":
+            yield GenerateResponse(action="next")
+            continue
+        enc, L = plan.enc, plan.L
+        if stream_frames > 0:
+            y, fed_cols = yield from _stream_batch(model, enc, L, max_new_tokens, stream_frames, plan.text, plan.sp)
+        else:
+            if L > 0:
                 y = model.generate_at(enc[:, L:], L, max_new_tokens, temperature=temperature, top_p=top_p,
-                                      top_k=top_k, seed=s, mask_im_end=mask_im_end)
+                                      top_k=top_k, seed=plan.sp.seed, mask_im_end=mask_im_end)
             else:
                 y = model.generate(enc, max_new_tokens, temperature=temperature, top_p=top_p, top_k=top_k,
-                                   seed=s, mask_im_end=mask_im_end)
-            if reuse_prefix and hasattr(model, "slot_pos"):
-                fed = model.slot_pos() - enc.shape[1]  # columns fed back while decoding
-                cached = np.concatenate([enc, (fed_cols if stream_frames > 0 else y)[:, :fed]], axis=1)
-            codes = np.ascontiguousarray(y[1:, :-1])  # y[1:, prompt_length:-1] of the reference
-            if (codes < 0).any():
-                raise AssertionError(f"Negative code found: {codes}")
-            dt = time.perf_counter() - t0
-            log.info("Batch %d: generated %d frames in %.2fs", batch_idx, y.shape[1], dt)
-            conv.append(P.Message(role="assistant", parts=[P.VQPart(codes=codes)], modality="voice"))
-            if stream_frames <= 0:
-                yield GenerateResponse(action="sample", codes=codes, text=batch_text)
-        yield GenerateResponse(action="next")
+                                   seed=plan.sp.seed, mask_im_end=mask_im_end)
+            fed = model.slot_pos() - enc.shape[1] if reuse_prefix else 0  # columns fed back while decoding
+            fed_cols = y[:, :fed]
+        codes = job.finish_batch(y, fed_cols)
+        if stream_frames <= 0:
+            yield GenerateResponse(action="sample", codes=codes, text=plan.text)
 
 
 def _stream_batch(model, enc, L, max_new_tokens, stream_frames, text, sp):
@@ -213,20 +281,34 @@ def load_model(checkpoint_path: str, device=0, precision="bf16", max_slots: int 
 
 
 def launch_thread_safe_queue(checkpoint_path, device, precision, compile: bool = False,
-                             model=None) -> "queue.Queue":
+                             model=None, max_slots: int = 1, tick_frames: int = 8) -> "queue.Queue":
     """inference.py:748-799: a daemon worker owning the model; returns its input queue once the
-    model is loaded.  `model` (optional) hands in an already-built DualARModel (tests)."""
-    input_queue: "queue.Queue" = queue.Queue()
+    model is loaded.  `model` (optional) hands in an already-built DualARModel (tests).
+
+    max_slots == 1: the reference's worker, one request at a time (generate_long on slot 0).
+    max_slots > 1: fishmi.batching.BatchedWorker -- up to max_slots requests decode together on
+    their own KV slots (batched hipGraph frames), same queue contract (BASELINE config 3)."""
     ready = threading.Event()
     failure: List[BaseException] = []
+    holder: dict = {}
 
     def worker():
         try:
-            m = model if model is not None else load_model(checkpoint_path, device, precision)
+            m = model if model is not None else load_model(checkpoint_path, device, precision, max_slots)
         except BaseException as e:  # surface load failures to the caller instead of hanging
             failure.append(e)
             ready.set()
             return
+        if max_slots > 1:
+            from .batching import BatchedWorker
+
+            w = BatchedWorker(m, max_slots, tick_frames)
+            holder["q"] = w.input
+            ready.set()
+            w.run()
+            return
+        input_queue: "queue.Queue" = queue.Queue()
+        holder["q"] = input_queue
         ready.set()
         while True:
             item = input_queue.get()
@@ -243,4 +325,4 @@ def launch_thread_safe_queue(checkpoint_path, device, precision, compile: bool =
     ready.wait()
     if failure:
         raise failure[0]
-    return input_queue
+    return holder["q"]

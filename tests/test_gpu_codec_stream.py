@@ -58,7 +58,7 @@ def test_interleaved_stream_contexts_equal_one_shot(golden):
     """Two stream contexts (fm_codec_stream_open) plus the handle's own stream, their chunks
     interleaved on one handle: each reproduces the one-shot decode of its own codes bit for bit
     (one context per streamed request in the TTS engine)."""
-    m = _codec(golden, "bf16", 64)
+    m = _codec(golden, "bf16", 160)
     rng = np.random.default_rng(21)
     C1, T = m.cfg.n_codebooks + 1, 150
     streams = []

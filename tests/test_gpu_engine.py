@@ -125,3 +125,47 @@ def test_load_model_from_checkpoint_dir(tmp_path):
     m = engine.load_model(_ckpt(tmp_path), "cuda:0", "bfloat16")
     assert m.tokenizer.semantic_begin_id == m.cfg.semantic_begin_id == 200
     assert m.cfg.im_end_id == 4
+
+
+@pytest.mark.parametrize("slots", [3, 12])
+def test_batched_worker_matches_serial(golden, tmp_path, slots):
+    """launch_thread_safe_queue(max_slots > 1): concurrent generate_long requests on batched KV slots
+    (fishmi.batching.BatchedWorker; 12 slots take the bstream batched linears) answer each request
+    with exactly its serial generate_long codes (fp32 validation mode), streamed and reused-prefix
+    requests included; the first request is the reference golden's."""
+    from fishmi import engine
+    from fishmi.llm import DualARModel
+
+    g = golden("engine.npz")
+    m = DualARModel.from_pretrained(_ckpt(tmp_path), device=0, precision="fp32", max_length=2560,
+                                    max_slots=slots)
+    reqs = [_request(g)]
+    texts = ["<|speaker:0|>Hello there. <|speaker:1|>Hi! How are you doing today?", "just one sentence",
+             "<|speaker:0|>a. <|speaker:1|>bb. <|speaker:0|>ccc dd ee."]
+    for i in range(7):
+        reqs.append(_request(g, text=texts[i % 3], top_k=30, seed=50 + i, max_new_tokens=9 + 3 * i,
+                             reuse_prefix=(i % 2 == 0), stream_frames=(5 if i % 3 == 1 else 0)))
+    serial = [list(engine.generate_long(model=m, **r)) for r in reqs]
+    q_in = engine.launch_thread_safe_queue(None, 0, "fp32", model=m, max_slots=slots)
+    qs = [queue.Queue() for _ in reqs]
+    for r, q in zip(reqs, qs):
+        q_in.put(engine.GenerateRequest(request=r, response_queue=q))
+    for i, (q, ref) in enumerate(zip(qs, serial)):
+        got = _drain(q)
+        assert all(w.status == "success" for w in got), got[-1].response
+
+        def batches(rs):
+            out = []
+            for r in rs:
+                if r.action == "sample" and r.stream is not None and r.stream > 0:
+                    out[-1] = np.concatenate([out[-1], r.codes], axis=1)
+                elif r.action == "sample":
+                    out.append(np.asarray(r.codes))
+            return out
+
+        a, b = batches([w.response for w in got]), batches(ref)
+        assert len(a) == len(b) >= 1, i
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y, err_msg=f"request {i}")
+    np.testing.assert_array_equal(serial[0][0].codes, g["codes_0"])
+    q_in.put(None)
