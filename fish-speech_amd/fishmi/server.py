@@ -15,7 +15,11 @@ Routes and contract, as the reference serves them (tools/server/views.py, api_ut
   GET  /v1/references/list     {"success": true, "reference_ids": [...]}
 Optional bearer auth (--api-key): 401 "Invalid token" otherwise (tools/api_server.py:33-45).
 
-    python -m fishmi.server --llama-checkpoint-path DIR --decoder-checkpoint-path codec.pth
+    python -m fishmi.server --llama-checkpoint-path DIR --decoder-checkpoint-path codec.pth [--slots 32]
+
+--slots N serves up to N requests at once on one GPU (fishmi.batching.BatchedWorker: batched decode
+frames, each request on its own KV slot); handlers run the blocking engine work in the thread pool, so
+concurrent HTTP requests reach the worker together.  One server process per GPU.
 """
 import argparse
 import io
@@ -171,14 +175,15 @@ def create_app(engine: "TTS.TTSInferenceEngine", max_text_length: int = 0, api_k
 
 
 def build_engine(llama_checkpoint_path: str, decoder_checkpoint_path: str, device=0, precision="bf16",
-                 compile: bool = False, max_frames: int = 2048):
-    """ModelManager (tools/server/model_manager.py): the LLM worker + the codec with its encoder."""
+                 compile: bool = False, max_frames: int = 2048, slots: int = 1, reuse_prefix: bool = False):
+    """ModelManager (tools/server/model_manager.py): the LLM worker + the codec with its encoder.
+    slots > 1: concurrent requests decode together on their own KV slots (fishmi.batching)."""
     from .codec import FishMICodec
     from .engine import launch_thread_safe_queue
 
-    q = launch_thread_safe_queue(llama_checkpoint_path, device, precision, compile)
+    q = launch_thread_safe_queue(llama_checkpoint_path, device, precision, compile, max_slots=slots)
     codec = FishMICodec.from_checkpoint(decoder_checkpoint_path, device, precision, max_frames, encoder=True)
-    return TTS.TTSInferenceEngine(q, codec, precision, compile)
+    return TTS.TTSInferenceEngine(q, codec, precision, compile, reuse_prefix=reuse_prefix)
 
 
 def main(argv=None):
@@ -194,6 +199,10 @@ def main(argv=None):
     ap.add_argument("--listen", default="127.0.0.1:8080")
     ap.add_argument("--workers", type=int, default=1)
     ap.add_argument("--api-key", default=None)
+    ap.add_argument("--slots", type=int, default=1,
+                    help="concurrent requests decoded together on one GPU (KV slots); 1 = the reference's serial worker")
+    ap.add_argument("--reuse-prefix", action="store_true",
+                    help="keep a request's conversation KV across its text batches (opt-in; default re-prefills)")
     a = ap.parse_args(argv)
     import uvicorn
 
@@ -210,7 +219,8 @@ def main(argv=None):
         log.warning("--half: fp16 is not built; the HIP path runs bf16 (the reference's default precision)")
     if a.compile:
         log.info("--compile: decode frames are always hipGraph-captured; the flag changes nothing")
-    engine = build_engine(a.llama_checkpoint_path, a.decoder_checkpoint_path, _device_index(a.device), "bf16")
+    engine = build_engine(a.llama_checkpoint_path, a.decoder_checkpoint_path, _device_index(a.device), "bf16",
+                          slots=a.slots, reuse_prefix=a.reuse_prefix)
     host, port = a.listen.rsplit(":", 1)
     uvicorn.run(create_app(engine, a.max_text_length, a.api_key), host=host, port=int(port), workers=1)
 
