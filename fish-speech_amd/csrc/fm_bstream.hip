@@ -25,6 +25,8 @@
 #include "fm_runtime.h"
 #include "fm_frag.h"
 
+#include <cmath>
+
 namespace {
 
 constexpr int BS_MAXW = 16;  // waves per block
@@ -133,6 +135,117 @@ __global__ __launch_bounds__(BS_MAXW * 64) void bstream_kernel(BstreamArgs<T> a)
     }
 }
 
+// bsacc_kernel: the same weight stream without a barrier per tile.  Block b takes K part
+// b % kparts and a balanced run of tiles (<= NTM); each wave keeps one pair of 16x16 accumulators
+// PER TILE in registers, streams its fragments through a ring TPI tiles deep, and only after the
+// whole run do the waves meet once: every (tile, wave) partial goes to LDS, then the epilogue of
+// all the block's tiles.  kparts is chosen so that tiles * kparts is a whole number of rounds of
+// the grid (no block streams twice as much as another).
+template <typename T, int SPW, int TPI, int NTM, int EPI>
+__global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
+    using F = Frag<T>;
+    extern __shared__ __attribute__((aligned(16))) f32x4_t bred[];  // [NTM][NW][2][64]
+    constexpr int U = SPW * TPI;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
+    const int kparts = a.kparts;
+    const int kp = blockIdx.x % kparts, gb = blockIdx.x / kparts, Gk = gridDim.x / kparts;
+    const int T_ = (a.N + 15) >> 4;
+    const int t0 = (int)((long long)gb * T_ / Gk), t1 = (int)((long long)(gb + 1) * T_ / Gk);
+    const int ntl = t1 - t0;  // host: 1 <= ntl <= NTM
+    const int S = a.K >> 5, Sp = S / kparts, s0 = kp * Sp;
+    const int wa = s0 + wave * Sp / NW, nst = s0 + (wave + 1) * Sp / NW - wa;  // host: 1 <= nst <= SPW
+    const int r = lane & 15, g = lane >> 4;
+    // weights first (they do not depend on X): ring slot u = (t % TPI) * SPW + j holds (tile t, step j)
+    const T* wbase = a.W + ((size_t)t0 * S + wa) * 512;
+    const int tl = ntl - 1, jl = nst - 1;
+    typename F::f fa[U];
+    auto issue = [&](int t, int j) {
+        const int tt = t < tl ? t : tl, jj = j < jl ? j : jl;
+        fa[(t % TPI) * SPW + j] = F::template load_w<true>(wbase + ((size_t)tt * S + jj) * 512, lane);
+    };
+#pragma unroll
+    for (int t = 0; t < TPI; ++t)
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) issue(t, j);
+    typename F::f xa[SPW], xb[SPW];
+    {
+        const int ra = r < a.R ? r : a.R - 1, rb = 16 + r < a.R ? 16 + r : a.R - 1;
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int jj = j < nst ? j : nst - 1;
+            const size_t k = (size_t)(wa + jj) * 32 + 8 * g;
+            xa[j] = F::load(a.X + (size_t)ra * a.ldx + k);
+            xb[j] = F::load(a.X + (size_t)rb * a.ldx + k);
+            if (j >= nst || r >= a.R) xa[j] = F::zero();
+            if (j >= nst || 16 + r >= a.R) xb[j] = F::zero();
+        }
+    }
+    f32x4_t acc[NTM][2];
+#pragma unroll
+    for (int t = 0; t < NTM; ++t) acc[t][0] = acc[t][1] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < NTM; ++t) {
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int u = (t % TPI) * SPW + j;
+            acc[t][0] = F::mma(fa[u], xa[j], acc[t][0]);
+            acc[t][1] = F::mma(fa[u], xb[j], acc[t][1]);
+            if (t + TPI < NTM) issue(t + TPI, j);
+            __builtin_amdgcn_sched_barrier(0);  // each refill right behind its consumer
+        }
+    }
+    // tiles >= ntl re-streamed the last tile (clamped loads): their accumulators are never read
+#pragma unroll
+    for (int t = 0; t < NTM; ++t) {
+        bred[((t * NW + wave) * 2 + 0) * 64 + lane] = acc[t][0];
+        bred[((t * NW + wave) * 2 + 1) * 64 + lane] = acc[t][1];
+    }
+    __syncthreads();
+    // epilogue over the block's tiles: C/D map of a 16x16 accumulator: row = 4*(lane>>4)+i, col = lane&15
+    if constexpr (EPI == EPI_SWIGLU8) {
+        const int no = ntl * 8 * a.R;
+        for (int o = threadIdx.x; o < no; o += blockDim.x) {
+            const int t = o / (8 * a.R), oo = o - t * 8 * a.R;
+            const int col = oo >> 3, row = oo & 7;
+            const int cg = col >> 4, i = row & 3;
+            const int lg = 16 * (row >> 2) + (col & 15), lu = 16 * ((row + 8) >> 2) + (col & 15);
+            float vg = 0.f, vu = 0.f;
+            for (int w = 0; w < NW; ++w) {
+                vg += bred[((t * NW + w) * 2 + cg) * 64 + lg][i];
+                vu += bred[((t * NW + w) * 2 + cg) * 64 + lu][i];
+            }
+            const int tile = t0 + t;
+            if (a.wscale) {
+                vg = rnd<T>(rnd<T>(vg) * ld(a.wscale, tile * 16 + row));
+                vu = rnd<T>(rnd<T>(vu) * ld(a.wscale, tile * 16 + 8 + row));
+            }
+            const int n = tile * 8 + row;
+            if (n < (a.N >> 1)) st(a.Y, (size_t)col * a.ldy + n, rnd<T>(silu_b(rnd<T>(vg))) * rnd<T>(vu));
+        }
+    } else {
+        const int no = ntl * 16 * a.R;
+        for (int o = threadIdx.x; o < no; o += blockDim.x) {
+            const int t = o / (16 * a.R), oo = o - t * 16 * a.R;
+            const int col = oo >> 4, row = oo & 15;
+            const int cg = col >> 4, ln = 16 * (row >> 2) + (col & 15), i = row & 3;
+            float v = 0.f;
+            for (int w = 0; w < NW; ++w) v += bred[((t * NW + w) * 2 + cg) * 64 + ln][i];
+            const int n = (t0 + t) * 16 + row;
+            if (n >= a.N) continue;
+            if constexpr (EPI == EPI_SLAB) {
+                a.Yf[((size_t)kp * a.R + col) * a.ldy + n] = v;
+            } else {
+                if (a.wscale) v = rnd<T>(rnd<T>(v) * ld(a.wscale, n));
+                if (a.bias) v += ld(a.bias, n);
+                if constexpr (EPI == EPI_STORE)
+                    st(a.Y, (size_t)col * a.ldy + n, v);
+                else
+                    a.Yf[(size_t)col * a.ldy + n] = rnd<T>(v);
+            }
+        }
+    }
+}
+
 // x = round(res + round(sum_kp slab[kp] + bias)) (llama.py:841-842 residual, the split-K sum in fp32
 // rounded once like the reference's one linear output), then optionally xn = RMSNorm(x) with two
 // roundings (llama.py:989-1000).  One 512-thread block per row: every thread's slab, residual and
@@ -236,9 +349,54 @@ int bs_num_cus() {
 //   EPI_SLAB: kparts 4 at K = 4096 (8 waves x 4 steps), kparts 8 at K = 9728 (8 waves x 4-5).
 // SPW is the smallest instantiated ring width >= ceil(Sp / NW).  fp32 holds twice the VGPRs per
 // fragment, so it runs TPI 1 (validation mode only).
+// bsacc_kernel geometry: 8 waves per block, one block per CU; K parts (EPI_SLAB only) so that
+// tiles * kparts is a whole number of grid rounds, at most NTM tiles per block
+static BstreamPlan bsacc_plan(int N, int K, int R, int epi, size_t esz) {
+    BstreamPlan p{};
+    const int S = K / 32, tiles = (N + 15) / 16, G = bs_num_cus();
+    if (R < 1 || R > 32 || K % 32 || S < 1 || esz != 2) return p;
+    int kparts = 1;
+    if (epi == EPI_SLAB) {
+        int best = 1;
+        double bw = 1e9;
+        for (int k = 1; k <= 8; k *= 2) {
+            if (S % k || S / k < 8) break;
+            const double per = (double)tiles * k / G, waste = std::ceil(per) / per;
+            if (std::ceil(per) <= 6 && waste < bw - 1e-3) {
+                bw = waste;
+                best = k;
+            }
+        }
+        kparts = best;
+    }
+    const int Sp = S / kparts, NW = std::min(8, Sp);
+    const int ntm = (tiles * kparts + G - 1) / G;
+    const int spw_need = (Sp + NW - 1) / NW;
+    int spw = 0;
+    for (int c : {2, 5, 10})
+        if (c >= spw_need) {
+            spw = c;
+            break;
+        }
+    if (!spw || ntm > 6) return p;
+    p.ok = true;
+    p.acc = 1;
+    p.kparts = kparts;
+    p.nw = NW;
+    p.spw = spw;
+    p.tpi = spw == 2 ? 4 : (spw == 5 ? 2 : 1);
+    p.ntm = ntm <= 2 ? 2 : (ntm <= 3 ? 3 : (ntm <= 5 ? 5 : 6));
+    p.grid = std::min(G, tiles * kparts) / kparts * kparts;
+    return p;
+}
+
 BstreamPlan bstream_plan(int N, int K, int R, int epi, size_t esz) {
     BstreamPlan p{};
     const FmTuning& tu = fm_tuning();
+    if (tu.bstream_acc) {
+        p = bsacc_plan(N, K, R, epi, esz);
+        if (p.ok) return p;
+    }
     const int S = K / 32, tiles = (N + 15) / 16;
     if (R < 1 || R > 32 || K % 32 || S < 1) return p;
     int kparts = 1;
@@ -270,10 +428,49 @@ BstreamPlan bstream_plan(int N, int K, int R, int epi, size_t esz) {
     return p;
 }
 
+template <typename T, int SPW, int TPI, int NTM>
+static void bsacc_go(hipStream_t s, const BstreamArgs<T>& a, int epi, int G, int NW) {
+    const size_t lds = (size_t)NTM * NW * 2 * 64 * sizeof(f32x4_t);
+    static bool big = false;
+    if (lds > 64 * 1024 && !big) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bsacc_kernel<T, SPW, TPI, NTM, EPI_STORE>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bsacc_kernel<T, SPW, TPI, NTM, EPI_SWIGLU8>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bsacc_kernel<T, SPW, TPI, NTM, EPI_F32>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bsacc_kernel<T, SPW, TPI, NTM, EPI_SLAB>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        big = true;
+    }
+    dim3 grid(G), block(NW * 64);
+    switch (epi) {
+        case EPI_STORE: bsacc_kernel<T, SPW, TPI, NTM, EPI_STORE><<<grid, block, lds, s>>>(a); break;
+        case EPI_SWIGLU8: bsacc_kernel<T, SPW, TPI, NTM, EPI_SWIGLU8><<<grid, block, lds, s>>>(a); break;
+        case EPI_F32: bsacc_kernel<T, SPW, TPI, NTM, EPI_F32><<<grid, block, lds, s>>>(a); break;
+        case EPI_SLAB: bsacc_kernel<T, SPW, TPI, NTM, EPI_SLAB><<<grid, block, lds, s>>>(a); break;
+        default: FMCHECK(false, "bsacc: unsupported epilogue");
+    }
+}
+
 template <typename T> bool launch_bstream(hipStream_t s, const BstreamArgs<T>& a0, int epi, const BstreamPlan& p) {
     if (!p.ok) return false;
     BstreamArgs<T> a = a0;
     a.kparts = p.kparts;
+    if (p.acc) {
+        if constexpr (sizeof(T) == 2) {
+            FMCHECK(epi != EPI_SWIGLU8 || a.N % 16 == 0, "bsacc: SwiGLU8 needs whole interleaved tiles");
+#define BSA(SPW, TPI, NTM)                                      \
+    if (p.spw == SPW && p.tpi == TPI && p.ntm == NTM) {         \
+        bsacc_go<T, SPW, TPI, NTM>(s, a, epi, p.grid, p.nw);    \
+        return true;                                            \
+    }
+            BSA(2, 4, 2) BSA(2, 4, 3) BSA(2, 4, 5) BSA(2, 4, 6) BSA(5, 2, 2) BSA(5, 2, 3) BSA(5, 2, 5)
+            BSA(5, 2, 6) BSA(10, 1, 2) BSA(10, 1, 3) BSA(10, 1, 5) BSA(10, 1, 6)
+#undef BSA
+        }
+        return false;
+    }
     FMCHECK(epi == EPI_SLAB || p.kparts == 1, "bstream: split K only into slabs");
     FMCHECK(epi != EPI_SWIGLU8 || a.N % 16 == 0, "bstream: SwiGLU8 needs whole interleaved tiles");
 #define BSG(SPW, TPI)                                    \

@@ -220,6 +220,7 @@ struct FmTuning {
     int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)
     int bstream_kparts = 0;  // bstream EPI_SLAB K parts (0: by K)
     int bstream_nw = 0;      // bstream waves per block (0: 16 whole-K, 8 split-K)
+    int bstream_acc = 0;     // 1: bsacc_kernel (per-tile register accumulators, one reduction at the end, balanced K parts)
     int rmsnorm_block = 0;   // 1: block-per-row RMSNorm (the pre-vectorisation kernel), 0: wave-per-row when shapes allow
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
@@ -250,6 +251,7 @@ template <typename T> struct BstreamArgs {
 struct BstreamPlan {
     bool ok = false;
     int kparts = 1, nw = 0, spw = 0, tpi = 1, grid = 0;
+    int acc = 0, ntm = 0;  // bsacc_kernel: tiles per block at most (register accumulators)
 };
 BstreamPlan bstream_plan(int N, int K, int R, int epi, size_t esz);
 template <typename T> bool launch_bstream(hipStream_t s, const BstreamArgs<T>& a, int epi, const BstreamPlan& p);

@@ -1824,6 +1824,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "bstream_kparts") {
             FMCHECK(value == 0 || value == 1 || value == 2 || value == 4 || value == 8, "bstream_kparts must be 0, 1, 2, 4 or 8");
             t.bstream_kparts = value;
+        } else if (k == "bstream_acc") {
+            t.bstream_acc = value;
         } else if (k == "bstream_nw") {
             FMCHECK(value >= 0 && value <= 16, "bstream_nw must be in [0, 16]");
             t.bstream_nw = value;
