@@ -146,6 +146,8 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
     using F = Frag<T>;
     extern __shared__ __attribute__((aligned(16))) f32x4_t bred[];  // [NTM][NW][2][64]
     constexpr int U = SPW * TPI;
+    const unsigned long long ts0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long ts1 = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
     const int kparts = a.kparts;
     const int kp = blockIdx.x % kparts, gb = blockIdx.x / kparts, Gk = gridDim.x / kparts;
@@ -192,8 +194,10 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
             acc[t][1] = F::mma(fa[u], xb[j], acc[t][1]);
             if (t + TPI < NTM) issue(t + TPI, j);
             __builtin_amdgcn_sched_barrier(0);  // each refill right behind its consumer
+            if (t == 0 && j == 0 && a.dbg) ts1 = __builtin_amdgcn_s_memrealtime();
         }
     }
+    const unsigned long long ts2 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     // tiles >= ntl re-streamed the last tile (clamped loads): their accumulators are never read
 #pragma unroll
     for (int t = 0; t < NTM; ++t) {
@@ -201,6 +205,26 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
         bred[((t * NW + wave) * 2 + 1) * 64 + lane] = acc[t][1];
     }
     __syncthreads();
+    const unsigned long long ts3 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    // developer stamps (scripts/b32_ts.py): {tag = (K << 16 | N >> 4) << 32 | block, start, first
+    // MFMA, streamed, end, barrier passed, tiles}, from wave 0 of the block
+    auto stamp = [&]() {
+        if (a.dbg && threadIdx.x == 0) {
+            const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long slot = atomicAdd(a.dbg, 1ull);
+            if (slot < (1ull << 20)) {
+                unsigned long long* q = a.dbg + 8 + slot * 8;
+                q[0] = ((unsigned long long)(((unsigned)a.K << 16) | ((unsigned)a.N >> 4)) << 32) | blockIdx.x;
+                q[1] = ts0;
+                q[2] = ts1;
+                q[3] = ts2;
+                q[4] = t4;
+                q[5] = ts3;
+                q[6] = (unsigned long long)ntl;
+                q[7] = 0;
+            }
+        }
+    };
     // epilogue over the block's tiles: C/D map of a 16x16 accumulator: row = 4*(lane>>4)+i, col = lane&15
     if constexpr (EPI == EPI_SWIGLU8) {
         const int no = ntl * 8 * a.R;
@@ -244,6 +268,7 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
             }
         }
     }
+    stamp();
 }
 
 // x = round(res + round(sum_kp slab[kp] + bias)) (llama.py:841-842 residual, the split-K sum in fp32

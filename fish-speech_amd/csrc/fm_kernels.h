@@ -220,7 +220,7 @@ struct FmTuning {
     int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)
     int bstream_kparts = 0;  // bstream EPI_SLAB K parts (0: by K)
     int bstream_nw = 0;      // bstream waves per block (0: 16 whole-K, 8 split-K)
-    int bstream_acc = 0;     // 1: bsacc_kernel (per-tile register accumulators, one reduction at the end, balanced K parts)
+    int bstream_acc = 1;     // 1: bsacc_kernel (per-tile register accumulators, one reduction at the end, balanced K parts); 0: bstream_kernel
     int rmsnorm_block = 0;   // 1: block-per-row RMSNorm (the pre-vectorisation kernel), 0: wave-per-row when shapes allow
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
@@ -247,6 +247,7 @@ template <typename T> struct BstreamArgs {
     float* Yf;       // EPI_F32 [R][ldy] | EPI_SLAB partial slabs [kparts][R][ldy]
     int kparts = 1;  // set by the launcher from the plan
     const T* wscale = nullptr;  // weight-only int8 row scales (EPI_SLAB: applied by finalize_norm)
+    unsigned long long* dbg = nullptr;  // developer per-block timestamps (fm_tune "debug_ts")
 };
 struct BstreamPlan {
     bool ok = false;

@@ -337,6 +337,7 @@ template <typename T> struct Run {
         if (!p.ok) return false;
         BstreamArgs<T> a{(const T*)W, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y, ldy, Yf};
         if (const auto* q = m->qinfo(W)) a.wscale = (const T*)q->scale;
+        a.dbg = fm_tuning().dbg;
         const int64_t bytes = (int64_t)N * K * E + (int64_t)R * K * E +
                               (int64_t)R * N * (epi == EPI_SLAB ? 4 * p.kparts : (epi == EPI_F32 ? 4 : E));
         const double flops = 2.0 * R * N * K;
