@@ -135,19 +135,34 @@ __global__ __launch_bounds__(BS_MAXW * 64) void bstream_kernel(BstreamArgs<T> a)
     }
 }
 
+// 8 bf16 of an X row -> round(round(x * rs) * w) (RMSNorm's two roundings, llama.py:989-1000)
+template <typename T>
+__device__ __forceinline__ typename Frag<T>::f bs_norm8(typename Frag<T>::f x, float rs, typename Frag<T>::f w) {
+    static_assert(sizeof(T) == 2, "bsacc runs bf16");
+    typename Frag<T>::f o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float x0 = __uint_as_float(x[i] << 16), x1 = __uint_as_float(x[i] & 0xffff0000u);
+        const float w0 = __uint_as_float(w[i] << 16), w1 = __uint_as_float(w[i] & 0xffff0000u);
+        const float y0 = rnd<T>(rnd<T>(x0 * rs) * w0), y1 = rnd<T>(rnd<T>(x1 * rs) * w1);
+        o[i] = (__float_as_uint(y0) >> 16) | (__float_as_uint(y1) & 0xffff0000u);
+    }
+    return o;
+}
+
 // bsacc_kernel: the same weight stream without a barrier per tile.  Block b takes K part
 // b % kparts and a balanced run of tiles (<= NTM); each wave keeps one pair of 16x16 accumulators
 // PER TILE in registers, streams its fragments through a ring TPI tiles deep, and only after the
 // whole run do the waves meet once: every (tile, wave) partial goes to LDS, then the epilogue of
 // all the block's tiles.  kparts is chosen so that tiles * kparts is a whole number of rounds of
 // the grid (no block streams twice as much as another).
-template <typename T, int SPW, int TPI, int NTM, int EPI>
+template <typename T, int SPW, int TPI, int NTM, int EPI, int PRO>
 __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
     using F = Frag<T>;
     extern __shared__ __attribute__((aligned(16))) f32x4_t bred[];  // [NTM][NW][2][64]
     constexpr int U = SPW * TPI;
     const unsigned long long ts0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    unsigned long long ts1 = 0;
+    unsigned long long ts1 = 0, tsx = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
     const int kparts = a.kparts;
     const int kp = blockIdx.x % kparts, gb = blockIdx.x / kparts, Gk = gridDim.x / kparts;
@@ -157,7 +172,8 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
     const int S = a.K >> 5, Sp = S / kparts, s0 = kp * Sp;
     const int wa = s0 + wave * Sp / NW, nst = s0 + (wave + 1) * Sp / NW - wa;  // host: 1 <= nst <= SPW
     const int r = lane & 15, g = lane >> 4;
-    // weights first (they do not depend on X): ring slot u = (t % TPI) * SPW + j holds (tile t, step j)
+    const int ra = r < a.R ? r : a.R - 1, rb = 16 + r < a.R ? 16 + r : a.R - 1;
+    // weights (they do not depend on X): ring slot u = (t % TPI) * SPW + j holds (tile t, step j)
     const T* wbase = a.W + ((size_t)t0 * S + wa) * 512;
     const int tl = ntl - 1, jl = nst - 1;
     typename F::f fa[U];
@@ -169,18 +185,55 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
     for (int t = 0; t < TPI; ++t)
 #pragma unroll
         for (int j = 0; j < SPW; ++j) issue(t, j);
-    typename F::f xa[SPW], xb[SPW];
-    {
-        const int ra = r < a.R ? r : a.R - 1, rb = 16 + r < a.R ? 16 + r : a.R - 1;
+    // X operands (issued before or after the weight ring: no measurable difference).  PRO_PRENORM also
+    // loads the norm weight and the producer's per-tile sums of squares here, laid out [R][K/16] by
+    // bsacc's EPI_SLABFIN (rows w + NW * i of wave w, tiles lane + 64 * jj; host: R <= 32, NW == 8,
+    // K / 16 <= 192)
+    typename F::f xa[SPW], xb[SPW], wn[PRO == PRO_PRENORM ? SPW : 1];
 #pragma unroll
-        for (int j = 0; j < SPW; ++j) {
-            const int jj = j < nst ? j : nst - 1;
-            const size_t k = (size_t)(wa + jj) * 32 + 8 * g;
-            xa[j] = F::load(a.X + (size_t)ra * a.ldx + k);
-            xb[j] = F::load(a.X + (size_t)rb * a.ldx + k);
-            if (j >= nst || r >= a.R) xa[j] = F::zero();
-            if (j >= nst || 16 + r >= a.R) xb[j] = F::zero();
+    for (int j = 0; j < SPW; ++j) {
+        const int jj = j < nst ? j : nst - 1;
+        const size_t k = (size_t)(wa + jj) * 32 + 8 * g;
+        xa[j] = F::load(a.X + (size_t)ra * a.ldx + k);
+        xb[j] = F::load(a.X + (size_t)rb * a.ldx + k);
+        if constexpr (PRO == PRO_PRENORM) wn[j] = F::load(a.nw + k);
+    }
+    float ssv[PRO == PRO_PRENORM ? 12 : 1];
+    if constexpr (PRO == PRO_PRENORM) {
+        const int nt = a.K >> 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 3; ++jj) {
+                const int row = wave + 8 * i, t = lane + 64 * jj;
+                const bool ok = row < a.R && t < nt;
+                const float v = a.ss_in[(size_t)(row < a.R ? row : 0) * nt + (ok ? t : 0)];  // [R][K/16]: coalesced
+                ssv[i * 3 + jj] = ok ? v : 0.f;
+            }
+    }
+    if constexpr (PRO == PRO_PRENORM) {
+        // 1/rms of each X row (wave w: rows w, w + 8, w + 16, w + 24), then every lane's two rows from LDS
+        __shared__ float rs_s[32];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float v = 1.0f / sqrtf(wave_sum(ssv[i * 3] + ssv[i * 3 + 1] + ssv[i * 3 + 2]) / (float)a.K + a.eps);
+            if (lane == 0 && wave + 8 * i < a.R) rs_s[wave + 8 * i] = v;
         }
+        // LDS-only barrier: __syncthreads() would also drain this wave's weight ring (its fence waits
+        // for every outstanding global load), serialising the stream behind the norm statistic
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (a.dbg) tsx = __builtin_amdgcn_s_memrealtime();
+        const float rsa = rs_s[ra], rsb = rs_s[rb];
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {  // round(round(x * rs) * w), llama.py:989-1000
+            xa[j] = bs_norm8<T>(xa[j], rsa, wn[j]);
+            xb[j] = bs_norm8<T>(xb[j], rsb, wn[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) {
+        if (j >= nst || r >= a.R) xa[j] = F::zero();
+        if (j >= nst || 16 + r >= a.R) xb[j] = F::zero();
     }
     f32x4_t acc[NTM][2];
 #pragma unroll
@@ -221,7 +274,7 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
                 q[4] = t4;
                 q[5] = ts3;
                 q[6] = (unsigned long long)ntl;
-                q[7] = 0;
+                q[7] = tsx;
             }
         }
     };
@@ -258,6 +311,9 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
             if (n >= a.N) continue;
             if constexpr (EPI == EPI_SLAB) {
                 a.Yf[((size_t)kp * a.R + col) * a.ldy + n] = v;
+            } else if constexpr (EPI == EPI_SLABFIN) {  // write-through: read by the tile group's last K part
+                __hip_atomic_store(a.Yf + ((size_t)kp * a.R + col) * a.ldy + n, v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 if (a.wscale) v = rnd<T>(rnd<T>(v) * ld(a.wscale, n));
                 if (a.bias) v += ld(a.bias, n);
@@ -265,6 +321,67 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
                     st(a.Y, (size_t)col * a.ldy + n, v);
                 else
                     a.Yf[(size_t)col * a.ldy + n] = rnd<T>(v);
+            }
+        }
+    }
+    if constexpr (EPI == EPI_SLABFIN) {
+        // hand-off in the write-through form (cdna_hip_programming.md split-K recipe, as the batch-1
+        // GEMV's EPI_SLABFIN): sc1 partial stores drained by every wave, one relaxed agent ticket per
+        // tile group, sc1 loads in the last arriver
+        __shared__ int last_s;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int tk = __hip_atomic_fetch_add(a.tickets + gb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = tk == kparts - 1;
+            if (last) __hip_atomic_store(a.tickets + gb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last_s = last;
+        }
+        __syncthreads();
+        if (last_s) {
+            // x = round(res + round(sum_kp partial + bias)) (llama.py:841-842; one rounding of the
+            // linear output, like finalize_norm_kernel), then each (tile, row of X)'s sum of x^2 over
+            // its 16 columns: o's low 4 bits index the column, so a 16-lane group is one tile row.
+            // Every partial and residual load of the thread goes out before the first is used
+            // (clamped indices, no load under a branch); kparts <= 8, 512 threads (host).
+            constexpr int OPT = (NTM * 16 * 32 + 511) / 512;
+            const int no = ntl * 16 * a.R;
+            float pv[OPT][8], rv[OPT];
+#pragma unroll
+            for (int u = 0; u < OPT; ++u) {
+                const int o0 = threadIdx.x + 512 * u, o = o0 < no ? o0 : no - 1;
+                const int t = o / (16 * a.R), oo = o - t * 16 * a.R;
+                const int col = oo >> 4, n = min((t0 + t) * 16 + (oo & 15), a.N - 1);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int qq = q < kparts ? q : kparts - 1;
+                    pv[u][q] = __hip_atomic_load(a.Yf + ((size_t)qq * a.R + col) * a.ldy + n, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+                }
+                rv[u] = ld(a.res, (size_t)col * a.ldr + n);
+            }
+#pragma unroll
+            for (int u = 0; u < OPT; ++u) {
+                const int o = threadIdx.x + 512 * u;
+                const int t = o / (16 * a.R), oo = o - t * 16 * a.R;
+                const int col = oo >> 4, row = oo & 15;
+                const int n = (t0 + t) * 16 + row;
+                const bool live = o < no && n < a.N;
+                float y = 0.f;
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (q < kparts) y += pv[u][q];
+                float x = 0.f;
+                if (live) {
+                    if (a.bias) y += ld(a.bias, n);
+                    if (a.wscale) y = rnd<T>(rnd<T>(y) * ld(a.wscale, n));
+                    x = rnd<T>(rv[u] + rnd<T>(y));
+                    st(a.res_out, (size_t)col * a.ldro + n, x);
+                }
+                float sq = x * x;
+#pragma unroll
+                for (int m = 1; m < 16; m <<= 1) sq += __shfl_xor(sq, m);
+                if (row == 0 && o < no) a.ss_out[(size_t)col * T_ + t0 + t] = sq;  // [R][N/16] (bsacc layout)
             }
         }
     }
@@ -381,7 +498,7 @@ static BstreamPlan bsacc_plan(int N, int K, int R, int epi, size_t esz) {
     const int S = K / 32, tiles = (N + 15) / 16, G = bs_num_cus();
     if (R < 1 || R > 32 || K % 32 || S < 1 || esz != 2) return p;
     int kparts = 1;
-    if (epi == EPI_SLAB) {
+    if (epi == EPI_SLAB || epi == EPI_SLABFIN) {
         int best = 1;
         double bw = 1e9;
         for (int k = 1; k <= 8; k *= 2) {
@@ -453,27 +570,47 @@ BstreamPlan bstream_plan(int N, int K, int R, int epi, size_t esz) {
     return p;
 }
 
+// > 64 KiB of dynamic LDS needs the kernel attribute, which must not be set inside a stream capture
+// (the first batched frame is captured): bsacc_init sets it for every instantiation up front
+template <typename T, int SPW, int TPI, int NTM, int EPI, int PRO>
+static void bsacc_attr() {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bsacc_kernel<T, SPW, TPI, NTM, EPI, PRO>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+template <typename T, int SPW, int TPI, int NTM>
+static void bsacc_attr_all() {
+    bsacc_attr<T, SPW, TPI, NTM, EPI_STORE, PRO_PLAIN>();
+    bsacc_attr<T, SPW, TPI, NTM, EPI_STORE, PRO_PRENORM>();
+    bsacc_attr<T, SPW, TPI, NTM, EPI_SWIGLU8, PRO_PLAIN>();
+    bsacc_attr<T, SPW, TPI, NTM, EPI_SWIGLU8, PRO_PRENORM>();
+    bsacc_attr<T, SPW, TPI, NTM, EPI_F32, PRO_PLAIN>();
+    bsacc_attr<T, SPW, TPI, NTM, EPI_SLAB, PRO_PLAIN>();
+    bsacc_attr<T, SPW, TPI, NTM, EPI_SLABFIN, PRO_PLAIN>();
+}
+template <typename T, int SPW, int TPI, int NTM, int EPI, int PRO>
+static void bsacc_launch(hipStream_t s, const BstreamArgs<T>& a, int G, int NW) {
+    const size_t lds = (size_t)NTM * NW * 2 * 64 * sizeof(f32x4_t);
+    bsacc_kernel<T, SPW, TPI, NTM, EPI, PRO><<<dim3(G), dim3(NW * 64), lds, s>>>(a);
+}
 template <typename T, int SPW, int TPI, int NTM>
 static void bsacc_go(hipStream_t s, const BstreamArgs<T>& a, int epi, int G, int NW) {
-    const size_t lds = (size_t)NTM * NW * 2 * 64 * sizeof(f32x4_t);
-    static bool big = false;
-    if (lds > 64 * 1024 && !big) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bsacc_kernel<T, SPW, TPI, NTM, EPI_STORE>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bsacc_kernel<T, SPW, TPI, NTM, EPI_SWIGLU8>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bsacc_kernel<T, SPW, TPI, NTM, EPI_F32>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bsacc_kernel<T, SPW, TPI, NTM, EPI_SLAB>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        big = true;
-    }
-    dim3 grid(G), block(NW * 64);
+    const bool pre = a.pro == PRO_PRENORM;
+    FMCHECK(!pre || (a.ss_in && a.nw && a.R <= 32 && NW == 8 && a.K / 16 <= 192 && (epi == EPI_STORE || epi == EPI_SWIGLU8)),
+            "bsacc: PRO_PRENORM needs ss_in / nw, R <= 32, 8 waves, K <= 3072 and a STORE or SWIGLU8 epilogue");
+    FMCHECK(epi != EPI_SLABFIN || (a.res && a.res_out && a.ss_out && a.tickets && a.Yf && NW == 8 && a.kparts <= 8),
+            "bsacc: EPI_SLABFIN needs res / res_out / ss_out / tickets / partials, 8 waves, <= 8 K parts");
     switch (epi) {
-        case EPI_STORE: bsacc_kernel<T, SPW, TPI, NTM, EPI_STORE><<<grid, block, lds, s>>>(a); break;
-        case EPI_SWIGLU8: bsacc_kernel<T, SPW, TPI, NTM, EPI_SWIGLU8><<<grid, block, lds, s>>>(a); break;
-        case EPI_F32: bsacc_kernel<T, SPW, TPI, NTM, EPI_F32><<<grid, block, lds, s>>>(a); break;
-        case EPI_SLAB: bsacc_kernel<T, SPW, TPI, NTM, EPI_SLAB><<<grid, block, lds, s>>>(a); break;
+        case EPI_STORE:
+            if (pre) bsacc_launch<T, SPW, TPI, NTM, EPI_STORE, PRO_PRENORM>(s, a, G, NW);
+            else bsacc_launch<T, SPW, TPI, NTM, EPI_STORE, PRO_PLAIN>(s, a, G, NW);
+            break;
+        case EPI_SWIGLU8:
+            if (pre) bsacc_launch<T, SPW, TPI, NTM, EPI_SWIGLU8, PRO_PRENORM>(s, a, G, NW);
+            else bsacc_launch<T, SPW, TPI, NTM, EPI_SWIGLU8, PRO_PLAIN>(s, a, G, NW);
+            break;
+        case EPI_F32: bsacc_launch<T, SPW, TPI, NTM, EPI_F32, PRO_PLAIN>(s, a, G, NW); break;
+        case EPI_SLAB: bsacc_launch<T, SPW, TPI, NTM, EPI_SLAB, PRO_PLAIN>(s, a, G, NW); break;
+        case EPI_SLABFIN: bsacc_launch<T, SPW, TPI, NTM, EPI_SLABFIN, PRO_PLAIN>(s, a, G, NW); break;
         default: FMCHECK(false, "bsacc: unsupported epilogue");
     }
 }
@@ -506,6 +643,17 @@ template <typename T> bool launch_bstream(hipStream_t s, const BstreamArgs<T>& a
     BSG(2, 2) BSG(4, 2) BSG(5, 2) BSG(2, 1) BSG(4, 1) BSG(5, 1) BSG(8, 1)
 #undef BSG
     return false;
+}
+
+void bsacc_init() {
+    static bool done = false;
+    if (done) return;
+    done = true;
+#define BSI(SPW, TPI, NTM) bsacc_attr_all<bf16_t, SPW, TPI, NTM>();
+    BSI(2, 4, 2) BSI(2, 4, 3) BSI(2, 4, 5) BSI(2, 4, 6) BSI(5, 2, 2) BSI(5, 2, 3) BSI(5, 2, 5) BSI(5, 2, 6)
+    BSI(10, 1, 2) BSI(10, 1, 3) BSI(10, 1, 5) BSI(10, 1, 6)
+#undef BSI
+    (void)hipGetLastError();  // an attribute the runtime declines must not linger as the sticky error
 }
 
 template <typename T> void launch_finalize_norm(hipStream_t s, const FinalizeArgs<T>& a) {

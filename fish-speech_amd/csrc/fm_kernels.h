@@ -220,6 +220,7 @@ struct FmTuning {
     int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)
     int bstream_kparts = 0;  // bstream EPI_SLAB K parts (0: by K)
     int bstream_nw = 0;      // bstream waves per block (0: 16 whole-K, 8 split-K)
+    int bstream_chain = 0;   // 1: bsacc SLABFIN / PRENORM chain instead of finalize_norm launches (measured 6.31 -> 6.75 ms per B=32 frame)
     int bstream_acc = 1;     // 1: bsacc_kernel (per-tile register accumulators, one reduction at the end, balanced K parts); 0: bstream_kernel
     int rmsnorm_block = 0;   // 1: block-per-row RMSNorm (the pre-vectorisation kernel), 0: wave-per-row when shapes allow
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
@@ -248,6 +249,21 @@ template <typename T> struct BstreamArgs {
     int kparts = 1;  // set by the launcher from the plan
     const T* wscale = nullptr;  // weight-only int8 row scales (EPI_SLAB: applied by finalize_norm)
     unsigned long long* dbg = nullptr;  // developer per-block timestamps (fm_tune "debug_ts")
+    // bsacc_kernel only -- PRO_PRENORM: X' = RMSNorm(X) from the producer's per-tile sums of squares
+    // ss_in [R][K/16] and the norm weight nw (llama.py:989-1000); EPI_SLABFIN: the last-arriving K
+    // part of each tile group finalises x = round(res + round(sum of partials)) into res_out and
+    // its per-tile sums of squares ss_out [R][N/16] (tickets: zero between launches).  (The batch-1
+    // GEMV's tile sums are [tiles][R]; the two chains never exchange them.)
+    int pro = 0;
+    const float* ss_in = nullptr;
+    const T* nw = nullptr;
+    float eps = 0.f;
+    const T* res = nullptr;
+    int ldr = 0;
+    T* res_out = nullptr;
+    int ldro = 0;
+    float* ss_out = nullptr;
+    int* tickets = nullptr;
 };
 struct BstreamPlan {
     bool ok = false;
@@ -255,6 +271,7 @@ struct BstreamPlan {
     int acc = 0, ntm = 0;  // bsacc_kernel: tiles per block at most (register accumulators)
 };
 BstreamPlan bstream_plan(int N, int K, int R, int epi, size_t esz);
+void bsacc_init();  // kernel attributes (> 64 KiB LDS) of every bsacc_kernel, outside any capture
 template <typename T> bool launch_bstream(hipStream_t s, const BstreamArgs<T>& a, int epi, const BstreamPlan& p);
 // x_out = round(res + round(sum of kparts slabs + bias)); if nw: xn_out = RMSNorm(x_out) * nw
 template <typename T> struct FinalizeArgs {

@@ -331,13 +331,34 @@ template <typename T> struct Run {
         return fm_tuning().bstream && bs_frame && R > GEMV_MAX_ROWS && R <= 32 && m->bsA;
     }
     // one bstream linear; returns false (nothing launched) when the shape is not eligible
+    // bsacc_kernel's fused prologue / epilogue operands (the batched SLABFIN / PRENORM chain)
+    struct BsExtra {
+        int pro = PRO_PLAIN;
+        const float* ss_in = nullptr;
+        const void* nw = nullptr;
+        const void* res = nullptr;
+        void* res_out = nullptr;
+        float* ss_out = nullptr;
+    };
     bool bs_linear(const void* W, const void* bias, const void* X, int ldx, int R, int N, int K, void* Y, int ldy,
-                   float* Yf, int epi, int* kparts_out = nullptr) {
+                   float* Yf, int epi, int* kparts_out = nullptr, const BsExtra* ex = nullptr) {
         const BstreamPlan p = bstream_plan(N, K, R, epi, E);
-        if (!p.ok) return false;
+        if (!p.ok || ((epi == EPI_SLABFIN || (ex && ex->pro == PRO_PRENORM)) && !p.acc)) return false;
         BstreamArgs<T> a{(const T*)W, (const T*)bias, (const T*)X, ldx, R, N, K, (T*)Y, ldy, Yf};
         if (const auto* q = m->qinfo(W)) a.wscale = (const T*)q->scale;
         a.dbg = fm_tuning().dbg;
+        if (ex) {
+            a.pro = ex->pro;
+            a.ss_in = ex->ss_in;
+            a.nw = (const T*)ex->nw;
+            a.eps = m->c.norm_eps;
+            a.res = (const T*)ex->res;
+            a.ldr = N;
+            a.res_out = (T*)ex->res_out;
+            a.ldro = N;
+            a.ss_out = ex->ss_out;
+            a.tickets = m->tickets;
+        }
         const int64_t bytes = (int64_t)N * K * E + (int64_t)R * K * E +
                               (int64_t)R * N * (epi == EPI_SLAB ? 4 * p.kparts : (epi == EPI_F32 ? 4 : E));
         const double flops = 2.0 * R * N * K;
@@ -351,6 +372,19 @@ template <typename T> struct Run {
     const void* wscale(const void* W) const {
         const auto* q = m->qinfo(W);
         return q ? q->scale : nullptr;
+    }
+    // The batched bf16 chain on bsacc_kernel (fm_tune bstream_chain): Wo and W2 finalise the residual
+    // rows and their tile sums of squares (EPI_SLABFIN), QKV and W13 normalise in their prologue
+    // (PRO_PRENORM) -- no finalize_norm launches.  Measured slower (B=32 frame 6.31 -> 6.75 ms): the
+    // prologue's X rows and tile sums arrive ~7 us into the launch (scripts/b32_ts.py "xready"),
+    // 3-4 us later than a plain prologue's, and the last K part's finalise adds 3-5 us to Wo / W2.
+    // x_ss: the stack's x rows are final and m->ssX holds their tile sums.
+    bool x_ss = false;
+    bool bs_chain(const StackDims& d, int R) const {
+        if (!fm_tuning().bstream_chain || E != 2 || R > 32) return false;
+        auto ok = [&](int N, int K, int epi) { return bstream_plan(N, K, R, epi, E).acc; };
+        return ok(d.nqkv(), d.dim, EPI_STORE) && ok(d.dim, d.nq(), EPI_SLABFIN) && ok(2 * d.inter, d.dim, EPI_SWIGLU8) &&
+               ok(d.dim, d.inter, EPI_SLABFIN);
     }
     void finalize_norm(const float* slab, int kparts, const void* bias, const void* res, void* out, const void* nw,
                        void* xn, int d, int R, const void* sc) {
@@ -382,7 +416,16 @@ template <typename T> struct Run {
                const float* rope, void* xb, void* hb, void* xnb) {
         const float eps = m->c.norm_eps;
         const bool bs = bs_use(R, is_fast);
-        if (bs) {
+        const bool chain = bs && bs_chain(d, R);
+        if (chain && x_ss) {  // QKV normalises x itself (attention_norm from the tile sums)
+            BsExtra e;
+            e.pro = PRO_PRENORM;
+            e.ss_in = m->ssX;
+            e.nw = L.an;
+            FMCHECK(bs_linear(L.wqkv, L.bqkv, xb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, EPI_STORE,
+                              nullptr, &e),
+                    "bsacc: no PRENORM QKV plan");
+        } else if (bs) {
             bs_norm_in(d, L, R, xb, xnb);
             if (!bs_linear(L.wqkv, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, EPI_STORE))
                 linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
@@ -445,6 +488,30 @@ template <typename T> struct Run {
             }
         }
         int kp = 0;
+        if (chain) {
+            BsExtra eo;  // h = x + wo(att), finalised with its tile sums by the last K part
+            eo.res = xb;
+            eo.res_out = hb;
+            eo.ss_out = m->ssH;
+            FMCHECK(bs_linear(L.wo, L.bo, m->att, d.nq(), R, d.dim, d.nq(), nullptr, d.dim, m->bsA, EPI_SLABFIN, &kp, &eo),
+                    "bsacc: no SLABFIN wo plan");
+            BsExtra e13;  // ffn_norm(h) in W1||W3's prologue
+            e13.pro = PRO_PRENORM;
+            e13.ss_in = m->ssH;
+            e13.nw = L.fn;
+            FMCHECK(bs_linear(L.w13, nullptr, hb, d.dim, R, 2 * d.inter, d.dim, m->act, d.inter, nullptr, EPI_SWIGLU8,
+                              nullptr, &e13),
+                    "bsacc: no PRENORM w13 plan");
+            BsExtra e2;  // x = h + w2(act), finalised with its tile sums
+            e2.res = hb;
+            e2.res_out = xb;
+            e2.ss_out = m->ssX;
+            FMCHECK(bs_linear(L.w2, nullptr, m->act, d.inter, R, d.dim, d.inter, nullptr, d.dim, m->bsB, EPI_SLABFIN, &kp,
+                              &e2),
+                    "bsacc: no SLABFIN w2 plan");
+            x_ss = true;
+            return;
+        }
         if (bs && bs_linear(L.wo, nullptr, m->att, d.nq(), R, d.dim, d.nq(), nullptr, d.dim, m->bsA, EPI_SLAB, &kp)) {
             finalize_norm(m->bsA, kp, L.bo, xb, hb, L.fn, xnb, d.dim, R, wscale(L.wo));  // h = x + wo(att); xn = ffn_norm(h)
         } else {
@@ -760,6 +827,7 @@ template <typename T> struct Run {
     }
 
     void slow_layers(int R, const int* rslot, const int* rpos) {
+        x_ss = false;
         for (int l = 0; l < m->sd.n_layer; ++l)
             block(m->sd, m->slow[l], R, rslot, rpos, -1, false, m->kc, m->vc, m->slot_stride,
                   (size_t)l * m->layer_stride, m->S, m->rope, m->x, m->h, m->xn);
@@ -785,6 +853,7 @@ template <typename T> struct Run {
 
     void fast_pass(int n, int cpos, bool with_head) {
         const fm_model_config& c = m->c;
+        x_ss = false;
         for (int l = 0; l < m->fdm.n_layer; ++l)
             block(m->fdm, m->fast[l], n, m->frame_slot, nullptr, cpos, true, m->fkc, m->fvc,
                   m->fslot_stride, (size_t)l * m->flayer_stride, m->C, m->frope, m->fx, m->fh, m->fxn);
@@ -1075,6 +1144,7 @@ static void* pack_w13(fm_llm* m, const std::string& p, int inter, int dim) {
 static void finalize(fm_llm* m) {
     if (m->finalized) return;
     const fm_model_config& c = m->c;
+    bsacc_init();
     for (auto& kv : m->w) FMCHECK(kv.second.set || kv.second.optional, "tensor not set: " + kv.first);
     if (m->quant) quantize_linears(m);
     for (auto& kv : m->w) {
@@ -1196,8 +1266,8 @@ static void finalize(fm_llm* m) {
     const int Rpart = std::max(m->max_slots, ATTN_PIECE);  // decode rows, or one prompt attention piece
     m->part = (float*)m->dalloc((size_t)Rpart * d.nh * std::max(m->maxsplit, FM_CEIL(m->S, 16)) * (d.hd + 2) * 4, false);
     m->attn_cnt = (int*)m->dalloc((size_t)R * d.nkv * sizeof(int));  // tickets: zeroed
-    m->ssX = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
-    m->ssH = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, GEMV_MAX_ROWS) * 4);
+    m->ssX = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, 32) * 4);  // batched chain: up to 32 rows
+    m->ssH = (float*)m->dalloc((size_t)(dmax / 16) * std::min(n, 32) * 4);
     {
         // arrival counters: one per 16-row tile of the largest decode GEMV (the slow head / W13)
         const int maxn = std::max({m->Nhead, 2 * c.intermediate_size, 2 * c.fast_intermediate_size, qkvmax, dmax, m->cb});  // W1||W3 is one 2*I-row linear on the batched path
@@ -1827,6 +1897,8 @@ int fm_tune(const char* key, int value) {
             t.bstream_kparts = value;
         } else if (k == "bstream_acc") {
             t.bstream_acc = value;
+        } else if (k == "bstream_chain") {
+            t.bstream_chain = value;
         } else if (k == "bstream_nw") {
             FMCHECK(value >= 0 && value <= 16, "bstream_nw must be in [0, 16]");
             t.bstream_nw = value;

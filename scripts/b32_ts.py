@@ -54,7 +54,7 @@ print(f"{'K':>6s} {'N':>6s} {'launch':>6s} {'blocks':>6s} {'span':>7s} {'disp':>
       f"{'barr':>6s} {'epi':>6s}  per ntl: blocks, end-from-launch (us)")
 for tag, Ls in sorted(by.items()):
     K, N = tag >> 16, (tag & 0xFFFF) * 16
-    sp, di, fi, stv, ba, ep = [], [], [], [], [], []
+    sp, di, fi, stv, ba, ep, xr = [], [], [], [], [], [], []
     byn = defaultdict(list)
     for a in Ls:
         t0 = a[:, 1].min()
@@ -64,6 +64,7 @@ for tag, Ls in sorted(by.items()):
         stv.append(np.mean(a[:, 3] - a[:, 2]))
         ba.append(np.mean(a[:, 5] - a[:, 3]))
         ep.append(np.mean(a[:, 4] - a[:, 5]))
+        xr.append(np.mean(a[:, 7] - a[:, 1]) if a[:, 7].min() > 0 else 0.0)
         for n in np.unique(a[:, 6]):
             sel = a[:, 6] == n
             byn[int(n)].append((int(sel.sum()), np.mean(a[sel, 4] - t0), np.max(a[sel, 4] - t0)))
@@ -71,4 +72,4 @@ for tag, Ls in sorted(by.items()):
     extra = "  ".join(f"ntl{n}: {np.mean([x[0] for x in v]):.0f} blk end {np.mean([x[1] for x in v]) / 100:.2f}/"
                       f"{np.mean([x[2] for x in v]) / 100:.2f}" for n, v in sorted(byn.items()))
     print(f"{K:6d} {N:6d} {len(Ls):6d} {len(Ls[0]):6d} {f(sp):7.2f} {f(di):6.2f} {f(fi):6.2f} {f(stv):6.2f} "
-          f"{f(ba):6.2f} {f(ep):6.2f}  {extra}")
+          f"{f(ba):6.2f} {f(ep):6.2f}  xready {f(xr):5.2f}  {extra}")

@@ -59,14 +59,31 @@ def test_long_context_bf16_vs_reference(golden):
     _teacher_case("llm_long_bf16.npz", golden)
 
 
-@pytest.mark.parametrize("prefill", ["batch", "single"])
-def test_config3_ragged_32_slots_bf16_vs_reference(prefill, golden):
+@pytest.fixture
+def knob():
+    from fishmi import native
+
+    set_ = {}
+
+    def put(key, value, default):
+        set_[key] = default
+        native.tune(key, value)
+
+    yield put
+    for k, d in set_.items():
+        native.tune(k, d)
+
+
+@pytest.mark.parametrize("prefill,chain", [("batch", 0), ("single", 0), ("batch", 1)])
+def test_config3_ragged_32_slots_bf16_vs_reference(prefill, chain, golden, knob):
     """32 distinct prompts (16..256 tokens) in permuted slots: first frame from prefill_batch (the
-    serving tick's path) or per-slot prefill, then batched decode frames (bstream linears,
+    serving tick's path) or per-slot prefill, then batched decode frames (bsacc_kernel linears,
     finalize_norm, attn_fd at 32 different positions), every slot teacher-forced with its own
-    reference columns.  Pooled over slots, the error is within BF16_RATIO x the reference's."""
+    reference columns.  Pooled over slots, the error is within BF16_RATIO x the reference's.
+    chain = 1: the fm_tune bstream_chain variant (bsacc SLABFIN / PRENORM, no finalize_norm)."""
     from fishmi.llm import DualARModel
 
+    knob("bstream_chain", chain, 0)
     g = golden("llm_ragged_bf16.npz")
     cfg = _cfg(g)
     B = int(g["lens"].size)
