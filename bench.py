@@ -42,8 +42,10 @@ def parse():
     ap.add_argument("--prompt-len", type=int, default=64)
     ap.add_argument("--first-chunk", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=4, help="oracle decode frames sampled")
-    ap.add_argument("--cpu-codec-frames", type=int, default=4, help="oracle codec frames sampled")
+    ap.add_argument("--cpu-frames", type=int, default=0,
+                    help="oracle decode frames timed (0: the whole utterance, --frames)")
+    ap.add_argument("--cpu-codec-frames", type=int, default=0,
+                    help="oracle codec frames timed (0: the whole utterance)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--batch", type=int, default=32,
                     help="throughput leg (BASELINE config 3): concurrent streams per GPU (0: skip)")
@@ -331,32 +333,62 @@ def int8_leg(cfg, codec, args, local):
 
 def cpu_baseline(cfg, ccfg, prompt, frames, n_frames, n_codec, seed):
     """The C oracle (oracle/, a restatement of the reference's CPU path) at full S2-Pro shapes on
-    the host cores: prompt pass + n_frames decode frames and a codec decode of n_codec frames,
-    extrapolated to the bench utterance (prefill + frames decode frames + codec of frames)."""
+    the host cores: the prompt pass + n_frames decode frames and a codec decode of n_codec frames.
+    n_frames = n_codec = frames (the default): the whole config-2 utterance, timed as it runs; a
+    smaller sample is extrapolated.  Also BASELINE config 1 (the reference's CPU plumbing case): a
+    16-token prompt + chat template, 32 greedy frames, on the tiny fixture model (tests/golden/llm_a)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
+    n_frames = n_frames or frames
+    n_codec = n_codec or frames
     llm = O.OracleLLM(cfg, True)
     llm.synth(seed, 5)
-    out = llm.generate(prompt, 1 + n_frames, temperature=0.8, top_p=0.8, top_k=30, seed=seed)
+    out = llm.generate(prompt, n_frames, temperature=0.8, top_p=0.8, top_k=30, seed=seed, mask_im_end=True)
     t_pre, t_fr = O.OracleLLM.last_generate_timing()
     n_fr = max(out.shape[1] - 1, 1)
     del llm
     codec = O.OracleCodec(ccfg)
     codec.synth(seed)
-    codes = np.ascontiguousarray(out[1:, :1].repeat(n_codec, axis=1))
+    codes = np.ascontiguousarray(out[1:, :n_codec]) if out.shape[1] >= n_codec else \
+        np.ascontiguousarray(out[1:, :1].repeat(n_codec, axis=1))
     t0 = time.perf_counter()
     codec.decode(codes)
     t_codec = time.perf_counter() - t0
     del codec
     per_frame, per_codec = t_fr / n_fr, t_codec / n_codec
+    whole = n_fr == frames - 1 and n_codec == frames
     est = t_pre + (frames - 1) * per_frame + frames * per_codec
+    # config 1: tiny fixture model, 16 text tokens inside the chat template, 32 greedy frames
+    from fishmi.checkpoint import load_llm_weights
+    from fishmi.config import DualARConfig
+
+    gold = os.path.join(ROOT, "tests", "golden")
+    c1 = DualARConfig.from_pretrained(os.path.join(gold, "llm_a"))
+    c1.im_end_id = 4
+    p1 = np.zeros((c1.num_codebooks + 1, 16 + 8), np.int32)
+    rng = np.random.default_rng(1)
+    p1[0] = rng.integers(16, c1.semantic_begin_id, p1.shape[1])
+    p1[0, :3], p1[0, -5:] = (1, 2, 3), (4, 1, 2, 3, 5)  # template specials around the 16 text ids
+    o1 = O.OracleLLM(c1, False)
+    o1.load(load_llm_weights(os.path.join(gold, "llm_a")))
+    t1 = time.perf_counter()
+    y1 = o1.generate(p1, 32, top_k=1)
+    t1 = time.perf_counter() - t1
+    del o1
+    what = (f"the whole config-2 utterance: {prompt.shape[1]}-token prompt pass {t_pre:.2f}s + {n_fr} decode frames "
+            f"{t_fr:.2f}s ({per_frame:.3f}s/frame) + codec decode of {n_codec} frames {t_codec:.2f}s = {est:.1f}s"
+            if whole else
+            f"{prompt.shape[1]}-token prompt pass {t_pre:.2f}s, {n_fr} decode frames {per_frame:.3f}s/frame, codec "
+            f"{n_codec} frames {per_codec:.3f}s/frame; extrapolated to prefill + {frames} frames + codec of "
+            f"{frames} frames = {est:.1f}s")
     return {"value": round(frames / FRAME_RATE / est, 5), "unit": "audio-sec/wall-sec",
             "cores": O.threads(), "kind": "port",
-            "sample": (f"C oracle at full S2-Pro shapes, bf16-rounded arithmetic: {prompt.shape[1]}-token "
-                       f"prompt pass {t_pre:.2f}s, {n_fr} decode frames {per_frame:.3f}s/frame, codec "
-                       f"{n_codec} frames {per_codec:.3f}s/frame; extrapolated to prefill + {frames} "
-                       f"frames + codec of {frames} frames = {est:.1f}s")}
+            "sample": f"C oracle at full S2-Pro shapes, bf16-rounded arithmetic, {what}",
+            "config1": {"workload": "BASELINE config 1: tiny fixture model (tests/golden/llm_a), 16 text ids in the "
+                                    "chat template, greedy, 32 frames, C oracle on CPU",
+                        "frames": int(y1.shape[1]), "ms": round(t1 * 1e3, 2),
+                        "frames_per_s": round(y1.shape[1] / t1, 1)}}
 
 
 def spawn_ranks(n):

@@ -189,6 +189,7 @@ typedef struct {
     float temperature, top_p; /* applied as bf16 tensors, like inference.py:305-306 */
     int top_k;
     uint64_t seed;
+    int mask_im_end;          /* fixed-length runs (benchmarks): <|im_end|> also at -inf */
 } orc_sampling;
 
 typedef struct {
@@ -634,7 +635,8 @@ static int one_frame(orc_llm* m, const orc_sampling* sp, uint64_t step, const in
     const int V = c->vocab_size, C = c->num_codebooks, cb = c->codebook_size;
     float* lg = m->lg;
     for (int i = 0; i < V; ++i) {
-        int allowed = (i >= c->semantic_begin_id && i <= c->semantic_end_id) || i == c->im_end_id;
+        int allowed = (i >= c->semantic_begin_id && i <= c->semantic_end_id) ||
+                      (i == c->im_end_id && !sp->mask_im_end);
         if (!allowed) lg[i] = -INFINITY;
     }
     int tok = orc_sample(lg, V, sp->temperature, sp->top_p, sp->top_k, m->bf16, sp->seed, step, 0);

@@ -26,7 +26,7 @@ _lib = None
 
 class SamplingC(ctypes.Structure):
     _fields_ = [("temperature", ctypes.c_float), ("top_p", ctypes.c_float),
-                ("top_k", ctypes.c_int), ("seed", ctypes.c_uint64)]
+                ("top_k", ctypes.c_int), ("seed", ctypes.c_uint64), ("mask_im_end", ctypes.c_int)]
 
 
 def build() -> str:
@@ -128,12 +128,12 @@ class OracleLLM:
         return out if logits else None
 
     def generate(self, prompt: np.ndarray, max_new: int, temperature=0.7, top_p=0.9, top_k=1,
-                 seed=0):
+                 seed=0, mask_im_end=False):
         p = np.ascontiguousarray(prompt, dtype=np.int32)
         C1, T = p.shape
         mx = max_new if (max_new and T + max_new <= self.cfg.max_seq_len) else self.cfg.max_seq_len - T
         out = np.zeros((C1, mx), np.int32)
-        sp = SamplingC(temperature, top_p, top_k, seed)
+        sp = SamplingC(temperature, top_p, top_k, seed, int(bool(mask_im_end)))
         n = _check(lib().orc_llm_generate(self.h, _i32p(p), T, max_new, ctypes.byref(sp), _i32p(out)))
         return out[:, :n]
 
