@@ -20,7 +20,7 @@ stops it -- but gives every request a KV slot of its own and advances all of the
 In the fp32 validation mode a batched frame computes every slot's row exactly as a batch-1 frame
 does, so each request's codes equal its serial generate_long codes (tests/test_batching.py on CPU
 with a scripted model, tests/test_gpu_engine.py on the GPU).  In bf16 the batched linears sum in a
-different order (bstream_kernel), within the bf16 parity bound of tests/test_gpu_00_timed_configs.py.
+different order (bsacc_kernel), within the bf16 parity bound of tests/test_gpu_00_timed_configs.py.
 """
 from __future__ import annotations
 
@@ -65,6 +65,7 @@ class BatchedWorker:
         self.free = list(range(self.max_slots))[::-1]
         self.stopping = False
         self.stats = {"ticks": 0, "frames": 0, "slot_frames": 0, "requests": 0}
+        self.on_done = None  # optional callback(item): the request has sent its last response
 
     # ---- responses ---------------------------------------------------------------------------
     @staticmethod
@@ -77,8 +78,11 @@ class BatchedWorker:
     def _fail(self, slot: int, e: Exception, item: Optional[GenerateRequest] = None):
         st = self.active.pop(slot, None)
         log.error("request failed: %s", traceback.format_exc())
-        self._put(st.item if st is not None else item, e)
+        item = st.item if st is not None else item
+        self._put(item, e)
         self.free.append(slot)
+        if self.on_done is not None:
+            self.on_done(item)
 
     # ---- per-slot state machine -----------------------------------------------------------------
     def _advance(self, slot: int) -> bool:
@@ -90,6 +94,8 @@ class BatchedWorker:
                 self.active.pop(slot)
                 self.free.append(slot)
                 self.stats["requests"] += 1
+                if self.on_done is not None:
+                    self.on_done(st.item)
                 return False
             if plan == "next":
                 self._put(st.item, GenerateResponse(action="next"))
@@ -146,9 +152,11 @@ class BatchedWorker:
             p = self.active[s].plan
             self._take(self.active[s], self.m.prefill(s, p.enc[:, p.L:], p.sp, pos0=p.L))
 
-    def tick(self) -> bool:
-        """One scheduling step; False once stopped and idle."""
-        block = not self.active and not self.pending and not self.stopping
+    def tick(self, block: Optional[bool] = None) -> bool:
+        """One scheduling step; False once stopped and idle.  block (default: when idle) waits for
+        the next request on the input queue."""
+        if block is None:
+            block = not self.active and not self.pending and not self.stopping
         while True:
             try:
                 item = self.input.get(block=block)

@@ -1,0 +1,302 @@
+"""Multi-GPU serving behind the reference's worker seam (BASELINE config 4).
+
+One process per GPU (torchrun), every rank a fishmi.batching.BatchedWorker on its own KV slots.
+Rank 0 keeps the reference's queue contract (inference.py:748-799): GenerateRequest(request,
+response_queue) in, WrappedGenerateResponse out, `None` stops -- so the TTS engine and the HTTP
+server above it are unchanged.  The ranks meet at synchronous ticks:
+
+  1. all_gather of (free slots, busy, outbox bytes, rank 0's queued requests, rank 0's stop flag);
+  2. the responses each rank produced since the last tick are gathered to rank 0 and put on their
+     requests' response queues (rank 0's own go straight there);
+  3. rank 0 hands its queued requests out round-robin over the ranks with free slots
+     (fishmi.scheduler.assign, a pure function of the gathered counts) and scatters them;
+  4. every rank runs one BatchedWorker tick (prefills, then up to tick_frames batched frames).
+
+The loop ends when rank 0 has seen `None` and no rank has queued, active or unsent work.  While
+idle, rank 0 waits at most `idle_wait` seconds for a request before the next tick, so the other
+ranks never sit in a collective past its timeout.
+
+Wire format: msgpack (numpy arrays as {shape, dtype, bytes}), over uint8 tensors on the default
+process group (RCCL with device tensors on the GPU box, gloo with host tensors in the CPU tests).
+Requests carry their prompt tokens; responses carry codes, so the vocoder runs on rank 0 as the
+reference's single-process server does.  There is no collective on the decode path.
+"""
+from __future__ import annotations
+
+import builtins
+import collections
+import logging
+import queue
+import threading
+from typing import Deque, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from .batching import BatchedWorker
+from .engine import GenerateRequest, GenerateResponse, WrappedGenerateResponse
+from .scheduler import _device, _dist, assign
+
+log = logging.getLogger("fishmi.dist_serving")
+
+
+# ---- wire format ----------------------------------------------------------------------------------
+def _enc(o):
+    try:
+        import torch
+
+        if isinstance(o, torch.Tensor):
+            o = o.detach().cpu().numpy()
+        elif isinstance(o, torch.device):
+            return str(o)
+    except ImportError:  # pragma: no cover
+        pass
+    if isinstance(o, np.ndarray):
+        a = np.ascontiguousarray(o)
+        return {"__nd__": True, "s": list(a.shape), "d": a.dtype.str, "b": a.tobytes()}
+    if isinstance(o, np.generic):
+        return o.item()
+    raise TypeError(f"cannot send {type(o).__name__} to another rank")
+
+
+def _dec(d):
+    if d.get("__nd__"):
+        return np.frombuffer(d["b"], dtype=np.dtype(d["d"])).reshape(d["s"]).copy()
+    return d
+
+
+def pack(obj) -> bytes:
+    import msgpack
+
+    return msgpack.packb(obj, default=_enc, use_bin_type=True)
+
+
+def unpack(b: bytes):
+    import msgpack
+
+    return msgpack.unpackb(b, object_hook=_dec, raw=False, strict_map_key=False)
+
+
+def _exc_to_wire(e: BaseException) -> dict:
+    return {"type": type(e).__name__, "msg": str(e)}
+
+
+def _exc_from_wire(d: dict) -> Exception:
+    t = getattr(builtins, d["type"], None)
+    if isinstance(t, type) and issubclass(t, Exception):
+        return t(d["msg"])
+    return RuntimeError(f"{d['type']}: {d['msg']}")
+
+
+def response_to_wire(w: Optional[WrappedGenerateResponse]) -> dict:
+    """None marks "the request is done" (no more responses follow)."""
+    if w is None:
+        return {"done": True}
+    if w.status == "error":
+        return {"status": "error", "exc": _exc_to_wire(w.response)}
+    r = w.response
+    return {"status": "success", "action": r.action, "codes": r.codes, "text": r.text, "stream": r.stream}
+
+
+def response_from_wire(d: dict) -> Optional[WrappedGenerateResponse]:
+    if d.get("done"):
+        return None
+    if d["status"] == "error":
+        return WrappedGenerateResponse(status="error", response=_exc_from_wire(d["exc"]))
+    return WrappedGenerateResponse(status="success", response=GenerateResponse(
+        action=d["action"], codes=d["codes"], text=d["text"], stream=d["stream"]))
+
+
+class _Outbox:
+    """A remote request's response_queue on the rank decoding it: responses wait for the next tick."""
+
+    def __init__(self, rid: int, sink: list):
+        self.rid, self.sink = rid, sink
+
+    def put(self, w):
+        self.sink.append((self.rid, w))
+
+
+# ---- the worker ---------------------------------------------------------------------------------
+class DistributedWorker:
+    STAT = 5  # free, busy, outbox bytes, queued (rank 0), stopping (rank 0)
+
+    def __init__(self, model, max_slots: Optional[int] = None, tick_frames: int = 8, idle_wait: float = 0.02):
+        dist = _dist()
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.dev = _device()
+        self.w = BatchedWorker(model, max_slots, tick_frames)
+        self.w.on_done = self._done
+        self.idle_wait = idle_wait
+        self.input: "queue.Queue" = queue.Queue()          # rank 0: the seam's queue
+        self.queued: Deque[Tuple[int, GenerateRequest]] = collections.deque()
+        self.routes: Dict[int, GenerateRequest] = {}         # rank 0: rid -> the caller's request
+        self.outbox: List[Tuple[int, Optional[WrappedGenerateResponse]]] = []
+        self._blob = b""  # packed outbox, sent at this tick's gather
+        self.next_id = 0
+        self.stopping = False
+        self.stats = {"ticks": 0, "served": 0, "sent_to": [0] * self.world}
+
+    def _done(self, item: GenerateRequest):
+        q = item.response_queue
+        if isinstance(q, _Outbox):
+            q.put(None)
+        else:
+            self.routes.pop(getattr(item, "_rid", None), None)
+        self.stats["served"] += 1
+
+    # ---- collectives ----------------------------------------------------------------------------
+    def _tensor(self, b: bytes, n: int):
+        import torch
+
+        t = torch.zeros(max(n, 1), dtype=torch.uint8)
+        if b:
+            t[: len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        return t.to(self.dev)
+
+    def _gather_outboxes(self, sizes: List[int]):
+        import torch
+
+        dist = _dist()
+        blob, self._blob = self._blob, b""
+        n = max(max(sizes), 1)
+        t = self._tensor(blob, n)
+        outs = [torch.empty_like(t) for _ in range(self.world)] if self.rank == 0 else None
+        dist.gather(t, outs, dst=0)
+        if self.rank != 0:
+            return
+        for r in range(1, self.world):
+            if sizes[r]:
+                for rid, d in unpack(outs[r][: sizes[r]].cpu().numpy().tobytes()):
+                    self._route(rid, response_from_wire(d))
+
+    def _route(self, rid: int, w: Optional[WrappedGenerateResponse]):
+        item = self.routes.get(rid)
+        if item is None:
+            log.error("response for unknown request %d", rid)
+            return
+        if w is None:
+            del self.routes[rid]
+        else:
+            item.response_queue.put(w)
+
+    def _scatter(self, take: List[int]) -> List[GenerateRequest]:
+        import torch
+
+        dist = _dist()
+        lens = torch.zeros(self.world, dtype=torch.int64, device=self.dev)
+        blobs = []
+        mine: List[GenerateRequest] = []
+        if self.rank == 0:
+            for r in range(self.world):
+                items = [self.queued.popleft() for _ in range(take[r])]
+                self.stats["sent_to"][r] += len(items)
+                if r == 0:
+                    mine = [it for _, it in items]
+                    blobs.append(b"")
+                else:
+                    blobs.append(pack([[rid, it.request] for rid, it in items]))
+                lens[r] = len(blobs[-1])
+        dist.broadcast(lens, src=0)
+        ln = lens.cpu().tolist()
+        n = max(max(ln), 1)
+        t = self._tensor(b"", n)
+        chunks = [self._tensor(b, n) for b in blobs] if self.rank == 0 else None
+        dist.scatter(t, chunks, src=0)
+        if self.rank == 0:
+            return mine
+        out = []
+        for rid, req in unpack(t[: ln[self.rank]].cpu().numpy().tobytes()):
+            out.append(GenerateRequest(request=req, response_queue=_Outbox(int(rid), self.outbox)))
+        return out
+
+    # ---- one tick -------------------------------------------------------------------------------
+    def _intake(self):
+        block = not self.routes and not self.queued and not self.stopping
+        first = True
+        while True:
+            try:
+                item = self.input.get(timeout=self.idle_wait) if (block and first) else self.input.get_nowait()
+            except queue.Empty:
+                return
+            first = False
+            if item is None:
+                self.stopping = True
+            elif not self.stopping:
+                rid = self.next_id
+                self.next_id += 1
+                item._rid = rid
+                self.routes[rid] = item
+                self.queued.append((rid, item))
+
+    def tick(self) -> bool:
+        """One synchronous tick on every rank; False (on every rank alike) once stopped and idle."""
+        import torch
+
+        dist = _dist()
+        self.stats["ticks"] += 1
+        if self.rank == 0:
+            self._intake()
+        wk = self.w
+        free = wk.max_slots - len(wk.active) - len(wk.pending)
+        busy = len(wk.active) + len(wk.pending)
+        if self.rank != 0 and self.outbox:  # this tick ships everything produced so far
+            self._blob = pack([[rid, response_to_wire(w)] for rid, w in self.outbox])
+            self.outbox.clear()  # _Outbox proxies hold this list: clear it in place
+        vec = torch.tensor([free, busy, len(self._blob), len(self.queued), int(self.stopping)], dtype=torch.int64,
+                           device=self.dev)
+        allv = [torch.zeros_like(vec) for _ in range(self.world)]
+        dist.all_gather(allv, vec)
+        st = np.stack([a.cpu().numpy() for a in allv])
+        if self.rank == 0:  # rank 0's own responses need no collective
+            for rid, w in self.outbox:
+                self._route(rid, w)
+            self.outbox.clear()
+        if st[1:, 2].any():
+            self._gather_outboxes(st[:, 2].tolist())
+        if st[0, 4] and not st[:, 1].any() and not st[1:, 2].any() and st[0, 3] == 0:
+            return False
+        take = assign(st[:, 0].tolist(), int(st[0, 3]))
+        if sum(take):
+            for it in self._scatter(take):
+                wk.pending.append(it)
+        if wk.active or wk.pending:
+            wk.tick(block=False)
+        return True
+
+    def run(self):
+        while self.tick():
+            pass
+        log.info("rank %d: %s", self.rank, self.stats)
+
+
+def launch_distributed_queue(checkpoint_path, device, precision, max_slots: int = 32, tick_frames: int = 8,
+                             model=None, idle_wait: float = 0.02):
+    """launch_thread_safe_queue across the process group: every rank loads the model on its own GPU
+    and runs a DistributedWorker in a daemon thread.  Returns (input queue, thread); only rank 0's
+    queue is served (requests put on another rank's queue are never read).  Put `None` on rank 0's
+    queue to stop every rank; join the thread to wait for it."""
+    from .engine import load_model
+
+    ready = threading.Event()
+    failure: List[BaseException] = []
+    holder: dict = {}
+
+    def worker():
+        try:
+            m = model if model is not None else load_model(checkpoint_path, device, precision, max_slots)
+            w = DistributedWorker(m, max_slots, tick_frames, idle_wait)
+        except BaseException as e:
+            failure.append(e)
+            ready.set()
+            return
+        holder["w"] = w
+        ready.set()
+        w.run()
+
+    th = threading.Thread(target=worker, daemon=True)
+    th.start()
+    ready.wait()
+    if failure:
+        raise failure[0]
+    holder["w"].thread = th
+    return holder["w"].input, th

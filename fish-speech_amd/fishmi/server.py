@@ -19,11 +19,19 @@ Optional bearer auth (--api-key): 401 "Invalid token" otherwise (tools/api_serve
 
 --slots N serves up to N requests at once on one GPU (fishmi.batching.BatchedWorker: batched decode
 frames, each request on its own KV slot); handlers run the blocking engine work in the thread pool, so
-concurrent HTTP requests reach the worker together.  One server process per GPU.
+concurrent HTTP requests reach the worker together.
+
+Several GPUs (BASELINE config 4): launch one process per GPU,
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m fishmi.server --slots 32 ...
+
+Rank 0 serves HTTP and vocodes; every rank decodes requests on its own KV slots
+(fishmi.dist_serving.DistributedWorker: requests scattered and codes gathered at ticks).
 """
 import argparse
 import io
 import logging
+import os
 from typing import Optional
 
 import numpy as np
@@ -175,13 +183,16 @@ def create_app(engine: "TTS.TTSInferenceEngine", max_text_length: int = 0, api_k
 
 
 def build_engine(llama_checkpoint_path: str, decoder_checkpoint_path: str, device=0, precision="bf16",
-                 compile: bool = False, max_frames: int = 2048, slots: int = 1, reuse_prefix: bool = False):
+                 compile: bool = False, max_frames: int = 2048, slots: int = 1, reuse_prefix: bool = False,
+                 llama_queue=None):
     """ModelManager (tools/server/model_manager.py): the LLM worker + the codec with its encoder.
-    slots > 1: concurrent requests decode together on their own KV slots (fishmi.batching)."""
+    slots > 1: concurrent requests decode together on their own KV slots (fishmi.batching).
+    llama_queue: an already-launched worker queue (the multi-GPU worker's, rank 0)."""
     from .codec import FishMICodec
     from .engine import launch_thread_safe_queue
 
-    q = launch_thread_safe_queue(llama_checkpoint_path, device, precision, compile, max_slots=slots)
+    q = llama_queue if llama_queue is not None else \
+        launch_thread_safe_queue(llama_checkpoint_path, device, precision, compile, max_slots=slots)
     codec = FishMICodec.from_checkpoint(decoder_checkpoint_path, device, precision, max_frames, encoder=True)
     return TTS.TTSInferenceEngine(q, codec, precision, compile, reuse_prefix=reuse_prefix)
 
@@ -219,10 +230,40 @@ def main(argv=None):
         log.warning("--half: fp16 is not built; the HIP path runs bf16 (the reference's default precision)")
     if a.compile:
         log.info("--compile: decode frames are always hipGraph-captured; the flag changes nothing")
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return _main_distributed(a)
     engine = build_engine(a.llama_checkpoint_path, a.decoder_checkpoint_path, _device_index(a.device), "bf16",
                           slots=a.slots, reuse_prefix=a.reuse_prefix)
     host, port = a.listen.rsplit(":", 1)
     uvicorn.run(create_app(engine, a.max_text_length, a.api_key), host=host, port=int(port), workers=1)
+
+
+def _main_distributed(a):
+    """One rank per GPU under torchrun: every rank decodes, rank 0 also serves HTTP and vocodes."""
+    import torch
+    import torch.distributed as dist
+    import uvicorn
+
+    from .dist_serving import launch_distributed_queue
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+    dist.init_process_group(backend)
+    try:
+        q, th = launch_distributed_queue(a.llama_checkpoint_path, local, "bf16", max_slots=max(a.slots, 1))
+        if dist.get_rank() == 0:
+            engine = build_engine(a.llama_checkpoint_path, a.decoder_checkpoint_path, local, "bf16",
+                                  reuse_prefix=a.reuse_prefix, llama_queue=q)
+            host, port = a.listen.rsplit(":", 1)
+            try:
+                uvicorn.run(create_app(engine, a.max_text_length, a.api_key), host=host, port=int(port), workers=1)
+            finally:
+                q.put(None)  # stops every rank's worker
+        th.join()
+    finally:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,142 @@
+"""Multi-GPU serving through the worker seam (fishmi.dist_serving, BASELINE config 4) on world_size-2
+gloo with the scripted model of tests/test_batching.py: requests put on rank 0's queue are decoded
+on both ranks' KV slots, and every request gets exactly the responses the serial worker
+(generate_long, inference.py:748-799) gives it alone, errors included, in order."""
+import os
+import queue
+import socket
+import time
+import traceback
+
+import numpy as np
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _serial(reqs):
+    from fishmi import engine
+    from test_batching import ScriptedModel
+
+    out = []
+    for r in reqs:
+        try:
+            out.append([engine.WrappedGenerateResponse("success", o)
+                        for o in engine.generate_long(model=ScriptedModel(1), **r)])
+        except Exception as e:
+            out.append([engine.WrappedGenerateResponse("error", e)])
+    return out
+
+
+def _check(got, ref, i):
+    from test_batching import _summary
+
+    if ref[-1].status == "error":
+        assert [g.status for g in got] == ["error"], i
+        assert type(got[0].response) is type(ref[0].response), i
+        assert str(got[0].response) == str(ref[0].response), i
+        return
+    a, b = _summary(got), _summary(ref)
+    assert [x[0] for x in a] == [x[0] for x in b], i
+    for (_, ca), (_, cb) in zip(a, b):
+        if ca is not None:
+            np.testing.assert_array_equal(ca, cb, err_msg=f"request {i}")
+
+
+def _collect(q, n_final):
+    """Responses until the request's last one ("next" of its last sample, or an error)."""
+    got, finals = [], 0
+    while finals < n_final:
+        w = q.get(timeout=60)
+        got.append(w)
+        if w.status == "error":
+            break
+        if w.response.action == "next":
+            finals += 1
+    return got
+
+
+def _worker(rank, world, port, out_q, slots, tick):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fishmi import engine
+        from fishmi.dist_serving import launch_distributed_queue
+        from test_batching import ScriptedModel, _requests
+
+        model = ScriptedModel(slots)
+        q_in, th = launch_distributed_queue(None, 0, "bf16", max_slots=slots, tick_frames=tick, model=model)
+        if rank == 0:
+            reqs = _requests()
+            reqs.append(dict(text="bad", max_new_tokens=6, seed=2, temperature=5.0))
+            reqs.append(dict(text="<|speaker:0|>long " * 4, max_new_tokens=30, seed=9, prompt_tokens=[
+                np.arange(40, dtype=np.int64).reshape(10, 4) % 128], prompt_text=["ref"]))
+            ref = _serial(reqs)
+            time.sleep(0.2)  # a few idle ticks first
+            qs = [queue.Queue() for _ in reqs]
+            for r, q in zip(reqs, qs):
+                q_in.put(engine.GenerateRequest(request=r, response_queue=q))
+            for i, (q, rf) in enumerate(zip(qs, ref)):
+                n_final = 0 if rf[-1].status == "error" else sum(w.response.action == "next" for w in rf)
+                _check(_collect(q, max(n_final, 1)), rf, i)
+            q_in.put(None)
+        th.join(timeout=120)
+        assert not th.is_alive()
+        decoded = [c for c in model.calls if c[0] in ("prefill", "prefill_batch")]
+        out_q.put((rank, "ok", len(decoded)))
+    except Exception:
+        out_q.put((rank, traceback.format_exc(), 0))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(slots, tick):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, slots, tick)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, msg, n = q.get(timeout=180)
+        res[rank] = (msg, n)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        assert res[r][0] == "ok", res[r][0]
+        assert res[r][1] > 0, f"rank {r} decoded nothing"
+
+
+def test_distributed_worker_world2_equals_serial():
+    _run(slots=2, tick=3)
+
+
+def test_distributed_worker_world2_one_slot_per_rank():
+    _run(slots=1, tick=8)
+
+
+def test_wire_roundtrip():
+    from fishmi import engine
+    from fishmi.dist_serving import pack, response_from_wire, response_to_wire, unpack
+
+    req = dict(text="hi", seed=3, prompt_tokens=[np.arange(12, dtype=np.int32).reshape(3, 4)], prompt_text=["a"],
+               top_p=np.float32(0.5), device="cuda:0", stream_frames=0)
+    back = unpack(pack(req))
+    np.testing.assert_array_equal(back["prompt_tokens"][0], req["prompt_tokens"][0])
+    assert back["prompt_tokens"][0].dtype == np.int32 and back["top_p"] == 0.5 and back["text"] == "hi"
+    w = engine.WrappedGenerateResponse("success", engine.GenerateResponse("sample", np.ones((2, 3), np.int32), "t", 1))
+    w2 = response_from_wire(unpack(pack(response_to_wire(w))))
+    assert w2.response.action == "sample" and w2.response.stream == 1 and w2.response.text == "t"
+    np.testing.assert_array_equal(w2.response.codes, w.response.codes)
+    e = response_from_wire(unpack(pack(response_to_wire(engine.WrappedGenerateResponse("error", ValueError("x"))))))
+    assert e.status == "error" and isinstance(e.response, ValueError) and str(e.response) == "x"
+    assert response_from_wire(unpack(pack(response_to_wire(None)))) is None

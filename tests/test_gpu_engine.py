@@ -169,3 +169,47 @@ def test_batched_worker_matches_serial(golden, tmp_path, slots):
             np.testing.assert_array_equal(x, y, err_msg=f"request {i}")
     np.testing.assert_array_equal(serial[0][0].codes, g["codes_0"])
     q_in.put(None)
+
+
+def test_distributed_worker_rccl_world1_matches_serial(golden, tmp_path):
+    """The multi-GPU serving worker (fishmi.dist_serving) over RCCL with device tensors, one rank:
+    requests and responses cross the tick collectives (scatter / gather of msgpack bytes on the
+    GPU) and each request still gets its serial generate_long codes (fp32).  The world-2 routing is
+    tests/test_dist_serving.py (gloo)."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from fishmi import engine
+    from fishmi.dist_serving import launch_distributed_queue
+    from fishmi.llm import DualARModel
+
+    g = golden("engine.npz")
+    m = DualARModel.from_pretrained(_ckpt(tmp_path), device=0, precision="fp32", max_length=2560, max_slots=4)
+    reqs = [_request(g)] + [_request(g, text=t, top_k=30, seed=70 + i, max_new_tokens=10 + 4 * i)
+                            for i, t in enumerate(["one two three", "<|speaker:0|>a b. <|speaker:1|>c d e."])]
+    serial = [list(engine.generate_long(model=m, **r)) for r in reqs]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        q_in, th = launch_distributed_queue(None, 0, "fp32", max_slots=4, tick_frames=4, model=m)
+        qs = [queue.Queue() for _ in reqs]
+        for r, q in zip(reqs, qs):
+            q_in.put(engine.GenerateRequest(request=r, response_queue=q))
+        for i, (q, ref) in enumerate(zip(qs, serial)):
+            got = _drain(q)
+            assert all(w.status == "success" for w in got), got[-1].response
+            a = [np.asarray(w.response.codes) for w in got if w.response.action == "sample"]
+            b = [np.asarray(r.codes) for r in ref if r.action == "sample"]
+            assert len(a) == len(b) >= 1, i
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y, err_msg=f"request {i}")
+        q_in.put(None)
+        th.join(timeout=60)
+        assert not th.is_alive()
+    finally:
+        dist.destroy_process_group()
