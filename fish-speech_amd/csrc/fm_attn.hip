@@ -577,18 +577,24 @@ template <typename T> __device__ __forceinline__ void cvt16(const u32x4_t v, flo
     }
 }
 
-constexpr int FD_TILE = 64, FD_GM = 4;
-template <typename T, int HD>
-__global__ __launch_bounds__(256) void attn_fd_kernel(AttnDecArgs<T> a) {
+constexpr int FD_GM = 4;
+// NW waves per block (4, 8 or 16): 16 NW positions per pass.  The batch-1 launches use wide blocks
+// and long splits, so below fd_min16 cached positions one block per kv head needs no cross-block
+// combine.
+template <typename T, int HD, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_fd_kernel(AttnDecArgs<T> a) {
     static_assert(HD % 32 == 0 && HD <= 128, "head_dim a multiple of 32 up to 128");
+    constexpr int NT = NW * 64, FD_TILE = 16 * NW;
     constexpr int QD = HD / 4;                      // K dims per lane
     constexpr int KL = QD * (int)sizeof(T) / 16;    // 16-B loads per K slice
     constexpr int VL = 8 * (int)sizeof(T) / 16;     // 16-B loads per V slice
     constexpr int half = HD / 2;
     __shared__ __attribute__((aligned(16))) float q_s[FD_GM][HD];
     __shared__ __attribute__((aligned(16))) float kv_new[2][HD];
-    __shared__ __attribute__((aligned(16))) float wml[4][FD_GM][2];
-    __shared__ __attribute__((aligned(16))) float ored[4][4][FD_GM][HD];  // [wave][V position group][head][dim] PV partials
+    __shared__ __attribute__((aligned(16))) float wml[NW][FD_GM][2];
+    // PV partials [wave][V position group][head][dim]; 16 waves fold the 4 groups by shuffles first
+    constexpr int OG = NW > 4 ? 1 : 4;
+    __shared__ __attribute__((aligned(16))) float ored[NW][OG][FD_GM][HD];
     __shared__ int flag;
     unsigned long long tz[7] = {0, 0, 0, 0, 0, 0, 0};
     DBG_TS(tz, 0)
@@ -601,10 +607,11 @@ __global__ __launch_bounds__(256) void attn_fd_kernel(AttnDecArgs<T> a) {
     const int slot = a.row_slot[r];
     const int pos = a.row_pos[r];
     const T* raw = a.qkv + (size_t)r * a.ldqkv;
-    float x0[2], x1[2];
+    constexpr int NI = (2 + FD_GM + NW - 1) / NW;  // q heads + new k + new v over the waves
+    float x0[NI], x1[NI];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int it = wave + 4 * i;
+    for (int i = 0; i < NI; ++i) {
+        const int it = wave + NW * i;
         const int row = it < g ? kvh * g + it : (it == g ? a.nh + kvh : a.nh + a.nkv + kvh);
         const bool ok = it < nitem && lane < half;
         const T* src = raw + (size_t)(it < nitem ? row : 0) * HD + 2 * (lane < half ? lane : 0);
@@ -642,8 +649,8 @@ __global__ __launch_bounds__(256) void attn_fd_kernel(AttnDecArgs<T> a) {
     // ---- q heads (+ new k / v in the owner): qk-norm (fp32 incl. weight, one rounding), RoPE
     const float* tab = a.rope + (size_t)pos * HD;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int it = wave + 4 * i;
+    for (int i = 0; i < NI; ++i) {
+        const int it = wave + NW * i;
         if (it >= nitem || (it >= g && !owner)) continue;
         const bool isq = it < g, isk = it == g;
         if (a.qk_norm && (isq || isk)) {
@@ -755,8 +762,15 @@ __global__ __launch_bounds__(256) void attn_fd_kernel(AttnDecArgs<T> a) {
     for (int h = 0; h < FD_GM; ++h) {
         if (h >= g) break;
         const float l = row_sum16(l_run[h]);
-        if (8 * l16 < HD) {
-            f32x4_t* dst = reinterpret_cast<f32x4_t*>(&ored[wave][qq][h][8 * l16]);
+        if constexpr (OG == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                o[h][e] += __shfl_xor(o[h][e], 16);
+                o[h][e] += __shfl_xor(o[h][e], 32);
+            }
+        }
+        if (8 * l16 < HD && (OG == 4 || qq == 0)) {
+            f32x4_t* dst = reinterpret_cast<f32x4_t*>(&ored[wave][OG == 4 ? qq : 0][h][8 * l16]);
             dst[0] = (f32x4_t){o[h][0], o[h][1], o[h][2], o[h][3]};
             dst[1] = (f32x4_t){o[h][4], o[h][5], o[h][6], o[h][7]};
         }
@@ -768,15 +782,20 @@ __global__ __launch_bounds__(256) void attn_fd_kernel(AttnDecArgs<T> a) {
     __syncthreads();
     DBG_TS(tz, 3)
     const bool single = nsp == 1;
-    for (int idx = threadIdx.x; idx < g * HD; idx += 256) {
+    for (int idx = threadIdx.x; idx < g * HD; idx += NT) {
         const int h = idx / HD, e = idx - h * HD;
-        const float M = fmaxf(fmaxf(wml[0][h][0], wml[1][h][0]), fmaxf(wml[2][h][0], wml[3][h][0]));
+        float M = wml[0][h][0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) M = fmaxf(M, wml[w][h][0]);
         float L = 0.f, O = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < NW; ++w) {
             const float sc = expf(wml[w][h][0] - M);  // a wave with no position: exp(-inf) = 0
             L += sc * wml[w][h][1];
-            O += sc * ((ored[w][0][h][e] + ored[w][1][h][e]) + (ored[w][2][h][e] + ored[w][3][h][e]));
+            if constexpr (OG == 4)
+                O += sc * ((ored[w][0][h][e] + ored[w][1][h][e]) + (ored[w][2][h][e] + ored[w][3][h][e]));
+            else
+                O += sc * ored[w][0][h][e];
         }
         if (single) {
             st(a.out + (size_t)r * a.nh * HD + (size_t)(kvh * g + h) * HD, e, O / L);
@@ -807,9 +826,10 @@ __global__ __launch_bounds__(256) void attn_fd_kernel(AttnDecArgs<T> a) {
     }
     __syncthreads();
     if (!flag) return;
+    DBG_TS(tz, 5)
     // lane q of a 16-lane group holds split q; group grp owns PP consecutive (dim pair) items of one
     // head.  Every load is unconditional (split index clamped) and issued before any is used.
-    constexpr int PP = FD_GM * HD / 32;
+    constexpr int PP = FD_GM * HD * 8 / NT;
     const int q = l16, grp = threadIdx.x >> 4;
     const int k0 = grp * PP, h = k0 / half, e0 = 2 * (k0 - h * half);
     if (h >= g) return;  // whole 16-lane groups
@@ -842,6 +862,10 @@ __global__ __launch_bounds__(256) void attn_fd_kernel(AttnDecArgs<T> a) {
             st(out, 2 * j, o0 / L);
             st(out, 2 * j + 1, o1 / L);
         }
+    }
+    if (a.dbg && threadIdx.x == 0) {  // the combiner: {start, .., partials stored, ticket won, end}
+        tz[6] = __builtin_amdgcn_s_memrealtime();
+        dbg_record(a.dbg, 0xFFFB, (unsigned)nsp, tz);
     }
 }
 
@@ -1638,10 +1662,26 @@ template <typename T> void launch_attn_fd(hipStream_t s, const AttnDecArgs<T>& a
     AttnDecArgs<T> a = a0;
     a.maxsplit = std::min(FD_NSP, FM_CEIL(a.S, a.cap));
     const dim3 grid(R, a.nkv, a.maxsplit);
+    if (a.nwb == 16) {
+        switch (a.hd) {
+            case 32: attn_fd_kernel<T, 32, 16><<<grid, 1024, 0, s>>>(a); break;
+            case 64: attn_fd_kernel<T, 64, 16><<<grid, 1024, 0, s>>>(a); break;
+            default: attn_fd_kernel<T, 128, 16><<<grid, 1024, 0, s>>>(a); break;
+        }
+        return;
+    }
+    if (a.nwb == 8) {
+        switch (a.hd) {
+            case 32: attn_fd_kernel<T, 32, 8><<<grid, 512, 0, s>>>(a); break;
+            case 64: attn_fd_kernel<T, 64, 8><<<grid, 512, 0, s>>>(a); break;
+            default: attn_fd_kernel<T, 128, 8><<<grid, 512, 0, s>>>(a); break;
+        }
+        return;
+    }
     switch (a.hd) {
-        case 32: attn_fd_kernel<T, 32><<<grid, 256, 0, s>>>(a); break;
-        case 64: attn_fd_kernel<T, 64><<<grid, 256, 0, s>>>(a); break;
-        default: attn_fd_kernel<T, 128><<<grid, 256, 0, s>>>(a); break;
+        case 32: attn_fd_kernel<T, 32, 4><<<grid, 256, 0, s>>>(a); break;
+        case 64: attn_fd_kernel<T, 64, 4><<<grid, 256, 0, s>>>(a); break;
+        default: attn_fd_kernel<T, 128, 4><<<grid, 256, 0, s>>>(a); break;
     }
 }
 template <typename T> void launch_attn_decode3(hipStream_t s, const AttnDecArgs<T>& a0, int R) {

@@ -162,6 +162,7 @@ template <typename T> struct FastFusedArgs {
     T* out;              // [R][nh*hd]
     unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
     float* qdbg = nullptr;    // per-op test hook (fm_op_qk_rope): q after qk-norm + RoPE [R][nh][hd]
+    int nwb = 4;              // attn_fd: waves per block (4, 8 or 16; 16 nwb positions per pass)
 };
 template <typename T> struct GemvArgs {
     const T* W;
@@ -213,6 +214,9 @@ struct FmTuning {
     int attn_fd = 1;         // 1: slow decode attention on attn_fd_kernel (flash-decode splits) where eligible
     int fd_min = 32;         // attn_fd: minimum positions per split at R <= 8
     int fd_min_batched = 512;  // attn_fd: minimum positions per split at R > 8 (B=32: one split below 512)
+    int fd_nw = 8;           // attn_fd at R <= 8: waves per block (4, 8 or 16) ...
+    int fd_min16 = 512;      // ... and splits of at least this many positions (8 or 16 waves; below it
+                             // one block per kv head, no cross-block combine)
     int prefill_attn = 1;    // 1: prompt-chunk attention on attn_prefill_kernel (bf16, head_dim 128, flash form)
     int prompt_gemm = 1;     // 1: prompt-chunk linears (R > 32) on the codec's LDS-tiled GEMM kernels
     int conv2 = 1;           // 1: codec GEMMs on the LDS-staged conv_gemm2_kernel, 0: conv_gemm_kernel
@@ -313,6 +317,7 @@ template <typename T> struct AttnDecArgs {
     T* out;              // [R][nh*hd]
     unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
     float* qdbg = nullptr;    // per-op test hook (fm_op_qk_rope): q after qk-norm + RoPE [R][nh][hd]
+    int nwb = 4;              // attn_fd: waves per block (4, 8 or 16; 16 nwb positions per pass)
 };
 // decode attention for the small-batch path (see fm_attn.hip): a.cap rows per block, a.maxsplit =
 // ceil(S / cap) blocks per (row, kv head), output straight to a.out (bf16 / T)

@@ -320,6 +320,10 @@ template <typename T> struct Run {
         if (fm_tuning().attn_fd && attn_fd_ok(aa.hd, aa.nh / aa.nkv)) {
             AttnDecArgs<T> b = aa;
             b.cap = std::max(16, R > GEMV_MAX_ROWS ? fm_tuning().fd_min_batched : fm_tuning().fd_min);
+            if (R <= GEMV_MAX_ROWS && fm_tuning().fd_nw > 4) {
+                b.nwb = fm_tuning().fd_nw;
+                b.cap = std::max(16, fm_tuning().fd_min16);
+            }
             launch_attn_fd<T>(s, b, R);
         } else if (fm_tuning().attn3 && R > GEMV_MAX_ROWS && aa.hd % 32 == 0 && aa.hd <= 128 && aa.nh / aa.nkv <= 6)
             launch_attn_decode3<T>(s, aa, R);
@@ -1887,6 +1891,12 @@ int fm_tune(const char* key, int value) {
         } else if (k == "fd_min") {
             FMCHECK(value >= 16 && value % 16 == 0, "fd_min must be a multiple of 16");
             t.fd_min = value;
+        } else if (k == "fd_nw") {
+            FMCHECK(value == 4 || value == 8 || value == 16, "fd_nw must be 4, 8 or 16");
+            t.fd_nw = value;
+        } else if (k == "fd_min16") {
+            FMCHECK(value >= 16 && value % 16 == 0, "fd_min16 must be a multiple of 16");
+            t.fd_min16 = value;
         } else if (k == "fd_min_batched") {
             FMCHECK(value >= 16 && value % 16 == 0, "fd_min_batched must be a multiple of 16");
             t.fd_min_batched = value;

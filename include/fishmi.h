@@ -173,7 +173,7 @@ int fm_llm_read_logits(fm_llm* h, int slot, float* slow_logits, float* fast_logi
 /* process-wide developer knobs selecting kernel variants (every variant stays under the default
    path's parity bar, tests/test_gpu_knobs.py): decode GEMV "gemv_nt" 0|1, "gemv_u" 2|4|8,
    "gemv_wpb" 4|8, "ksb_blocks" n, "ksb_balance" 0|1; attention "attn_fd" 0|1, "attn3" 0|1,
-   "attn_cap" n, "attn_cap_batched" n, "fd_min" n, "fd_min_batched" n, "attn_wo" 0|1,
+   "attn_cap" n, "attn_cap_batched" n, "fd_min" n, "fd_min_batched" n, "fd_nw" 4|8|16, "fd_min16" n, "attn_wo" 0|1,
    "batched_fused_attn" 0|1; batched linears "bstream" 0|1, "bstream_acc" 0|1, "bstream_chain" 0|1, "bstream_kparts" n, "bstream_nw" n,
    "linear_u32" n, "linear_fill" n; prompt "prefill_attn", "prompt_gemm"; codec "conv2",
    "conv_splitk"; "sampler_fast" 0|1, "rmsnorm_block" 0|1, "debug_ts" n.  They apply to launches

@@ -22,3 +22,14 @@ span = (rows[b][2] - rows[a][2]) / 1e3
 print(f"--- one frame: span {span:.1f} us, kernel sum {sum(tot.values()):.1f} us")
 for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
     print(f"  {v:8.1f} us  {k}")
+gaps = defaultdict(float)
+cnt = defaultdict(int)
+prev = rows[a][2]
+for r in rows[a + 1:b + 1]:
+    k = r[0].split("(")[0].replace("void ", "").split("<")[0][:40]
+    gaps[k] += (r[1] - prev) / 1e3
+    cnt[k] += 1
+    prev = r[2]
+print(f"--- gaps before each kernel class (sum {sum(gaps.values()):.1f} us over {sum(cnt.values())} launches)")
+for k, v in sorted(gaps.items(), key=lambda kv: -kv[1]):
+    print(f"  {v:8.1f} us  {cnt[k]:4d} x  {k}")

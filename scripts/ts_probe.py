@@ -48,6 +48,21 @@ for tag, name, labels in ((0xFFFE, "fast_attn2", ("load", "prep", "scores", "pv+
         aux = a[:, 0].astype(np.int64) & 0xFFFFFFFF
         print(f"{name} phases (us):", " ".join(f"{l} {v:.2f}" for l, v in zip(labels, d)),
               "| blocks", len(a), "aux mean", round(float(aux.mean()), 1))
+cmb = rec[(rec[:, 0] >> 32) == 0xFFFB].astype(np.float64)
+fd = rec[(rec[:, 0] >> 32) == 0xFFFC].astype(np.float64)
+if len(cmb) and len(fd):
+    # per launch: first block start .. combiner end, and the combiner's drain+ticket / combine times
+    print(f"attn_fd combiner: stored->ticket {np.mean(cmb[:, 6] - cmb[:, 5]) / 100:.2f} us, "
+          f"combine {np.mean(cmb[:, 7] - cmb[:, 6]) / 100:.2f} us, block start->end {np.mean(cmb[:, 7] - cmb[:, 1]) / 100:.2f} us, "
+          f"splits {np.mean(cmb[:, 0].astype(np.int64) & 0xFFFF):.1f}")
+    st = np.sort(fd[:, 1])
+    ends = np.sort(cmb[:, 7])
+    # launches: cluster block starts with gaps > 20 us
+    cut = np.where(np.diff(st) > 2000)[0]
+    firsts = np.concatenate([[st[0]], st[cut + 1]])
+    n = min(len(firsts), len(ends) // 8)
+    spans = [(ends[8 * i + 7] - firsts[i]) / 100 for i in range(n)]
+    print(f"attn_fd in-kernel span (first block start .. last combiner end): mean {np.mean(spans):.2f} us over {n} launches")
 if os.environ.get("TS_SK"):
     for tag in sorted(set((rec[:, 0] >> 32).tolist())):
         a = rec[(rec[:, 0] >> 32) == tag].astype(np.float64)
