@@ -60,10 +60,75 @@ constexpr int gemv_wpe(int pro, int epi) { return pro == PRO_PRENORM && epi == E
 // Q8 (weight-only int8): the weight stream is a.Wq, one ring slot = one 64-k unit (1 KiB per wave,
 // as a T fragment is), dequantised exactly to two T fragments in registers; each output is
 // round(round(acc) * wscale[row]) (WeightOnlyInt8Linear.forward, quantize.py:228-229).
-template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8>
-__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(gemv_wpe(PRO, EPI))))
-void gemv_kernel(GemvArgs<T> a) {
+// ---- chain hand-off (one launch, stages in sequence; cdna_hip_programming.md §6 Guideline 16,
+// write-through form): every byte a later stage of the launch reads is stored sc1 and drained
+// (s_waitcnt vmcnt(0)) by its storing wave before the block's one arrival on a sharded counter;
+// the consumer polls the counter (sc1 loads, one lane per shard), and EVERY load of handed-off
+// bytes is an sc1 load (buffer_load_dwordx4 / global_load_dword sc1), so no acquire fence.
+struct ChainWait {
+    const unsigned* cnt = nullptr;  // the producing stage's 8 arrival shards (null: stage 0)
+    unsigned target = 0;            // its block count
+    int* err = nullptr;             // set on a timed-out wait (host re-zeroes the counters)
+};
+__device__ __forceinline__ void chain_wait(const ChainWait& cw) {
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        for (unsigned it = 0;; ++it) {
+            unsigned v = lane < 8 ? __hip_atomic_load(cw.cnt + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            if (__shfl(v, 0) >= cw.target) break;
+            if (it > (1u << 16)) {  // bounded (~0.1 s; a stage takes tens of us): the host sees err, resets
+                if (lane == 0) __hip_atomic_store(cw.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+}
+// 8 elements of T at X + off (elements) as an sc1 load through a buffer descriptor of X
+template <typename T> __device__ __forceinline__ C8<T> load_c8_sc1(const T* X, int nbytes, int off) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, nbytes, 0x00020000);
+    C8<T> c;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 2); ++i)
+        c.v[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off * (int)sizeof(T) + 16 * i, 0, 16);
+    return c;
+}
+template <typename T> __device__ __forceinline__ float ld_sc1(const T* p, size_t i) {
+    if constexpr (sizeof(T) == 2) {
+        const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t*>(p + (i & ~(size_t)1)), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        return __uint_as_float((i & 1) ? (w & 0xffff0000u) : (w << 16));
+    } else {
+        return __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+// element i of a run of consecutive lanes holding consecutive even-aligned elements, stored
+// write-through: bf16 as (even, odd) pairs in one 4-byte store by the even lane.  Every lane of
+// the run executes this (the odd lane's value travels by shuffle).
+template <typename T> __device__ __forceinline__ void st_sc1_run(T* p, size_t i, float v) {
+    if constexpr (sizeof(T) == 2) {
+        const float nb = __shfl_down(v, 1);
+        if ((i & 1) == 0)
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(p + i), (uint32_t)f2bf(v) | ((uint32_t)f2bf(nb) << 16),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// The GEMV body for block (bxi, ks) of a grid with nks K slices.  CH (chain stage, R == 1, whole
+// K per block): the weight ring goes out first, then the wait for the producing stage, then the
+// prologue's loads (sc1); outputs a later stage reads are stored sc1 (the caller arrives).
+template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8, bool CH>
+__device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, const int ks, const int nks,
+                                          const ChainWait& cw) {
     static_assert(!(Q8 && (EPI == EPI_SWIGLU || EPI == EPI_SLAB || PRO == PRO_FATT)), "no int8 form");
+    static_assert(!CH || (!Q8 && (PRO == PRO_PLAIN || PRO == PRO_PRENORM) &&
+                          (EPI == EPI_STORE || EPI == EPI_SWIGLU8 || EPI == EPI_SLABFIN)), "no chain form");
     // X items preloaded per thread ahead of the weight ring: PRO_PRENORM's operand is one dim-wide
     // row per stream (2 items per thread at R = 1), and its register budget is what lets the
     // 1216-block W1||W3 grid stay resident (5 waves per SIMD)
@@ -73,9 +138,8 @@ void gemv_kernel(GemvArgs<T> a) {
     constexpr int NTH = WPB * 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int n0 = blockIdx.x * 16;
-    const int ks = blockIdx.y;
-    const int Kb = a.K / gridDim.y;  // host guarantees a multiple of 32 (64 with Q8)
+    const int n0 = bxi * 16;
+    const int Kb = a.K / nks;  // host guarantees a multiple of 32 (64 with Q8)
     const int kbeg = ks * Kb;
     const int R = a.R;
     const int xstride = Kb + 8;  // +16 B per row: conflict-free ds_read_b128 across rows
@@ -89,13 +153,17 @@ void gemv_kernel(GemvArgs<T> a) {
     // EPI_SLABFIN: the residual element this thread will finalise, loaded in the first round trip
     // (unconditional, clamped index: a load under a branch drains vmcnt before the MFMAs)
     float res_pre = 0.f;
-    if constexpr (EPI == EPI_SLABFIN) {
+    auto load_res = [&]() {
         const int tt = min((int)threadIdx.x, 16 * a.R - 1);
-        const int col = tt >> 4, nn = min(blockIdx.x * 16 + (tt & 15), a.N - 1);
+        const int col = tt >> 4, nn = min(bxi * 16 + (tt & 15), a.N - 1);
         int ri = a.residx ? a.residx[(size_t)col * a.xidx_ld + a.xidx_col] : col;
         if (a.residx && a.xidx_rows > 0) ri = ri < 0 ? 0 : (ri >= a.xidx_rows ? a.xidx_rows - 1 : ri);
-        res_pre = ld(a.res + (size_t)ri * a.ldr, nn);
-    }
+        if constexpr (CH)
+            res_pre = ld_sc1(a.res + (size_t)ri * a.ldr, nn);
+        else
+            res_pre = ld(a.res + (size_t)ri * a.ldr, nn);
+    };
+    if constexpr (EPI == EPI_SLABFIN && !CH) load_res();
     unsigned long long tsA = 0, tsB = 0;  // PRO_PRENORM: tile sums staged / X' written
     const int r = lane & 15, g = lane >> 4;
     constexpr int KU = Q8 ? 64 : 32;  // k per ring slot
@@ -107,7 +175,7 @@ void gemv_kernel(GemvArgs<T> a) {
     // the compiler drain vmcnt(0) before every MFMA (no pipelining at all), so tail slots re-load
     // the run's last fragment (a cache hit) instead of being predicated off.
     const int ilast = nmy > 0 ? nmy - 1 : 0;
-    const size_t run0 = ((size_t)blockIdx.x * S + sb0 + (nmy > 0 ? wa : 0)) * (Q8 ? 1024 : 512);
+    const size_t run0 = ((size_t)bxi * S + sb0 + (nmy > 0 ? wa : 0)) * (Q8 ? 1024 : 512);
     const T* wrun = Q8 ? nullptr : a.W + run0;
     const T* wrun2 = (EPI == EPI_SWIGLU) ? a.W2 + run0 : nullptr;
     const unsigned char* qrun = Q8 ? a.Wq + run0 : nullptr;
@@ -132,7 +200,7 @@ void gemv_kernel(GemvArgs<T> a) {
         // weight ring starts after it (its block reductions would otherwise wait on weights)
         __shared__ float red_s[16];
         const int nch = a.K >> 3;
-        const bool writer = (blockIdx.x == 0 && ks == 0);
+        const bool writer = (bxi == 0 && ks == 0);
         for (int rr = 0; rr < R; ++rr) {
             int xi = a.xidx ? a.xidx[(size_t)rr * a.xidx_ld + a.xidx_col] : rr;
             if (a.xidx_rows > 0) xi = xi < 0 ? 0 : (xi >= a.xidx_rows ? a.xidx_rows - 1 : xi);  // defence in depth
@@ -238,18 +306,29 @@ void gemv_kernel(GemvArgs<T> a) {
         const int h0 = kbeg / hd, h1 = (kbeg + Kb) / hd;
         for (int hb = h0 + 8 * wave; hb < h1; hb += 8 * WPB)
             fast_attn_heads8_lds<T>(at, hb, h1, lane, raw_s, kv_s, qn_s, kn_s, tab_s, xs + (size_t)(hb - h0) * hd,
-                                    blockIdx.x == 0, slot);
+                                    bxi == 0, slot);
     } else {
         // PRO_PLAIN / PRO_PRENORM: (row, 8-element chunk) items of the slice, up to PRE_N per
         // thread preloaded ahead of the weight ring (the rest, large R x Kb only, after it)
         const int nch = Kb >> 3, nitem = R * nch;
+        const int xbytes = (R - 1) * a.ldx * (int)sizeof(T) + a.K * (int)sizeof(T);  // CH: X's descriptor range
+        auto ldx8 = [&](int rr, int cc) -> C8<T> {
+            if constexpr (CH) return load_c8_sc1(a.X, xbytes, rr * a.ldx + kbeg + 8 * cc);
+            else return load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc);
+        };
+        if constexpr (CH) {  // chain stage: the weight ring first (no dependency), then the wait
+#pragma unroll
+            for (int u = 0; u < U; ++u) issue(u, u);
+            if (cw.cnt) chain_wait(cw);
+            if constexpr (EPI == EPI_SLABFIN) load_res();
+        }
         C8<T> xc[PRE_N], wc[PRO == PRO_PRENORM ? PRE_N : 1];
 #pragma unroll
         for (int q = 0; q < PRE_N; ++q) {
             const int it = threadIdx.x + NTH * q;
             if (it < nitem) {
                 const int rr = it / nch, cc = it - rr * nch;
-                xc[q] = load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc);
+                xc[q] = ldx8(rr, cc);
                 if constexpr (PRO == PRO_PRENORM) wc[q] = load_c8(a.nw + kbeg + 8 * cc);
             }
         }
@@ -264,11 +343,16 @@ void gemv_kernel(GemvArgs<T> a) {
 #pragma unroll
             for (int q = 0; q < GEMV_SSQ; ++q) {
                 const int e = threadIdx.x + NTH * q;
-                ssv[q] = a.ss_in[e < nss ? e : nss - 1];
+                if constexpr (CH)
+                    ssv[q] = __hip_atomic_load(a.ss_in + (e < nss ? e : nss - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    ssv[q] = a.ss_in[e < nss ? e : nss - 1];
             }
         }
+        if constexpr (!CH) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) issue(u, u);
+            for (int u = 0; u < U; ++u) issue(u, u);
+        }
         if constexpr (PRO == PRO_PRENORM) {
             // stage the tile sums in `red` (free until the cross-wave reduction), then every wave
             // reduces each row's sums itself: per-row 1/rms in the wave's LDS slot (a register
@@ -278,7 +362,8 @@ void gemv_kernel(GemvArgs<T> a) {
                 const int e = threadIdx.x + NTH * q;  // last sum (same value), and no branch lets
                 red[e < nss ? e : nss - 1] = ssv[q];  // the compiler sink a load past the ring
             }
-            for (int e = threadIdx.x + NTH * GEMV_SSQ; e < nss; e += NTH) red[e] = a.ss_in[e];  // R * K large
+            for (int e = threadIdx.x + NTH * GEMV_SSQ; e < nss; e += NTH)  // R * K large
+                red[e] = CH ? __hip_atomic_load(a.ss_in + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.ss_in[e];
             __syncthreads();
             if (a.dbg) tsA = __builtin_amdgcn_s_memrealtime();
             const int nt = a.K >> 4;
@@ -292,7 +377,7 @@ void gemv_kernel(GemvArgs<T> a) {
                 if (lane == 0) rsw[rr] = v;
             }
             __builtin_amdgcn_wave_barrier();
-            const bool writer = blockIdx.x == 0 && ks == 0 && a.xn_out;
+            const bool writer = bxi == 0 && ks == 0 && a.xn_out;
             auto put = [&](int rr, int cc, const C8<T>& xq, const C8<T>& wq) {
                 float xv[8], wv[8];
                 c8_to_f(xq, xv);
@@ -312,7 +397,7 @@ void gemv_kernel(GemvArgs<T> a) {
             }
             for (int it = threadIdx.x + NTH * PRE_N; it < nitem; it += NTH) {
                 const int rr = it / nch, cc = it - rr * nch;
-                put(rr, cc, load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc), load_c8(a.nw + kbeg + 8 * cc));
+                put(rr, cc, ldx8(rr, cc), load_c8(a.nw + kbeg + 8 * cc));
             }
             if (a.dbg) tsB = __builtin_amdgcn_s_memrealtime();
         } else {
@@ -326,8 +411,7 @@ void gemv_kernel(GemvArgs<T> a) {
             }
             for (int it = threadIdx.x + NTH * PRE_N; it < nitem; it += NTH) {  // large R x Kb
                 const int rr = it / nch, cc = it - rr * nch;
-                *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) =
-                    load_c8(a.X + (size_t)rr * a.ldx + kbeg + 8 * cc);
+                *reinterpret_cast<C8<T>*>(xs + (size_t)rr * xstride + 8 * cc) = ldx8(rr, cc);
             }
         }
     }
@@ -378,7 +462,7 @@ void gemv_kernel(GemvArgs<T> a) {
             const unsigned long long slot = atomicAdd(a.dbg, 1ull);
             if (slot < (1ull << 20)) {
                 unsigned long long* q = a.dbg + 8 + slot * 8;
-                q[0] = ((unsigned long long)a.N << 32) | ((unsigned long long)blockIdx.y << 16) | blockIdx.x;
+                q[0] = ((unsigned long long)a.N << 32) | ((unsigned long long)ks << 16) | bxi;
                 q[1] = ts0;
                 q[2] = ts1;
                 q[3] = ts2;
@@ -394,8 +478,8 @@ void gemv_kernel(GemvArgs<T> a) {
     if constexpr (EPI == EPI_SWIGLU8) {  // rows 0-7 gate, 8-15 up of the same 8 outputs
         for (int o = threadIdx.x; o < 8 * R; o += NTH) {
             const int row = o / R, col = o - row * R;
-            const int n = blockIdx.x * 8 + row;
-            if (n >= (a.N >> 1)) continue;
+            const int n = bxi * 8 + row;
+            if (!CH && n >= (a.N >> 1)) continue;  // (CH: N % 16 == 0, host-checked)
             float v0 = 0.f, v1 = 0.f;
 #pragma unroll
             for (int w = 0; w < WPB; ++w) {
@@ -404,7 +488,11 @@ void gemv_kernel(GemvArgs<T> a) {
             }
             v0 = wsc(v0, n0 + row);
             v1 = wsc(v1, n0 + row + 8);
-            st(a.Y, (size_t)col * a.ldy + n, rnd<T>(silu_g(rnd<T>(v0))) * rnd<T>(v1));
+            const float y = rnd<T>(silu_g(rnd<T>(v0))) * rnd<T>(v1);
+            if constexpr (CH)
+                st_sc1_run(a.Y, (size_t)col * a.ldy + n, y);
+            else
+                st(a.Y, (size_t)col * a.ldy + n, y);
         }
         stamp();
         return;
@@ -412,7 +500,7 @@ void gemv_kernel(GemvArgs<T> a) {
     for (int o = threadIdx.x; o < 16 * R; o += NTH) {
         const int row = o / R, col = o - row * R;
         const int n = n0 + row;
-        if (n >= a.N) continue;
+        if (!CH && n >= a.N) continue;  // (CH: N % 16 == 0, host-checked: every lane of a run stores)
         float v0 = 0.f, v1 = 0.f;
 #pragma unroll
         for (int w = 0; w < WPB; ++w) {
@@ -424,7 +512,7 @@ void gemv_kernel(GemvArgs<T> a) {
             a.Yf[((size_t)ks * R + col) * a.ldy + n] = v0;
         } else if constexpr (EPI == EPI_SLABFIN) {
             if (a.bias && ks == 0) v0 += ld(a.bias, n);
-            if (gridDim.y == 1) {  // whole K in this block: finalise from LDS below
+            if (nks == 1) {  // whole K in this block: finalise from LDS below
                 fin[col * 16 + (n - n0)] = v0;
             } else {  // write-through (sc1) partial: visible to the tile's reducer without a fence
                 __hip_atomic_store(a.Yf + ((size_t)ks * R + col) * a.ldy + n, v0, __ATOMIC_RELAXED,
@@ -435,7 +523,10 @@ void gemv_kernel(GemvArgs<T> a) {
             if (a.bias) v0 += ld(a.bias, n);
             const size_t yi = (size_t)col * a.ldy + n;
             if constexpr (EPI == EPI_STORE) {
-                st(a.Y, yi, v0);
+                if constexpr (CH)
+                    st_sc1_run(a.Y, yi, v0);
+                else
+                    st(a.Y, yi, v0);
             } else if constexpr (EPI == EPI_SWIGLU) {
                 const float ga = rnd<T>(v0), ub = rnd<T>(v1);
                 st(a.Y, yi, rnd<T>(silu_g(ga)) * ub);
@@ -450,15 +541,14 @@ void gemv_kernel(GemvArgs<T> a) {
         // the consumer's RMSNorm.  Hand-off in its write-through form (cdna_hip_programming.md §5,
         // split-K recipe): sc1 partial stores drained by every wave, a relaxed agent ticket, sc1
         // loads in the reducer -- no release / acquire fence.  ksb == 1: straight from LDS.
-        const int ksb = gridDim.y;
+        const int ksb = nks;
         if (ksb > 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (ksb > 1) {
             if (threadIdx.x == 0) {
-                const int t = __hip_atomic_fetch_add(a.tickets + blockIdx.x, 1, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
+                const int t = __hip_atomic_fetch_add(a.tickets + bxi, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const int last = t == ksb - 1;
-                if (last) __hip_atomic_store(a.tickets + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (last) __hip_atomic_store(a.tickets + bxi, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 flag[0] = last;
             }
             __syncthreads();
@@ -478,14 +568,69 @@ void gemv_kernel(GemvArgs<T> a) {
                     y += __hip_atomic_load(a.Yf + ((size_t)q * R + col) * a.ldy + n, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
             const float x = rnd<T>(res_pre + rnd<T>(wsc(y, n)));
-            st(a.res_out, (size_t)col * a.ldro + n, x);
+            if constexpr (CH)
+                st_sc1_run(a.res_out, (size_t)col * a.ldro + n, x);
+            else
+                st(a.res_out, (size_t)col * a.ldro + n, x);
             float sq = x * x;
 #pragma unroll
             for (int m = 1; m < 16; m <<= 1) sq += __shfl_xor(sq, m);
-            if ((t & 15) == 0) a.ss_out[(size_t)blockIdx.x * R + col] = sq;
+            if ((t & 15) == 0) {
+                if constexpr (CH)
+                    __hip_atomic_store(a.ss_out + (size_t)bxi * R + col, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    a.ss_out[(size_t)bxi * R + col] = sq;
+            }
         }
     }
     stamp();
+}
+
+template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(gemv_wpe(PRO, EPI))))
+void gemv_kernel(GemvArgs<T> a) {
+    gemv_body<T, PRO, EPI, NT, U, WPB, Q8, false>(a, blockIdx.x, blockIdx.y, gridDim.y, ChainWait{});
+}
+
+// One launch running up to GEMV_CHAIN_MAX dependent batch-1 GEMVs (fm_llm.cpp: a layer's wo, w1||w3,
+// w2 and the next layer's qkv).  Stage s owns blocks [off[s], off[s+1]) (dispatch is in block
+// order, so a waiting block only waits on blocks already resident or done); a stage's blocks
+// issue their weight ring, then wait for every block of stage s - 1 to arrive.  The last block of
+// the last stage to arrive resets every counter of the launch (all waits have passed by then), so
+// the next launch starts from zero (first use: zeroed at allocation).
+template <typename T, bool NT, int U, int WPB>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 2 ? 5 : 2)))
+void gemv_chain_kernel(GemvChainArgs<T> c) {
+    int s = 0;
+    while (s + 1 < c.n && (int)blockIdx.x >= c.off[s + 1]) ++s;
+    const int bxi = blockIdx.x - c.off[s];
+    ChainWait cw;
+    if (s > 0) {
+        cw.cnt = c.cnt + 8 * (s - 1);
+        cw.target = (unsigned)(c.off[s] - c.off[s - 1]);
+        cw.err = c.err;
+    }
+    const GemvArgs<T>& a = c.st[s];
+    switch (c.kind[s]) {
+        case GEMV_CHAIN_WO_W2: gemv_body<T, PRO_PLAIN, EPI_SLABFIN, NT, U, WPB, false, true>(a, bxi, 0, 1, cw); break;
+        case GEMV_CHAIN_W13: gemv_body<T, PRO_PRENORM, EPI_SWIGLU8, NT, U, WPB, false, true>(a, bxi, 0, 1, cw); break;
+        default: gemv_body<T, PRO_PRENORM, EPI_STORE, NT, U, WPB, false, true>(a, bxi, 0, 1, cw); break;
+    }
+    // publish: every storing wave drains its write-through stores, then one arrival per block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s + 1 < c.n) {
+            __hip_atomic_fetch_add(c.cnt + 8 * s + (blockIdx.x & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const unsigned last = (unsigned)(c.off[s + 1] - c.off[s]) - 1u;
+            if (__hip_atomic_fetch_add(c.cnt + 8 * (GEMV_CHAIN_MAX - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                last) {
+                for (int i = 0; i < 8 * GEMV_CHAIN_MAX; ++i)
+                    __hip_atomic_store(c.cnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
 }
 
 template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8 = false>
@@ -574,5 +719,25 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
 #undef GO
 }
 
+template <typename T> void launch_gemv_chain(hipStream_t s, const GemvChainArgs<T>& c0) {
+    FMCHECK(c0.n >= 2 && c0.n <= GEMV_CHAIN_MAX && c0.cnt && c0.err, "gemv chain: 2..4 stages, counters set");
+    GemvChainArgs<T> c = c0;
+    size_t lds = 0;
+    c.off[0] = 0;
+    for (int i = 0; i < c.n; ++i) {
+        GemvArgs<T>& a = c.st[i];
+        FMCHECK(a.R == 1 && a.N % 16 == 0 && a.K % 32 == 0 && !a.Wq && !a.xidx && !a.residx,
+                "gemv chain: one row, N % 16 == 0, no gathers, no int8");
+        FMCHECK(a.K <= 4096 || c.kind[i] == GEMV_CHAIN_WO_W2, "gemv chain: PRO_PRENORM needs K <= 4096");
+        a.dbg = fm_tuning().dbg;
+        c.off[i + 1] = c.off[i] + a.N / 16;
+        lds = std::max(lds, gemv_lds_bytes(1, a.K, sizeof(T)));
+    }
+    FMCHECK(lds <= 64 * 1024, "gemv chain: LDS budget");
+    gemv_chain_kernel<T, true, 8, 4><<<c.off[c.n], 256, lds, s>>>(c);
+}
+
+template void launch_gemv_chain<bf16_t>(hipStream_t, const GemvChainArgs<bf16_t>&);
+template void launch_gemv_chain<float>(hipStream_t, const GemvChainArgs<float>&);
 template void launch_gemv<bf16_t>(hipStream_t, const GemvArgs<bf16_t>&, int, int, int);
 template void launch_gemv<float>(hipStream_t, const GemvArgs<float>&, int, int, int);

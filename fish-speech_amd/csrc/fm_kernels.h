@@ -228,6 +228,7 @@ struct FmTuning {
     int bstream_acc = 1;     // 1: bsacc_kernel (per-tile register accumulators, one reduction at the end, balanced K parts); 0: bstream_kernel
     int rmsnorm_block = 0;   // 1: block-per-row RMSNorm (the pre-vectorisation kernel), 0: wave-per-row when shapes allow
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
+    int gemv_chain = 0;      // 1: batch-1 decode runs wo -> w1||w3 -> w2 -> next qkv as one launch (gemv_chain_kernel)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
 };
 FmTuning& fm_tuning();
@@ -240,6 +241,21 @@ inline size_t gemv_lds_bytes(int R, int Kb, size_t esz) {
            8 * 8 * sizeof(float);
 }
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb);
+// batch-1 GEMV chain (fm_gemv.hip gemv_chain_kernel): 2..GEMV_CHAIN_MAX dependent GEMVs in one launch,
+// whole K per block, one row.  Stage kinds: wo / w2 (PRO_PLAIN, EPI_SLABFIN), w1||w3 (PRO_PRENORM,
+// EPI_SWIGLU8), qkv (PRO_PRENORM, EPI_STORE).  cnt: 8 * GEMV_CHAIN_MAX zeroed words (the launch
+// leaves them zeroed); err: set when a wait timed out.
+constexpr int GEMV_CHAIN_MAX = 4;
+enum { GEMV_CHAIN_WO_W2 = 0, GEMV_CHAIN_W13 = 1, GEMV_CHAIN_QKV = 2 };
+template <typename T> struct GemvChainArgs {
+    GemvArgs<T> st[GEMV_CHAIN_MAX];
+    int kind[GEMV_CHAIN_MAX];
+    int off[GEMV_CHAIN_MAX + 1];
+    int n;
+    unsigned* cnt;
+    int* err;
+};
+template <typename T> void launch_gemv_chain(hipStream_t s, const GemvChainArgs<T>& c);
 
 // ---- batched decode weight streaming with register-resident X, 8 < R <= 32 (fm_bstream.hip) ---
 template <typename T> struct BstreamArgs {

@@ -96,6 +96,12 @@ struct fm_llm {
     void *x = nullptr, *h = nullptr, *xn = nullptr, *qkv = nullptr, *q = nullptr, *att = nullptr,
          *act = nullptr;
     void *xl = nullptr, *xnl = nullptr, *fx = nullptr, *fh = nullptr, *fxn = nullptr;
+    // batch-1 GEMV chain (fm_tune gemv_chain): layer outputs alternate between x / x2 (fx / fx2), so no
+    // launch re-reads a residual row it has already read and a later stage rewrites
+    void *x2 = nullptr, *fx2 = nullptr;
+    unsigned* chain_cnt = nullptr;  // [8 * GEMV_CHAIN_MAX] arrival shards (zeroed; each launch re-zeroes them)
+    int* chain_err = nullptr;       // a chain wait timed out
+    int* h_chain_err = nullptr;     // pinned copy, read after the host's stream sync
     void* plast = nullptr;  // batched prefill: the last prompt row of each request [max_slots][dim]
     float *part = nullptr, *logits = nullptr, *flogits = nullptr;
     void* act2 = nullptr;  // batched path: [R][2 * inter] output of the interleaved W1||W3
@@ -146,6 +152,7 @@ struct fm_llm {
         for (void* p : allocs) (void)hipFree(p);
         if (h_cols) (void)hipHostFree(h_cols);
         if (h_hist) (void)hipHostFree(h_hist);
+        if (h_chain_err) (void)hipHostFree(h_chain_err);
         if (stream) (void)hipStreamDestroy(stream);
     }
     void* dalloc(size_t bytes, bool zero = true) {
@@ -554,7 +561,66 @@ template <typename T> struct Run {
         a.eps = m->c.norm_eps;
         return a;
     }
+    // ---- batch-1 GEMV chain: consecutive GEMVs of one row are deferred and launched together
+    // (gemv_chain_kernel), up to GEMV_CHAIN_MAX per launch; any other launch flushes them first
+    struct ChainSt {
+        GemvArgs<T> a;
+        int kind;
+        int64_t bytes;
+        double flops;
+    };
+    std::vector<ChainSt> chain;
+    int chain_kind(const GemvArgs<T>& a, int pro, int epi, int ksb) const {
+        const FmTuning& t = fm_tuning();
+        if (!t.gemv_chain || m->prof.on || ksb != 1 || a.R != 1 || a.Wq || m->qinfo(a.W) || !t.gemv_nt ||
+            t.gemv_u != 8 || t.gemv_wpb != 4 || a.N % 16 || a.xidx || a.residx || a.xn_out)
+            return -1;
+        if (pro == PRO_PLAIN && epi == EPI_SLABFIN) return GEMV_CHAIN_WO_W2;
+        if (pro == PRO_PRENORM && epi == EPI_SWIGLU8 && a.K <= 4096) return GEMV_CHAIN_W13;
+        if (pro == PRO_PRENORM && epi == EPI_STORE && a.K <= 4096) return GEMV_CHAIN_QKV;
+        return -1;
+    }
+    void chain_flush() {
+        if (chain.empty()) return;
+        std::vector<ChainSt> c;
+        c.swap(chain);
+        if (c.size() == 1) {
+            static const int pro_of[3] = {PRO_PLAIN, PRO_PRENORM, PRO_PRENORM};
+            static const int epi_of[3] = {EPI_SLABFIN, EPI_SWIGLU8, EPI_STORE};
+            gemv_now(c[0].a, pro_of[c[0].kind], epi_of[c[0].kind], 1, "linear");
+            return;
+        }
+        GemvChainArgs<T> g{};
+        int64_t bytes = 0;
+        double flops = 0;
+        g.n = (int)c.size();
+        for (int i = 0; i < g.n; ++i) {
+            g.st[i] = c[i].a;
+            if (!g.st[i].tickets) g.st[i].tickets = m->tickets;
+            g.kind[i] = c[i].kind;
+            bytes += c[i].bytes;
+            flops += c[i].flops;
+        }
+        g.cnt = m->chain_cnt;
+        g.err = m->chain_err;
+        hipStream_t st = s;
+        auto go = [st, g] { launch_gemv_chain<T>(st, g); };
+        m->prof.record("linear", bytes, go);
+        m->prof.run(s, "linear", bytes, flops, go);
+    }
     void gemv(GemvArgs<T> a, int pro, int epi, int ksb, const char* cls) {
+        const int kind = chain_kind(a, pro, epi, ksb);
+        if (kind < 0) {
+            chain_flush();
+            gemv_now(a, pro, epi, ksb, cls);
+            return;
+        }
+        const size_t E = sizeof(T);
+        const int64_t bytes = (int64_t)a.N * a.K * E + (int64_t)a.K * E;
+        chain.push_back(ChainSt{a, kind, bytes, 2.0 * a.N * a.K});
+        if ((int)chain.size() == GEMV_CHAIN_MAX) chain_flush();
+    }
+    void gemv_now(GemvArgs<T> a, int pro, int epi, int ksb, const char* cls) {
         if (const auto* q = m->qinfo(a.W)) {  // weight-only int8: the int8 stream, whole 64-k units per slice
             a.Wq = q->q8;
             a.wscale = (const T*)q->scale;
@@ -570,10 +636,12 @@ template <typename T> struct Run {
         m->prof.run(s, cls, bytes, flops, go);
     }
     template <typename F> void run_(const char* cls, int64_t bytes, double flops, F&& f) {
+        chain_flush();
         m->prof.run(s, cls, bytes, flops, std::forward<F>(f));
     }
     // run + record for fm_llm_kernel_bench: `go` must capture by value (it is replayed later)
     template <typename F> void run_rec(const char* cls, F go) {
+        chain_flush();
         m->prof.record(cls, 0, go);
         m->prof.run(s, cls, 0, 0, go);
     }
@@ -594,9 +662,10 @@ template <typename T> struct Run {
     // are always finalised by the producing GEMV (EPI_SLABFIN: x / h in bf16 plus per-tile sums of
     // squares ssX / ssH), so every RMSNorm consumer is PRO_PRENORM.  x_in: the first layer's input
     // (plain rows, or an embedding table + xidx gather), whose norm is computed in place.
+    // xo: where W2 writes the block's output row (xb itself unless the chain alternates buffers)
     void block_small(const StackDims& d, const LayerW& L, int n, bool first, const void* x_in, int ldx_in,
                      const int32_t* xidx, int xcol, void* xb, void* hb, bool is_fast, int cpos, int layer,
-                     const KsbPlan& kp) {
+                     const KsbPlan& kp, void* xo) {
         const int C1 = m->C1;
         const float scale = 1.0f / sqrtf((float)d.hd);
         FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), m->frame_slot, d.nh, d.nkv, d.hd, d.qk_norm,
@@ -720,7 +789,7 @@ template <typename T> struct Run {
             a.ldy = d.dim;
             a.res = (const T*)hb;
             a.ldr = d.dim;
-            a.res_out = (T*)xb;
+            a.res_out = (T*)xo;
             a.ldro = d.dim;
             a.ss_out = m->ssX;
             a.tickets = m->tickets;
@@ -728,11 +797,15 @@ template <typename T> struct Run {
         }
     }
 
+    // the residual row of layer l: x (in place) or, in chain mode, x / x2 alternating
+    void* xbuf(void* x0, void* x1, int l) const { return (fm_tuning().gemv_chain && (l & 1)) ? x1 : x0; }
+    void* xfin = nullptr;  // the slow stack's output row (head_small's input when pending)
     void slow_small(int n) {
         const KsbPlan kp = plan(m->sd, n);
         for (int l = 0; l < m->sd.n_layer; ++l)
-            block_small(m->sd, m->slow[l], n, l == 0, m->x, m->c.dim, nullptr, 0, m->x, m->h, false, 0, l,
-                        kp);
+            block_small(m->sd, m->slow[l], n, l == 0, m->x, m->c.dim, nullptr, 0, xbuf(m->x, m->x2, l), m->h, false, 0,
+                        l, kp, xbuf(m->x, m->x2, l + 1));
+        xfin = xbuf(m->x, m->x2, m->sd.n_layer);
     }
 
     // final norm (+ pending residual) -> constrained head logits and the fast-model hidden
@@ -748,8 +821,9 @@ template <typename T> struct Run {
         a.ldy = m->Nhead;
         a.xn_out = (T*)m->xnl;
         a.ldxo = c.dim;
-        if (pending) {  // the last slow layer's W2 finalised x (m->x) and its sums of squares
-            a.X = (const T*)m->x;
+        const void* xs = xfin ? xfin : m->x;
+        if (pending) {  // the last slow layer's W2 finalised x (xs) and its sums of squares
+            a.X = (const T*)xs;
             a.ldx = c.dim;
             a.ss_in = m->ssX;
             gemv(a, PRO_PRENORM, EPI_F32, 1, "linear");
@@ -758,7 +832,7 @@ template <typename T> struct Run {
             a.ldx = c.dim;
             gemv(a, PRO_NORM, EPI_F32, 1, "linear");
         }
-        const void* hid = c.norm_fastlayer_input ? m->xnl : (pending ? m->x : xlast);
+        const void* hid = c.norm_fastlayer_input ? m->xnl : (pending ? xs : xlast);
         if (m->fproj_w) {
             GemvArgs<T> p = ga();
             p.W = (const T*)m->fproj_w;
@@ -783,7 +857,8 @@ template <typename T> struct Run {
             const bool first = l == 0;
             const void* xin = cc == 0 ? hidden : m->femb;
             const int32_t* xidx = cc == 0 ? nullptr : m->cols;
-            block_small(m->fdm, m->fast[l], n, first, xin, c.fast_dim, xidx, cc, m->fx, m->fh, true, cc, l, kp);
+            block_small(m->fdm, m->fast[l], n, first, xin, c.fast_dim, xidx, cc, xbuf(m->fx, m->fx2, l), m->fh, true,
+                        cc, l, kp, xbuf(m->fx, m->fx2, l + 1));
         }
         if (with_head) {
             GemvArgs<T> a = ga();
@@ -794,7 +869,7 @@ template <typename T> struct Run {
             a.K = c.fast_dim;
             a.Yf = m->flogits;
             a.ldy = m->cb;
-            a.X = (const T*)m->fx;
+            a.X = (const T*)xbuf(m->fx, m->fx2, m->fdm.n_layer);
             a.ldx = c.fast_dim;
             a.ss_in = m->ssX;
             gemv(a, PRO_PRENORM, EPI_F32, 1, "linear");
@@ -826,6 +901,7 @@ template <typename T> struct Run {
         const KsbPlan kp = plan(m->sd, n);
         const void* hid = head_small(nullptr, true, n, kp.w2);
         frame_tail_small(n, true, true, hid);
+        chain_flush();
         launch_finish(s, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10, m->C1,
                       1, m->sp);
     }
@@ -841,6 +917,7 @@ template <typename T> struct Run {
     // final norm -> constrained head logits; hidden for the fast model (llama.py:447-466, 826)
     void head_and_hidden(const void* xlast, int n) {
         const fm_model_config& c = m->c;
+        chain_flush();
         run_("norm", 0, 0, [&] {
             launch_rmsnorm<T>(s, (const T*)xlast, c.dim, (const T*)m->norm, c.dim, c.norm_eps, (T*)m->xnl,
                               c.dim, n);
@@ -935,6 +1012,7 @@ template <typename T> struct Run {
         head_and_hidden(m->x, n);
         frame_tail(n, true, true);
         bs_frame = false;
+        chain_flush();
         launch_finish(s, n, m->frame_slot, m->frame_pos, m->cols, m->C1, m->tok_in, m->ras, m->C1 * 10,
                       m->C1, 1, m->sp);
     }
@@ -951,6 +1029,7 @@ template <typename T> struct Run {
                 for (int q = 0; q < C1; ++q) rows[(size_t)r * C1 + q] = tokens[(size_t)q * Tn + t0 + r];
                 rp[r] = pos0 + t0 + r;
             }
+            chain_flush();
             HIPCHK(hipMemcpyAsync(m->ptok, rows.data(), (size_t)R * C1 * 4, hipMemcpyHostToDevice, s));
             HIPCHK(hipMemcpyAsync(m->prow_slot, rs.data(), (size_t)R * 4, hipMemcpyHostToDevice, s));
             HIPCHK(hipMemcpyAsync(m->prow_pos, rp.data(), (size_t)R * 4, hipMemcpyHostToDevice, s));
@@ -994,6 +1073,7 @@ template <typename T> struct Run {
                     t = 0;
                 }
             }
+            chain_flush();
             HIPCHK(hipMemcpyAsync(m->ptok, rows.data(), (size_t)R * C1 * 4, hipMemcpyHostToDevice, s));
             HIPCHK(hipMemcpyAsync(m->prow_slot, rs.data(), (size_t)R * 4, hipMemcpyHostToDevice, s));
             HIPCHK(hipMemcpyAsync(m->prow_pos, rp.data(), (size_t)R * 4, hipMemcpyHostToDevice, s));
@@ -1001,6 +1081,7 @@ template <typename T> struct Run {
                             m->c.semantic_begin_id, m->c.semantic_end_id, m->c.scale_codebook_embeddings,
                             (T*)m->x, nullptr);
             slow_layers(R, m->prow_slot, m->prow_pos);
+            chain_flush();
             for (const auto& l : lasts)
                 HIPCHK(hipMemcpyAsync((char*)m->plast + (size_t)l[0] * dim * E, (const char*)m->x + (size_t)l[1] * dim * E,
                                       (size_t)dim * E, hipMemcpyDeviceToDevice, s));
@@ -1266,6 +1347,12 @@ static void finalize(fm_llm* m) {
     m->fx = m->dalloc((size_t)n * dmax * E);
     m->fh = m->dalloc((size_t)n * dmax * E);
     m->fxn = m->dalloc((size_t)n * dmax * E);
+    m->x2 = m->dalloc((size_t)std::min(n, GEMV_MAX_ROWS) * dmax * E);
+    m->fx2 = m->dalloc((size_t)std::min(n, GEMV_MAX_ROWS) * dmax * E);
+    m->chain_cnt = (unsigned*)m->dalloc(8 * GEMV_CHAIN_MAX * sizeof(unsigned));
+    m->chain_err = (int*)m->dalloc(16 * sizeof(int));
+    HIPCHK(hipHostMalloc((void**)&m->h_chain_err, 16 * sizeof(int), hipHostMallocDefault));
+    m->h_chain_err[0] = 0;
     m->maxsplit = FM_CEIL(m->S, ATTN_SPLIT);
     const int Rpart = std::max(m->max_slots, ATTN_PIECE);  // decode rows, or one prompt attention piece
     m->part = (float*)m->dalloc((size_t)Rpart * d.nh * std::max(m->maxsplit, FM_CEIL(m->S, 16)) * (d.hd + 2) * 4, false);
@@ -1312,9 +1399,11 @@ template <typename F> static int with_prec(fm_llm* m, F&& f) {
     if (m->prec == FM_PREC_BF16) {
         Run<bf16_t> r(m);
         f(r);
+        r.chain_flush();
     } else {
         Run<float> r(m);
         f(r);
+        r.chain_flush();
     }
     return 0;
 }
@@ -1363,6 +1452,20 @@ static void upload_frame_rows(fm_llm* m, const int32_t* slots, int n) {
     HIPCHK(hipMemcpyAsync(m->frame_pos, p.data(), (size_t)n * 4, hipMemcpyHostToDevice, m->stream));
     HIPCHK(hipStreamSynchronize(m->stream));
     m->uploaded_slots = s;
+}
+
+// gemv chain health: the error word travels to pinned memory behind the frames; after the
+// host's stream sync, a timed-out hand-off wait (a hang avoided) resets the counters and fails
+static void chain_err_async(fm_llm* m) {
+    if (fm_tuning().gemv_chain)
+        HIPCHK(hipMemcpyAsync(m->h_chain_err, m->chain_err, sizeof(int), hipMemcpyDeviceToHost, m->stream));
+}
+static void chain_err_check(fm_llm* m) {
+    if (!m->h_chain_err || !m->h_chain_err[0]) return;
+    m->h_chain_err[0] = 0;
+    HIPCHK(hipMemset(m->chain_cnt, 0, 8 * GEMV_CHAIN_MAX * sizeof(unsigned)));
+    HIPCHK(hipMemset(m->chain_err, 0, 16 * sizeof(int)));
+    throw FmError{FM_ERR_STATE, "gemv chain: a stage hand-off wait timed out (counters reset)"};
 }
 
 // one decode frame for the uploaded rows (graph replay when enabled), async
@@ -1632,7 +1735,9 @@ int fm_llm_decode(fm_llm* m, const int32_t* slots, int n, int32_t* cols) {
         upload_frame_rows(m, slots, n);
         launch_frame(m, n);
         HIPCHK(hipMemcpyAsync(m->h_cols, m->cols, (size_t)n * m->C1 * 4, hipMemcpyDeviceToHost, m->stream));
+        chain_err_async(m);
         HIPCHK(hipStreamSynchronize(m->stream));
+        chain_err_check(m);
         m->prof.collect();
         for (int i = 0; i < n; ++i) {
             m->host_pos[slots[i]]++;
@@ -1667,7 +1772,9 @@ int fm_llm_decode_frames(fm_llm* m, const int32_t* slots, int n, int nframes, in
             launch_frame(m, n);
             HIPCHK(hipMemcpyAsync(m->h_hist + per * k, m->cols, per * 4, hipMemcpyDeviceToHost, m->stream));
         }
+        chain_err_async(m);
         HIPCHK(hipStreamSynchronize(m->stream));
+        chain_err_check(m);
         m->prof.collect();
         for (int i = 0; i < n; ++i) {
             m->host_pos[slots[i]] += nframes;
@@ -1712,7 +1819,9 @@ static void do_generate(fm_llm* m, int slot, const int32_t* prompt, int T, int p
             n++;
             if (hc[0] == c.im_end_id) break;
         }
+        chain_err_async(m);
         HIPCHK(hipStreamSynchronize(m->stream));
+        chain_err_check(m);
         m->prof.collect();
         (void)hipEventDestroy(ev[0]);
         (void)hipEventDestroy(ev[1]);
@@ -1891,6 +2000,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "fd_min") {
             FMCHECK(value >= 16 && value % 16 == 0, "fd_min must be a multiple of 16");
             t.fd_min = value;
+        } else if (k == "gemv_chain") {
+            t.gemv_chain = value != 0;
         } else if (k == "fd_nw") {
             FMCHECK(value == 4 || value == 8 || value == 16, "fd_nw must be 4, 8 or 16");
             t.fd_nw = value;
