@@ -65,25 +65,32 @@ constexpr int gemv_wpe(int pro, int epi) { return pro == PRO_PRENORM && epi == E
 // (s_waitcnt vmcnt(0)) by its storing wave before the block's one arrival on a sharded counter;
 // the consumer polls the counter (sc1 loads, one lane per shard), and EVERY load of handed-off
 // bytes is an sc1 load (buffer_load_dwordx4 / global_load_dword sc1), so no acquire fence.
+// Counter words, one 128-B line each (GEMV_CHAIN_LINE words apart): per stage s, 8 arrival shards
+// (block b adds to shard b & 7), a top word that each shard's last arriver increments, and 8 done
+// replicas that the top's last arriver sets.  A waiting block polls only the replica of its shard
+// (the polls of a thousand waiting blocks spread over 8 lines that nothing else touches).
+__device__ __forceinline__ unsigned* chain_word(unsigned* cnt, int s, int k) {
+    return cnt + (s * GEMV_CHAIN_SLOTS + k) * GEMV_CHAIN_LINE;
+}
 struct ChainWait {
-    const unsigned* cnt = nullptr;  // the producing stage's 8 arrival shards (null: stage 0)
-    unsigned target = 0;            // its block count
-    int* err = nullptr;             // set on a timed-out wait (host re-zeroes the counters)
+    const unsigned* done = nullptr;  // the producing stage's done replica (null: stage 0)
+    int sleep = 4;                   // s_sleep between polls (1, 4 or 16)
+    int* err = nullptr;              // set on a timed-out wait (host re-zeroes the counters)
 };
 __device__ __forceinline__ void chain_wait(const ChainWait& cw) {
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
+    if (threadIdx.x == 0) {
         for (unsigned it = 0;; ++it) {
-            unsigned v = lane < 8 ? __hip_atomic_load(cw.cnt + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 4);
-            if (__shfl(v, 0) >= cw.target) break;
+            if (__hip_atomic_load(cw.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
             if (it > (1u << 16)) {  // bounded (~0.1 s; a stage takes tens of us): the host sees err, resets
-                if (lane == 0) __hip_atomic_store(cw.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(cw.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            if (cw.sleep <= 1)
+                __builtin_amdgcn_s_sleep(1);
+            else if (cw.sleep <= 4)
+                __builtin_amdgcn_s_sleep(4);
+            else
+                __builtin_amdgcn_s_sleep(16);
         }
     }
     __syncthreads();
@@ -128,7 +135,8 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
                                           const ChainWait& cw) {
     static_assert(!(Q8 && (EPI == EPI_SWIGLU || EPI == EPI_SLAB || PRO == PRO_FATT)), "no int8 form");
     static_assert(!CH || (!Q8 && (PRO == PRO_PLAIN || PRO == PRO_PRENORM) &&
-                          (EPI == EPI_STORE || EPI == EPI_SWIGLU8 || EPI == EPI_SLABFIN)), "no chain form");
+                          (EPI == EPI_STORE || EPI == EPI_SWIGLU8 || EPI == EPI_SLABFIN || EPI == EPI_F32)),
+                  "no chain form");
     // X items preloaded per thread ahead of the weight ring: PRO_PRENORM's operand is one dim-wide
     // row per stream (2 items per thread at R = 1), and its register budget is what lets the
     // 1216-block W1||W3 grid stay resident (5 waves per SIMD)
@@ -319,7 +327,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
         if constexpr (CH) {  // chain stage: the weight ring first (no dependency), then the wait
 #pragma unroll
             for (int u = 0; u < U; ++u) issue(u, u);
-            if (cw.cnt) chain_wait(cw);
+            if (cw.done) chain_wait(cw);
             if constexpr (EPI == EPI_SLABFIN) load_res();
         }
         C8<T> xc[PRE_N], wc[PRO == PRO_PRENORM ? PRE_N : 1];
@@ -606,28 +614,36 @@ void gemv_chain_kernel(GemvChainArgs<T> c) {
     const int bxi = blockIdx.x - c.off[s];
     ChainWait cw;
     if (s > 0) {
-        cw.cnt = c.cnt + 8 * (s - 1);
-        cw.target = (unsigned)(c.off[s] - c.off[s - 1]);
+        cw.done = chain_word(c.cnt, s - 1, 9 + (blockIdx.x & 7));
+        cw.sleep = c.sleep;
         cw.err = c.err;
     }
     const GemvArgs<T>& a = c.st[s];
     switch (c.kind[s]) {
         case GEMV_CHAIN_WO_W2: gemv_body<T, PRO_PLAIN, EPI_SLABFIN, NT, U, WPB, false, true>(a, bxi, 0, 1, cw); break;
         case GEMV_CHAIN_W13: gemv_body<T, PRO_PRENORM, EPI_SWIGLU8, NT, U, WPB, false, true>(a, bxi, 0, 1, cw); break;
-        default: gemv_body<T, PRO_PRENORM, EPI_STORE, NT, U, WPB, false, true>(a, bxi, 0, 1, cw); break;
+        case GEMV_CHAIN_QKV: gemv_body<T, PRO_PRENORM, EPI_STORE, NT, U, WPB, false, true>(a, bxi, 0, 1, cw); break;
+        default: gemv_body<T, PRO_PRENORM, EPI_F32, NT, U, WPB, false, true>(a, bxi, 0, 1, cw); break;
     }
     // publish: every storing wave drains its write-through stores, then one arrival per block
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (s + 1 < c.n) {
-            __hip_atomic_fetch_add(c.cnt + 8 * s + (blockIdx.x & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            const unsigned last = (unsigned)(c.off[s + 1] - c.off[s]) - 1u;
-            if (__hip_atomic_fetch_add(c.cnt + 8 * (GEMV_CHAIN_MAX - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                last) {
-                for (int i = 0; i < 8 * GEMV_CHAIN_MAX; ++i)
-                    __hip_atomic_store(c.cnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int k = blockIdx.x & 7;
+        // blocks of this stage in shard k: b in [off[s], off[s+1]) with b % 8 == k
+        const unsigned tot = (unsigned)((c.off[s + 1] + 7 - k) / 8 - (c.off[s] + 7 - k) / 8);
+        if (__hip_atomic_fetch_add(chain_word(c.cnt, s, k), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tot - 1) {
+            const unsigned ne = (unsigned)min(8, c.off[s + 1] - c.off[s]);
+            if (__hip_atomic_fetch_add(chain_word(c.cnt, s, 8), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ne - 1) {
+                if (s + 1 < c.n) {  // stage complete: release its waiters
+                    for (int r = 0; r < 8; ++r)
+                        __hip_atomic_store(chain_word(c.cnt, s, 9 + r), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    // the launch is complete and every wait has passed: zero the words for the next one
+                    for (int q = 0; q < c.n; ++q)
+                        for (int j = 0; j < GEMV_CHAIN_SLOTS; ++j)
+                            __hip_atomic_store(chain_word(c.cnt, q, j), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
     }
@@ -726,8 +742,9 @@ template <typename T> void launch_gemv_chain(hipStream_t s, const GemvChainArgs<
     c.off[0] = 0;
     for (int i = 0; i < c.n; ++i) {
         GemvArgs<T>& a = c.st[i];
-        FMCHECK(a.R == 1 && a.N % 16 == 0 && a.K % 32 == 0 && !a.Wq && !a.xidx && !a.residx,
-                "gemv chain: one row, N % 16 == 0, no gathers, no int8");
+        FMCHECK(a.R == 1 && a.N % 16 == 0 && a.K % 32 == 0 && !a.Wq && !a.xidx,
+                "gemv chain: one row, N % 16 == 0, no X gather, no int8");
+        FMCHECK(c.kind[i] != GEMV_CHAIN_HEAD || i == c.n - 1, "gemv chain: the fp32 head stage ends the launch");
         FMCHECK(a.K <= 4096 || c.kind[i] == GEMV_CHAIN_WO_W2, "gemv chain: PRO_PRENORM needs K <= 4096");
         a.dbg = fm_tuning().dbg;
         c.off[i + 1] = c.off[i] + a.N / 16;

@@ -228,6 +228,8 @@ struct FmTuning {
     int bstream_acc = 1;     // 1: bsacc_kernel (per-tile register accumulators, one reduction at the end, balanced K parts); 0: bstream_kernel
     int rmsnorm_block = 0;   // 1: block-per-row RMSNorm (the pre-vectorisation kernel), 0: wave-per-row when shapes allow
     int ksb_balance = 0;     // 1: prefer grids that are whole multiples of 256 blocks (one per CU)
+    int chain_max = 4;       // gemv_chain: GEMVs per launch at most (2..4)
+    int chain_sleep = 4;     // gemv_chain: s_sleep argument between a waiting block's polls (1, 4 or 16)
     int gemv_chain = 0;      // 1: batch-1 decode runs wo -> w1||w3 -> w2 -> next qkv as one launch (gemv_chain_kernel)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
 };
@@ -242,11 +244,15 @@ inline size_t gemv_lds_bytes(int R, int Kb, size_t esz) {
 }
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb);
 // batch-1 GEMV chain (fm_gemv.hip gemv_chain_kernel): 2..GEMV_CHAIN_MAX dependent GEMVs in one launch,
-// whole K per block, one row.  Stage kinds: wo / w2 (PRO_PLAIN, EPI_SLABFIN), w1||w3 (PRO_PRENORM,
-// EPI_SWIGLU8), qkv (PRO_PRENORM, EPI_STORE).  cnt: 8 * GEMV_CHAIN_MAX zeroed words (the launch
+// whole K per block, one row.  Stage kinds: wo / w2 (PRO_PLAIN, EPI_SLABFIN; the residual may be a
+// gathered row), w1||w3 (PRO_PRENORM, EPI_SWIGLU8), qkv (PRO_PRENORM, EPI_STORE), and as the last
+// stage only, a head (PRO_PRENORM, EPI_F32; its outputs are read by later launches).  cnt: GEMV_CHAIN_WORDS zeroed words (the launch
 // leaves them zeroed); err: set when a wait timed out.
 constexpr int GEMV_CHAIN_MAX = 4;
-enum { GEMV_CHAIN_WO_W2 = 0, GEMV_CHAIN_W13 = 1, GEMV_CHAIN_QKV = 2 };
+constexpr int GEMV_CHAIN_LINE = 32;  // counter words one 128-B line apart
+constexpr int GEMV_CHAIN_SLOTS = 17;  // per stage: 8 arrival shards, 1 top word, 8 done replicas
+constexpr int GEMV_CHAIN_WORDS = GEMV_CHAIN_MAX * GEMV_CHAIN_SLOTS * GEMV_CHAIN_LINE;
+enum { GEMV_CHAIN_WO_W2 = 0, GEMV_CHAIN_W13 = 1, GEMV_CHAIN_QKV = 2, GEMV_CHAIN_HEAD = 3 };
 template <typename T> struct GemvChainArgs {
     GemvArgs<T> st[GEMV_CHAIN_MAX];
     int kind[GEMV_CHAIN_MAX];
@@ -254,6 +260,7 @@ template <typename T> struct GemvChainArgs {
     int n;
     unsigned* cnt;
     int* err;
+    int sleep;  // s_sleep between polls (fm_tune chain_sleep)
 };
 template <typename T> void launch_gemv_chain(hipStream_t s, const GemvChainArgs<T>& c);
 

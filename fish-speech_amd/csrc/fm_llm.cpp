@@ -99,7 +99,7 @@ struct fm_llm {
     // batch-1 GEMV chain (fm_tune gemv_chain): layer outputs alternate between x / x2 (fx / fx2), so no
     // launch re-reads a residual row it has already read and a later stage rewrites
     void *x2 = nullptr, *fx2 = nullptr;
-    unsigned* chain_cnt = nullptr;  // [8 * GEMV_CHAIN_MAX] arrival shards (zeroed; each launch re-zeroes them)
+    unsigned* chain_cnt = nullptr;  // [GEMV_CHAIN_WORDS] arrival counters (zeroed; each launch re-zeroes them)
     int* chain_err = nullptr;       // a chain wait timed out
     int* h_chain_err = nullptr;     // pinned copy, read after the host's stream sync
     void* plast = nullptr;  // batched prefill: the last prompt row of each request [max_slots][dim]
@@ -573,11 +573,14 @@ template <typename T> struct Run {
     int chain_kind(const GemvArgs<T>& a, int pro, int epi, int ksb) const {
         const FmTuning& t = fm_tuning();
         if (!t.gemv_chain || m->prof.on || ksb != 1 || a.R != 1 || a.Wq || m->qinfo(a.W) || !t.gemv_nt ||
-            t.gemv_u != 8 || t.gemv_wpb != 4 || a.N % 16 || a.xidx || a.residx || a.xn_out)
+            t.gemv_u != 8 || t.gemv_wpb != 4 || a.N % 16 || a.xidx)
             return -1;
         if (pro == PRO_PLAIN && epi == EPI_SLABFIN) return GEMV_CHAIN_WO_W2;
-        if (pro == PRO_PRENORM && epi == EPI_SWIGLU8 && a.K <= 4096) return GEMV_CHAIN_W13;
-        if (pro == PRO_PRENORM && epi == EPI_STORE && a.K <= 4096) return GEMV_CHAIN_QKV;
+        if (a.xn_out || a.K > 4096 || pro != PRO_PRENORM) return a.xn_out && pro == PRO_PRENORM && epi == EPI_F32 &&
+                                                                    a.K <= 4096 ? GEMV_CHAIN_HEAD : -1;
+        if (epi == EPI_SWIGLU8) return GEMV_CHAIN_W13;
+        if (epi == EPI_STORE) return GEMV_CHAIN_QKV;
+        if (epi == EPI_F32) return GEMV_CHAIN_HEAD;
         return -1;
     }
     void chain_flush() {
@@ -585,8 +588,8 @@ template <typename T> struct Run {
         std::vector<ChainSt> c;
         c.swap(chain);
         if (c.size() == 1) {
-            static const int pro_of[3] = {PRO_PLAIN, PRO_PRENORM, PRO_PRENORM};
-            static const int epi_of[3] = {EPI_SLABFIN, EPI_SWIGLU8, EPI_STORE};
+            static const int pro_of[4] = {PRO_PLAIN, PRO_PRENORM, PRO_PRENORM, PRO_PRENORM};
+            static const int epi_of[4] = {EPI_SLABFIN, EPI_SWIGLU8, EPI_STORE, EPI_F32};
             gemv_now(c[0].a, pro_of[c[0].kind], epi_of[c[0].kind], 1, "linear");
             return;
         }
@@ -603,6 +606,7 @@ template <typename T> struct Run {
         }
         g.cnt = m->chain_cnt;
         g.err = m->chain_err;
+        g.sleep = fm_tuning().chain_sleep;
         hipStream_t st = s;
         auto go = [st, g] { launch_gemv_chain<T>(st, g); };
         m->prof.record("linear", bytes, go);
@@ -618,7 +622,8 @@ template <typename T> struct Run {
         const size_t E = sizeof(T);
         const int64_t bytes = (int64_t)a.N * a.K * E + (int64_t)a.K * E;
         chain.push_back(ChainSt{a, kind, bytes, 2.0 * a.N * a.K});
-        if ((int)chain.size() == GEMV_CHAIN_MAX) chain_flush();
+        if ((int)chain.size() >= std::min(GEMV_CHAIN_MAX, fm_tuning().chain_max) || kind == GEMV_CHAIN_HEAD)
+            chain_flush();
     }
     void gemv_now(GemvArgs<T> a, int pro, int epi, int ksb, const char* cls) {
         if (const auto* q = m->qinfo(a.W)) {  // weight-only int8: the int8 stream, whole 64-k units per slice
@@ -1349,7 +1354,7 @@ static void finalize(fm_llm* m) {
     m->fxn = m->dalloc((size_t)n * dmax * E);
     m->x2 = m->dalloc((size_t)std::min(n, GEMV_MAX_ROWS) * dmax * E);
     m->fx2 = m->dalloc((size_t)std::min(n, GEMV_MAX_ROWS) * dmax * E);
-    m->chain_cnt = (unsigned*)m->dalloc(8 * GEMV_CHAIN_MAX * sizeof(unsigned));
+    m->chain_cnt = (unsigned*)m->dalloc(GEMV_CHAIN_WORDS * sizeof(unsigned));
     m->chain_err = (int*)m->dalloc(16 * sizeof(int));
     HIPCHK(hipHostMalloc((void**)&m->h_chain_err, 16 * sizeof(int), hipHostMallocDefault));
     m->h_chain_err[0] = 0;
@@ -1463,7 +1468,7 @@ static void chain_err_async(fm_llm* m) {
 static void chain_err_check(fm_llm* m) {
     if (!m->h_chain_err || !m->h_chain_err[0]) return;
     m->h_chain_err[0] = 0;
-    HIPCHK(hipMemset(m->chain_cnt, 0, 8 * GEMV_CHAIN_MAX * sizeof(unsigned)));
+    HIPCHK(hipMemset(m->chain_cnt, 0, GEMV_CHAIN_WORDS * sizeof(unsigned)));
     HIPCHK(hipMemset(m->chain_err, 0, 16 * sizeof(int)));
     throw FmError{FM_ERR_STATE, "gemv chain: a stage hand-off wait timed out (counters reset)"};
 }
@@ -2000,6 +2005,12 @@ int fm_tune(const char* key, int value) {
         } else if (k == "fd_min") {
             FMCHECK(value >= 16 && value % 16 == 0, "fd_min must be a multiple of 16");
             t.fd_min = value;
+        } else if (k == "chain_max") {
+            FMCHECK(value >= 2 && value <= GEMV_CHAIN_MAX, "chain_max must be 2..4");
+            t.chain_max = value;
+        } else if (k == "chain_sleep") {
+            FMCHECK(value == 1 || value == 4 || value == 16, "chain_sleep must be 1, 4 or 16");
+            t.chain_sleep = value;
         } else if (k == "gemv_chain") {
             t.gemv_chain = value != 0;
         } else if (k == "fd_nw") {
