@@ -206,7 +206,8 @@ class _Stream:
 def serve(queue: TickQueue, max_concurrent: int, start: Callable[[int, Request], np.ndarray],
           step: Callable[[List[int], int], np.ndarray], finish: Callable[[int, Request, np.ndarray], np.ndarray],
           tick_frames: int = 16, im_end: Optional[int] = None,
-          start_batch: Optional[Callable[[List[tuple]], np.ndarray]] = None) -> Dict[str, int]:
+          start_batch: Optional[Callable[[List[tuple]], np.ndarray]] = None,
+          progress: Optional[Callable[[int, Request, List[np.ndarray]], None]] = None) -> Dict[str, int]:
     """Per-rank serving loop over the tick queue.
 
     start(slot, req) prefills the request into its KV slot and returns the first column (C+1,);
@@ -214,6 +215,8 @@ def serve(queue: TickQueue, max_concurrent: int, start: Callable[[int, Request],
     their first columns (n, C+1) (fm_llm_prefill_batch).
     step(slots, n) decodes n batched frames for the slots and returns (n, len(slots), C+1).
     finish(slot, req, cols (C+1, N)) turns the stream into its result payload (PCM or codes).
+    progress(slot, req, cols), when given, sees every live stream's columns so far after each
+    tick's decode (a consumer may start on all but the newest, which may be the dropped last one).
     A stream ends after req.frames columns, or at the column whose main token is `im_end`. The
     last column is dropped either way, like `codes = y[1:, T:-1]` in generate_long
     (inference.py:683-688).
@@ -254,6 +257,8 @@ def serve(queue: TickQueue, max_concurrent: int, start: Callable[[int, Request],
                     st.done += 1
                 if st.done >= st.req.frames or (im_end is not None and st.cols[-1][0] == im_end):
                     done_now.append(slot)
+                elif progress is not None:
+                    progress(slot, st.req, st.cols)
         for slot in done_now:
             st = active.pop(slot)
             cols = np.stack(st.cols, 1)[:, :-1]  # codes = y[1:, T:-1]: the last column is dropped

@@ -76,15 +76,25 @@ def _worker(rank, world, port, q, n_req, conc, batched=False):
         def step(live, n):
             return np.stack([np.stack([step_col(s) for s in live]) for _ in range(n)])
 
+        seen = {}
+
+        def progress(slot, req, cols):  # growing prefixes of the stream, never rewritten
+            prev = seen.get(req.id, [])
+            assert len(cols) > len(prev) and all(np.array_equal(a, b) for a, b in zip(prev, cols))
+            seen[req.id] = [c.copy() for c in cols]
+
         def finish(slot, req, cols):
             del slots[slot]
+            prev = seen.get(req.id)
+            if prev:  # all but the newest column a consumer saw are the stream's final columns
+                np.testing.assert_array_equal(np.stack(prev[:-1], 1), cols[:, :len(prev) - 1])
             return np.ascontiguousarray(cols[1:]).reshape(-1).astype(np.int32)
 
         def start_batch(pairs):  # a tick's new requests at once (fm_llm_prefill_batch's seam)
             return np.stack([start(slot, req) for slot, req in pairs])
 
         stats = S.serve(queue, conc, start, step, finish, tick_frames=6, im_end=IM_END,
-                        start_batch=start_batch if batched else None)
+                        start_batch=start_batch if batched else None, progress=progress)
         res = [(r.id, r.rank, r.data.tolist()) for r in queue.results] if rank == 0 else None
         q.put((rank, stats, peak[0], res))
     finally:
