@@ -215,7 +215,7 @@ struct FmTuning {
     int fd_min = 32;         // attn_fd: minimum positions per split at R <= 8
     int fd_min_batched = 512;  // attn_fd: minimum positions per split at R > 8 (B=32: one split below 512)
     int fd_nw = 8;           // attn_fd at R <= 8: waves per block (4, 8 or 16) ...
-    int fd_min16 = 512;      // ... and splits of at least this many positions (8 or 16 waves; below it
+    int fd_min16 = 256;      // ... and splits of at least this many positions (8 or 16 waves; below it
                              // one block per kv head, no cross-block combine)
     int prefill_attn = 1;    // 1: prompt-chunk attention on attn_prefill_kernel (bf16, head_dim 128, flash form)
     int prompt_gemm = 1;     // 1: prompt-chunk linears (R > 32) on the codec's LDS-tiled GEMM kernels

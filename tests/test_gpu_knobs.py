@@ -15,7 +15,7 @@ from test_gpu_llm import _bf16_vs_reference, _cfg, _model
 pytestmark = pytest.mark.gpu
 
 # FmTuning's defaults (fm_kernels.h), restored after every test
-DEFAULTS = {"attn3": 1, "attn_fd": 1, "fd_min": 32, "fd_nw": 8, "fd_min16": 512, "gemv_chain": 0, "gemv_nt": 1, "gemv_u": 8, "gemv_wpb": 4,
+DEFAULTS = {"attn3": 1, "attn_fd": 1, "fd_min": 32, "fd_nw": 8, "fd_min16": 256, "gemv_chain": 0, "gemv_nt": 1, "gemv_u": 8, "gemv_wpb": 4,
             "ksb_balance": 0, "ksb_blocks": 512, "attn_cap": 32, "prefill_attn": 1, "prompt_gemm": 1,
             "conv2": 1, "conv_splitk": 1}
 
