@@ -7,6 +7,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// The in-launch hand-offs (split-K partials, attention split combines, the GEMV chain) are the
+// write-through form of cdna_hip_programming.md §6 Guideline 16: sc1 stores drained by
+// s_waitcnt vmcnt(0), relaxed agent counters, sc1 loads.  That form is measured on gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "libfishmi kernels are written for gfx950 (MI355X): build with --offload-arch=gfx950"
+#endif
+
 typedef uint16_t bf16_t;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
