@@ -18,6 +18,7 @@
 #include "fm_kernels.h"
 #include "fm_runtime.h"
 #include "fm_attn_dev.h"
+#include "fm_frag.h"
 
 // normalise (optional) + rope one head held as pairs by a wave (lane p owns pair p, p+64)
 template <typename T>
@@ -578,6 +579,31 @@ template <typename T> __device__ __forceinline__ void cvt16(const u32x4_t v, flo
 }
 
 constexpr int FD_GM = 4;
+// v summed over the wave's four 16-lane rows (lanes l, l ^ 16, l ^ 32, l ^ 48) by two VALU half
+// exchanges (v_permlane32_swap, v_permlane16_swap) instead of LDS-routed shuffles
+__device__ __forceinline__ float sum_rows4(float v, int lane) {
+    const unsigned u = __float_as_uint(v);
+    const auto r32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);  // [0]: vdst, [1]: src
+    v += __uint_as_float(lane < 32 ? r32[1] : r32[0]);                   // + lane ^ 32
+    const unsigned w = __float_as_uint(v);
+    const auto r16 = __builtin_amdgcn_permlane16_swap(w, w, false, false);
+    return v + __uint_as_float(((lane >> 4) & 1) ? r16[0] : r16[1]);      // + lane ^ 16
+}
+// 8 floats (T-exact values) as one MFMA fragment of T
+template <typename T> __device__ __forceinline__ typename Frag<T>::f frag_f32(const float* v) {
+    typename Frag<T>::f f;
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f[i] = hi_pair(v[2 * i], v[2 * i + 1]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f.lo[i] = v[i];
+            f.hi[i] = v[4 + i];
+        }
+    }
+    return f;
+}
 // NW waves per block (4, 8 or 16): 16 NW positions per pass.  The batch-1 launches use wide blocks
 // and long splits, so below fd_min16 cached positions one block per kv head needs no cross-block
 // combine.
@@ -585,8 +611,6 @@ template <typename T, int HD, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_fd_kernel(AttnDecArgs<T> a) {
     static_assert(HD % 32 == 0 && HD <= 128, "head_dim a multiple of 32 up to 128");
     constexpr int NT = NW * 64, FD_TILE = 16 * NW;
-    constexpr int QD = HD / 4;                      // K dims per lane
-    constexpr int KL = QD * (int)sizeof(T) / 16;    // 16-B loads per K slice
     constexpr int VL = 8 * (int)sizeof(T) / 16;     // 16-B loads per V slice
     constexpr int half = HD / 2;
     __shared__ __attribute__((aligned(16))) float q_s[FD_GM][HD];
@@ -631,12 +655,15 @@ __global__ __launch_bounds__(NW * 64) void attn_fd_kernel(AttnDecArgs<T> a) {
     T* kc = a.kc + base;
     T* vc = a.vc + base;
     const int vd = 8 * l16 < HD ? 8 * l16 : HD - 8;
-    u32x4_t kb[KL], vb[4][VL];
+    // K as MFMA B fragments: lane (l16, qq) holds K[position l16 of its wave's 16][32 ks + 8 qq, + 8)
+    using F = Frag<T>;
+    constexpr int NKS = HD / 32;
+    typename F::f kb[NKS];
+    u32x4_t vb[4][VL];
     auto issue = [&](int jb) {
         const int jk = min(jb + 16 * wave + l16, jend - 1);
-        const u32x4_t* pk = reinterpret_cast<const u32x4_t*>(kc + (size_t)jk * HD + qq * QD);
 #pragma unroll
-        for (int c = 0; c < KL; ++c) kb[c] = pk[c];
+        for (int ks = 0; ks < NKS; ++ks) kb[ks] = F::load(kc + (size_t)jk * HD + 32 * ks + 8 * qq);
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
             const int jv = min(jb + 16 * wave + 4 * it + qq, jend - 1);
@@ -686,28 +713,41 @@ __global__ __launch_bounds__(NW * 64) void attn_fd_kernel(AttnDecArgs<T> a) {
             }
         }
     }
-    __syncthreads();
+    lds_barrier();  // q_s / kv_new; pass 0's K / V loads stay in flight
     DBG_TS(tz, 1)
-    // ---- passes: per wave online softmax over its 16 positions of each pass
-    float m_run[FD_GM], l_run[FD_GM], o[FD_GM][8];
+    // ---- q heads as the MFMA A operand: head h in row 4h (the other rows zero), so that the
+    // accumulator's first register holds S[head qq][position l16] in every lane
+    const int qh = l16 >> 2;
+    const bool qrow = (l16 & 3) == 0 && qh < g;
+    typename F::f qa[NKS];
 #pragma unroll
-    for (int h = 0; h < FD_GM; ++h) {
-        m_run[h] = -INFINITY;
-        l_run[h] = 0.f;
+    for (int ks = 0; ks < NKS; ++ks) {
+        float qv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qv[e] = qrow ? q_s[qh][32 * ks + 8 * qq + e] : 0.f;
+        qa[ks] = frag_f32<T>(qv);
+    }
+    // ---- passes: S = Q K^T of the wave's 16 positions on one MFMA chain (lane (l16, qq): head qq,
+    // position l16), online softmax per head = per 16-lane row (DPP), P through the wave's LDS rows,
+    // P V on the VALU in fp32 (lane: positions 4 it + qq, dims vd, every head)
+    __shared__ __attribute__((aligned(16))) float p_s[NW][16][FD_GM];
+    float m_run = -INFINITY, l_run = 0.f, o[FD_GM][8];
+#pragma unroll
+    for (int h = 0; h < FD_GM; ++h)
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[h][e] = 0.f;
-    }
     const int npass = (jend - j0 + FD_TILE - 1) / FD_TILE;
     for (int pa = 0; pa < npass; ++pa) {
         const int jb = j0 + pa * FD_TILE;
-        float kf[QD], vf[4][8];
+        const int jk = jb + 16 * wave + l16;
+        if (owner && jk == pos) {  // the new row from LDS, not the cache row loaded before it was written
 #pragma unroll
-        for (int c = 0; c < KL; ++c) {
-            float t[16 / sizeof(T)];
-            cvt16<T>(kb[c], t);
-#pragma unroll
-            for (int u = 0; u < (int)(16 / sizeof(T)); ++u) kf[c * (16 / sizeof(T)) + u] = t[u];
+            for (int ks = 0; ks < NKS; ++ks) kb[ks] = frag_f32<T>(&kv_new[0][32 * ks + 8 * qq]);
         }
+        f32x4_t sc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) sc = F::mma(qa[ks], kb[ks], sc);
+        float vf[4][8];
 #pragma unroll
         for (int it = 0; it < 4; ++it)
 #pragma unroll
@@ -717,69 +757,68 @@ __global__ __launch_bounds__(NW * 64) void attn_fd_kernel(AttnDecArgs<T> a) {
 #pragma unroll
                 for (int u = 0; u < (int)(16 / sizeof(T)); ++u) vf[it][c * (16 / sizeof(T)) + u] = t[u];
             }
-        issue(jb + FD_TILE);  // next pass (clamped: the last pass re-loads rows it already has)
-        const int jk = jb + 16 * wave + l16;
-        const bool kval = jk < jend;
-        if (owner) {  // the new row from LDS, not the cache row loaded before it was written
-            if (min(jk, jend - 1) == pos)
-#pragma unroll
-                for (int c = 0; c < QD; ++c) kf[c] = kv_new[0][qq * QD + c];
+        // next pass; none after the last (the fold's barrier would wait for loads nobody reads)
+        if (pa + 1 < npass) issue(jb + FD_TILE);
+        if (owner) {
 #pragma unroll
             for (int it = 0; it < 4; ++it)
                 if (min(jb + 16 * wave + 4 * it + qq, jend - 1) == pos)
 #pragma unroll
                     for (int e = 0; e < 8; ++e) vf[it][e] = kv_new[1][vd + e];
         }
+        const bool kval = jk < jend && qq < g;
+        {
+            const float sv = kval ? sc[0] * a.scale : -INFINITY;
+            const float mnew = fmaxf(m_run, row_max16(sv));
+            const float alpha = mnew == -INFINITY ? 1.f : expf(m_run - mnew);
+            const float p = kval ? expf(sv - mnew) : 0.f;
+            m_run = mnew;
+            l_run = l_run * alpha + p;
+            p_s[wave][l16][qq] = p;
 #pragma unroll
-        for (int h = 0; h < FD_GM; ++h) {
-            if (h >= g) break;
-            float d = 0.f;
+            for (int h = 0; h < FD_GM; ++h) {
+                if (h >= g) break;
+                const float ah = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(alpha), 16 * h));
 #pragma unroll
-            for (int c = 0; c < QD; ++c) d += q_s[h][qq * QD + c] * kf[c];
-            d += __shfl_xor(d, 16);
-            d += __shfl_xor(d, 32);
-            const float s = kval ? d * a.scale : -INFINITY;
-            const float mx = row_max16(s);
-            const float mnew = fmaxf(m_run[h], mx);
-            const float alpha = mnew == -INFINITY ? 1.f : expf(m_run[h] - mnew);
-            const float p = kval ? expf(s - mnew) : 0.f;
-            m_run[h] = mnew;
-            l_run[h] = l_run[h] * alpha + p;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[h][e] *= alpha;
-#pragma unroll
-            for (int it = 0; it < 4; ++it) {
-                const float pv = __shfl(p, 4 * it + qq);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) o[h][e] += pv * vf[it][e];
+                for (int e = 0; e < 8; ++e) o[h][e] *= ah;
             }
         }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const f32x4_t pv = *reinterpret_cast<const f32x4_t*>(&p_s[wave][4 * it + qq][0]);
+#pragma unroll
+            for (int h = 0; h < FD_GM; ++h) {
+                if (h >= g) break;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[h][e] += pv[h] * vf[it][e];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // p_s is rewritten by the next pass
     }
     DBG_TS(tz, 2)
     // ---- fold the block's waves: PV partials of the 4 V position groups through LDS (no
     // cross-row shuffles), (max, sum) per wave and head
+    const float lrow = row_sum16(l_run);  // row qq: head qq's sum
+    if (l16 == 0 && qq < g) {
+        wml[wave][qq][0] = m_run;
+        wml[wave][qq][1] = lrow;
+    }
 #pragma unroll
     for (int h = 0; h < FD_GM; ++h) {
         if (h >= g) break;
-        const float l = row_sum16(l_run[h]);
         if constexpr (OG == 1) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                o[h][e] += __shfl_xor(o[h][e], 16);
-                o[h][e] += __shfl_xor(o[h][e], 32);
-            }
+            for (int e = 0; e < 8; ++e) o[h][e] = sum_rows4(o[h][e], lane);
         }
         if (8 * l16 < HD && (OG == 4 || qq == 0)) {
             f32x4_t* dst = reinterpret_cast<f32x4_t*>(&ored[wave][OG == 4 ? qq : 0][h][8 * l16]);
             dst[0] = (f32x4_t){o[h][0], o[h][1], o[h][2], o[h][3]};
             dst[1] = (f32x4_t){o[h][4], o[h][5], o[h][6], o[h][7]};
         }
-        if (lane == 0) {
-            wml[wave][h][0] = m_run[h];
-            wml[wave][h][1] = l;
-        }
     }
-    __syncthreads();
+    DBG_TS(tz, 5)
+    lds_barrier();  // ored / wml (the owner's K / V row stores need not have landed)
     DBG_TS(tz, 3)
     const bool single = nsp == 1;
     for (int idx = threadIdx.x; idx < g * HD; idx += NT) {

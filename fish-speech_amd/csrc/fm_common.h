@@ -74,6 +74,10 @@ template <typename T> __device__ __forceinline__ void store8(T* p, const float (
     }
 }
 
+// workgroup barrier for LDS hand-offs only: unlike __syncthreads() it does not make the wave
+// wait for its outstanding global loads and stores (the release fence's vmcnt(0))
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // developer phase timestamps: one 8-word record {tag << 32 | aux, t0..t6} per call
 __device__ __forceinline__ void dbg_record(unsigned long long* dbg, unsigned tag, unsigned aux,
                                            const unsigned long long (&t)[7]) {

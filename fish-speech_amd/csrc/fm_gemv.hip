@@ -172,6 +172,40 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
             res_pre = ld(a.res + (size_t)ri * a.ldr, nn);
     };
     if constexpr (EPI == EPI_SLABFIN && !CH) load_res();
+    // KV prefetch (GemvArgs::pf_kc): slot and pos go out with the prologue's round trip, the sector
+    // loads after the weight ring (the ring never waits on them; in-order vmcnt retires them before
+    // the ring's refills).  GEMV_PF 4-byte loads per thread, one per 64-B sector, unconditional and
+    // clamped to a valid address when off (a load under a branch drains vmcnt before the MFMAs).
+    constexpr bool PFOK = !CH && !Q8 && (PRO == PRO_NORM || PRO == PRO_PRENORM) && EPI == EPI_STORE;
+    constexpr int GEMV_PF = 2;
+    int pf_s = 0, pf_p = 0;
+    if constexpr (PFOK) {
+        const int32_t* ps = a.pf_kc ? a.pf_slot : reinterpret_cast<const int32_t*>(a.X);
+        const int32_t* pq = a.pf_kc ? a.pf_pos : reinterpret_cast<const int32_t*>(a.X);
+        pf_s = ps[0];
+        pf_p = pq[0];
+    }
+    float pfw[GEMV_PF];
+    auto pf_issue = [&]() {
+        if constexpr (PFOK) {
+            const bool on = a.pf_kc != nullptr;
+            const int nkv = on ? a.pf_nkv : 1;
+            const int h = bxi % nkv, j = bxi / nkv, nb = ((int)gridDim.x - 1 - h) / nkv + 1;
+            const int spr = on ? a.pf_hd * (int)sizeof(T) / 64 : 1;  // 64-B sectors per cached row
+            const int np = on ? pf_p + 1 : 0;
+            const int total = 2 * np * spr;                            // K rows, then V rows
+            const size_t base = on ? (size_t)pf_s * a.pf_slot_stride + a.pf_layer_off + (size_t)h * a.pf_S * a.pf_hd : 0;
+#pragma unroll
+            for (int q = 0; q < GEMV_PF; ++q) {
+                const int i = (j + nb * q) * (WPB * 64) + (int)threadIdx.x;
+                const bool ok = i < total;
+                const int ii = ok ? i : 0, row = ii / spr, sec = ii - row * spr;
+                const bool isv = row >= np;
+                const T* src = ok ? (isv ? a.pf_vc : a.pf_kc) + base + (size_t)(isv ? row - np : row) * a.pf_hd : a.X;
+                pfw[q] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(src) + (ok ? sec * 64 : 0));
+            }
+        }
+    };
     unsigned long long tsA = 0, tsB = 0;  // PRO_PRENORM: tile sums staged / X' written
     const int r = lane & 15, g = lane >> 4;
     constexpr int KU = Q8 ? 64 : 32;  // k per ring slot
@@ -251,6 +285,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) issue(u, u);
+        pf_issue();
     } else if constexpr (PRO == PRO_FATT) {
         // One row (host).  Round trip 1: slot, the raw q|k|v row, qk-norm weights, RoPE row; then
         // the weight ring; round trip 2: the cpos cached K/V rows of every kv head (they need the
@@ -360,6 +395,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
         if constexpr (!CH) {
 #pragma unroll
             for (int u = 0; u < U; ++u) issue(u, u);
+            pf_issue();
         }
         if constexpr (PRO == PRO_PRENORM) {
             // stage the tile sums in `red` (free until the cross-wave reduction), then every wave
@@ -446,6 +482,10 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
             }
             issue(i + u + U, u);
         }
+    }
+    if constexpr (PFOK) {  // keep the prefetch loads (long retired: the ring's refills were issued after them)
+#pragma unroll
+        for (int q = 0; q < GEMV_PF; ++q) asm volatile("" ::"v"(pfw[q]));
     }
     // weight-only int8 output: round(round(acc) * scale of the packed row)
     auto wsc = [&](float v, int prow) {

@@ -196,6 +196,16 @@ template <typename T> struct GemvArgs {
     // each output is round(round(acc) * wscale[packed row]) (WeightOnlyInt8Linear, quantize.py:228-229)
     const unsigned char* Wq;
     const T* wscale;
+    // optional KV prefetch (batch-1 QKV GEMV, fm_tune kv_prefetch): while the weights stream, the
+    // cached K / V rows the next attention launch reads (positions 0 .. pos of row 0's slot) are
+    // pulled into L2: block b loads kv head b % pf_nkv, which under round-robin workgroup placement
+    // is the XCD that attention block (kv head h = XCD h) runs on.  Speed only, never correctness.
+    const T* pf_kc;          // null: off
+    const T* pf_vc;
+    const int32_t* pf_slot;  // row 0's slot / position (device, as the attention reads them)
+    const int32_t* pf_pos;
+    size_t pf_slot_stride, pf_layer_off;
+    int pf_S, pf_nkv, pf_hd;
 };
 // developer knobs for the decode GEMV (fm_tune): weight load policy and split-K policy
 struct FmTuning {
@@ -215,6 +225,7 @@ struct FmTuning {
     int fd_min = 32;         // attn_fd: minimum positions per split at R <= 8
     int fd_min_batched = 512;  // attn_fd: minimum positions per split at R > 8 (B=32: one split below 512)
     int fd_nw = 8;           // attn_fd at R <= 8: waves per block (4, 8 or 16) ...
+    int fd_nw_batched = 4;   // attn_fd at R > 8: waves per block (4, 8 or 16)
     int fd_min16 = 256;      // ... and splits of at least this many positions (8 or 16 waves; below it
                              // one block per kv head, no cross-block combine)
     int prefill_attn = 1;    // 1: prompt-chunk attention on attn_prefill_kernel (bf16, head_dim 128, flash form)
@@ -224,6 +235,7 @@ struct FmTuning {
     int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)
     int bstream_kparts = 0;  // bstream EPI_SLAB K parts (0: by K)
     int bstream_nw = 0;      // bstream waves per block (0: 16 whole-K, 8 split-K)
+    int kv_prefetch = 1;     // 1: the batch-1 QKV GEMV pulls the next attention's K / V rows into L2
     int bstream_chain = 0;   // 1: bsacc SLABFIN / PRENORM chain instead of finalize_norm launches (measured 6.31 -> 6.75 ms per B=32 frame)
     int bstream_acc = 1;     // 1: bsacc_kernel (per-tile register accumulators, one reduction at the end, balanced K parts); 0: bstream_kernel
     int rmsnorm_block = 0;   // 1: block-per-row RMSNorm (the pre-vectorisation kernel), 0: wave-per-row when shapes allow

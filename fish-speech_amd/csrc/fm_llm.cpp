@@ -330,6 +330,8 @@ template <typename T> struct Run {
             if (R <= GEMV_MAX_ROWS && fm_tuning().fd_nw > 4) {
                 b.nwb = fm_tuning().fd_nw;
                 b.cap = std::max(16, fm_tuning().fd_min16);
+            } else if (R > GEMV_MAX_ROWS && fm_tuning().fd_nw_batched > 4) {
+                b.nwb = fm_tuning().fd_nw_batched;
             }
             launch_attn_fd<T>(s, b, R);
         } else if (fm_tuning().attn3 && R > GEMV_MAX_ROWS && aa.hd % 32 == 0 && aa.hd <= 128 && aa.nh / aa.nkv <= 6)
@@ -465,7 +467,9 @@ template <typename T> struct Run {
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
             hipStream_t st = s;
-            run_rec("attn", [st, aa, R] { attn_slow_on(st, aa, R); });
+            auto go = [st, aa, R] { attn_slow_on(st, aa, R); };
+            m->prof.record("attn_slow", 0, go);  // the slow model's launches alone (fm_llm_kernel_bench)
+            run_rec("attn", go);
         } else if (is_fast && fm_tuning().batched_fused_attn && fixed_pos >= 0 && fixed_pos < 16 && d.hd <= 256) {
             FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), rslot, d.nh, d.nkv, d.hd, d.qk_norm, eps,
                                 (const T*)L.qn, (const T*)L.kn, rope, (T*)kc, (T*)vc, sstride, loff, Sc,
@@ -693,6 +697,17 @@ template <typename T> struct Run {
             a.K = d.dim;
             a.Y = (T*)m->qkv;
             a.ldy = d.nqkv();
+            if (!is_fast && n == 1 && fm_tuning().kv_prefetch) {  // the attention's K / V rows into L2
+                a.pf_kc = (const T*)m->kc;
+                a.pf_vc = (const T*)m->vc;
+                a.pf_slot = m->frame_slot;
+                a.pf_pos = m->frame_pos;
+                a.pf_slot_stride = m->slot_stride;
+                a.pf_layer_off = (size_t)layer * m->layer_stride;
+                a.pf_S = m->S;
+                a.pf_nkv = d.nkv;
+                a.pf_hd = d.hd;
+            }
             const int epi = EPI_STORE;
             if (first) {
                 a.X = (const T*)x_in;
@@ -721,7 +736,9 @@ template <typename T> struct Run {
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
             hipStream_t st = s;
-            run_rec("attn", [st, aa, n] { attn_slow_on(st, aa, n); });
+            auto go = [st, aa, n] { attn_slow_on(st, aa, n); };
+            m->prof.record("attn_slow", 0, go);  // the slow model's launches alone (fm_llm_kernel_bench)
+            run_rec("attn", go);
         } else if (!att_wo) {
             hipStream_t st = s;
             const bool f2 = cpos < 16 && d.hd <= 256;
@@ -2016,12 +2033,17 @@ int fm_tune(const char* key, int value) {
         } else if (k == "fd_nw") {
             FMCHECK(value == 4 || value == 8 || value == 16, "fd_nw must be 4, 8 or 16");
             t.fd_nw = value;
+        } else if (k == "fd_nw_batched") {
+            FMCHECK(value == 4 || value == 8 || value == 16, "fd_nw_batched must be 4, 8 or 16");
+            t.fd_nw_batched = value;
         } else if (k == "fd_min16") {
             FMCHECK(value >= 16 && value % 16 == 0, "fd_min16 must be a multiple of 16");
             t.fd_min16 = value;
         } else if (k == "fd_min_batched") {
             FMCHECK(value >= 16 && value % 16 == 0, "fd_min_batched must be a multiple of 16");
             t.fd_min_batched = value;
+        } else if (k == "kv_prefetch") {
+            t.kv_prefetch = value != 0;
         } else if (k == "bstream") {
             t.bstream = value != 0;
         } else if (k == "bstream_kparts") {
