@@ -225,6 +225,7 @@ struct FmTuning {
     int fd_min = 32;         // attn_fd: minimum positions per split at R <= 8
     int fd_min_batched = 512;  // attn_fd: minimum positions per split at R > 8 (B=32: one split below 512)
     int fd_nw = 8;           // attn_fd at R <= 8: waves per block (4, 8 or 16) ...
+    int fin_ksb = 0;         // batch-1 wo / w2 (EPI_SLABFIN) split-K factor (0: whole K whenever the x slice fits LDS)
     int fd_nw_batched = 4;   // attn_fd at R > 8: waves per block (4, 8 or 16)
     int fd_min16 = 256;      // ... and splits of at least this many positions (8 or 16 waves; below it
                              // one block per kv head, no cross-block combine)

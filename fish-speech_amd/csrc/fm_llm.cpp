@@ -661,6 +661,8 @@ template <typename T> struct Run {
     // cross-block hand-off) whenever the x slice fits the LDS budget, else split K
     KsbPlan plan(const StackDims& d, int n) {
         auto fin_ksb = [&](int N, int K) {
+            const int fk = fm_tuning().fin_ksb;  // developer override (split-K factor)
+            if (fk > 0 && K % (32 * fk) == 0) return fk;
             // (splitting K further to fill more CUs measured slower at B = 1: 4.37 -> 4.74 ms per
             // frame at 320 blocks, the split-K hand-off costs more than the idle CUs)
             return gemv_lds_bytes(n, K, E) <= 120 * 1024 ? 1 : pick_ksb(N, K, n, E);
@@ -2033,6 +2035,9 @@ int fm_tune(const char* key, int value) {
         } else if (k == "fd_nw") {
             FMCHECK(value == 4 || value == 8 || value == 16, "fd_nw must be 4, 8 or 16");
             t.fd_nw = value;
+        } else if (k == "fin_ksb") {
+            FMCHECK(value >= 0 && value <= KSB_MAX, "fin_ksb must be in [0, KSB_MAX]");
+            t.fin_ksb = value;
         } else if (k == "fd_nw_batched") {
             FMCHECK(value == 4 || value == 8 || value == 16, "fd_nw_batched must be 4, 8 or 16");
             t.fd_nw_batched = value;

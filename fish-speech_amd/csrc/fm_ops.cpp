@@ -7,7 +7,7 @@
 //                   statistic from the producing GEMV's per-tile sums of squares), or the
 //                   standalone row kernel of the batched / prefill path
 //   fm_op_qk_rope   QK-norm (llama.py:861-863) + RoPE with the bf16 table (llama.py:1003-1037)
-//                   inside the fused decode attention kernels (slow attn_decode2, fast attn2)
+//                   inside the fused decode attention kernels (slow attn_fd / attn_decode2, fast attn2)
 //   fm_op_decode_attn  the whole slow decode attention (QK-norm, RoPE, KV write, scaled dot-product
 //                   attention over the cache, llama.py:883-945) on R rows with caller K/V caches
 //   fm_op_prompt_attn  the prompt-chunk causal attention (llama.py:883-946) over a cache prefix,
@@ -173,7 +173,7 @@ void qk_rope_t(hipStream_t s, int kernel, const float* qkv, int nh, int nkv, int
     const int rs[2] = {0, pos};
     b.put(row, rs, 8);
     const float scale = 1.0f / sqrtf((float)hd);
-    if (kernel == 0 || kernel == 2) {  // slow decode attention
+    if (kernel == 0 || kernel == 2 || kernel == 3) {  // slow decode attention
         AttnDecArgs<T> a{raw, ld, row, row + 1, nh, nkv, hd, qk_norm, eps, qnd, knd, rope, kc, vc, stride, 0, S,
                          1, scale, nullptr};
         a.cap = attn2_cap(hd, nh / nkv, sizeof(T));
@@ -185,6 +185,12 @@ void qk_rope_t(hipStream_t s, int kernel, const float* qkv, int nh, int nkv, int
         // kernel 0: attn_decode2 (the B <= 8 decode path), 2: attn_dec3 (the batched frame)
         if (kernel == 2) {
             launch_attn_decode3<T>(s, a, 1);
+        } else if (kernel == 3) {  // attn_fd as the batch-1 decode runs it (8-wave blocks)
+            FMCHECK(attn_fd_ok(hd, nh / nkv), "attn_fd: head_dim 32, 64 or 128, at most 4 q heads per kv head");
+            a.cap = std::max(16, fm_tuning().fd_min16);
+            a.nwb = fm_tuning().fd_nw;
+            a.maxsplit = FM_CEIL(S, a.cap);
+            launch_attn_fd<T>(s, a, 1);
         } else {
             a.maxsplit = FM_CEIL(S, a.cap);
             launch_attn_decode2<T>(s, a, 1);
@@ -356,7 +362,8 @@ int fm_op_qk_rope(int device, int precision, int kernel, const float* qkv, int n
     return fm_guard([&] {
         FMCHECK(qkv && q_out && k_out, "null argument");
         FMCHECK(!qk_norm || (qn && kn), "qk_norm needs both norm weights");
-        FMCHECK(kernel >= 0 && kernel <= 2, "kernel must be 0 (slow attn_decode2), 1 (fast attn2) or 2 (slow attn_dec3)");
+        FMCHECK(kernel >= 0 && kernel <= 3,
+                "kernel must be 0 (slow attn_decode2), 1 (fast attn2), 2 (slow attn_dec3) or 3 (slow attn_fd)");
         FMCHECK(nh >= 1 && nkv >= 1 && nh % nkv == 0 && nh / nkv <= 16, "bad head counts");
         FMCHECK(hd >= 8 && hd <= 256 && hd % 8 == 0, "bad head_dim");
         FMCHECK(pos >= 0 && pos < 65536, "bad position");

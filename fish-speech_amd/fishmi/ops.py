@@ -34,8 +34,8 @@ def rmsnorm(x, w, eps, precision="bf16", mode="prologue_prenorm", device=0):
 def qk_rope(qkv_row, nh, nkv, hd, pos, rope_base, qn=None, kn=None, eps=1e-6, precision="bf16",
             kernel="slow", device=0):
     """q (nh, hd) and k (nkv, hd) after qk-norm (if weights given) and RoPE at `pos`, as computed
-    inside a decode attention kernel: "slow" attn_decode2 (B <= 8), "slow3" attn_dec3 (batched
-    frames), "fast" fast_attn2."""
+    inside a decode attention kernel: "fd" attn_fd (the slow model's production kernel), "slow"
+    attn_decode2, "slow3" attn_dec3, "fast" fast_attn2."""
     raw = np.ascontiguousarray(qkv_row, np.float32).reshape(-1)
     assert raw.size == (nh + 2 * nkv) * hd
     qk = qn is not None
@@ -43,7 +43,7 @@ def qk_rope(qkv_row, nh, nkv, hd, pos, rope_base, qn=None, kn=None, eps=1e-6, pr
     kn_ = np.ascontiguousarray(kn if qk else np.ones(hd), np.float32)
     q = np.zeros(nh * hd, np.float32)
     k = np.zeros(nkv * hd, np.float32)
-    kid = {"slow": 0, "fast": 1, "slow3": 2}[kernel]  # attn_decode2 / fast_attn2 / attn_dec3
+    kid = {"slow": 0, "fast": 1, "slow3": 2, "fd": 3}[kernel]  # attn_decode2 / fast_attn2 / attn_dec3 / attn_fd
     native.check(native.lib().fm_op_qk_rope(device, _prec(precision), kid,
                                             native.f32p(raw), nh, nkv, hd, native.f32p(qn_), native.f32p(kn_),
                                             int(qk), float(eps), float(rope_base), int(pos), native.f32p(q),

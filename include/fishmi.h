@@ -172,8 +172,10 @@ int fm_llm_force(fm_llm* h, int slot, const int32_t* col);
 int fm_llm_read_logits(fm_llm* h, int slot, float* slow_logits, float* fast_logits);
 /* process-wide developer knobs selecting kernel variants (every variant stays under the default
    path's parity bar, tests/test_gpu_knobs.py): decode GEMV "gemv_nt" 0|1, "gemv_u" 2|4|8,
-   "gemv_wpb" 4|8, "ksb_blocks" n, "ksb_balance" 0|1; attention "attn_fd" 0|1, "attn3" 0|1,
-   "attn_cap" n, "attn_cap_batched" n, "fd_min" n, "fd_min_batched" n, "fd_nw" 4|8|16, "fd_min16" n, "attn_wo" 0|1,
+   "gemv_wpb" 4|8, "ksb_blocks" n, "ksb_balance" 0|1, "fin_ksb" n, "kv_prefetch" 0|1, "gemv_chain" 0|1,
+   "chain_max" 2..4, "chain_sleep" 1|4|16; attention "attn_fd" 0|1, "attn3" 0|1,
+   "attn_cap" n, "attn_cap_batched" n, "fd_min" n, "fd_min_batched" n, "fd_nw" 4|8|16, "fd_min16" n,
+   "fd_nw_batched" 4|8|16, "attn_wo" 0|1,
    "batched_fused_attn" 0|1; batched linears "bstream" 0|1, "bstream_acc" 0|1, "bstream_chain" 0|1, "bstream_kparts" n, "bstream_nw" n,
    "linear_u32" n, "linear_fill" n; prompt "prefill_attn", "prompt_gemm"; codec "conv2",
    "conv_splitk"; "sampler_fast" 0|1, "rmsnorm_block" 0|1, "debug_ts" n.  They apply to launches
@@ -195,7 +197,8 @@ int fm_llm_close(fm_llm* h);
 int fm_op_rmsnorm(int device, int precision, int mode, const float* x, const float* w, int R, int d,
                   float eps, float* y);
 /* QK-norm (llama.py:861-863) + RoPE with the bf16 table (llama.py:1003-1037) at position pos, as the
-   fused decode attention computes them: kernel 0 = slow attn_decode2, 1 = fast-model attention.
+   fused decode attention computes them: kernel 0 = slow attn_decode2, 1 = fast-model attention,
+   2 = slow attn_dec3, 3 = slow attn_fd (the production kernel).
    qkv: one raw projection row [(nh + 2 nkv) * hd]; q_out [nh * hd], k_out [nkv * hd] (the k row as
    written to the KV cache). */
 int fm_op_qk_rope(int device, int precision, int kernel, const float* qkv, int nh, int nkv, int hd,

@@ -5,7 +5,8 @@ fm_op_* hooks of the C ABI (each runs ONE production kernel on the given operand
   * RMSNorm (llama.py:989-1000): the decode GEMV prologue (statistic from the row; statistic from
     the producer's per-tile sums of squares) and the standalone row kernel;
   * QK-norm (llama.py:861-863) and RoPE with the bf16 table (llama.py:1003-1037) inside the slow
-    (attn_decode2) and fast (fast_attn2) decode attention kernels, q and the cached k;
+    (attn_fd, the production kernel; attn_decode2 / attn_dec3) and fast (fast_attn2) decode
+    attention kernels, q and the cached k;
   * the Dual-AR input embedding (llama.py:399-420).
 
 Bounds: bf16 within 1 bf16 ulp per element (measured: 100% bit-exact).  fp32
@@ -54,7 +55,7 @@ def test_rmsnorm(mode, precision, golden):
     _check(y, ref, precision)
 
 
-@pytest.mark.parametrize("kernel", ["slow", "slow3", "fast"])
+@pytest.mark.parametrize("kernel", ["fd", "slow", "slow3", "fast"])
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_qk_norm(kernel, precision, golden):
     """qk-norm alone: position 0 (RoPE is the identity there), every head of ops.npz's q fed both
@@ -71,7 +72,7 @@ def test_qk_norm(kernel, precision, golden):
             _check(k, ref[i, j], precision)
 
 
-@pytest.mark.parametrize("kernel", ["slow", "slow3", "fast"])
+@pytest.mark.parametrize("kernel", ["fd", "slow", "slow3", "fast"])
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_rope(kernel, precision, golden):
     """RoPE with the bf16 cos/sin table at the golden positions (the fast model's kernel only covers
