@@ -145,6 +145,17 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
     for (int i = 0; i < nw; ++i) t += scratch[i];
     return t;
 }
+// block_sum over LDS-only barriers: the waves do not wait for their outstanding global loads
+__device__ __forceinline__ float block_sum_lds(float v, float* scratch) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    v = wave_sum(v);
+    lds_barrier();
+    if (lane == 0) scratch[w] = v;
+    lds_barrier();
+    float t = 0.f;
+    for (int i = 0; i < nw; ++i) t += scratch[i];
+    return t;
+}
 __device__ __forceinline__ float block_max(float v, float* scratch) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
     v = wave_max(v);

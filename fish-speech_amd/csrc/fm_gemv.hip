@@ -238,8 +238,11 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
     // BEFORE the weight ring is issued, so the in-order vmcnt waits of the staging below do not
     // queue behind weight bytes.
     if constexpr (PRO == PRO_NORM) {
-        // full-row statistic from the row itself (first layer: embeddings / gathered rows); the
-        // weight ring starts after it (its block reductions would otherwise wait on weights)
+        // full-row statistic from the row itself (first layer: embeddings / gathered rows).  The
+        // weight ring goes out first: the statistic's block reductions use LDS-only barriers, so
+        // they do not wait for it
+#pragma unroll
+        for (int u = 0; u < U; ++u) issue(u, u);
         __shared__ float red_s[16];
         const int nch = a.K >> 3;
         const bool writer = (bxi == 0 && ks == 0);
@@ -260,7 +263,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
                     for (int u = 0; u < 8; ++u) ss += xv[j][u] * xv[j][u];
                 }
             }
-            ss = block_sum(ss, red_s);
+            ss = block_sum_lds(ss, red_s);
             const float rs = 1.0f / sqrtf(ss / (float)a.K + a.eps);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -281,10 +284,8 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
                     for (int u = 0; u < 8; ++u) st(a.xn_out, (size_t)rr * a.ldxo + k + u, xn[u]);
                 }
             }
-            __syncthreads();
+            lds_barrier();  // red_s is reused by the next row
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) issue(u, u);
         pf_issue();
     } else if constexpr (PRO == PRO_FATT) {
         // One row (host).  Round trip 1: slot, the raw q|k|v row, qk-norm weights, RoPE row; then
@@ -459,7 +460,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
             }
         }
     }
-    __syncthreads();
+    lds_barrier();  // X' staged; the weight ring stays in flight (each MFMA waits for its own fragment)
 
     const unsigned long long ts1 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     // ---------------- main loop: ring of U fragments per wave ------------------------------------
