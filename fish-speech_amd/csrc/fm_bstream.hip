@@ -179,7 +179,9 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
     typename F::f fa[U];
     auto issue = [&](int t, int j) {
         const int tt = t < tl ? t : tl, jj = j < jl ? j : jl;
-        fa[(t % TPI) * SPW + j] = F::template load_w<true>(wbase + ((size_t)tt * S + jj) * 512, lane);
+        const bool past = a.dummy_tail && (t > tl || j > jl);  // not this block's: one cached fragment
+        const T* dsrc = a.W + (a.dummy_tail == 2 ? (size_t)((blockIdx.x * 8 + wave) & 255) % ((size_t)T_ * S) * 512 : 0);
+        fa[(t % TPI) * SPW + j] = F::template load_w<true>(past ? dsrc : wbase + ((size_t)tt * S + jj) * 512, lane);
     };
 #pragma unroll
     for (int t = 0; t < TPI; ++t)
@@ -619,6 +621,7 @@ template <typename T> bool launch_bstream(hipStream_t s, const BstreamArgs<T>& a
     if (!p.ok) return false;
     BstreamArgs<T> a = a0;
     a.kparts = p.kparts;
+    a.dummy_tail = fm_tuning().bs_dummy;
     if (p.acc) {
         if constexpr (sizeof(T) == 2) {
             FMCHECK(epi != EPI_SWIGLU8 || a.N % 16 == 0, "bsacc: SwiGLU8 needs whole interleaved tiles");

@@ -214,22 +214,28 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
     typename G::f fa[Q8 ? 1 : U], fb[NACC == 2 ? U : 1];
     u32x4_t fq[Q8 ? U : 1];
     // Fragment i of the run into ring slot u.  Branch-free on purpose: a load under a branch makes
-    // the compiler drain vmcnt(0) before every MFMA (no pipelining at all), so tail slots re-load
-    // the run's last fragment (a cache hit) instead of being predicated off.
+    // the compiler drain vmcnt(0) before every MFMA (no pipelining at all), so tail slots load a
+    // fixed fragment (fm_tune gemv_dummy: one per (block, wave), a cache hit) instead of being
+    // predicated off.
     const int ilast = nmy > 0 ? nmy - 1 : 0;
     const size_t run0 = ((size_t)bxi * S + sb0 + (nmy > 0 ? wa : 0)) * (Q8 ? 1024 : 512);
     const T* wrun = Q8 ? nullptr : a.W + run0;
     const T* wrun2 = (EPI == EPI_SWIGLU) ? a.W2 + run0 : nullptr;
     const unsigned char* qrun = Q8 ? a.Wq + run0 : nullptr;
+    const bool dtail = a.dummy_tail != 0;
+    // dummy_tail 2: the fixed fragment differs per (block, wave) over 256 fragments (no hot line)
+    // (bounded by the matrix's own fragment count: ceil(N / 16) tiles x S k-steps)
+    const size_t dfr = a.dummy_tail == 2 ? (size_t)((bxi * WPB + wave) & 255) % ((size_t)((a.N + 15) >> 4) * S) : 0;
     auto issue = [&](int i, int u) {
         const size_t ii = (size_t)(i < ilast ? i : ilast);
+        const bool past = dtail && i > ilast;  // beyond the run: one fixed (cached) fragment
         if constexpr (Q8) {
-            const u32x4_t* p = reinterpret_cast<const u32x4_t*>(qrun + ii * 1024 + lane * 16);
+            const u32x4_t* p = reinterpret_cast<const u32x4_t*>((past ? a.Wq + dfr * 1024 : qrun + ii * 1024) + lane * 16);
             if constexpr (NT) fq[u] = __builtin_nontemporal_load(p);
             else fq[u] = *p;
         } else {
-            fa[u] = G::template load_w<NT>(wrun + ii * 512, lane);
-            if constexpr (NACC == 2) fb[u] = G::template load_w<NT>(wrun2 + ii * 512, lane);
+            fa[u] = G::template load_w<NT>(past ? a.W + dfr * 512 : wrun + ii * 512, lane);
+            if constexpr (NACC == 2) fb[u] = G::template load_w<NT>(past ? a.W + dfr * 512 : wrun2 + ii * 512, lane);
         }
     };
 

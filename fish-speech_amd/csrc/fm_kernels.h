@@ -206,6 +206,7 @@ template <typename T> struct GemvArgs {
     const int32_t* pf_pos;
     size_t pf_slot_stride, pf_layer_off;
     int pf_S, pf_nkv, pf_hd;
+    int dummy_tail;  // ring slots past the wave's run load one fixed fragment (else the run's last)
 };
 // developer knobs for the decode GEMV (fm_tune): weight load policy and split-K policy
 struct FmTuning {
@@ -236,6 +237,11 @@ struct FmTuning {
     int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)
     int bstream_kparts = 0;  // bstream EPI_SLAB K parts (0: by K)
     int bstream_nw = 0;      // bstream waves per block (0: 16 whole-K, 8 split-K)
+    // ring slots past a wave's run (tail of the decode GEMV ring, bsacc tiles / steps a block does
+    // not own): 0 re-load the run's last fragment, 1 one fixed fragment, 2 a fixed fragment per
+    // (block, wave) over 256 of them.  B=1 frame 4.447 / 4.47 / 4.398 ms, B=32 6.51 / 6.44 / 6.42 ms
+    int bs_dummy = 2;
+    int gemv_dummy = 2;
     int kv_prefetch = 1;     // 1: the batch-1 QKV GEMV pulls the next attention's K / V rows into L2
     int bstream_chain = 0;   // 1: bsacc SLABFIN / PRENORM chain instead of finalize_norm launches (measured 6.31 -> 6.75 ms per B=32 frame)
     int bstream_acc = 1;     // 1: bsacc_kernel (per-tile register accumulators, one reduction at the end, balanced K parts); 0: bstream_kernel
@@ -304,6 +310,7 @@ template <typename T> struct BstreamArgs {
     int ldro = 0;
     float* ss_out = nullptr;
     int* tickets = nullptr;
+    int dummy_tail = 0;  // bsacc: ring slots past the block's tiles / steps load one cached fragment
 };
 struct BstreamPlan {
     bool ok = false;

@@ -563,6 +563,7 @@ template <typename T> struct Run {
     GemvArgs<T> ga() {
         GemvArgs<T> a{};
         a.eps = m->c.norm_eps;
+        a.dummy_tail = fm_tuning().gemv_dummy;
         return a;
     }
     // ---- batch-1 GEMV chain: consecutive GEMVs of one row are deferred and launched together
@@ -2047,6 +2048,12 @@ int fm_tune(const char* key, int value) {
         } else if (k == "fd_min_batched") {
             FMCHECK(value >= 16 && value % 16 == 0, "fd_min_batched must be a multiple of 16");
             t.fd_min_batched = value;
+        } else if (k == "gemv_dummy") {
+            FMCHECK(value >= 0 && value <= 2, "gemv_dummy must be 0, 1 or 2");
+            t.gemv_dummy = value;
+        } else if (k == "bs_dummy") {
+            FMCHECK(value >= 0 && value <= 2, "bs_dummy must be 0, 1 or 2");
+            t.bs_dummy = value;
         } else if (k == "kv_prefetch") {
             t.kv_prefetch = value != 0;
         } else if (k == "bstream") {

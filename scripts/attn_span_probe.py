@@ -51,7 +51,9 @@ for rep in range(2):
         m.decode_frames([0], 100)  # positions 124 .. 224 (config 2 averages ~172)
         t1 = time.perf_counter()
         us, n, b = m.kernel_bench("attn", 20)
-        print(f"rep {rep} {v}: graph frame {(t1 - t0) / 100 * 1e3:.3f} ms; attn replay {us:.2f} us x {n}")
+        ul, nl, bl = m.kernel_bench("linear", 20)
+        print(f"rep {rep} {v}: graph frame {(t1 - t0) / 100 * 1e3:.3f} ms; attn replay {us:.2f} us x {n}; "
+              f"linear replay {ul:.2f} us x {nl} ({bl / nl / ul / 1e3:.1f} GB/s)")
 for cls in ("attn", "linear"):
     us, n, b = m.kernel_bench(cls, 20)
     print(f"kernel_bench {cls}: {us:.2f} us per launch, {n} launches per frame, {us * n / 1e3:.3f} ms per frame")
