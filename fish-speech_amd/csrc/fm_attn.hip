@@ -630,7 +630,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fd_kernel(AttnDecArgs<T> a) {
     // loads do not depend on pos and go out with it (clamped, unconditional)
     const int slot = a.row_slot[r];
     const int pos = a.row_pos[r];
-    const T* raw = a.qkv + (size_t)r * a.ldqkv;
     constexpr int NI = (2 + FD_GM + NW - 1) / NW;  // q heads + new k + new v over the waves
     float x0[NI], x1[NI];
 #pragma unroll
@@ -638,8 +637,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fd_kernel(AttnDecArgs<T> a) {
         const int it = wave + NW * i;
         const int row = it < g ? kvh * g + it : (it == g ? a.nh + kvh : a.nh + a.nkv + kvh);
         const bool ok = it < nitem && lane < half;
-        const T* src = raw + (size_t)(it < nitem ? row : 0) * HD + 2 * (lane < half ? lane : 0);
-        const float v0 = ld(src, 0), v1 = ld(src, 1);
+        float v0, v1;
+        raw_pair<T>(a.qkv, a.ldqkv, a.qslab, a.qslab_kp, gridDim.x, a.qbias, r,
+                    (size_t)(it < nitem ? row : 0) * HD + 2 * (lane < half ? lane : 0), v0, v1);
         x0[i] = ok ? v0 : 0.f;
         x1[i] = ok ? v1 : 0.f;
     }

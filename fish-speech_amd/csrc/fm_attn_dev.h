@@ -23,12 +23,33 @@ template <typename T> __device__ __forceinline__ void ld_pair(const T* p, float&
         x1 = ld(p, 1);
     }
 }
+// elements e, e + 1 of raw projection row r: from the T row, or (qslab) round(sum of the kp fp32
+// K-part slabs [kp][R][ld] + bias) -- the one rounding the projection's own epilogue does
+template <typename T>
+__device__ __forceinline__ void raw_pair(const T* qkv, int ldq, const float* qslab, int kp, int R, const T* bias,
+                                         int r, size_t e, float& x0, float& x1) {
+    if (qslab) {
+        const size_t i = (size_t)r * ldq + e, st = (size_t)R * ldq;
+        float a = qslab[i], b = qslab[i + 1];
+        for (int q = 1; q < kp; ++q) {
+            a += qslab[q * st + i];
+            b += qslab[q * st + i + 1];
+        }
+        if (bias) {
+            a += ld(bias, e);
+            b += ld(bias, e + 1);
+        }
+        x0 = rnd<T>(a);
+        x1 = rnd<T>(b);
+    } else {
+        ld_pair<T>(qkv + (size_t)r * ldq + e, x0, x1);
+    }
+}
 
 template <typename T>
 __device__ __forceinline__ void fast_attn_head(const FastFusedArgs<T>& a, int r, int h, int lane,
                                                unsigned long long (&tz)[7]) {
     const int hd = a.hd, g = a.nh / a.nkv, kvh = h / g, cpos = a.cpos, half = hd >> 1;
-    const T* raw = a.qkv + (size_t)r * a.ldqkv;
     const float* tab = a.rope + (size_t)cpos * hd;
     const int slot = a.row_slot[r];
     float q0[2], q1[2], k0[2], k1[2], v0[2], v1[2], qw0[2], qw1[2], kw0[2], kw1[2], c_[2], s_[2];
@@ -37,9 +58,11 @@ __device__ __forceinline__ void fast_attn_head(const FastFusedArgs<T>& a, int r,
         const int p = lane + 64 * u;
         const bool ok = p < half;
         const int pp = ok ? p : 0;
-        ld_pair<T>(raw + (size_t)h * hd + 2 * pp, q0[u], q1[u]);
-        ld_pair<T>(raw + (size_t)(a.nh + kvh) * hd + 2 * pp, k0[u], k1[u]);
-        ld_pair<T>(raw + (size_t)(a.nh + a.nkv + kvh) * hd + 2 * pp, v0[u], v1[u]);
+        raw_pair<T>(a.qkv, a.ldqkv, a.qslab, a.qslab_kp, gridDim.x, a.qbias, r, (size_t)h * hd + 2 * pp, q0[u], q1[u]);
+        raw_pair<T>(a.qkv, a.ldqkv, a.qslab, a.qslab_kp, gridDim.x, a.qbias, r, (size_t)(a.nh + kvh) * hd + 2 * pp,
+                    k0[u], k1[u]);
+        raw_pair<T>(a.qkv, a.ldqkv, a.qslab, a.qslab_kp, gridDim.x, a.qbias, r,
+                    (size_t)(a.nh + a.nkv + kvh) * hd + 2 * pp, v0[u], v1[u]);
         qw0[u] = a.qk_norm ? ld(a.qn, 2 * pp) : 1.f;
         qw1[u] = a.qk_norm ? ld(a.qn, 2 * pp + 1) : 1.f;
         kw0[u] = a.qk_norm ? ld(a.kn, 2 * pp) : 1.f;

@@ -163,6 +163,11 @@ template <typename T> struct FastFusedArgs {
     unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
     float* qdbg = nullptr;    // per-op test hook (fm_op_qk_rope): q after qk-norm + RoPE [R][nh][hd]
     int nwb = 4;              // attn_fd: waves per block (4, 8 or 16; 16 nwb positions per pass)
+    // batched frames (fm_tune bs_qkv_slab): the QKV projection left qslab_kp fp32 K-part slabs
+    // [kp][R][ldqkv] (no bias) instead of qkv; the attention reads round(sum + qbias) itself
+    const float* qslab = nullptr;
+    int qslab_kp = 1;
+    const T* qbias = nullptr;
 };
 template <typename T> struct GemvArgs {
     const T* W;
@@ -242,6 +247,8 @@ struct FmTuning {
     // (block, wave) over 256 of them.  B=1 frame 4.447 / 4.47 / 4.398 ms, B=32 6.51 / 6.44 / 6.42 ms
     int bs_dummy = 2;
     int gemv_dummy = 2;
+    int bs_qkv_slab = 1;     // batched frames: QKV as K-part slabs summed by the attention (balanced
+                             // grid: 384 tiles x 2 K parts over 256 CUs; B=32 frame 6.48 -> 6.33 ms)
     int kv_prefetch = 1;     // 1: the batch-1 QKV GEMV pulls the next attention's K / V rows into L2
     int bstream_chain = 0;   // 1: bsacc SLABFIN / PRENORM chain instead of finalize_norm launches (measured 6.31 -> 6.75 ms per B=32 frame)
     int bstream_acc = 1;     // 1: bsacc_kernel (per-tile register accumulators, one reduction at the end, balanced K parts); 0: bstream_kernel
@@ -361,6 +368,9 @@ template <typename T> struct AttnDecArgs {
     unsigned long long* dbg;  // developer timestamps (fm_tune "debug_ts")
     float* qdbg = nullptr;    // per-op test hook (fm_op_qk_rope): q after qk-norm + RoPE [R][nh][hd]
     int nwb = 4;              // attn_fd: waves per block (4, 8 or 16; 16 nwb positions per pass)
+    const float* qslab = nullptr;  // as FastFusedArgs: K-part slabs of the QKV projection (attn_fd)
+    int qslab_kp = 1;
+    const T* qbias = nullptr;
 };
 // decode attention for the small-batch path (see fm_attn.hip): a.cap rows per block, a.maxsplit =
 // ceil(S / cap) blocks per (row, kv head), output straight to a.out (bf16 / T)

@@ -112,6 +112,7 @@ struct fm_llm {
     long long skpart_cap = 0;             //   floats
     float *slabA = nullptr, *slabB = nullptr;  // split-K partials of wo / w2 (small-batch path)
     float *bsA = nullptr, *bsB = nullptr;      // bstream K-part slabs of wo / w2 (batched path)
+    float* bsQ = nullptr;                      // K-part slabs of the batched QKV (fm_tune bs_qkv_slab)
     // rows / slots
     int *frame_slot = nullptr, *frame_pos = nullptr, *prow_slot = nullptr, *prow_pos = nullptr;
     int32_t *tok_in = nullptr, *cols = nullptr, *ptok = nullptr, *ras = nullptr;
@@ -428,6 +429,8 @@ template <typename T> struct Run {
                int fixed_pos, bool is_fast, void* kc, void* vc, size_t sstride, size_t loff, int Sc,
                const float* rope, void* xb, void* hb, void* xnb) {
         const float eps = m->c.norm_eps;
+        const float* qslab = nullptr;  // the QKV projection's K-part slabs (bs_qkv_slab) instead of m->qkv
+        int qslab_kp = 1;
         const bool bs = bs_use(R, is_fast);
         const bool chain = bs && bs_chain(d, R);
         if (chain && x_ss) {  // QKV normalises x itself (attention_norm from the tile sums)
@@ -440,7 +443,22 @@ template <typename T> struct Run {
                     "bsacc: no PRENORM QKV plan");
         } else if (bs) {
             bs_norm_in(d, L, R, xb, xnb);
-            if (!bs_linear(L.wqkv, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, EPI_STORE))
+            // fm_tune bs_qkv_slab: K-part slabs (a grid of whole rounds: 384 QKV tiles x 2 parts over
+            // 256 CUs) summed + biased + rounded by the fused attention that reads them
+            int kp = 0;
+            // (bsQ holds BS_KPARTS x 32 rows of either stack's width; the plan never exceeds those)
+            // (only where the attention below is one of the fused kernels that read the slabs)
+            const bool fused_fast = is_fast && fixed_pos >= 0 && fixed_pos < 16 && d.hd <= 256;
+            const bool fused_slow = !is_fast && rows_distinct_slots && fm_tuning().attn_fd &&
+                                    attn_fd_ok(d.hd, d.nh / d.nkv);
+            // (weight-only int8 keeps the STORE epilogue: its row scales apply before the rounding)
+            const bool slab_ok = fm_tuning().bs_qkv_slab && fm_tuning().batched_fused_attn && m->bsQ && R <= 32 &&
+                                 (fused_fast || fused_slow) && !m->qinfo(L.wqkv);
+            if (slab_ok && bs_linear(L.wqkv, nullptr, xnb, d.dim, R, d.nqkv(), d.dim, nullptr, d.nqkv(), m->bsQ,
+                                     EPI_SLAB, &kp)) {
+                qslab = m->bsQ;
+                qslab_kp = kp;
+            } else if (!bs_linear(L.wqkv, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, EPI_STORE))
                 linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
                        nullptr, EPI_STORE, "linear");
         } else {
@@ -466,6 +484,10 @@ template <typename T> struct Run {
             aa.cnt = m->attn_cnt;
             aa.dbg = fm_tuning().dbg;
             aa.out = (T*)m->att;
+            aa.qslab = qslab;
+            aa.qslab_kp = qslab_kp;
+            aa.qbias = (const T*)L.bqkv;
+            FMCHECK(!qslab || (fm_tuning().attn_fd && attn_fd_ok(d.hd, d.nh / d.nkv)), "bs_qkv_slab needs attn_fd");
             hipStream_t st = s;
             auto go = [st, aa, R] { attn_slow_on(st, aa, R); };
             m->prof.record("attn_slow", 0, go);  // the slow model's launches alone (fm_llm_kernel_bench)
@@ -475,6 +497,9 @@ template <typename T> struct Run {
                                 (const T*)L.qn, (const T*)L.kn, rope, (T*)kc, (T*)vc, sstride, loff, Sc,
                                 fixed_pos, scale, (T*)m->att};
             fa.dbg = fm_tuning().dbg;
+            fa.qslab = qslab;
+            fa.qslab_kp = qslab_kp;
+            fa.qbias = (const T*)L.bqkv;
             hipStream_t st = s;
             run_rec("attn", [st, fa, R] { launch_fast_attn2<T>(st, fa, R); });
         } else {
@@ -1397,6 +1422,7 @@ static void finalize(fm_llm* m) {
     if (n > GEMV_MAX_ROWS) {  // [BS_KPARTS][32][dmax] fp32 each
         m->bsA = (float*)m->dalloc((size_t)BS_KPARTS * 32 * dmax * 4, false);
         m->bsB = (float*)m->dalloc((size_t)BS_KPARTS * 32 * dmax * 4, false);
+        m->bsQ = (float*)m->dalloc((size_t)BS_KPARTS * 32 * std::max(m->sd.nqkv(), m->fdm.nqkv()) * 4, false);
     }
     m->logits = (float*)m->dalloc((size_t)n * m->Nhead * 4);
     m->flogits = (float*)m->dalloc((size_t)n * m->cb * 4);
@@ -2054,6 +2080,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "bs_dummy") {
             FMCHECK(value >= 0 && value <= 2, "bs_dummy must be 0, 1 or 2");
             t.bs_dummy = value;
+        } else if (k == "bs_qkv_slab") {
+            t.bs_qkv_slab = value != 0;
         } else if (k == "kv_prefetch") {
             t.kv_prefetch = value != 0;
         } else if (k == "bstream") {

@@ -176,7 +176,7 @@ int fm_llm_read_logits(fm_llm* h, int slot, float* slow_logits, float* fast_logi
    "chain_max" 2..4, "chain_sleep" 1|4|16; attention "attn_fd" 0|1, "attn3" 0|1,
    "attn_cap" n, "attn_cap_batched" n, "fd_min" n, "fd_min_batched" n, "fd_nw" 4|8|16, "fd_min16" n,
    "fd_nw_batched" 4|8|16, "attn_wo" 0|1,
-   "batched_fused_attn" 0|1; batched linears "bstream" 0|1, "bstream_acc" 0|1, "bstream_chain" 0|1, "bstream_kparts" n, "bstream_nw" n, "bs_dummy" 0|1|2,
+   "batched_fused_attn" 0|1; batched linears "bstream" 0|1, "bstream_acc" 0|1, "bstream_chain" 0|1, "bstream_kparts" n, "bstream_nw" n, "bs_dummy" 0|1|2, "bs_qkv_slab" 0|1,
    "linear_u32" n, "linear_fill" n; prompt "prefill_attn", "prompt_gemm"; codec "conv2",
    "conv_splitk"; "sampler_fast" 0|1, "rmsnorm_block" 0|1, "debug_ts" n.  They apply to launches
    recorded after the call (graphs captured earlier keep theirs). */

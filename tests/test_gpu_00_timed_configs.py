@@ -74,16 +74,19 @@ def knob():
         native.tune(k, d)
 
 
-@pytest.mark.parametrize("prefill,chain", [("batch", 0), ("single", 0), ("batch", 1)])
-def test_config3_ragged_32_slots_bf16_vs_reference(prefill, chain, golden, knob):
+@pytest.mark.parametrize("prefill,chain,slab", [("batch", 0, 1), ("single", 0, 1), ("batch", 1, 1), ("batch", 0, 0)])
+def test_config3_ragged_32_slots_bf16_vs_reference(prefill, chain, slab, golden, knob):
     """32 distinct prompts (16..256 tokens) in permuted slots: first frame from prefill_batch (the
     serving tick's path) or per-slot prefill, then batched decode frames (bsacc_kernel linears,
     finalize_norm, attn_fd at 32 different positions), every slot teacher-forced with its own
     reference columns.  Pooled over slots, the error is within BF16_RATIO x the reference's.
-    chain = 1: the fm_tune bstream_chain variant (bsacc SLABFIN / PRENORM, no finalize_norm)."""
+    chain = 1: the fm_tune bstream_chain variant (bsacc SLABFIN / PRENORM, no finalize_norm);
+    slab = 0: the QKV projection's own STORE epilogue instead of K-part slabs summed by the attention
+    (fm_tune bs_qkv_slab)."""
     from fishmi.llm import DualARModel
 
     knob("bstream_chain", chain, 0)
+    knob("bs_qkv_slab", slab, 1)
     g = golden("llm_ragged_bf16.npz")
     cfg = _cfg(g)
     B = int(g["lens"].size)

@@ -401,7 +401,8 @@ def test_batched_slots_past_gemv_match_single(n, bstream, golden, knob):
                                    {"bstream_acc": 0, "bstream_nw": 16}, {"bstream_acc": 0, "bstream_kparts": 2},
                                    {"batched_fused_attn": 0}, {"attn_cap_batched": 32},
                                    {"fd_min_batched": 64}, {"bstream": 0, "linear_u32": 8}, {"bstream_acc": 0},
-                                   {"fd_nw_batched": 8}, {"fd_nw_batched": 16, "fd_min_batched": 64}])
+                                   {"fd_nw_batched": 8}, {"fd_nw_batched": 16, "fd_min_batched": 64},
+                                   {"bs_qkv_slab": 0}])
 def test_batched_wide_split_k_matches_single(knobs, golden, knob):
     """S2-Pro widths, 20 slots: the batched linears (bf16 production: bsacc_kernel; fp32 validation
     mode: bstream_kernel, whose K-part slabs + finalize_norm the default runs), whole-K linear_kernel,
@@ -410,7 +411,8 @@ def test_batched_wide_split_k_matches_single(knobs, golden, knob):
     from fishmi.llm import DualARModel
 
     defaults = {"bstream": 1, "linear_fill": 0, "bstream_nw": 0, "bstream_kparts": 0, "batched_fused_attn": 1,
-                "attn_cap_batched": 128, "fd_min_batched": 512, "linear_u32": 4, "bstream_acc": 1, "fd_nw_batched": 4}
+                "attn_cap_batched": 128, "fd_min_batched": 512, "linear_u32": 4, "bstream_acc": 1, "fd_nw_batched": 4,
+                "bs_qkv_slab": 1}
     for k, v in knobs.items():
         knob(k, v, defaults[k])
 
