@@ -40,7 +40,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--frames", type=int, default=216)
     ap.add_argument("--prompt-len", type=int, default=64)
-    ap.add_argument("--first-chunk", type=int, default=8)
+    ap.add_argument("--first-chunk", type=int, default=1,
+                    help="frames in the first vocoded chunk (later chunks grow 4x)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=0,
                     help="oracle decode frames timed (0: the whole utterance, --frames)")
@@ -75,23 +76,36 @@ def make_prompt(cfg, T, seed):
 
 def utterance(llm, codec, prompt, sp, frames, first_chunk):
     """Request -> PCM for one stream.  Returns (pcm, timings in seconds).  The vocoder streams:
-    the first chunk is decoded as soon as its frames exist, the rest continues the same codec
-    stream (carried causal state, fm_codec_decode_chunk), so no frame is vocoded twice."""
+    each chunk of frames is vocoded as soon as its frames exist -- first_chunk frames, then chunks
+    growing 4x, so a chunk's generation (4^k frames at ~10x real time) takes less time than the
+    audio already delivered (>= 4^k frames) takes to play -- continuing one codec stream (carried
+    causal state, fm_codec_decode_chunk), so no frame is vocoded twice and the waveform is
+    bit-identical to a one-shot decode (tests/test_gpu_codec_stream.py)."""
     t0 = time.perf_counter()
     col0 = llm.prefill(0, prompt, sp)
     t1 = time.perf_counter()
-    f0 = min(first_chunk, frames)
-    head = llm.decode_frames([0], f0 - 1)[:, 0, :]
-    cols = np.concatenate([col0[None], head], axis=0)          # (f0, C+1)
     codec.stream_reset()
-    pcm0 = codec.decode_chunk(np.ascontiguousarray(cols[:, 1:].T))  # first audio chunk
-    t2 = time.perf_counter()
-    rest = llm.decode_frames([0], frames - f0)[:, 0, :]
-    t3 = time.perf_counter()
-    pcm = np.concatenate([pcm0, codec.decode_chunk(np.ascontiguousarray(rest[:, 1:].T))])
+    pcm, done, n = [], 0, min(first_chunk, frames)
+    cols = col0[None]
+    first = decode = vocode = 0.0
+    while done < frames:
+        ta = time.perf_counter()
+        if n > cols.shape[0]:
+            cols = np.concatenate([cols, llm.decode_frames([0], n - cols.shape[0])[:, 0, :]], axis=0)
+        tb = time.perf_counter()
+        pcm.append(codec.decode_chunk(np.ascontiguousarray(cols[:, 1:].T)))
+        tc = time.perf_counter()
+        if done == 0:
+            first = tc - t0
+        else:
+            decode += tb - ta
+            vocode += tc - tb
+        done += n
+        cols = cols[:0]
+        n = min(4 * n, frames - done)
     t4 = time.perf_counter()
-    return pcm, dict(first=t2 - t0, prefill=t1 - t0, head=t2 - t1, decode=t3 - t2, codec=t4 - t3,
-                     total=t4 - t0)
+    return np.concatenate(pcm), dict(first=first, prefill=t1 - t0, head=first - (t1 - t0), decode=decode,
+                                     codec=vocode, total=t4 - t0)
 
 
 def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world):
@@ -605,7 +619,8 @@ def main():
                                    f"prompt + {args.frames} Dual-AR frames (top_k 30, top_p 0.8, temp 0.8) "
                                    f"+ codec decode [1,10,{args.frames}] -> {args.frames * 2048} samples",
                        "global_batch": world, "frames": args.frames, "prompt_len": args.prompt_len,
-                       "first_chunk_frames": args.first_chunk, "parallelism": f"dp{world}"},
+                       "first_chunk_frames": args.first_chunk, "vocoder_chunks": "first_chunk_frames, then growing 4x",
+                       "parallelism": f"dp{world}"},
             "p50_first_sample_ms": round(float(np.median(firsts)) * 1e3, 2),
             "p90_first_sample_ms": round(float(np.percentile(firsts, 90)) * 1e3, 2),
             "per_stream_rtf": round(args.frames / FRAME_RATE / np.mean([t["total"] for t in tms]), 4),
