@@ -237,8 +237,9 @@ def encode_leg(ccfg, device, seconds, seed):
 def longform_leg(ccfg, device, turns, frames_per_turn, seed):
     """BASELINE config 5 on one GPU: voice clone from 30 s of reference audio (codec encode), then
     `turns` speaker turns of `frames_per_turn` frames through the native generate_long (conversation
-    growing with each turn's codes, prefix KV reused), codes streamed 22 frames at a time into the
-    causal streamed vocoder.  Synthetic S2-Pro weights and a synthetic tokenizer at the S2-Pro vocab
+    growing with each turn's codes, prefix KV reused), codes streamed into the causal streamed
+    vocoder in chunks of 1, 4, 16, then 64 frames per turn (each chunk generated faster than the
+    audio before it plays).  Synthetic S2-Pro weights and a synthetic tokenizer at the S2-Pro vocab
     layout; <|im_end|> masked so every turn has its full length.  Timed from the request (reference
     audio in host memory) to the last PCM sample."""
     import tempfile
@@ -276,8 +277,8 @@ def longform_leg(ccfg, device, turns, frames_per_turn, seed):
         firsts, samples, turn_t0 = [], 0, t0
         for o in E.generate_long(model=llm, text=text, max_new_tokens=frames_per_turn, top_p=0.8, top_k=30,
                                  temperature=0.8, chunk_length=200, prompt_text=["a thirty second reference"],
-                                 prompt_tokens=[ptok], seed=seed, stream_frames=22, mask_im_end=True,
-                                 reuse_prefix=True):
+                                 prompt_tokens=[ptok], seed=seed, stream_frames=1, stream_growth=4,
+                                 stream_max=64, mask_im_end=True, reuse_prefix=True):
             if o.action != "sample":
                 continue
             if o.stream == 0:
@@ -298,8 +299,8 @@ def longform_leg(ccfg, device, turns, frames_per_turn, seed):
     f = np.array(firsts) * 1e3
     return {"workload": f"BASELINE config 5: voice clone from {n / ccfg.sample_rate:.1f} s of reference audio "
                         f"({ref_codes} code frames, HIP encode) + {turns} speaker turns x {frames_per_turn} frames "
-                        f"through generate_long (prefix KV reused across turns), codes streamed 22 frames at a "
-                        f"time into the causal streamed vocoder; bf16, synthetic weights + tokenizer",
+                        f"through generate_long (prefix KV reused across turns), codes streamed in chunks of 1, 4, 16, "
+                        f"then 64 frames into the causal streamed vocoder; bf16, synthetic weights + tokenizer",
             "value": round(audio_s / wall, 3), "unit": "audio-sec/wall-sec", "audio_s": round(audio_s, 2),
             "wall_s": round(wall, 3), "first_sample_ms": round(float(f[0]), 2),
             "turn_first_chunk_ms_p50": round(float(np.median(f)), 2),

@@ -173,8 +173,8 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
                   temperature: float = 1.0, compile: bool = False, iterative_prompt: bool = True,
                   chunk_length: int = 512, prompt_text: Optional[Union[str, List[str]]] = None,
                   prompt_tokens=None, seed: Optional[int] = None,
-                  reuse_prefix: bool = False, stream_frames: int = 0,
-                  mask_im_end: bool = False) -> Iterator[GenerateResponse]:
+                  reuse_prefix: bool = False, stream_frames: int = 0, stream_growth: int = 1,
+                  stream_max: int = 0, mask_im_end: bool = False) -> Iterator[GenerateResponse]:
     """inference.py:523-733 on the native model (slot 0).  `device`, `decode_one_token`, `compile`,
     `iterative_prompt` and `repetition_penalty` are accepted for signature compatibility; like
     the reference, repetition_penalty is not applied (RAS is, inside the sampler).
@@ -189,7 +189,10 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
 
     stream_frames > 0 (BASELINE config 5's streamed vocoder): each batch's codes are yielded as they
     are decoded, `stream_frames` columns at a time (GenerateResponse.stream = chunk index), instead of
-    once per batch; their concatenation equals the batch's codes.  mask_im_end: fixed-length
+    once per batch; their concatenation equals the batch's codes.  stream_growth > 1: each chunk is
+    that many times the previous one (up to stream_max frames when > 0) -- a first chunk of one
+    frame reaches the vocoder right after the prompt, and a chunk of k frames always takes less
+    time to generate than the audio already streamed takes to play.  mask_im_end: fixed-length
     generation for benchmarks (the semantic bias keeps <|im_end|> at -inf)."""
     job = ConversationJob(model, text=text, tokenizer=tokenizer, num_samples=num_samples,
                           max_new_tokens=max_new_tokens, top_p=top_p, top_k=top_k, temperature=temperature,
@@ -205,7 +208,8 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
             continue
         enc, L = plan.enc, plan.L
         if stream_frames > 0:
-            y, fed_cols = yield from _stream_batch(model, enc, L, max_new_tokens, stream_frames, plan.text, plan.sp)
+            y, fed_cols = yield from _stream_batch(model, enc, L, max_new_tokens, stream_frames, plan.text, plan.sp,
+                                                   stream_growth, stream_max)
         else:
             if L > 0:
                 y = model.generate_at(enc[:, L:], L, max_new_tokens, temperature=temperature, top_p=top_p,
@@ -220,10 +224,11 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
             yield GenerateResponse(action="sample", codes=codes, text=plan.text)
 
 
-def _stream_batch(model, enc, L, max_new_tokens, stream_frames, text, sp):
+def _stream_batch(model, enc, L, max_new_tokens, stream_frames, text, sp, growth=1, cap=0):
     """One generate() of generate_long, decoded `stream_frames` frames at a time (prefill, then
-    decode_frames chunks on slot 0): yields the confirmed code columns of each chunk, returns
-    (y (C+1, n) as generate() would, every column fed back to the model)."""
+    decode_frames chunks on slot 0; with growth > 1 the chunks grow geometrically up to cap): yields
+    the confirmed code columns of each chunk, returns (y (C+1, n) as generate() would, every column
+    fed back to the model)."""
     T = enc.shape[1]
     mx = max_new_tokens if (max_new_tokens and T + max_new_tokens <= model.cfg.max_seq_len) \
         else model.cfg.max_seq_len - T
@@ -231,9 +236,12 @@ def _stream_batch(model, enc, L, max_new_tokens, stream_frames, text, sp):
     cols = [model.prefill(0, enc[:, L:], sp, pos0=L)]
     fed = []
     done = cols[0][0] == im_end or mx <= 1
-    emitted, chunk = 0, 0
+    emitted, chunk, step = 0, 0, stream_frames
     while not done:
-        k = min(stream_frames, mx - len(cols))
+        k = min(step, mx - len(cols))
+        step = step * max(1, growth)
+        if cap > 0:
+            step = min(step, cap)
         out = model.decode_frames([0], k)[:, 0, :]
         fed.extend([cols[-1]] + list(out[:-1]))  # frame j feeds the column sampled before it
         for c in out:

@@ -142,6 +142,18 @@ def test_streamed_generation_and_vocoding(golden, tmp_path):
     assert len(per_batch) == len(whole) == 2
     for w, parts in zip(whole, per_batch):
         np.testing.assert_array_equal(np.concatenate(parts, axis=1), w.codes)
+    # geometric chunks (the config-5 bench schedule: 1, 4, 8, 8, ... frames) give the same codes
+    grown = [o for o in E.generate_long(stream_frames=1, stream_growth=4, stream_max=8, **kw) if o.action == "sample"]
+    per_batch, cur = [], None
+    for c in grown:
+        if c.stream == 0:
+            assert c.codes.shape[1] == 1
+            cur = []
+            per_batch.append(cur)
+        cur.append(c.codes)
+    assert len(per_batch) == 2 and max(c.codes.shape[1] for c in grown) <= 8
+    for w, parts in zip(whole, per_batch):
+        np.testing.assert_array_equal(np.concatenate(parts, axis=1), w.codes)
     codec = _codec(golden)
     q = E.launch_thread_safe_queue(None, 0, "bf16", model=m)
     eng = TTSInferenceEngine(q, codec, stream_frames=5)
