@@ -1,5 +1,6 @@
 """C-ABI boundary checks that need no GPU: the library loads and exports every symbol the
 header declares (no compute calls)."""
+import ast
 import os
 import re
 import subprocess
@@ -37,6 +38,19 @@ def test_library_loads_without_gpu():
     assert L.fm_device_count() >= 0
     for s in _header_symbols():
         assert hasattr(L, s)
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libfishmi.so not built")
+def test_library_maps_torch_hip_runtime_first():
+    """A fresh process that loads fishmi first must end up on torch's libamdhip64 (one HIP runtime
+    per process; the other order leaves torch with "No HIP GPUs are available" on the box)."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from fishmi import native; native.lib()\n"
+            "maps = [l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l]\n"
+            "print(sorted(set(maps)))\n") % os.path.join(ROOT, "fish-speech_amd")
+    out = subprocess.check_output(["python3", "-c", code], text=True, timeout=300)
+    paths = ast.literal_eval(out.strip().splitlines()[-1])
+    assert len(paths) == 1 and "/torch/lib/" in paths[0], paths
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libfishmi.so not built")
