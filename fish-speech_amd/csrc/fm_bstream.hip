@@ -407,37 +407,76 @@ __global__ __launch_bounds__(FN_THREADS) void finalize_norm_kernel(FinalizeArgs<
         const int i = 8 * (threadIdx.x + FN_THREADS * c);
         if (a.nw && i < a.d) load8(a.nw + i, wn[c]);
     }
+    float x[FN_CPT][8];  // residual rows, also in flight before the slab adds
 #pragma unroll
     for (int c = 0; c < FN_CPT; ++c) {
         const int i = 8 * (threadIdx.x + FN_THREADS * c);
-        if (i < a.d) {
-            float y[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, x[8];
-            for (int q = 0; q < a.kparts; ++q) {
-                const float* sp = a.slab + ((size_t)q * a.R + r) * a.lds + i;
+        if (i < a.d) load8(a.res + (size_t)r * a.ldr + i, x[c]);
+    }
+    // slab sums, K parts in order (fp32 add order = the reference restatement's), four parts'
+    // loads for both chunks issued before the adds that consume them
+    float y[FN_CPT][8];
+#pragma unroll
+    for (int c = 0; c < FN_CPT; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[c][j] = 0.f;
+    {
+        int q = 0;
+        for (; q + 4 <= a.kparts; q += 4) {
+            f32x4_t p[4][FN_CPT][2];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int c = 0; c < FN_CPT; ++c) {
+                    const int i = 8 * (threadIdx.x + FN_THREADS * c);
+                    const float* sp = a.slab + ((size_t)(q + u) * a.R + r) * a.lds + (i < a.d ? i : 0);
+                    p[u][c][0] = *reinterpret_cast<const f32x4_t*>(sp);
+                    p[u][c][1] = *reinterpret_cast<const f32x4_t*>(sp + 4);
+                }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int c = 0; c < FN_CPT; ++c)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        y[c][j] += p[u][c][0][j];
+                        y[c][4 + j] += p[u][c][1][j];
+                    }
+        }
+        for (; q < a.kparts; ++q) {
+#pragma unroll
+            for (int c = 0; c < FN_CPT; ++c) {
+                const int i = 8 * (threadIdx.x + FN_THREADS * c);
+                const float* sp = a.slab + ((size_t)q * a.R + r) * a.lds + (i < a.d ? i : 0);
                 const f32x4_t p0 = *reinterpret_cast<const f32x4_t*>(sp);
                 const f32x4_t p1 = *reinterpret_cast<const f32x4_t*>(sp + 4);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    y[j] += p0[j];
-                    y[4 + j] += p1[j];
+                    y[c][j] += p0[j];
+                    y[c][4 + j] += p1[j];
                 }
             }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < FN_CPT; ++c) {
+        const int i = 8 * (threadIdx.x + FN_THREADS * c);
+        if (i < a.d) {
             if (a.bias) {
                 float b[8];
                 load8(a.bias + i, b);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) y[j] += b[j];
+                for (int j = 0; j < 8; ++j) y[c][j] += b[j];
             }
             if (a.wscale) {  // weight-only int8 linear output
                 float sc[8];
                 load8(a.wscale + i, sc);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) y[j] = rnd<T>(rnd<T>(y[j]) * sc[j]);
+                for (int j = 0; j < 8; ++j) y[c][j] = rnd<T>(rnd<T>(y[c][j]) * sc[j]);
             }
-            load8(a.res + (size_t)r * a.ldr + i, x);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                v[c][j] = rnd<T>(x[j] + rnd<T>(y[j]));
+                v[c][j] = rnd<T>(x[c][j] + rnd<T>(y[c][j]));
                 ss += v[c][j] * v[c][j];
             }
             T* xo = a.x_out + (size_t)r * a.ldx + i;
