@@ -167,6 +167,8 @@ class BatchedWorker:
                 self.stopping = True
             elif not self.stopping:
                 self.pending.append(item)
+            else:  # after the stop sentinel: answered, never silently dropped
+                self._put(item, RuntimeError("the LLM worker is stopping"))
         starting: List[int] = []
         while self.pending and self.free:
             item = self.pending.popleft()
@@ -181,10 +183,20 @@ class BatchedWorker:
         while starting:
             try:
                 self._prefill(starting)
-            except Exception as e:
+            except Exception:
+                # one bad request must not take down the cohort: the slots that have no first column
+                # yet are prefilled again one at a time, and only those that fail get the error
+                ok = []
                 for s in starting:
-                    self._fail(s, e)
-                break
+                    if self.active[s].cols:
+                        ok.append(s)
+                        continue
+                    try:
+                        self._prefill([s])
+                        ok.append(s)
+                    except Exception as e:
+                        self._fail(s, e)
+                starting = ok
             nxt = []
             for s in starting:
                 if self.active[s].done:
@@ -230,6 +242,22 @@ class BatchedWorker:
         except Exception as e:
             self._fail(slot, e)
 
+    def fail_all(self, e: Exception):
+        """Answer every active and waiting request with `e` and free their slots (a failure outside the
+        per-request guards: the requests are lost, the callers are not left waiting)."""
+        for s in list(self.active):
+            self._fail(s, e)
+        while self.pending:
+            item = self.pending.popleft()
+            self._put(item, e)
+            if self.on_done is not None:
+                self.on_done(item)
+
     def run(self):
-        while self.tick():
-            pass
+        while True:
+            try:
+                if not self.tick():
+                    return
+            except Exception as e:  # keep serving: the requests in flight get the error
+                log.error("worker tick failed: %s", traceback.format_exc())
+                self.fail_all(e)

@@ -18,13 +18,30 @@ ranks never sit in a collective past its timeout.
 
 Wire format: msgpack (numpy arrays as {shape, dtype, bytes}), over uint8 tensors on the default
 process group (RCCL with device tensors on the GPU box, gloo with host tensors in the CPU tests).
-Requests carry their prompt tokens; responses carry codes, so the vocoder runs on rank 0 as the
-reference's single-process server does.  There is no collective on the decode path.
+Requests carry their prompt tokens.  With a `vocoder` (a FishMICodec per rank), every "sample"
+response is vocoded on the rank that decoded it -- one-shot, or the request's own causal codec
+stream for streamed chunks -- and travels with its float32 PCM (GenerateResponse.audio) beside the
+codes, so rank 0 vocodes only its own share (SURVEY.md §8e: the return direction carries audio;
+the TTS engine forwards the PCM).  float32 rather than int16 keeps every byte the single-process
+engine would produce (the int16 conversions happen where they do there); at config-4 rates that is
+~0.2 MB per audio second over xGMI.  There is no collective on the decode path.
+
+Stragglers: the ticks are synchronous, so a rank's long step delays everyone's next tick.  A tick's
+work per rank is bounded: at most `tick_frames` batched frames, and the prefills of the text batches
+starting on that rank (the prompt linears run as one GEMM over all of them, ~10-45 ms for
+256-1400-token prompts); requests are dealt one at a time round-robin over the ranks with free
+slots (scheduler.assign), so prompt work spreads over the ranks instead of queueing behind one.
+
+Failures: an exception that escapes a tick (a collective error, a wire decode error, a bug) fails
+every request this rank holds -- routed, queued, active -- with that error, then tears the process
+group down so the other ranks' next collective fails too and they do the same; rank 0 keeps
+answering later requests with the error instead of leaving their callers blocked.
 """
 from __future__ import annotations
 
 import builtins
 import collections
+import dataclasses
 import logging
 import queue
 import threading
@@ -94,7 +111,8 @@ def response_to_wire(w: Optional[WrappedGenerateResponse]) -> dict:
     if w.status == "error":
         return {"status": "error", "exc": _exc_to_wire(w.response)}
     r = w.response
-    return {"status": "success", "action": r.action, "codes": r.codes, "text": r.text, "stream": r.stream}
+    return {"status": "success", "action": r.action, "codes": r.codes, "text": r.text, "stream": r.stream,
+            "audio": getattr(r, "audio", None)}
 
 
 def response_from_wire(d: dict) -> Optional[WrappedGenerateResponse]:
@@ -103,7 +121,7 @@ def response_from_wire(d: dict) -> Optional[WrappedGenerateResponse]:
     if d["status"] == "error":
         return WrappedGenerateResponse(status="error", response=_exc_from_wire(d["exc"]))
     return WrappedGenerateResponse(status="success", response=GenerateResponse(
-        action=d["action"], codes=d["codes"], text=d["text"], stream=d["stream"]))
+        action=d["action"], codes=d["codes"], text=d["text"], stream=d["stream"], audio=d.get("audio")))
 
 
 class _Outbox:
@@ -116,14 +134,47 @@ class _Outbox:
         self.sink.append((self.rid, w))
 
 
+class _Vocoding:
+    """A request's response queue on the rank that decodes it, with a vocoder: each "sample" response
+    gets its PCM here (VQManager.decode_vq_tokens, vq_manager.py:16-21, or the request's own causal
+    stream for latency="balanced" chunks) before it moves on."""
+
+    def __init__(self, inner, vocoder):
+        self.inner, self.voc, self.ctx = inner, vocoder, None
+
+    def put(self, w):
+        if w is not None and w.status == "success" and isinstance(w.response, GenerateResponse) \
+                and w.response.action == "sample" and w.response.codes is not None:
+            r = w.response
+            codes = np.asarray(r.codes)
+            if r.stream is not None:  # chunk k of one text batch's stream: this request's codec state
+                if r.stream == 0 or self.ctx is None:
+                    self.close()
+                    self.ctx = self.voc.open_stream()
+                pcm = self.ctx.decode_chunk(codes)
+            else:
+                pcm = self.voc.decode_codes(codes)
+            w = WrappedGenerateResponse(status="success", response=dataclasses.replace(
+                r, audio=np.ascontiguousarray(pcm, dtype=np.float32)))
+        self.inner.put(w)
+
+    def close(self):
+        if self.ctx is not None:
+            self.ctx.close()
+            self.ctx = None
+
+
 # ---- the worker ---------------------------------------------------------------------------------
 class DistributedWorker:
     STAT = 5  # free, busy, outbox bytes, queued (rank 0), stopping (rank 0)
 
-    def __init__(self, model, max_slots: Optional[int] = None, tick_frames: int = 8, idle_wait: float = 0.02):
+    def __init__(self, model, max_slots: Optional[int] = None, tick_frames: int = 8, idle_wait: float = 0.02,
+                 vocoder=None, device=None):
         dist = _dist()
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
-        self.dev = _device()
+        # the collectives' device: explicit (the caller's GPU), never this thread's current device
+        self.dev = device if device is not None else _device()
+        self.vocoder = vocoder  # a FishMICodec on this rank's GPU: vocode where the codes are decoded
         self.w = BatchedWorker(model, max_slots, tick_frames)
         self.w.on_done = self._done
         self.idle_wait = idle_wait
@@ -134,10 +185,22 @@ class DistributedWorker:
         self._blob = b""  # packed outbox, sent at this tick's gather
         self.next_id = 0
         self.stopping = False
+        self.failed: Optional[BaseException] = None
         self.stats = {"ticks": 0, "served": 0, "sent_to": [0] * self.world}
+
+    def _wrap(self, item: GenerateRequest) -> GenerateRequest:
+        if self.vocoder is None:
+            return item
+        w = GenerateRequest(request=item.request, response_queue=_Vocoding(item.response_queue, self.vocoder))
+        if hasattr(item, "_rid"):
+            w._rid = item._rid
+        return w
 
     def _done(self, item: GenerateRequest):
         q = item.response_queue
+        if isinstance(q, _Vocoding):
+            q.close()
+            q = q.inner
         if isinstance(q, _Outbox):
             q.put(None)
         else:
@@ -258,24 +321,53 @@ class DistributedWorker:
         take = assign(st[:, 0].tolist(), int(st[0, 3]))
         if sum(take):
             for it in self._scatter(take):
-                wk.pending.append(it)
+                wk.pending.append(self._wrap(it))
         if wk.active or wk.pending:
             wk.tick(block=False)
         return True
 
-    def run(self):
-        while self.tick():
+    def _fail_everything(self, e: BaseException):
+        """A tick raised: every request this rank holds gets the error; then the process group goes
+        down so no other rank waits in a collective for this one."""
+        err = e if isinstance(e, Exception) else RuntimeError(repr(e))
+        log.error("rank %d: serving loop failed: %r", self.rank, e)
+        self.w.fail_all(err)  # active + pending (their queues: callers, outboxes)
+        if self.rank == 0:
+            for rid, item in list(self.routes.items()):  # queued here or decoding on another rank
+                item.response_queue.put(WrappedGenerateResponse(status="error", response=err))
+            self.routes.clear()
+            self.queued.clear()
+        try:
+            _dist().destroy_process_group()
+        except Exception:  # pragma: no cover - already torn down
             pass
+
+    def run(self):
+        try:
+            while self.tick():
+                pass
+        except BaseException as e:
+            self._fail_everything(e)
+            self.failed = e
+            if self.rank == 0:  # later requests are answered, not left blocking their callers
+                while True:
+                    item = self.input.get()
+                    if item is None:
+                        break
+                    item.response_queue.put(WrappedGenerateResponse(status="error", response=RuntimeError(
+                        f"the multi-GPU LLM worker failed: {e!r}")))
+            return
         log.info("rank %d: %s", self.rank, self.stats)
 
 
 def launch_distributed_queue(checkpoint_path, device, precision, max_slots: int = 32, tick_frames: int = 8,
-                             model=None, idle_wait: float = 0.02):
+                             model=None, idle_wait: float = 0.02, vocoder=None):
     """launch_thread_safe_queue across the process group: every rank loads the model on its own GPU
     and runs a DistributedWorker in a daemon thread.  Returns (input queue, thread); only rank 0's
     queue is served (requests put on another rank's queue are never read).  Put `None` on rank 0's
-    queue to stop every rank; join the thread to wait for it."""
-    from .engine import load_model
+    queue to stop every rank; join the thread to wait for it.  vocoder: this rank's codec (or a
+    callable building it on the worker thread): responses then carry their PCM."""
+    from .engine import _device_index, load_model
 
     ready = threading.Event()
     failure: List[BaseException] = []
@@ -283,8 +375,15 @@ def launch_distributed_queue(checkpoint_path, device, precision, max_slots: int 
 
     def worker():
         try:
+            dev = None
+            if _dist().get_backend() == "nccl":  # the current device is per thread: set it here
+                import torch
+
+                torch.cuda.set_device(_device_index(device))
+                dev = torch.device("cuda", _device_index(device))
             m = model if model is not None else load_model(checkpoint_path, device, precision, max_slots)
-            w = DistributedWorker(m, max_slots, tick_frames, idle_wait)
+            voc = vocoder() if callable(vocoder) else vocoder
+            w = DistributedWorker(m, max_slots, tick_frames, idle_wait, vocoder=voc, device=dev)
         except BaseException as e:
             failure.append(e)
             ready.set()

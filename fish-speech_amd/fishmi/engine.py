@@ -40,6 +40,9 @@ class GenerateResponse:
     # The chunks of one batch are consecutive code columns of one causal stream: vocode them with
     # the codec's carried state (FishMICodec.stream_reset at chunk 0, then decode_chunk).
     stream: Optional[int] = None
+    # multi-GPU serving (fishmi.dist_serving with a vocoder): the float32 PCM of these codes, vocoded
+    # on the rank that decoded them; the TTS engine then only forwards it
+    audio: Optional[np.ndarray] = None
 
 
 @dataclass

@@ -23,7 +23,7 @@ _lib = None
 ABI_SYMBOLS = [
     "fm_device_count", "fm_last_error", "fm_llm_open", "fm_llm_set_quant", "fm_llm_set_tensor", "fm_llm_synth_tensor",
     "fm_llm_finalize", "fm_llm_prefill", "fm_llm_prefill_batch", "fm_llm_decode", "fm_llm_decode_frames", "fm_llm_generate", "fm_llm_generate_at", "fm_llm_prefill_at", "fm_llm_slot_pos", "fm_llm_teacher_step",
-    "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph", "fm_tune", "fm_debug_ts_read",
+    "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph", "fm_llm_debug_vec", "fm_tune", "fm_debug_ts_read",
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
     "fm_codec_finalize", "fm_codec_decode", "fm_codec_stream_reset", "fm_codec_decode_chunk",
     "fm_codec_stream_open", "fm_codec_stream_decode", "fm_codec_stream_close",
@@ -88,6 +88,7 @@ def lib():
     L.fm_llm_kernel_bench.argtypes = [vp, ctypes.c_char_p, i32, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.fm_llm_use_graph.argtypes = [vp, i32]
+    L.fm_llm_debug_vec.argtypes = [vp, ctypes.c_char_p, i32, pf32, i64]
     L.fm_tune.argtypes = [ctypes.c_char_p, i32]
     L.fm_debug_ts_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), i64, ctypes.POINTER(ctypes.c_int64)]
     L.fm_llm_close.argtypes = [vp]

@@ -239,7 +239,8 @@ def main(argv=None):
 
 
 def _main_distributed(a):
-    """One rank per GPU under torchrun: every rank decodes, rank 0 also serves HTTP and vocodes."""
+    """One rank per GPU under torchrun: every rank decodes and vocodes what it decoded (its own codec
+    handle); rank 0 also serves HTTP (its engine's codec encodes the voice-clone references)."""
     import torch
     import torch.distributed as dist
     import uvicorn
@@ -252,7 +253,13 @@ def _main_distributed(a):
         torch.cuda.set_device(local)
     dist.init_process_group(backend)
     try:
-        q, th = launch_distributed_queue(a.llama_checkpoint_path, local, "bf16", max_slots=max(a.slots, 1))
+        from .codec import FishMICodec
+
+        def vocoder():
+            return FishMICodec.from_checkpoint(a.decoder_checkpoint_path, local, "bf16", 2048, encoder=False)
+
+        q, th = launch_distributed_queue(a.llama_checkpoint_path, local, "bf16", max_slots=max(a.slots, 1),
+                                         vocoder=vocoder)
         if dist.get_rank() == 0:
             engine = build_engine(a.llama_checkpoint_path, a.decoder_checkpoint_path, local, "bf16",
                                   reuse_prefix=a.reuse_prefix, llama_queue=q)

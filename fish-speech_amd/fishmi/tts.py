@@ -247,6 +247,8 @@ class TTSInferenceEngine:
         batch's causal stream, whose carried codec state belongs to the calling request alone:
         `streams` is that request's holder ({"ctx": CodecStream}); chunk 0 replaces its context
         with a fresh one.  Without a holder the handle's own stream is used (one caller only)."""
+        if getattr(result, "audio", None) is not None:  # vocoded where it was decoded (dist_serving)
+            return np.asarray(result.audio, np.float32)
         if result.stream is not None:  # a chunk of one batch's causal stream: carried codec state
             codes = np.asarray(result.codes)
             with self._codec_lock:

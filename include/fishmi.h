@@ -160,6 +160,10 @@ int fm_llm_profile_read(fm_llm* h, const char* kernel_class, double* total_ms, i
 int fm_llm_kernel_bench(fm_llm* h, const char* kernel_class, int reps, double* avg_us,
                         int64_t* launches, int64_t* bytes);
 int fm_llm_use_graph(fm_llm* h, int enable);
+/* developer hook: row 0 of an activation buffer of the decode path ("qkv", "att", "fh", "act",
+   "fx", "fx2", "xl", "xnl": bf16/fp32 storage as floats) or, for name "gran", op `index`'s vector
+   of the last persistent fast pass (fm_pass.hip exchange granules; n = its length) */
+int fm_llm_debug_vec(fm_llm* h, const char* name, int index, float* out, int64_t n);
 /* Teacher forcing on the PRODUCTION decode path (parity with the reference's own teacher-forced
    forward_generate / forward_generate_fast, llama.py:390-466, 798-827): while a slot is forced,
    every sampler of its frames (prefill and decode, graph-replayed or eager, batch-1 GEMV path or

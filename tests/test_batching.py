@@ -203,3 +203,48 @@ def test_launch_thread_safe_queue_batched():
             if o.codes is not None:
                 np.testing.assert_array_equal(g.response.codes, o.codes)
     q_in.put(None)
+
+
+def test_batched_prefill_failure_fails_only_its_request():
+    """A batch prefill that raises is retried slot by slot: only the request whose prompt fails gets
+    the error, the rest of the cohort is served (one bad request took down the cohort)."""
+    from fishmi import engine
+    from fishmi.batching import BatchedWorker
+
+    class Flaky(ScriptedModel):
+        def prefill(self, slot, prompt, sp, pos0=0):
+            if np.asarray(prompt).shape[1] > 0 and getattr(self, "poison", None) == slot:
+                raise ValueError("poisoned prompt")
+            return super().prefill(slot, prompt, sp, pos0)
+
+    mb = Flaky(3)
+    w = BatchedWorker(mb, 3, tick_frames=4)
+    qs = [queue.Queue() for _ in range(3)]
+    for i, q in enumerate(qs):
+        w.input.put(engine.GenerateRequest(request=dict(text=f"r{i}", max_new_tokens=5, seed=i), response_queue=q))
+    mb.poison = 1  # the slot the second request lands on (slots are handed out 0, 1, 2)
+    w.input.put(None)
+    w.run()
+    got = [[q.get() for _ in range(q.qsize())] for q in qs]
+    assert [g[0].status for g in got] == ["success", "error", "success"]
+    assert "poisoned" in str(got[1][0].response)
+    for i in (0, 2):
+        ref = list(engine.generate_long(model=ScriptedModel(1), text=f"r{i}", max_new_tokens=5, seed=i))
+        assert [g.response.action for g in got[i]] == [o.action for o in ref]
+        np.testing.assert_array_equal(got[i][0].response.codes, ref[0].codes)
+
+
+def test_requests_after_stop_are_answered():
+    """A request queued behind the `None` sentinel gets an error response instead of being dropped."""
+    from fishmi import engine
+    from fishmi.batching import BatchedWorker
+
+    w = BatchedWorker(ScriptedModel(2), 2, tick_frames=4)
+    q1, q2 = queue.Queue(), queue.Queue()
+    w.input.put(engine.GenerateRequest(request=dict(text="a", max_new_tokens=4, seed=1), response_queue=q1))
+    w.input.put(None)
+    w.input.put(engine.GenerateRequest(request=dict(text="b", max_new_tokens=4, seed=2), response_queue=q2))
+    w.run()
+    assert q1.get().status == "success"
+    late = q2.get(timeout=5)
+    assert late.status == "error" and "stopping" in str(late.response)

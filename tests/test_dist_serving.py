@@ -59,18 +59,56 @@ def _collect(q, n_final):
     return got
 
 
-def _worker(rank, world, port, out_q, slots, tick):
+class ScriptedVocoder:
+    """Stands in for FishMICodec: PCM is a per-column function of the codes (HOP samples a column),
+    so a causal stream of chunks vocodes to the one-shot decode of their concatenation."""
+    HOP = 4
+
+    def __init__(self):
+        self.calls = 0
+
+    def decode_codes(self, codes):
+        self.calls += 1
+        c = np.asarray(codes, np.int64)
+        col = (c * np.arange(1, c.shape[0] + 1)[:, None]).sum(0) % 997
+        return np.repeat(col.astype(np.float32) / 997.0, self.HOP)
+
+    def open_stream(self):
+        voc = self
+
+        class _S:
+            def decode_chunk(self, codes):
+                return voc.decode_codes(codes)
+
+            def close(self):
+                pass
+
+        return _S()
+
+
+def _worker(rank, world, port, out_q, slots, tick, mode="plain"):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from fishmi import engine
-        from fishmi.dist_serving import launch_distributed_queue
+        from fishmi.dist_serving import DistributedWorker, launch_distributed_queue
         from test_batching import ScriptedModel, _requests
 
         model = ScriptedModel(slots)
-        q_in, th = launch_distributed_queue(None, 0, "bf16", max_slots=slots, tick_frames=tick, model=model)
+        voc = ScriptedVocoder() if mode == "vocode" else None
+        if mode == "fail" and rank == 1:  # a tick that raises outside every per-request guard
+            orig = DistributedWorker.tick
+
+            def bad_tick(self):
+                if self.stats["ticks"] >= 12:
+                    raise RuntimeError("injected tick failure")
+                return orig(self)
+
+            DistributedWorker.tick = bad_tick
+        q_in, th = launch_distributed_queue(None, 0, "bf16", max_slots=slots, tick_frames=tick, model=model,
+                                            vocoder=voc)
         if rank == 0:
             reqs = _requests()
             reqs.append(dict(text="bad", max_new_tokens=6, seed=2, temperature=5.0))
@@ -81,27 +119,49 @@ def _worker(rank, world, port, out_q, slots, tick):
             qs = [queue.Queue() for _ in reqs]
             for r, q in zip(reqs, qs):
                 q_in.put(engine.GenerateRequest(request=r, response_queue=q))
-            for i, (q, rf) in enumerate(zip(qs, ref)):
-                n_final = 0 if rf[-1].status == "error" else sum(w.response.action == "next" for w in rf)
-                _check(_collect(q, max(n_final, 1)), rf, i)
+            if mode == "fail":
+                # every request ends (answered or failed); none leaves its caller blocked
+                errs = 0
+                for i, (q, rf) in enumerate(zip(qs, ref)):
+                    n_final = 0 if rf[-1].status == "error" else sum(w.response.action == "next" for w in rf)
+                    got = _collect(q, max(n_final, 1))
+                    errs += got[-1].status == "error"
+                assert errs >= 2, errs  # the "bad" request + at least one failed by the injected error
+                late = queue.Queue()  # a request after the failure is answered too
+                q_in.put(engine.GenerateRequest(request=reqs[0], response_queue=late))
+                assert late.get(timeout=30).status == "error"
+            else:
+                for i, (q, rf) in enumerate(zip(qs, ref)):
+                    n_final = 0 if rf[-1].status == "error" else sum(w.response.action == "next" for w in rf)
+                    got = _collect(q, max(n_final, 1))
+                    _check(got, rf, i)
+                    if voc is not None:  # every sample carries the PCM of its own codes
+                        for w in got:
+                            if w.status == "success" and w.response.action == "sample":
+                                assert w.response.audio is not None, i
+                                np.testing.assert_array_equal(w.response.audio,
+                                                              ScriptedVocoder().decode_codes(w.response.codes))
             q_in.put(None)
         th.join(timeout=120)
         assert not th.is_alive()
         decoded = [c for c in model.calls if c[0] in ("prefill", "prefill_batch")]
+        if voc is not None:
+            assert voc.calls > 0, f"rank {rank} vocoded nothing"
         out_q.put((rank, "ok", len(decoded)))
     except Exception:
         out_q.put((rank, traceback.format_exc(), 0))
     finally:
-        dist.destroy_process_group()
+        if dist.is_initialized():
+            dist.destroy_process_group()
 
 
-def _run(slots, tick):
+def _run(slots, tick, mode="plain"):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, slots, tick)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, slots, tick, mode)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -113,7 +173,7 @@ def _run(slots, tick):
         assert p.exitcode == 0
     for r in range(2):
         assert res[r][0] == "ok", res[r][0]
-        assert res[r][1] > 0, f"rank {r} decoded nothing"
+        assert res[r][1] > 0 or mode == "fail", f"rank {r} decoded nothing"
 
 
 def test_distributed_worker_world2_equals_serial():
@@ -122,6 +182,19 @@ def test_distributed_worker_world2_equals_serial():
 
 def test_distributed_worker_world2_one_slot_per_rank():
     _run(slots=1, tick=8)
+
+
+def test_distributed_worker_world2_vocodes_per_rank():
+    """Each rank vocodes the samples it decoded; every response's PCM equals the one-shot decode of
+    its codes (streamed chunks included), and both ranks' vocoders ran."""
+    _run(slots=2, tick=3, mode="vocode")
+
+
+def test_distributed_worker_world2_tick_failure_fails_requests():
+    """A tick on rank 1 raises outside every per-request guard: rank 0's callers all get an answer
+    (the requests in flight fail with the error), later requests are answered with an error, and
+    both worker threads end instead of hanging in a collective."""
+    _run(slots=2, tick=3, mode="fail")
 
 
 def test_wire_roundtrip():
@@ -133,10 +206,13 @@ def test_wire_roundtrip():
     back = unpack(pack(req))
     np.testing.assert_array_equal(back["prompt_tokens"][0], req["prompt_tokens"][0])
     assert back["prompt_tokens"][0].dtype == np.int32 and back["top_p"] == 0.5 and back["text"] == "hi"
-    w = engine.WrappedGenerateResponse("success", engine.GenerateResponse("sample", np.ones((2, 3), np.int32), "t", 1))
+    w = engine.WrappedGenerateResponse("success", engine.GenerateResponse("sample", np.ones((2, 3), np.int32), "t", 1,
+                                                                          np.linspace(-1, 1, 7, dtype=np.float32)))
     w2 = response_from_wire(unpack(pack(response_to_wire(w))))
     assert w2.response.action == "sample" and w2.response.stream == 1 and w2.response.text == "t"
     np.testing.assert_array_equal(w2.response.codes, w.response.codes)
+    np.testing.assert_array_equal(w2.response.audio, w.response.audio)
+    assert w2.response.audio.dtype == np.float32
     e = response_from_wire(unpack(pack(response_to_wire(engine.WrappedGenerateResponse("error", ValueError("x"))))))
     assert e.status == "error" and isinstance(e.response, ValueError) and str(e.response) == "x"
     assert response_from_wire(unpack(pack(response_to_wire(None)))) is None
