@@ -1740,16 +1740,10 @@ template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFused
 }
 template <typename T> void launch_sample_radix(hipStream_t s, const SampleArgs& a, int R) {
     // dynamic LDS: the row's values, or the sorted keys of the top_k > 64 path (top_k lives on the
-    // device, per slot, so every launch reserves the larger)
+    // device, per slot, so every launch reserves the larger); the kernels' attributes allow up to
+    // 160 KiB (sample_init, run at model finalize outside any capture)
     const size_t lds = std::max(sizeof(float) * a.Nl, sizeof(uint64_t) * (size_t)sw_pow2(a.Nl));
-    static bool big = false;
-    if (lds > 64 * 1024 && !big) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sample_fast_kernel<T>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sample_radix_kernel<T>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        big = true;
-    }
+    FMCHECK(lds + 8 * 1024 <= 160 * 1024, "sampler: vocabulary too wide for the LDS row");
     if (a.Nl <= 256 * SF_PER && fm_tuning().sampler_fast)
         sample_fast_kernel<T><<<R, 256, lds, s>>>(a);
     else
@@ -1765,5 +1759,12 @@ template void launch_fast_attn2<bf16_t>(hipStream_t, const FastFusedArgs<bf16_t>
 template void launch_fast_attn2<float>(hipStream_t, const FastFusedArgs<float>&, int);
 template void launch_fast_attn_fused<bf16_t>(hipStream_t, const FastFusedArgs<bf16_t>&, int);
 template void launch_fast_attn_fused<float>(hipStream_t, const FastFusedArgs<float>&, int);
+void sample_init() {
+    const void* k[] = {reinterpret_cast<const void*>(&sample_fast_kernel<bf16_t>),
+                       reinterpret_cast<const void*>(&sample_radix_kernel<bf16_t>),
+                       reinterpret_cast<const void*>(&sample_fast_kernel<float>),
+                       reinterpret_cast<const void*>(&sample_radix_kernel<float>)};
+    for (const void* f : k) HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
+}
 template void launch_sample_radix<bf16_t>(hipStream_t, const SampleArgs&, int);
 template void launch_sample_radix<float>(hipStream_t, const SampleArgs&, int);

@@ -260,6 +260,8 @@ struct FmTuning {
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
     int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1)
     int pass_mode = 0;       // developer: PassArgs::mode
+    int pass_nap = 2;        // PassArgs::sweep_nap
+    int pass_prefetch = 12;  // PassArgs::prefetch
     int pass_spin = 0;       // developer: hand-off poll bound exponent (0: default 2^20 polls)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
 };
@@ -333,17 +335,19 @@ struct PassArgs {
     int* err;                 // set when a hand-off wait timed out
     int nwg;                  // workgroups (one per CU)
     int spin_log2;            // each hand-off wait gives up after 2^spin_log2 polls (0: 2^16)
+    int sweep_nap;            // s_sleep between a sweep's polls of the granules still missing (1 .. 32)
     int mode;                 // developer timing modes (fm_tune pass_mode; results wrong): 1 consumers skip the
                               // input-row wait, 2 consumers skip the dot products too
     unsigned long long* dbg;  // developer phase stamps (fm_tune debug_ts) or null
     int off_ring, off_xbuf, off_resx, off_resh, off_raw, off_kvs, off_red, off_sc, off_opt, off_lyt, off_attc,
-        off_flg, off_dbg;  // LDS byte offsets (pass_lds)
+        off_flg, off_junk, off_dbg;  // LDS byte offsets (pass_lds)
+    int prefetch;  // fills past the ring pulled into L2 while the ring is full (0: none)
 };
 constexpr int PASS_NWM = 4;    // exchange waves per workgroup
 constexpr int PASS_NC = 4;     // consumer waves per workgroup (plus one loader wave)
 constexpr int PASS_RING_KB = 64;  // LDS weight ring (fm_tune pass_cfg picks its slots x fill size)
 struct PassLds {
-    int ring, xbuf, resx, resh, raw, kvs, red, sc, opt, lyt, attc, flg, dbg;
+    int ring, xbuf, resx, resh, raw, kvs, red, sc, opt, lyt, attc, flg, junk, dbg;
     size_t bytes;
 };
 PassLds pass_lds(int kmax, int dim, int nqkv, int nkv, int S, int hd, int maxrows, int nop);
@@ -462,6 +466,7 @@ template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFused
 // fast-model attention, one wave per q head (cpos < 16 cached rows, hd <= 256)
 template <typename T> void launch_fast_attn2(hipStream_t s, const FastFusedArgs<T>& a, int R);
 template <typename T> void launch_sample_radix(hipStream_t s, const SampleArgs& a, int R);
+void sample_init();  // sampler kernel attributes (dynamic LDS past 64 KiB), outside any capture
 template <typename T>
 void launch_attn_combine(hipStream_t s, const float* part, const int* row_pos, int R, int nh, int hd,
                          int split, int maxsplit, T* out);

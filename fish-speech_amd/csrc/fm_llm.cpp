@@ -5,8 +5,11 @@
 // frame (one decode_one_token_ar for n slots, inference.py:96-181) is a fixed kernel sequence
 // that reads every dynamic value (tokens, positions, steps) from device memory, so it is
 // captured once per batch size into a hipGraph and replayed.
+#include <dlfcn.h>
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <signal.h>
 
 #include <algorithm>
 #include <array>
@@ -15,6 +18,38 @@
 #include "fm_codec.h"
 #include "fm_kernels.h"
 #include "fm_runtime.h"
+
+// developer: FISHMI_SEGV_TRACE=1 prints the native stack (module + offset per frame) of a host
+// fault before the default action (the rocprofv3 fault investigation)
+namespace {
+void segv_trace(int sig, siginfo_t* si, void*) {
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    fprintf(stderr, "fishmi: signal %d at address %p, %d frames\n", sig, si ? si->si_addr : nullptr, n);
+    for (int i = 0; i < n; ++i) {
+        Dl_info d{};
+        if (dladdr(fr[i], &d) && d.dli_fname)
+            fprintf(stderr, "  #%d %s +0x%lx (%s)\n", i, d.dli_fname,
+                    (unsigned long)((const char*)fr[i] - (const char*)d.dli_fbase), d.dli_sname ? d.dli_sname : "?");
+        else
+            fprintf(stderr, "  #%d %p\n", i, fr[i]);
+    }
+    fflush(stderr);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+struct SegvTraceInstaller {
+    SegvTraceInstaller() {
+        const char* e = getenv("FISHMI_SEGV_TRACE");
+        if (!e || e[0] != '1') return;
+        struct sigaction sa {};
+        sa.sa_sigaction = segv_trace;
+        sa.sa_flags = SA_SIGINFO;
+        sigaction(SIGSEGV, &sa, nullptr);
+        sigaction(SIGBUS, &sa, nullptr);
+    }
+} g_segv_trace;
+}  // namespace
 
 static thread_local std::string g_err;
 void fm_set_error(const std::string& s) { g_err = s; }
@@ -962,6 +997,7 @@ template <typename T> struct Run {
         a.nwg = m->pnwg;
         a.spin_log2 = fm_tuning().pass_spin;
         a.mode = fm_tuning().pass_mode;
+        a.sweep_nap = fm_tuning().pass_nap;
         a.dbg = fm_tuning().dbg;
         const PassLds L = pass_lds(std::max({a.dim, a.nq, a.inter}), a.dim, a.nqkv, a.nkv, a.S, a.hd,
                                    pass_maxrows_for(a.nqkv, a.dim, a.inter, a.nhead, a.nwg), a.nop);
@@ -977,6 +1013,8 @@ template <typename T> struct Run {
         a.off_lyt = L.lyt;
         a.off_attc = L.attc;
         a.off_flg = L.flg;
+        a.off_junk = L.junk;
+        a.prefetch = fm_tuning().pass_prefetch;
         a.off_dbg = L.dbg;
         int64_t bytes = 0;  // weight bytes streamed
         for (int o = 0; o < a.nop; ++o) {
@@ -1443,6 +1481,7 @@ static void finalize(fm_llm* m) {
     if (m->finalized) return;
     const fm_model_config& c = m->c;
     bsacc_init();
+    sample_init();
     for (auto& kv : m->w) FMCHECK(kv.second.set || kv.second.optional, "tensor not set: " + kv.first);
     if (m->quant) quantize_linears(m);
     pass_prepare(m);  // (row-major copies: before the linears are packed)
@@ -2267,8 +2306,14 @@ int fm_tune(const char* key, int value) {
             FMCHECK(value >= 0 && value <= 4, "pass_cfg must be 0..4");
             t.pass_cfg = value;
         } else if (k == "pass_mode") {
-            FMCHECK(value >= 0 && value <= 3, "pass_mode must be 0..3");
+            FMCHECK(value >= 0 && value <= 15, "pass_mode must be 0..15");
             t.pass_mode = value;
+        } else if (k == "pass_nap") {
+            FMCHECK(value >= 1 && value <= 32, "pass_nap must be 1..32");
+            t.pass_nap = value;
+        } else if (k == "pass_prefetch") {
+            FMCHECK(value >= 0 && value <= 64, "pass_prefetch must be 0..64");
+            t.pass_prefetch = value;
         } else if (k == "pass_spin") {
             FMCHECK(value >= 0 && value < 28, "pass_spin must be 0 (default) or a poll-bound exponent < 28");
             t.pass_spin = value;

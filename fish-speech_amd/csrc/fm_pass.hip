@@ -142,6 +142,21 @@ typedef __attribute__((address_space(1))) int g_i32;
 // LDS words shared between the roles: volatile LDS accesses (ds_read / ds_write, never cached)
 typedef __attribute__((address_space(3))) volatile unsigned lds_vu32;
 
+// the same, default cache policy: a prefetch whose bytes land in a junk LDS slot and stay in L2
+// (MALL) for the real (nt) fill that follows
+__device__ __forceinline__ void glds16_pf(const void* gsrc, uint32_t lds_base) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_base)
+        : "memory");
+}
+
 // one 1 KiB fragment by LDS-DMA: lane l's 16 bytes at gsrc -> LDS lds_base + 16 l, non-temporal
 // (nt-weights row: each weight byte is read once a pass).  M0 is saved and restored in the same
 // statement (compiler-reserved); the DMA is invisible to hipcc's waitcnt bookkeeping, so every
@@ -157,6 +172,16 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
         : "=&s"(keep)
         : "v"(gsrc), "s"(lds_base)
         : "memory");
+}
+
+// s_sleep with a run-time argument (its operand is an immediate): 64 x n cycles, n in 1 .. 32
+__device__ __forceinline__ void sleep_n(int n) {
+    if (n <= 1) __builtin_amdgcn_s_sleep(1);
+    else if (n <= 2) __builtin_amdgcn_s_sleep(2);
+    else if (n <= 4) __builtin_amdgcn_s_sleep(4);
+    else if (n <= 8) __builtin_amdgcn_s_sleep(8);
+    else if (n <= 16) __builtin_amdgcn_s_sleep(16);
+    else __builtin_amdgcn_s_sleep(32);
 }
 
 // bounded spin on an LDS word until (word - target) >= 0 as signed (monotonic counters)
@@ -179,7 +204,7 @@ __device__ __forceinline__ bool lds_wait_ge(const lds_vu32* w, unsigned target, 
 // matches; bounded.
 template <int NJ>
 __device__ __forceinline__ void sweep_nj(const u64* g, int P, unsigned tag, uint32_t* dst, int t, int* err,
-                                         unsigned limit) {
+                                         unsigned limit, int nap) {
     asm volatile("" : "+v"(t));  // keep the address arithmetic here (not hoisted out of the caller's loop)
     uint32_t pend = 0;
 #pragma unroll
@@ -188,9 +213,10 @@ __device__ __forceinline__ void sweep_nj(const u64* g, int P, unsigned tag, uint
     for (unsigned spin = 0;; ++spin) {
         u64 v[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int p = min(t + 256 * j, P - 1);
-            v[j] = __hip_atomic_load((g_u64*)(g + p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int j = 0; j < NJ; ++j) {  // only the granules still missing (a poll costs the weight stream)
+            v[j] = 0;
+            if ((pend >> j) & 1u)
+                v[j] = __hip_atomic_load((g_u64*)(g + t + 256 * j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -206,187 +232,147 @@ __device__ __forceinline__ void sweep_nj(const u64* g, int P, unsigned tag, uint
             __hip_atomic_store((g_i32*)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        sleep_n(nap);
     }
 }
 __device__ __forceinline__ void sweep(const u64* g, int P, unsigned tag, uint32_t* dst, int t, int* err,
-                                      unsigned limit) {
+                                      unsigned limit, int nap) {
     const int nj = (P + 255) >> 8;
-    if (nj <= 2) sweep_nj<2>(g, P, tag, dst, t, err, limit);
-    else if (nj <= 4) sweep_nj<4>(g, P, tag, dst, t, err, limit);
-    else if (nj <= 6) sweep_nj<6>(g, P, tag, dst, t, err, limit);
-    else if (nj <= 8) sweep_nj<8>(g, P, tag, dst, t, err, limit);
-    else if (nj <= 12) sweep_nj<12>(g, P, tag, dst, t, err, limit);
-    else if (nj <= 16) sweep_nj<16>(g, P, tag, dst, t, err, limit);
-    else sweep_nj<20>(g, P, tag, dst, t, err, limit);
+    if (nj <= 2) sweep_nj<2>(g, P, tag, dst, t, err, limit, nap);
+    else if (nj <= 4) sweep_nj<4>(g, P, tag, dst, t, err, limit, nap);
+    else if (nj <= 6) sweep_nj<6>(g, P, tag, dst, t, err, limit, nap);
+    else if (nj <= 8) sweep_nj<8>(g, P, tag, dst, t, err, limit, nap);
+    else if (nj <= 12) sweep_nj<12>(g, P, tag, dst, t, err, limit, nap);
+    else if (nj <= 16) sweep_nj<16>(g, P, tag, dst, t, err, limit, nap);
+    else sweep_nj<20>(g, P, tag, dst, t, err, limit, nap);
 }
 
-// Fast-model attention of heads hbase .. hbase + 7 (< nh, two whole kv groups when nh / nkv == 4)
-// at position cpos: one wave, 8 lanes per head (lane sub owns RoPE pairs sub, sub + 8, ...); every
-// operand in LDS, passed as LDS byte offsets so the accesses are ds_ reads out of line: raw = the
-// q|k|v row (q and k are rewritten in place after QK-norm + RoPE: a kv group's heads all live in
-// this wave), kvs = the cached rows [nkv][k|v][cpos][hd], qn / kn = this layer's QK-norm weights,
-// tab = the RoPE row at cpos, pscr = probability scratch [8 heads][16], out = the attention row.
-// Scores: lane sub takes positions sub and sub + 8 whole (128-wide dots); softmax across the
-// head's 8 lanes; output: lane sub's pairs summed over the positions in order.  The roundings of
-// fast_attn_heads8_lds (fm_attn_dev.h, the launch-per-op path: llama.py:861-975 in bf16); the
-// fp32 orders of the dots and of the softmax denominator differ.  store_kv: the first q head of
-// each kv group writes the new k / v of cpos to the cache (kc / vc at the slot's layer base).
+// Fast-model attention of heads hbase .. hbase + 3 (< nh) at position cpos (<= 15): one wave, 16
+// lanes per head, lane c owning dims [8c, 8c + 8) (one 16-byte chunk; hd <= 128).  Every operand is
+// in LDS: raw = the q|k|v row, kvs = the cached rows [nkv][k|v][cpos][hd], qn / kn = this layer's
+// QK-norm weights, tab = the RoPE row at cpos (cos, sin per pair), out = the attention row.
+//  * q and k chunks: QK-norm (sum of squares over the head's 16 lanes) and RoPE on the lane's own
+//    interleaved pairs, in registers;
+//  * scores: per position one 8-wide partial dot (v_dot2c_f32_bf16) per lane, summed across the
+//    head's 16-lane row by DPP, kept by lane j;
+//  * softmax across the 16 lanes; output: p_j read from lane j, the lane's 8 dims summed over the
+//    positions in order.
+// The roundings of fast_attn_heads8_lds (fm_attn_dev.h, the launch-per-op path: llama.py:861-975 in
+// bf16); the fp32 orders of the dots and of the softmax denominator differ.  store_kv: the lanes
+// of each kv group's first q head write the new k / v of cpos to the cache (kc / vc at the slot's
+// layer base).
 typedef __attribute__((address_space(3))) bf16_t lds_bf16_t;
 typedef __attribute__((address_space(3))) float lds_f32_t;
 typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
 typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
 struct AttnLds {
-    uint32_t raw, kvs, qn, kn, tab, psc, out;
+    uint32_t raw, kvs, qn, kn, tab, out;
 };
-__device__ __noinline__ void pass_attn8(int nh, int nkv, int hd, int cpos, int qk_norm, float eps, float scale,
-                                        int hbase, int lane, AttnLds o, bf16_t* kc_base, bf16_t* vc_base,
-                                        size_t kv_head_stride, bool store_kv) {
-    lds_bf16_t* raw = (lds_bf16_t*)(size_t)o.raw;
-    const lds_bf16_t* kvs = (const lds_bf16_t*)(size_t)o.kvs;
-    const lds_bf16_t* qn = (const lds_bf16_t*)(size_t)o.qn;
-    const lds_bf16_t* kn = (const lds_bf16_t*)(size_t)o.kn;
+__device__ __forceinline__ void pass_attn4(int nh, int nkv, int hd, int cpos, int qk_norm, float eps, float scale,
+                                           int hbase, int lane, AttnLds o, bf16_t* kc_base, bf16_t* vc_base,
+                                           size_t kv_head_stride, bool store_kv) {
+    const lds_u32x4_t* raw = (const lds_u32x4_t*)(size_t)o.raw;
+    const lds_u32x4_t* kvs = (const lds_u32x4_t*)(size_t)o.kvs;
+    const lds_u32x4_t* qn = (const lds_u32x4_t*)(size_t)o.qn;
+    const lds_u32x4_t* kn = (const lds_u32x4_t*)(size_t)o.kn;
     const lds_f32_t* tab = (const lds_f32_t*)(size_t)o.tab;
-    lds_f32_t* psc = (lds_f32_t*)(size_t)o.psc;
-    lds_bf16_t* out = (lds_bf16_t*)(size_t)o.out;
-    const int g = nh / nkv, PP = hd >> 4;
-    const int sub = lane & 7, hl = lane >> 3, h = hbase + hl;
-    const bool live = h < nh;
-    const int hh = live ? h : hbase, kvh = hh / g;
-    const bool kv_writer = live && hh == kvh * g;  // the kv group's first head
-    float q0[FATT_MAXPP], q1[FATT_MAXPP], k0[FATT_MAXPP], k1[FATT_MAXPP];
-    auto pr = [&](int i) { return 2 * (sub + 8 * (i < PP ? i : 0)); };
-    auto ldp = [&](const lds_bf16_t* p, float& x0, float& x1) {
-        const uint32_t w = *(const lds_u32_t*)p;
-        x0 = lo_f(w);
-        x1 = hi_f(w);
-    };
-    lds_bf16_t* qrow = raw + (size_t)hh * hd;
-    lds_bf16_t* krow = raw + (size_t)(nh + kvh) * hd;
-    const lds_bf16_t* vrow = raw + (size_t)(nh + nkv + kvh) * hd;
+    lds_u32x4_t* out = (lds_u32x4_t*)(size_t)o.out;
+    asm volatile("" : "+v"(lane));  // keep the lane-dependent addressing here (not hoisted out of the caller's op loop)
+    const int c = lane & 15, hl = lane >> 4, h = hbase + hl, nck = hd >> 3, g = nh / nkv;
+    const bool live = h < nh && c < nck;
+    const int hh = h < nh ? h : hbase, kvh = hh / g, cc = c < nck ? c : 0;
+    const u32x4_t qw = raw[hh * nck + cc], kw = raw[(nh + kvh) * nck + cc], vw = raw[(nh + nkv + kvh) * nck + cc];
+    // QK-norm + RoPE of one chunk; dead lanes hold zeros (they add nothing to the head's sums)
+    auto prep = [&](u32x4_t w, const lds_u32x4_t* nwt) {
+        float x[8];
 #pragma unroll
-    for (int i = 0; i < FATT_MAXPP; ++i) {
-        ldp(qrow + pr(i), q0[i], q1[i]);
-        ldp(krow + pr(i), k0[i], k1[i]);
-        if (i >= PP) q0[i] = q1[i] = k0[i] = k1[i] = 0.f;
-    }
-    auto sum8 = [](float v) {
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        return v;
-    };
-    auto prep = [&](float (&x0)[FATT_MAXPP], float (&x1)[FATT_MAXPP], const lds_bf16_t* w) {
+        for (int e = 0; e < 4; ++e) {
+            x[2 * e] = live ? lo_f(w[e]) : 0.f;
+            x[2 * e + 1] = live ? hi_f(w[e]) : 0.f;
+        }
         if (qk_norm) {
             float ss = 0.f;
 #pragma unroll
-            for (int i = 0; i < FATT_MAXPP; ++i) ss += x0[i] * x0[i] + x1[i] * x1[i];
-            ss = sum8(ss);
+            for (int e = 0; e < 8; ++e) ss += x[e] * x[e];
+            ss = row_sum16(ss);
             const float rs = 1.0f / sqrtf(ss / (float)hd + eps);
+            const u32x4_t nv = nwt[cc];
 #pragma unroll
-            for (int i = 0; i < FATT_MAXPP; ++i) {
-                float w0, w1;
-                ldp(w + pr(i), w0, w1);
-                x0[i] = bfround((x0[i] * rs) * w0);
-                x1[i] = bfround((x1[i] * rs) * w1);
+            for (int e = 0; e < 4; ++e) {
+                x[2 * e] = bfround((x[2 * e] * rs) * lo_f(nv[e]));
+                x[2 * e + 1] = bfround((x[2 * e + 1] * rs) * hi_f(nv[e]));
             }
         }
+        u32x4_t r;
 #pragma unroll
-        for (int i = 0; i < FATT_MAXPP; ++i) {
-            const float c = tab[pr(i)], s = tab[pr(i) + 1];
-            const float y0 = bfround(x0[i] * c - x1[i] * s);
-            const float y1 = bfround(x1[i] * c + x0[i] * s);
-            x0[i] = y0;
-            x1[i] = y1;
+        for (int e = 0; e < 4; ++e) {
+            const float cs = tab[8 * cc + 2 * e], sn = tab[8 * cc + 2 * e + 1];
+            r[e] = pack2(bfround(x[2 * e] * cs - x[2 * e + 1] * sn), bfround(x[2 * e + 1] * cs + x[2 * e] * sn));
         }
+        return r;
     };
-    prep(q0, q1, qn);
-    prep(k0, k1, kn);
-    // prepped q / k back into raw (every lane of the wave has read the raw values above)
-    if (live) {
-#pragma unroll
-        for (int i = 0; i < FATT_MAXPP; ++i)
-            if (i < PP) *(lds_u32_t*)(qrow + pr(i)) = pack2(q0[i], q1[i]);
+    const u32x4_t qp = prep(qw, qn), kp = prep(kw, kn);
+    if (store_kv && live && hh % g == 0) {
+        *reinterpret_cast<u32x4_t*>(kc_base + (size_t)kvh * kv_head_stride + (size_t)cpos * hd + 8 * c) = kp;
+        *reinterpret_cast<u32x4_t*>(vc_base + (size_t)kvh * kv_head_stride + (size_t)cpos * hd + 8 * c) = vw;
     }
-    if (kv_writer) {
+    // scores: position j's 16 partial dots summed across the head's row (DPP), kept by lane j
+    const lds_u32x4_t* K = kvs + (size_t)(2 * kvh) * cpos * nck;
+    const lds_u32x4_t* V = K + (size_t)cpos * nck;
+    float sc = -INFINITY;
+    for (int jb = 0; jb <= cpos; jb += 4) {  // four positions' rows in flight at once
+        u32x4_t kk[4];
 #pragma unroll
-        for (int i = 0; i < FATT_MAXPP; ++i)
-            if (i < PP) *(lds_u32_t*)(krow + pr(i)) = pack2(k0[i], k1[i]);
-        if (store_kv) {
-            bf16_t* kr = kc_base + (size_t)kvh * kv_head_stride + (size_t)cpos * hd;
-            bf16_t* vr = vc_base + (size_t)kvh * kv_head_stride + (size_t)cpos * hd;
+        for (int u = 0; u < 4; ++u) kk[u] = jb + u < cpos ? K[(jb + u) * nck + cc] : kp;
 #pragma unroll
-            for (int i = 0; i < FATT_MAXPP; ++i) {
-                if (i < PP) {
-                    *reinterpret_cast<uint32_t*>(kr + pr(i)) = pack2(k0[i], k1[i]);
-                    *reinterpret_cast<uint32_t*>(vr + pr(i)) = *(const lds_u32_t*)(vrow + pr(i));
+        for (int u = 0; u < 4; ++u) {
+            const float d = row_sum16(dot8(kk[u], qp, 0.f));
+            if (c == jb + u && jb + u <= cpos) sc = bfround(bfround(d) * scale);
+        }
+    }
+    const float mx = row_max16(sc);
+    const float ex = c <= cpos ? expf(sc - mx) : 0.f;
+    const float p = bfround(ex / row_sum16(ex));
+    // output: p_j read from lane j of each head's row (four v_readlane, one per row), the lane's
+    // 8 dims summed over the positions in order
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int jb = 0; jb <= cpos; jb += 4) {
+        u32x4_t vv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) vv[u] = jb + u < cpos ? V[(jb + u) * nck + cc] : vw;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = jb + u;
+            if (j <= cpos) {
+                const float p0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), j));
+                const float p1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 16 + j));
+                const float p2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 32 + j));
+                const float p3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), 48 + j));
+                const float pj = hl == 0 ? p0 : (hl == 1 ? p1 : (hl == 2 ? p2 : p3));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    acc[2 * e] += pj * lo_f(vv[u][e]);
+                    acc[2 * e + 1] += pj * hi_f(vv[u][e]);
                 }
             }
         }
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // scores: lane sub -> positions j = sub, sub + 8 (clamped reads, masked results)
-    const lds_bf16_t* K = kvs + (size_t)(2 * kvh) * cpos * hd;
-    const lds_bf16_t* V = K + (size_t)cpos * hd;
-    const int nck = hd / 8;  // 16-byte chunks of a row
-    float s2[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const int j = sub + 8 * r;
-        const lds_bf16_t* kr = j < cpos ? K + (size_t)j * hd : krow;
-        float d = 0.f;
-        for (int c = 0; c < nck; ++c) {
-            const u32x4_t qv = *(const lds_u32x4_t*)(qrow + 8 * c);
-            const u32x4_t kv = *(const lds_u32x4_t*)(kr + 8 * c);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) d += lo_f(qv[e]) * lo_f(kv[e]) + hi_f(qv[e]) * hi_f(kv[e]);
-        }
-        s2[r] = j <= cpos ? bfround(bfround(d) * scale) : -INFINITY;
-    }
-    auto max8 = [](float v) {
-        v = fmaxf(v, __shfl_xor(v, 1));
-        v = fmaxf(v, __shfl_xor(v, 2));
-        return fmaxf(v, __shfl_xor(v, 4));
-    };
-    const float mx = max8(fmaxf(s2[0], s2[1]));
-    float e2[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) e2[r] = sub + 8 * r <= cpos ? expf(s2[r] - mx) : 0.f;
-    const float den = sum8(e2[0] + e2[1]);
-    lds_f32_t* ph = psc + hl * 16;
-#pragma unroll
-    for (int r = 0; r < 2; ++r) ph[sub + 8 * r] = bfround(e2[r] / den);  // 0 past cpos
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // output: lane sub's pairs, positions in order (p = 0 past cpos adds exact zeros)
-    float o0[FATT_MAXPP], o1[FATT_MAXPP];
-#pragma unroll
-    for (int i = 0; i < FATT_MAXPP; ++i) o0[i] = o1[i] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const float p = ph[j];
-        const lds_bf16_t* vr = j < cpos ? V + (size_t)j * hd : vrow;
-#pragma unroll
-        for (int i = 0; i < FATT_MAXPP; ++i) {
-            float v0, v1;
-            ldp(vr + pr(i), v0, v1);
-            o0[i] += p * v0;
-            o1[i] += p * v1;
-        }
-    }
     if (live) {
-        lds_bf16_t* op = out + (size_t)hl * hd;
+        u32x4_t r;
 #pragma unroll
-        for (int i = 0; i < FATT_MAXPP; ++i)
-            if (i < PP) *(lds_u32_t*)(op + pr(i)) = pack2(o0[i], o1[i]);
+        for (int e = 0; e < 4; ++e) r[e] = pack2(acc[2 * e], acc[2 * e + 1]);
+        out[hl * nck + c] = r;
     }
 }
 
 }  // namespace
 
 // LDS words of the role hand-offs (u32 offsets inside the flag block)
-enum { F_FULL = 0, F_FREE = 8, F_A = 16, F_B = 17, F_X = 18, F_WORDS = 32 };
+enum { F_FULL = 0, F_FREE = 8, F_A = 16, F_B = 17, F_X = 18, F_R = 19, F_AT = 20, F_WORDS = 32 };
+// F_R: layers whose q|k|v row is in raw (the attention may start); F_AT: consumer waves' attention
+// calls done
 
 // NC consumer waves, a ring of NSLOT slots of PS_FILL 1 KiB fragments, PS_INFL fills in flight
 template <int NC, int NSLOT, int PS_FILL, int PS_INFL>
@@ -436,6 +422,17 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
     }
     __syncthreads();  // the only workgroup barrier
 
+    // one wave's share of a layer's attention: 4 heads per call, wave w8 of nw8 (the exchange waves
+    // first, then the consumers); workgroup 0 stores the new k / v of cpos
+    auto attention = [&](int layer, bool store_kv, int w8, int nw8) {
+        const size_t cb = (size_t)a.row_slot[0] * a.slot_stride + (size_t)layer * a.layer_stride;
+        for (int hb = 4 * w8; hb < a.nh; hb += 4 * nw8) {
+            AttnLds ao{lds_off(raw), lds_off(kvs), lds_off(aqn), lds_off(akn), lds_off(atab), lds_off(xbuf + (size_t)hb * a.hd)};
+            pass_attn4(a.nh, a.nkv, a.hd, a.cpos, a.qk_norm, a.eps, a.scale, hb, lane, ao, a.kc + cb, a.vc + cb,
+                       (size_t)a.S * a.hd, store_kv);
+        }
+    };
+
     if (wave == 0) {
         // ---------------------------------- loader -------------------------------------------
         // fills in sequence; fill s -> slot s % NSLOT once its previous occupant (s - NSLOT) is
@@ -443,14 +440,32 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
         // flight, and before waiting for a slot every landed fill is published (a full ring with
         // unpublished fills would deadlock the consumers).
         const uint32_t ring0 = __builtin_amdgcn_readfirstlane(lds_off(ring));
-        int pend[PS_INFL + 1];
-        int np = 0;
-        auto publish_oldest = [&]() {
-            const int s = pend[0];
+        const uint32_t junk = __builtin_amdgcn_readfirstlane(lds_off(smem + a.off_junk));
+        int pub = 0, next = 0;  // fills [pub, next) are issued and not yet published (sequence order)
+        // prefetch cursor: while the ring is full (a seam), the fills after it are pulled into L2
+        // (op po, fill pfi of it; sequence number pfs), at most a.prefetch fills past the ring
+        int po = 0, pfi = 0, pfs = 0;
+        Geom pg = opt_get(opt, 0);
+        auto prefetch_one = [&](int limit_s) {
+            while (po < nop && pfi >= nfills(pg.nfr)) {
+                if (++po < nop) pg = opt_get(opt, po);
+                pfi = 0;
+            }
+            if (po >= nop || pfs >= limit_s) return false;
+            const int f0 = pfi * PS_FILL;
+            const bf16_t* src = pg.w + (size_t)f0 * PS_FR + lane * 8;
 #pragma unroll
-            for (int i = 0; i < PS_INFL; ++i) pend[i] = pend[i + 1];
-            --np;
-            if (lane == 0) flg[F_FULL + s % NSLOT] = (unsigned)s + 1u;
+            for (int i = 0; i < PS_FILL; ++i) {
+                const int ok = f0 + i < pg.nfr;
+                glds16_pf(src + (ok ? (size_t)i * PS_FR : 0), junk);
+            }
+            ++pfi;
+            ++pfs;
+            return true;
+        };
+        auto publish_oldest = [&]() {
+            if (lane == 0) flg[F_FULL + pub % NSLOT] = (unsigned)pub + 1u;
+            ++pub;
         };
         for (int o = 0; o < nop; ++o) {
             const Geom g = opt_get(opt, o);
@@ -459,8 +474,34 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
                 const int s = g.s0 + fi, slot = s % NSLOT;
                 if (s >= NSLOT && (int)(flg[F_FREE + slot] - (unsigned)(s - NSLOT + 1)) < 0) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    while (np > 0) publish_oldest();
-                    if (!lds_wait_ge(flg + F_FREE + slot, (unsigned)(s - NSLOT + 1), limit, a.err)) return;
+                    while (pub < next) publish_oldest();
+                    // the ring is full: pull the fills after it into L2 while the slot stays taken
+                    if (pfs < s) {  // (never re-prefetch what is already in the ring)
+                        while (po < nop && pg.s0 + pfi < s) {
+                            if (pfi + 1 < nfills(pg.nfr)) ++pfi;
+                            else if (++po < nop) { pg = opt_get(opt, po); pfi = 0; }
+                        }
+                        pfs = s;
+                    }
+                    int inflight = 0;
+                    for (unsigned spin = 0;; ++spin) {
+                        if ((int)(flg[F_FREE + slot] - (unsigned)(s - NSLOT + 1)) >= 0) break;
+                        if (inflight < 48 / PS_FILL && prefetch_one(s + a.prefetch)) {
+                            ++inflight;  // (vmcnt is 6 bits: at most 63 loads outstanding)
+                            continue;
+                        }
+                        if (inflight > 0) {
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            inflight = 0;
+                            continue;
+                        }
+                        if (spin > limit) {
+                            __hip_atomic_store((g_i32*)a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            return;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    asm volatile("" ::: "memory");
                 }
                 const int f0 = fi * PS_FILL;
                 const bf16_t* src = g.w + (size_t)f0 * PS_FR + lane * 8;
@@ -470,15 +511,15 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
                     const int ok = f0 + i < g.nfr;
                     glds16(src + (ok ? (size_t)i * PS_FR : 0), dst + (uint32_t)(ok ? i : PS_FILL - 1) * 1024);
                 }
-                pend[np++] = s;
-                if (np > PS_INFL) {
+                next = s + 1;
+                if (next - pub > PS_INFL) {
                     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PS_INFL * PS_FILL) : "memory");
                     publish_oldest();
                 }
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        while (np > 0) publish_oldest();
+        while (pub < next) publish_oldest();
         return;
     }
 
@@ -487,8 +528,14 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
         const int c = wave - 1;
         const uint32_t ring0 = lds_off(ring);
         for (int o = 0; o < nop; ++o) {
-            if (!(a.mode & 1) && !lds_wait_ge(flg + F_B, (unsigned)(o + 1), limit, a.err)) return;  // op o's input row is in xbuf
             const Geom g = opt_get(opt, o);
+            if (g.kind == OP_WO && !(a.mode & 1)) {  // heads 16 + 4c ... of this layer's attention
+                if (!lds_wait_ge(flg + F_R, (unsigned)g.layer + 1u, limit, a.err)) return;
+                attention(g.layer, wg == 0, PASS_NWM + c, PASS_NWM + NC);
+                if (lane == 0)
+                    __hip_atomic_fetch_add((unsigned*)(flg + F_AT), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (!(a.mode & 1) && !lds_wait_ge(flg + F_B, (unsigned)(o + 1), limit, a.err)) return;  // op o's input row is in xbuf
             const int nf = nfills(g.nfr);
             float acc = 0.f;
             int cur = -1;
@@ -611,17 +658,6 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
                 akn[i] = L.kn[i];
             }
     };
-    // every q head's attention (4 exchange waves x 8 heads) from LDS into xbuf; workgroup 0 stores
-    // the new k / v of cpos
-    auto attention = [&](int layer, bool store_kv) {
-        const size_t cb = (size_t)slot * a.slot_stride + (size_t)layer * a.layer_stride;
-        for (int hb = 8 * x; hb < a.nh; hb += 8 * PASS_NWM) {
-            AttnLds ao{lds_off(raw), lds_off(kvs), lds_off(aqn), lds_off(akn), lds_off(atab),
-                       lds_off(smem + a.off_sc) + (uint32_t)(x * 8 * 16 * 4), lds_off(xbuf + (size_t)hb * hd)};
-            pass_attn8(a.nh, a.nkv, hd, a.cpos, a.qk_norm, a.eps, a.scale, hb, lane, ao, a.kc + cb, a.vc + cb,
-                       (size_t)a.S * hd, store_kv);
-        }
-    };
     unsigned long long ts[7] = {0, 0, 0, 0, 0, 0, 0}, tatt = 0;
     auto stamp = [&](int i) {
         if (a.dbg && t == 0) ts[i] = __builtin_amdgcn_s_memrealtime();
@@ -631,6 +667,7 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
         if (t == 0) flg[F_B] = (unsigned)nready;
     };
 
+    if (a.mode & 8) return;  // developer: the weight stream alone (with pass_mode 3)
     // ---- initial seam: the pass input row -> resx, its attention_norm -> xbuf
     {
         const bf16_t* x0 = a.x_in;
@@ -659,9 +696,14 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
         float y = 0.f;
         if (t < g.nout) {
             float s[2] = {0.f, 0.f};
-            for (int q = 0; q < g.rpo; ++q) {
-                const int r = t * g.rpo + q, f0 = r * g.fpr, f1 = f0 + g.fpr - 1;
-                for (int fi = f0 / PS_FILL; fi <= f1 / PS_FILL; ++fi) s[q] += red[r * NC + (g.s0 + fi) % NC];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (q < g.rpo) {
+                    const int r = t * g.rpo + q, f0 = r * g.fpr, f1 = f0 + g.fpr - 1;
+                    float acc = 0.f;
+                    for (int fi = f0 / PS_FILL; fi <= f1 / PS_FILL; ++fi) acc += red[r * NC + (g.s0 + fi) % NC];
+                    s[q] = acc;
+                }
             }
             const int n = g.o0 + t;
             const PassLayer& L = lyt[g.layer < a.nlayer ? g.layer : a.nlayer - 1];
@@ -690,21 +732,24 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
         if (o + 1 < nop) {
             const Geom gn = opt_get(opt, o + 1);
             if (gn.kind == OP_WO) {  // q|k|v -> raw, then every head's attention -> xbuf
-                sweep(gv, a.nqkv / 2, tag, reinterpret_cast<uint32_t*>(raw), t, a.err, limit);
+                sweep(gv, a.nqkv / 2, tag, reinterpret_cast<uint32_t*>(raw), t, a.err, limit, a.sweep_nap);
                 stamp(3);
                 ex_sync();
                 stamp(4);
-                attention(gn.layer, wg == 0);
+                if (t == 0) flg[F_R] = (unsigned)gn.layer + 1u;  // the consumers take heads 16 ...
+                attention(gn.layer, wg == 0, x, PASS_NWM + NC);
                 if (a.dbg && t == 0) tatt = __builtin_amdgcn_s_memrealtime() - ts[4];
+                if (!(a.mode & 1)) lds_wait_ge(flg + F_AT, (unsigned)(NC * (gn.layer + 1)), limit, a.err);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             } else if (gn.kind == OP_W2) {  // the SwiGLU row straight in
-                sweep(gv, a.inter / 2, tag, x32, t, a.err, limit);
+                sweep(gv, a.inter / 2, tag, x32, t, a.err, limit, a.sweep_nap);
                 stamp(3);
                 stamp(4);
             } else {  // next layer's QKV, W13, head: the residual row + its RMSNorm
                 const PassLayer& L = lyt[gn.layer < a.nlayer ? gn.layer : a.nlayer - 1];
                 load_nw(gn.kind == OP_QKV ? L.an : (gn.kind == OP_W13 ? L.fn : a.hnorm));
                 uint32_t* r32 = gn.kind == OP_W13 ? rh32 : rx32;
-                sweep(gv, dim / 2, tag, r32, t, a.err, limit);
+                sweep(gv, dim / 2, tag, r32, t, a.err, limit, a.sweep_nap);
                 stage_ss(r32);
                 stamp(3);
                 ex_sync();
@@ -717,9 +762,9 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
             if (gn.kind == OP_QKV) load_kvs(gn.layer);
         } else if (a.tail_attn) {  // head-less pass ending in a QKV: that layer's K/V store
             if (wg == 0) {
-                sweep(gv, a.nqkv / 2, tag, reinterpret_cast<uint32_t*>(raw), t, a.err, limit);
+                sweep(gv, a.nqkv / 2, tag, reinterpret_cast<uint32_t*>(raw), t, a.err, limit, a.sweep_nap);
                 ex_sync();
-                attention(g.layer, true);
+                attention(g.layer, true, x, PASS_NWM);  // (the consumers have left)
             }
             stamp(5);
         }
@@ -767,7 +812,7 @@ PassLds pass_lds(int kmax, int dim, int nqkv, int nkv, int S, int hd, int maxrow
     L.red = (int)o;
     o = al(o + (size_t)maxrows * PASS_NC * 4);  // [rows][NC]
     L.sc = (int)o;
-    o = al(o + (size_t)PASS_NWM * 8 * 16 * 4);  // attention probabilities [4 waves][8 heads][16]
+    o = al(o + 16);  // (spare)
     L.opt = (int)o;
     o = al(o + (size_t)nop * 12 * 4);  // per-op geometry [nop][12]
     L.lyt = (int)o;
@@ -776,6 +821,8 @@ PassLds pass_lds(int kmax, int dim, int nqkv, int nkv, int S, int hd, int maxrow
     o = al(o + (size_t)hd * 4 + 2 * (size_t)hd * 2);  // RoPE row (fp32), q_norm, k_norm
     L.flg = (int)o;
     o = al(o + (size_t)F_WORDS * 4);
+    L.junk = (int)o;
+    o = al(o + 1024);  // the prefetch DMAs' landing slot
     L.dbg = (int)o;
     L.bytes = al(o + (size_t)PASS_NC * 64 * 8);  // developer stamps
     return L;
@@ -787,8 +834,8 @@ bool pass_shapes_ok(int dim, int nq, int nqkv, int inter, int nhead, int nh, int
     auto k_ok = [](int K) { return K > 0 && K % PS_FR == 0 && K / PS_FR <= 8 * (PASS_NC - 1); };
     auto n_ok = [&](int N) { return N > 0 && N % 2 == 0 && (N / 2) <= 256 * PS_NJ_MAX && N / 2 >= nwg; };
     return nwg > 0 && k_ok(dim) && k_ok(nq) && k_ok(inter) && n_ok(dim) && n_ok(nqkv) && n_ok(inter) &&
-           n_ok(nhead) && nq == nh * hd && nqkv == (nh + 2 * nkv) * hd && hd % 16 == 0 && hd <= 16 * FATT_MAXPP &&
-           nkv > 0 && nh % nkv == 0 && (nh / nkv) * 2 <= 8 && 8 % (nh / nkv) == 0 && S - 1 < 16 &&
+           n_ok(nhead) && nq == nh * hd && nqkv == (nh + 2 * nkv) * hd && hd % 16 == 0 && hd <= 128 &&
+           nkv > 0 && nh % nkv == 0 && S - 1 < 16 &&
            dim / 2 <= 256 * PS_NJN;
 }
 
@@ -815,7 +862,7 @@ void launch_pass(hipStream_t s, const PassArgs& a) {
     FMCHECK(L.bytes <= 160 * 1024 && a.off_ring == L.ring && a.off_xbuf == L.xbuf &&
                 a.off_resx == L.resx && a.off_resh == L.resh && a.off_raw == L.raw && a.off_kvs == L.kvs &&
                 a.off_red == L.red && a.off_sc == L.sc && a.off_opt == L.opt && a.off_lyt == L.lyt &&
-                a.off_attc == L.attc && a.off_flg == L.flg && a.off_dbg == L.dbg,
+                a.off_attc == L.attc && a.off_flg == L.flg && a.off_junk == L.junk && a.off_dbg == L.dbg,
             "pass: LDS layout");
     FMCHECK(a.nop >= 1 && a.nop <= 4 * a.nlayer + 1 && a.nop < 255 && a.cpos >= 0 && a.cpos < a.S,
             "pass: op count / cpos");

@@ -53,10 +53,11 @@ def lib():
     # the one both use; if this library pulled /opt/rocm's in first, torch's later device init
     # fails ("No HIP GPUs are available", measured on the MI355X box), which would break every
     # torch.distributed / RCCL caller that loads fishmi first.  Map torch's runtime first.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    if not os.environ.get("FISHMI_NO_TORCH_FIRST"):  # (developer: the rocprofv3 fault investigation)
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64
     f32 = ctypes.c_float

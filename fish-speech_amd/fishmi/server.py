@@ -13,6 +13,12 @@ Routes and contract, as the reference serves them (tools/server/views.py, api_ut
                                which its DAC does not have, so this route is broken
                                there; here it decodes each token matrix through the codec.
   GET  /v1/references/list     {"success": true, "reference_ids": [...]}
+  POST /v1/references/add      {id, audio (bytes), text} as msgpack, JSON (audio base64) or
+                               multipart/form-data -> {success, message, reference_id};
+                               400 bad input, 409 id exists, 500 file-system error
+  DELETE /v1/references/delete {reference_id} -> 404 unknown id
+  POST /v1/references/update   {old_reference_id, new_reference_id} (rename) -> 404 / 409 / 400
+                               (tools/server/views.py:208-470)
 Optional bearer auth (--api-key): 401 "Invalid token" otherwise (tools/api_server.py:33-45).
 
     python -m fishmi.server --llama-checkpoint-path DIR --decoder-checkpoint-path codec.pth [--slots 32]
@@ -79,7 +85,7 @@ def create_app(engine: "TTS.TTSInferenceEngine", max_text_length: int = 0, api_k
         accept = request.headers.get("accept", "").lower()
         return "application/json" in accept and "application/msgpack" not in accept
 
-    def respond(request: Request, obj: dict):
+    def respond(request: Request, obj: dict, status: int = 200):
         if wants_json(request):  # bytes fields travel base64-encoded in JSON
             import base64
 
@@ -90,8 +96,8 @@ def create_app(engine: "TTS.TTSInferenceEngine", max_text_length: int = 0, api_k
                     return [enc(x) for x in v]
                 return v
 
-            return JSONResponse({k: enc(v) for k, v in obj.items()})
-        return Response(msgpack.packb(obj, use_bin_type=True), media_type="application/msgpack")
+            return JSONResponse({k: enc(v) for k, v in obj.items()}, status_code=status)
+        return Response(msgpack.packb(obj, use_bin_type=True), media_type="application/msgpack", status_code=status)
 
     @app.get("/v1/health")
     @app.post("/v1/health")
@@ -177,7 +183,99 @@ def create_app(engine: "TTS.TTSInferenceEngine", max_text_length: int = 0, api_k
 
     @app.get("/v1/references/list")
     async def list_refs(request: Request):
-        return respond(request, {"success": True, "reference_ids": engine.list_reference_ids(), "message": "Success"})
+        try:
+            ids = engine.list_reference_ids()
+        except Exception as e:
+            log.error("listing references failed: %s", e)
+            return respond(request, {"success": False, "reference_ids": [], "message": "Internal server error occurred"},
+                           500)
+        return respond(request, {"success": True, "reference_ids": ids,
+                                 "message": f"Found {len(ids)} reference voices"})
+
+    async def fields(request: Request) -> dict:
+        """msgpack / JSON body, or multipart/form-data (parsed with the stdlib email parser: the
+        multipart package FastAPI's Form() needs is absent here)."""
+        ct = request.headers.get("content-type", "")
+        if ct.split(";")[0].strip().lower() != "multipart/form-data":
+            return await body(request)
+        from email.parser import BytesParser
+        from email.policy import HTTP
+
+        raw = await request.body()
+        msg = BytesParser(policy=HTTP).parsebytes(b"Content-Type: " + ct.encode() + b"\r\n\r\n" + raw)
+        out = {}
+        for part in msg.iter_parts():
+            name = part.get_param("name", header="content-disposition")
+            if name:
+                data = part.get_payload(decode=True) or b""
+                out[name] = data if part.get_filename() is not None else data.decode("utf-8", "replace")
+        return out
+
+    def ref_reply(request: Request, ok: bool, message: str, status: int = 200, **ids):
+        return respond(request, {"success": ok, "message": message, **ids}, status)
+
+    @app.post("/v1/references/add")
+    async def add_ref(request: Request):
+        rid = ""
+        try:
+            d = await fields(request)
+            rid, audio, text = d.get("id") or "", d.get("audio"), d.get("text") or ""
+            if isinstance(audio, str):  # JSON: base64
+                import base64
+
+                audio = base64.b64decode(audio)
+            engine.add_reference(rid, audio or b"", text)
+            return ref_reply(request, True, f"Reference voice '{rid}' added successfully", reference_id=rid)
+        except FileExistsError:
+            return ref_reply(request, False, f"Reference ID '{rid}' already exists", 409, reference_id=rid)
+        except ValueError as e:
+            return ref_reply(request, False, str(e), 400, reference_id=rid)
+        except OSError as e:
+            log.error("adding reference %r: %s", rid, e)
+            return ref_reply(request, False, "File system error occurred", 500, reference_id=rid)
+        except Exception as e:
+            log.error("adding reference %r: %s", rid, e)
+            return ref_reply(request, False, "Internal server error occurred", 500, reference_id=rid)
+
+    @app.delete("/v1/references/delete")
+    async def delete_ref(request: Request):
+        rid = ""
+        try:
+            d = await fields(request)
+            rid = d.get("reference_id") or ""
+            engine.delete_reference(rid)
+            return ref_reply(request, True, f"Reference voice '{rid}' deleted successfully", reference_id=rid)
+        except FileNotFoundError:
+            return ref_reply(request, False, f"Reference ID '{rid}' not found", 404, reference_id=rid)
+        except ValueError as e:
+            return ref_reply(request, False, str(e), 400, reference_id=rid)
+        except OSError as e:
+            log.error("deleting reference %r: %s", rid, e)
+            return ref_reply(request, False, "File system error occurred", 500, reference_id=rid)
+        except Exception as e:
+            log.error("deleting reference %r: %s", rid, e)
+            return ref_reply(request, False, "Internal server error occurred", 500, reference_id=rid)
+
+    @app.post("/v1/references/update")
+    async def update_ref(request: Request):
+        old = new = ""
+        try:
+            d = await fields(request)
+            old, new = d.get("old_reference_id") or "", d.get("new_reference_id") or ""
+            engine.rename_reference(old, new)
+            return ref_reply(request, True, f"Reference voice renamed from '{old}' to '{new}' successfully",
+                             old_reference_id=old, new_reference_id=new)
+        except FileNotFoundError as e:
+            return ref_reply(request, False, str(e), 404, old_reference_id=old, new_reference_id=new)
+        except FileExistsError:
+            return ref_reply(request, False, f"Reference ID '{new}' already exists", 409,
+                             old_reference_id=old, new_reference_id=new)
+        except ValueError as e:
+            return ref_reply(request, False, str(e), 400, old_reference_id=old, new_reference_id=new)
+        except OSError as e:
+            log.error("renaming reference %r: %s", old, e)
+            return ref_reply(request, False, "File system error occurred", 500,
+                             old_reference_id=old, new_reference_id=new)
 
     return app
 

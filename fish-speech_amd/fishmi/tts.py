@@ -219,6 +219,72 @@ class TTSInferenceEngine:
                 out.append(d.name)
         return sorted(out)
 
+    # ---- reference management (inference_engine/reference_loader.py:167-271, views.py:380-470)
+    def add_reference(self, ref_id: str, audio: bytes, text: str) -> None:
+        """references/<id>/sample.wav + sample.lab.  ValueError: bad id / text / audio;
+        FileExistsError: the id exists."""
+        if not ref_id or not ref_id.strip():
+            raise ValueError("Reference ID cannot be empty")
+        if not text or not text.strip():
+            raise ValueError("Reference text cannot be empty")
+        if not valid_reference_id(ref_id):
+            raise ValueError("Reference ID contains invalid characters. Only alphanumeric, hyphens, "
+                             "underscores, and spaces are allowed." if len(ref_id) <= 255 else
+                             "Reference ID is too long. Maximum length is 255 characters.")
+        if not audio:
+            raise ValueError("Audio file is empty or could not be read")
+        folder = self.references_dir / ref_id
+        if folder.exists():
+            raise FileExistsError(f"Reference ID '{ref_id}' already exists")
+        try:
+            folder.mkdir(parents=True, exist_ok=False)
+            (folder / "sample.wav").write_bytes(audio)
+            (folder / "sample.lab").write_text(text, encoding="utf-8")
+        except Exception:
+            import shutil
+
+            shutil.rmtree(folder, ignore_errors=True)
+            raise
+        self.ref_by_id.pop(ref_id, None)
+
+    def delete_reference(self, ref_id: str) -> None:
+        """FileNotFoundError: no such id."""
+        if not ref_id or not ref_id.strip():
+            raise ValueError("Reference ID cannot be empty")
+        if not valid_reference_id(ref_id):
+            raise ValueError(f"invalid reference_id {ref_id!r}")
+        folder = self.references_dir / ref_id
+        if not folder.exists():
+            raise FileNotFoundError(f"Reference ID '{ref_id}' does not exist")
+        import shutil
+
+        try:
+            shutil.rmtree(folder)
+        except Exception as e:
+            raise OSError(f"Failed to delete reference '{ref_id}': {e}")
+        self.ref_by_id.pop(ref_id, None)
+
+    def rename_reference(self, old_id: str, new_id: str) -> None:
+        """FileNotFoundError: no old id; FileExistsError: the new id exists; ValueError: bad ids."""
+        if not old_id or not old_id.strip():
+            raise ValueError("Old reference ID cannot be empty")
+        if not new_id or not new_id.strip():
+            raise ValueError("New reference ID cannot be empty")
+        if old_id == new_id:
+            raise ValueError("New reference ID must be different from old reference ID")
+        if not valid_reference_id(new_id):
+            raise ValueError("New reference ID contains invalid characters or is too long")
+        if not valid_reference_id(old_id):
+            raise FileNotFoundError(f"Reference ID '{old_id}' not found")
+        old, new = self.references_dir / old_id, self.references_dir / new_id
+        if not old.is_dir():
+            raise FileNotFoundError(f"Reference ID '{old_id}' not found")
+        if new.exists():
+            raise FileExistsError(f"Reference ID '{new_id}' already exists")
+        old.rename(new)
+        if old_id in self.ref_by_id:
+            self.ref_by_id[new_id] = self.ref_by_id.pop(old_id)
+
     # ---- LLM request (inference_engine/__init__.py:144-177) ---------------------------------
     def send_Llama_request(self, req, prompt_tokens: list, prompt_texts: list) -> "queue.Queue":
         request = dict(device=getattr(self.decoder_model, "device", 0), max_new_tokens=req.max_new_tokens,

@@ -114,4 +114,6 @@ if os.environ.get("STAMPS"):
               f"{np.median(d(4, 5)):5.2f} | {np.median(d(5, 6)):5.2f} ({np.median(q[:, 7] & 0xFFFFFFFF) / 100.0:5.2f}) | {np.median(seam):6.2f} {seam.max():6.2f} | "
               f"{(q[:, 2].max() - q[:, 2].min()) / 100.0:5.2f} | {np.median(q[:, 7] >> 32) / 100.0:5.2f}")
     print(f"pass span {(r[:, 6].max() - r[:, 1].min()) / 100.0:.1f} us")
+    q = r[o == 0][:, 7] & 0xFFFFFFFF
+    print(f"attention (exchange waves' share) {np.median(q) / 100.0:.2f} us")
     m2.close()

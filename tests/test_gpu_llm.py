@@ -302,6 +302,58 @@ def test_top_k_above_64_matches_oracle_fp32(name, golden):
             m.use_graph(True)
 
 
+def test_top_k_above_64_at_s2_pro_head_width(golden):
+    """The samplers' wide path (top_k > 64) at the production head widths (slow head: the 4096
+    semantic tokens + <|im_end|> of a 155776-token vocabulary; fast head: 4096 codes), bf16: a free
+    slot samples each frame, a twin slot replays that column forced and taps the logits its
+    samplers were handed; every emitted token equals the C oracle's draw (logits_to_probs +
+    multinomial, inference.py:43-93, with RAS, inference.py:117-144) on those same logits."""
+    import oracle as O
+    from fishmi import native
+    from fishmi.llm import DualARModel
+
+    g = golden("llm_wide_bf16.npz")
+    cfg = _cfg("llm_wide")
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 2)
+    C, cb, sb = cfg.num_codebooks, cfg.codebook_size, cfg.semantic_begin_id
+    allowed = np.zeros(cfg.vocab_size, bool)
+    allowed[sb: cfg.semantic_end_id + 1] = True
+    n_new = 8
+    try:
+        for fast in (1, 0):
+            native.tune("sampler_fast", fast)
+            m.use_graph(fast == 1)
+            for top_k, top_p, temp, seed in ((100, 1.0, 0.9, 5), (1000, 0.99, 1.3, 6), (4096, 0.95, 0.7, 7)):
+                sp = DualARModel.sampling(temperature=temp, top_p=top_p, top_k=top_k, seed=seed, mask_im_end=True)
+                prev = np.zeros((C + 1, 10), np.int64)
+                for i in range(n_new):
+                    col = m.prefill(1, g["prompt"], sp) if i == 0 else m.decode([1])[0]
+                    m.force(0, col)
+                    if i == 0:
+                        m.prefill(0, g["prompt"], sp)
+                    else:
+                        m.decode([0])
+                    slow, fl = m.read_logits(0)
+                    m.force(0, None)
+                    lg = np.where(allowed, slow, -np.inf).astype(np.float32)
+                    tok = O.sample(lg, temp, top_p, top_k, seed, i, 0)
+                    if i > 0:
+                        hi = O.sample(lg, 1.0, 0.9, top_k, seed, i, 1)
+                        if (prev[0] == tok).any() and sb <= tok <= cfg.semantic_end_id:
+                            tok = hi
+                    want = [tok, min(max(tok - sb, 0), cb - 1)]
+                    for q in range(1, C):
+                        want.append(O.sample(fl[q - 1], temp, top_p, top_k, seed, i, 1 + q))
+                    np.testing.assert_array_equal(col, want, err_msg=f"frame {i} top_k {top_k} sampler_fast {fast}")
+                    if i > 0:
+                        prev = np.roll(prev, -1, axis=1)
+                        prev[:, -1] = col
+    finally:
+        native.tune("sampler_fast", 1)
+        m.use_graph(True)
+        m.close()
+
+
 def test_im_end_stops_and_masking(golden):
     """generate() stops after emitting <|im_end|> (inference.py:233); mask_im_end forbids it."""
     m, g, cfg = _model("llm_a", "fp32", golden)

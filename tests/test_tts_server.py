@@ -146,6 +146,60 @@ def test_http_health_and_auth():
     assert c.post("/v1/health").json() == {"status": "ok"}
 
 
+def test_http_reference_management(tmp_path):
+    """/v1/references/add | list | update | delete (tools/server/views.py:208-470): the reference's
+    status codes (400 bad input, 404 unknown id, 409 existing id) and folder layout (sample.wav +
+    sample.lab), over msgpack, JSON (base64 audio) and multipart/form-data; the added voice is then
+    usable as a reference_id."""
+    import base64
+
+    from fastapi.testclient import TestClient
+
+    from fishmi.server import create_app
+    from fishmi.tts import ServeTTSRequest
+
+    eng, seen = _engine(tmp_path=tmp_path)
+    c = TestClient(create_app(eng))
+    wav = _wav(np.sin(np.arange(4410) * 0.05), 44100)
+    mp = lambda d: dict(content=msgpack.packb(d, use_bin_type=True),  # noqa: E731
+                        headers={"Content-Type": "application/msgpack"})
+    r = c.post("/v1/references/add", **mp({"id": "alice", "audio": wav, "text": "alice says hi"}))
+    assert r.status_code == 200
+    assert msgpack.unpackb(r.content, raw=False) == {"success": True, "reference_id": "alice",
+                                                      "message": "Reference voice 'alice' added successfully"}
+    assert (tmp_path / "alice" / "sample.wav").read_bytes() == wav
+    assert (tmp_path / "alice" / "sample.lab").read_text() == "alice says hi"
+    assert c.post("/v1/references/add", **mp({"id": "alice", "audio": wav, "text": "x"})).status_code == 409
+    assert c.post("/v1/references/add", **mp({"id": "bad/id", "audio": wav, "text": "x"})).status_code == 400
+    assert c.post("/v1/references/add", **mp({"id": "e", "audio": wav, "text": " "})).status_code == 400
+    assert c.post("/v1/references/add", **mp({"id": "e", "audio": b"", "text": "t"})).status_code == 400
+    r = c.post("/v1/references/add?format=json", json={"id": "bob", "audio": base64.b64encode(wav).decode(),
+                                                       "text": "bob text"})
+    assert r.status_code == 200 and r.json()["success"] is True
+    r = c.post("/v1/references/add", data={"id": "carol", "text": "carol text"},
+               files={"audio": ("c.wav", wav, "audio/wav")})
+    assert r.status_code == 200 and (tmp_path / "carol" / "sample.wav").read_bytes() == wav
+    r = c.get("/v1/references/list?format=json")
+    assert r.json()["reference_ids"] == ["alice", "bob", "carol"]
+    # the added voice conditions a request by id
+    list(eng.inference(ServeTTSRequest(text="x", reference_id="alice", use_memory_cache="on")))
+    assert seen[-1]["prompt_text"] == ["alice says hi"]
+    # rename: cache entry follows; 409 onto an existing id, 404 from an unknown one, 400 same id
+    r = c.post("/v1/references/update?format=json", json={"old_reference_id": "alice", "new_reference_id": "alicia"})
+    assert r.status_code == 200 and r.json()["new_reference_id"] == "alicia"
+    assert "alicia" in eng.ref_by_id and "alice" not in eng.ref_by_id
+    assert c.post("/v1/references/update", json={"old_reference_id": "bob",
+                                                 "new_reference_id": "carol"}).status_code == 409
+    assert c.post("/v1/references/update", json={"old_reference_id": "nobody",
+                                                 "new_reference_id": "x"}).status_code == 404
+    assert c.post("/v1/references/update", json={"old_reference_id": "bob",
+                                                 "new_reference_id": "bob"}).status_code == 400
+    r = c.request("DELETE", "/v1/references/delete?format=json", json={"reference_id": "bob"})
+    assert r.status_code == 200 and not (tmp_path / "bob").exists()
+    assert c.request("DELETE", "/v1/references/delete", json={"reference_id": "bob"}).status_code == 404
+    assert c.get("/v1/references/list?format=json").json()["reference_ids"] == ["alicia", "carol"]
+
+
 def test_http_tts_wav_and_stream_json_and_msgpack():
     from fishmi.tts import wav_chunk_header
 
