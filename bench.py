@@ -460,25 +460,35 @@ def pmc_gemv_traffic(timeout_s=150):
         f"{vals['WRITE_SIZE'] / 1e6:.3f} MB written per gemv_kernel launch")
 
 
-def copy_peak_gbps(nbytes=2 << 30, reps=10):
-    """Measured device-to-device copy rate (read + write bytes / time; SURVEY.md §8d asks for the
-    measured STREAM-like peak beside the vendor figure). torch's copy kernel on the current stream,
-    HIP events."""
+def stream_peak_gbps(nbytes=2 << 30, reps=10):
+    """Measured HBM stream peak (SURVEY.md §8d's STREAM-like figure beside the vendor 8 TB/s):
+    libfishmi's fm_stream_peak, a non-temporal float4 read stream and a float4 copy over 2 GiB
+    buffers (far past the 256 MiB MALL), HIP events.  The read stream is the ceiling a weight
+    stream can reach; the copy counts read + written bytes."""
+    from fishmi import native
+
+    r, c = native.stream_peak(0, nbytes, reps)
+    return round(r, 1), round(c, 1)
+
+
+def box_identity():
+    """Which machine and GPU a line was measured on (so per-box speed differences can be checked)."""
+    import socket
+
     import torch
 
-    a = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
-    b = torch.empty_like(a)
-    b.copy_(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    gbps = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del a, b
-    torch.cuda.empty_cache()
-    return round(gbps, 1)
+    out = {"host": socket.gethostname()}
+    try:
+        p = torch.cuda.get_device_properties(0)
+        out["gpu"] = p.name
+        uuid = getattr(p, "uuid", None)
+        if uuid is not None:
+            out["gpu_uuid"] = str(uuid)
+        out["pci_bus_id"] = getattr(p, "pci_bus_id", None)
+        out["cus"] = p.multi_processor_count
+    except Exception as e:  # identity is informative only
+        out["error"] = str(e)
+    return out
 
 
 def main():
@@ -589,7 +599,8 @@ def main():
     if rank == 0 and not args.no_int8:
         llm.close()
         q8 = int8_leg(cfg, codec, args, local)
-    copy_gbps = copy_peak_gbps() if rank == 0 else None
+    stream_gbps = stream_peak_gbps() if rank == 0 else (None, None)
+    box = box_identity() if rank == 0 else None
     traffic, traffic_note = None, "not measured (--no-pmc or N>1)"
     if rank == 0 and world == 1 and not args.no_pmc:
         traffic, traffic_note = pmc_gemv_traffic()
@@ -631,7 +642,12 @@ def main():
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "traffic_source": traffic_note,
-                         "copy_peak_measured": copy_gbps,
+                         "stream_peak_measured": {"read": stream_gbps[0], "copy": stream_gbps[1], "unit": "GB/s",
+                                                  "frac_of_read_peak": round(achieved / stream_gbps[0], 4)
+                                                  if stream_gbps[0] else None,
+                                                  "method": "fm_stream_peak: non-temporal float4 read "
+                                                            "stream / float4 copy (read + write bytes), "
+                                                            "2 GiB buffers, 10 launches, HIP events"},
                          "bytes_per_launch": int(per_launch),
                          "avg_launch_us": round(avg_us, 3), "launches_per_frame": int(lin_n),
                          "method": "one frame's GEMV launches replayed x20 as a graph, HIP events on "
@@ -648,6 +664,7 @@ def main():
             "longform": longf,
             "int8": q8,
             "cpu_baseline": cpu,
+            "box": box,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -50,6 +50,19 @@ template <> struct Frag<bf16_t> {
             }
         }
     }
+    // 8 int4 codes (nibble e = k e of the lane's 8) -> 8 bf16 values bf16(fma(q - 8, s, z)), RNE
+    // (the weight-only int4 dequantisation, launch_quant4 / quantize.py:139-160's affine form)
+    static __device__ __forceinline__ f dq4(uint32_t w, float s, float z) {
+        f o;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const float v0 = __fmaf_rn((float)((w >> (8 * p)) & 15u) - 8.f, s, z);
+            const float v1 = __fmaf_rn((float)((w >> (8 * p + 4)) & 15u) - 8.f, s, z);
+            o[p] = (uint32_t)__builtin_bit_cast(uint16_t, static_cast<__bf16>(v0)) |
+                   ((uint32_t)__builtin_bit_cast(uint16_t, static_cast<__bf16>(v1)) << 16);
+        }
+        return o;
+    }
     static __device__ __forceinline__ f32x4_t mma(f a, f b, f32x4_t c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
                                                        __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);

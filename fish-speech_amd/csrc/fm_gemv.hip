@@ -57,9 +57,13 @@ constexpr int GEMV_PRE = 8;   // (row, chunk) items of X preloaded per thread be
 constexpr int gemv_wpe(int pro, int epi) { return pro == PRO_PRENORM && epi == EPI_SWIGLU8 ? 5 : (pro == PRO_FATT ? 1 : 3); }
 
 // WPB waves per block share one 16-row tile, each streaming a contiguous run of its k-steps.
-// Q8 (weight-only int8): the weight stream is a.Wq, one ring slot = one 64-k unit (1 KiB per wave,
+// QM 1 (weight-only int8): the weight stream is a.Wq, one ring slot = one 64-k unit (1 KiB per wave,
 // as a T fragment is), dequantised exactly to two T fragments in registers; each output is
 // round(round(acc) * wscale[row]) (WeightOnlyInt8Linear.forward, quantize.py:228-229).
+// QM 2 (weight-only int4, bf16): one ring slot = one 128-k unit of 4-bit codes (1 KiB per wave) plus
+// the lane's row (scale, zero) of that unit's group (a.wsz, group size a multiple of 128), each code
+// dequantised to bf16(fma(q - 8, scale, zero)) -- the value the int4 model's bf16 weight copy holds
+// (launch_quant4), so the GEMV computes the same linear the T-fragment kernels do.
 // ---- chain hand-off (one launch, stages in sequence; cdna_hip_programming.md §6 Guideline 16,
 // write-through form): every byte a later stage of the launch reads is stored sc1 and drained
 // (s_waitcnt vmcnt(0)) by its storing wave before the block's one arrival on a sharded counter;
@@ -130,11 +134,13 @@ template <typename T> __device__ __forceinline__ void st_sc1_run(T* p, size_t i,
 // The GEMV body for block (bxi, ks) of a grid with nks K slices.  CH (chain stage, R == 1, whole
 // K per block): the weight ring goes out first, then the wait for the producing stage, then the
 // prologue's loads (sc1); outputs a later stage reads are stored sc1 (the caller arrives).
-template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8, bool CH>
+template <typename T, int PRO, int EPI, bool NT, int U, int WPB, int QM, bool CH>
 __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, const int ks, const int nks,
                                           const ChainWait& cw) {
-    static_assert(!(Q8 && (EPI == EPI_SWIGLU || EPI == EPI_SLAB || PRO == PRO_FATT)), "no int8 form");
-    static_assert(!CH || (!Q8 && (PRO == PRO_PLAIN || PRO == PRO_PRENORM) &&
+    constexpr bool Q8 = QM == 1, Q4 = QM == 2, QQ = QM != 0;
+    static_assert(!(QQ && (EPI == EPI_SWIGLU || EPI == EPI_SLAB || PRO == PRO_FATT)), "no quantized form");
+    static_assert(!Q4 || sizeof(T) == 2, "int4: bf16 only");
+    static_assert(!CH || (!QQ && (PRO == PRO_PLAIN || PRO == PRO_PRENORM) &&
                           (EPI == EPI_STORE || EPI == EPI_SWIGLU8 || EPI == EPI_SLABFIN || EPI == EPI_F32)),
                   "no chain form");
     // X items preloaded per thread ahead of the weight ring: PRO_PRENORM's operand is one dim-wide
@@ -147,7 +153,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n0 = bxi * 16;
-    const int Kb = a.K / nks;  // host guarantees a multiple of 32 (64 with Q8)
+    const int Kb = a.K / nks;  // host guarantees a multiple of 32 (64 int8, 128 int4)
     const int kbeg = ks * Kb;
     const int R = a.R;
     const int xstride = Kb + 8;  // +16 B per row: conflict-free ds_read_b128 across rows
@@ -176,7 +182,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
     // loads after the weight ring (the ring never waits on them; in-order vmcnt retires them before
     // the ring's refills).  GEMV_PF 4-byte loads per thread, one per 64-B sector, unconditional and
     // clamped to a valid address when off (a load under a branch drains vmcnt before the MFMAs).
-    constexpr bool PFOK = !CH && !Q8 && (PRO == PRO_NORM || PRO == PRO_PRENORM) && EPI == EPI_STORE;
+    constexpr bool PFOK = !CH && !QQ && (PRO == PRO_NORM || PRO == PRO_PRENORM) && EPI == EPI_STORE;
     constexpr int GEMV_PF = 2;
     int pf_s = 0, pf_p = 0;
     if constexpr (PFOK) {
@@ -208,20 +214,22 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
     };
     unsigned long long tsA = 0, tsB = 0;  // PRO_PRENORM: tile sums staged / X' written
     const int r = lane & 15, g = lane >> 4;
-    constexpr int KU = Q8 ? 64 : 32;  // k per ring slot
+    constexpr int KU = Q4 ? 128 : (Q8 ? 64 : 32);  // k per ring slot
     const int S = a.K / KU, Sb = Kb / KU, sb0 = ks * Sb;
     const int wa = (wave * Sb) / WPB, wb = ((wave + 1) * Sb) / WPB, nmy = wb - wa;
-    typename G::f fa[Q8 ? 1 : U], fb[NACC == 2 ? U : 1];
-    u32x4_t fq[Q8 ? U : 1];
+    typename G::f fa[QQ ? 1 : U], fb[NACC == 2 ? U : 1];
+    u32x4_t fq[QQ ? U : 1];
+    uint32_t fz[Q4 ? U : 1];  // int4: the lane's row (scale, zero) per ring slot
     // Fragment i of the run into ring slot u.  Branch-free on purpose: a load under a branch makes
     // the compiler drain vmcnt(0) before every MFMA (no pipelining at all), so tail slots load a
     // fixed fragment (fm_tune gemv_dummy: one per (block, wave), a cache hit) instead of being
     // predicated off.
     const int ilast = nmy > 0 ? nmy - 1 : 0;
-    const size_t run0 = ((size_t)bxi * S + sb0 + (nmy > 0 ? wa : 0)) * (Q8 ? 1024 : 512);
-    const T* wrun = Q8 ? nullptr : a.W + run0;
+    const size_t run0 = ((size_t)bxi * S + sb0 + (nmy > 0 ? wa : 0)) * (QQ ? 1024 : 512);
+    const T* wrun = QQ ? nullptr : a.W + run0;
     const T* wrun2 = (EPI == EPI_SWIGLU) ? a.W2 + run0 : nullptr;
-    const unsigned char* qrun = Q8 ? a.Wq + run0 : nullptr;
+    const unsigned char* qrun = QQ ? a.Wq + run0 : nullptr;
+    const uint32_t* zrun = Q4 ? a.wsz + (run0 >> 10) * 16 + (lane & 15) : nullptr;
     const bool dtail = a.dummy_tail != 0;
     // dummy_tail 2: the fixed fragment differs per (block, wave) over 256 fragments (no hot line)
     // (bounded by the matrix's own fragment count: ceil(N / 16) tiles x S k-steps)
@@ -229,10 +237,11 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
     auto issue = [&](int i, int u) {
         const size_t ii = (size_t)(i < ilast ? i : ilast);
         const bool past = dtail && i > ilast;  // beyond the run: one fixed (cached) fragment
-        if constexpr (Q8) {
+        if constexpr (QQ) {
             const u32x4_t* p = reinterpret_cast<const u32x4_t*>((past ? a.Wq + dfr * 1024 : qrun + ii * 1024) + lane * 16);
             if constexpr (NT) fq[u] = __builtin_nontemporal_load(p);
             else fq[u] = *p;
+            if constexpr (Q4) fz[u] = past ? a.wsz[dfr * 16 + (lane & 15)] : zrun[ii * 16];
         } else {
             fa[u] = G::template load_w<NT>(past ? a.W + dfr * 512 : wrun + ii * 512, lane);
             if constexpr (NACC == 2) fb[u] = G::template load_w<NT>(past ? a.W + dfr * 512 : wrun2 + ii * 512, lane);
@@ -476,7 +485,12 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (i + u < nmy) {
-                if constexpr (Q8) {
+                if constexpr (Q4) {
+                    const float zs = __uint_as_float(fz[u] << 16), zz = __uint_as_float(fz[u] & 0xffff0000u);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc0 = G::mma(G::dq4(fq[u][j], zs, zz), G::load(xp + (size_t)(i + u) * 128 + 32 * j), acc0);
+                } else if constexpr (Q8) {
                     typename G::f w0, w1;
                     G::dq8(fq[u], w0, w1);
                     acc0 = G::mma(w0, G::load(xp + (size_t)(i + u) * 64), acc0);
@@ -641,10 +655,10 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
     stamp();
 }
 
-template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8>
+template <typename T, int PRO, int EPI, bool NT, int U, int WPB, int QM>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(gemv_wpe(PRO, EPI))))
 void gemv_kernel(GemvArgs<T> a) {
-    gemv_body<T, PRO, EPI, NT, U, WPB, Q8, false>(a, blockIdx.x, blockIdx.y, gridDim.y, ChainWait{});
+    gemv_body<T, PRO, EPI, NT, U, WPB, QM, false>(a, blockIdx.x, blockIdx.y, gridDim.y, ChainWait{});
 }
 
 // One launch running up to GEMV_CHAIN_MAX dependent batch-1 GEMVs (fm_llm.cpp: a layer's wo, w1||w3,
@@ -696,17 +710,17 @@ void gemv_chain_kernel(GemvChainArgs<T> c) {
     }
 }
 
-template <typename T, int PRO, int EPI, bool NT, int U, int WPB, bool Q8 = false>
+template <typename T, int PRO, int EPI, bool NT, int U, int WPB, int QM = 0>
 static void gemv_launch(hipStream_t s, const GemvArgs<T>& a0, dim3 grid, size_t lds) {
     GemvArgs<T> a = a0;
     a.dbg = fm_tuning().dbg;
     static bool big = false;  // > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
     if (lds > 64 * 1024 && !big) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<T, PRO, EPI, NT, U, WPB, Q8>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_kernel<T, PRO, EPI, NT, U, WPB, QM>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         big = true;
     }
-    gemv_kernel<T, PRO, EPI, NT, U, WPB, Q8><<<grid, WPB * 64, lds, s>>>(a);
+    gemv_kernel<T, PRO, EPI, NT, U, WPB, QM><<<grid, WPB * 64, lds, s>>>(a);
 }
 
 template <typename T, int PRO, int EPI, bool NT, int U>
@@ -747,7 +761,18 @@ static void gemv_go(hipStream_t s, const GemvArgs<T>& a, int ksb) {
 template <typename T, int PRO, int EPI>
 static void gemv_go_q8(hipStream_t s, const GemvArgs<T>& a, int ksb) {
     FMCHECK(a.K % (64 * ksb) == 0 && a.wscale, "int8 GEMV: K slices must be whole 64-k units, scales set");
-    gemv_launch<T, PRO, EPI, true, 8, 4, true>(s, a, dim3(FM_CEIL(a.N, 16), ksb), gemv_lds_bytes(a.R, a.K / ksb, sizeof(T)));
+    gemv_launch<T, PRO, EPI, true, 8, 4, 1>(s, a, dim3(FM_CEIL(a.N, 16), ksb), gemv_lds_bytes(a.R, a.K / ksb, sizeof(T)));
+}
+
+// weight-only int4 (bf16): the same configuration over 128-k units
+template <typename T, int PRO, int EPI>
+static void gemv_go_q4(hipStream_t s, const GemvArgs<T>& a, int ksb) {
+    if constexpr (sizeof(T) == 2) {
+        FMCHECK(a.K % (128 * ksb) == 0 && a.wsz && !a.wscale, "int4 GEMV: K slices must be whole 128-k units, (scale, zero) set");
+        gemv_launch<T, PRO, EPI, true, 8, 4, 2>(s, a, dim3(FM_CEIL(a.N, 16), ksb), gemv_lds_bytes(a.R, a.K / ksb, sizeof(T)));
+    } else {
+        FMCHECK(false, "int4 GEMV: bf16 only");
+    }
 }
 
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb) {
@@ -760,14 +785,15 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
     if (a.Wq) {
 #define GQ(P, E)                                           \
     if (pro == P && epi == E) {                            \
-        gemv_go_q8<T, P, E>(s, a, ksb);                    \
+        if (a.wsz) gemv_go_q4<T, P, E>(s, a, ksb);         \
+        else gemv_go_q8<T, P, E>(s, a, ksb);               \
         return;                                            \
     }
         GQ(PRO_PLAIN, EPI_STORE) GQ(PRO_PLAIN, EPI_SLABFIN) GQ(PRO_PLAIN, EPI_F32)
         GQ(PRO_NORM, EPI_STORE) GQ(PRO_NORM, EPI_F32)
         GQ(PRO_PRENORM, EPI_STORE) GQ(PRO_PRENORM, EPI_F32) GQ(PRO_PRENORM, EPI_SWIGLU8)
 #undef GQ
-        FMCHECK(false, "int8 GEMV: no kernel for this prologue / epilogue");
+        FMCHECK(false, "int8 / int4 GEMV: no kernel for this prologue / epilogue");
     }
 #define GO(P, E)                                           \
     if (pro == P && epi == E) {                            \

@@ -23,6 +23,20 @@ template <typename T> void launch_i8_to(hipStream_t s, const int8_t* q, int64_t 
 // int8 row-major [N][K] -> the int8 decode-GEMV layout: [ceil(N/16)][K/64] units of 1 KiB, lane l
 // (row l & 15, k-offset 8 * (l >> 4)) holding 8 bytes of k-step 2u then 8 bytes of k-step 2u + 1
 void launch_pack_q8(hipStream_t s, const int8_t* src, int N, int K, int8_t* dst);
+// Weight-only int4, groupwise affine (tools/llama/quantize.py:57-160, WeightOnlyInt4QuantHandler
+// :352-418), bf16 only.  quant4: per (row, group of gs along K) of a row-major bf16 [N][K] w, the
+// reference's group_quantize_tensor in its bf16 arithmetic (every op computed in fp32 and rounded to
+// bf16, as torch does): scale = bf16(bf16(max - min) clamped to bf16(1e-6) / 15), zero =
+// bf16(min + scale * 8), q = clamp(round_half_even(bf16(bf16(w - (zero - scale * 8)) / scale)), 0, 15);
+// writes q (one code per byte, row-major), sz[n][g] = scale bits | zero bits << 16, and rewrites w
+// with bf16(fma(q - 8, scale, zero)) (the dequantised weight every bf16 kernel then reads).
+void launch_quant4(hipStream_t s, bf16_t* w, int N, int K, int gs, uint8_t* q, uint32_t* sz);
+// codes row-major [N][K] -> the int4 decode-GEMV layout: [ceil(N/16)][K/128] units of 1 KiB, lane l
+// (row l & 15, k-offset 8 * (l >> 4)) holding word j = the 8 codes of k-step j of the unit (nibble e:
+// k = 128 u + 32 j + 8 (l >> 4) + e)
+void launch_pack_q4(hipStream_t s, const uint8_t* q, int N, int K, uint8_t* dst);
+// sz [N][K/gs] -> [ceil(N/16)][K/128][16 rows] (gs a multiple of 128: one group per unit)
+void launch_pack_sz4(hipStream_t s, const uint32_t* sz, int N, int K, int gs, uint32_t* dst);
 
 template <typename T> struct LinearArgs {
     const T* W;      // [N(padded to 16)][K] row-major (nn.Linear layout)
@@ -201,6 +215,9 @@ template <typename T> struct GemvArgs {
     // each output is round(round(acc) * wscale[packed row]) (WeightOnlyInt8Linear, quantize.py:228-229)
     const unsigned char* Wq;
     const T* wscale;
+    // weight-only int4 (bf16): Wq holds 4-bit codes ([tiles][K/128][64 lanes][16 B], launch_pack_q4)
+    // and wsz each (tile, 128-k unit, row)'s group (scale, zero) as bf16 pairs (launch_pack_sz4)
+    const uint32_t* wsz;
     // optional KV prefetch (batch-1 QKV GEMV, fm_tune kv_prefetch): while the weights stream, the
     // cached K / V rows the next attention launch reads (positions 0 .. pos of row 0's slot) are
     // pulled into L2: block b loads kv head b % pf_nkv, which under round-robin workgroup placement
@@ -257,6 +274,7 @@ struct FmTuning {
     int chain_max = 4;       // gemv_chain: GEMVs per launch at most (2..4)
     int chain_sleep = 4;     // gemv_chain: s_sleep argument between a waiting block's polls (1, 4 or 16)
     int gemv_chain = 0;      // 1: batch-1 decode runs wo -> w1||w3 -> w2 -> next qkv as one launch (gemv_chain_kernel)
+    int int4_stream = 1;     // weight-only int4: 1 the batch <= 8 GEMVs stream the 4-bit codes, 0 the dequantised bf16 copy
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
     int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1)
     int pass_mode = 0;       // developer: PassArgs::mode

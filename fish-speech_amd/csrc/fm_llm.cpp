@@ -180,9 +180,11 @@ struct fm_llm {
     std::vector<void*> allocs;
     // weight-only int8 (fm_llm_set_quant): packed T pointer of a linear -> its int8 form
     int quant = FM_QUANT_NONE;
+    int q4_gs = 0;  // int4: group size along K
     struct QInfo {
-        const unsigned char* q8 = nullptr;  // packed int8 decode-GEMV layout
-        const void* scale = nullptr;        // [rows padded to 16] in packed row order
+        const unsigned char* q8 = nullptr;  // packed int8 (int4: 4-bit codes) decode-GEMV layout
+        const void* scale = nullptr;        // int8: [rows padded to 16] in packed row order
+        const uint32_t* sz = nullptr;       // int4: packed (scale, zero) per (tile, 128-k unit, row)
     };
     std::map<const void*, QInfo> qmap;
     const QInfo* qinfo(const void* W) const {
@@ -703,12 +705,22 @@ template <typename T> struct Run {
             chain_flush();
     }
     void gemv_now(GemvArgs<T> a, int pro, int epi, int ksb, const char* cls) {
-        if (const auto* q = m->qinfo(a.W)) {  // weight-only int8: the int8 stream, whole 64-k units per slice
+        int64_t wbytes = (int64_t)a.N * a.K * E * (epi == EPI_SWIGLU ? 2 : 1);
+        const auto* q = m->qinfo(a.W);
+        if (q && q->sz && !fm_tuning().int4_stream) q = nullptr;  // int4 model on its dequantised bf16 weights
+        if (q) {
             a.Wq = q->q8;
-            a.wscale = (const T*)q->scale;
-            while (ksb > 1 && (a.K / ksb) % 64) ksb /= 2;
+            if (q->sz) {  // weight-only int4: 4-bit codes + group (scale, zero), whole 128-k units per slice
+                a.wsz = q->sz;
+                a.wscale = nullptr;
+                while (ksb > 1 && (a.K / ksb) % 128) ksb /= 2;
+                wbytes = (int64_t)a.N * a.K / 2 + (int64_t)(a.N + 15) / 16 * 16 * (a.K / 128) * 4;
+            } else {  // weight-only int8: the int8 stream, whole 64-k units per slice
+                a.wscale = (const T*)q->scale;
+                while (ksb > 1 && (a.K / ksb) % 64) ksb /= 2;
+                wbytes = (int64_t)a.N * a.K;
+            }
         }
-        const int64_t wbytes = (int64_t)a.N * a.K * (a.Wq ? 1 : E) * (epi == EPI_SWIGLU ? 2 : 1);
         const int64_t bytes = wbytes + (int64_t)a.R * a.K * E;
         const double flops = 2.0 * a.R * a.N * a.K * (epi == EPI_SWIGLU ? 2 : 1);
         hipStream_t st = s;
@@ -1311,10 +1323,45 @@ static void* pack_q8_dev(fm_llm* m, const void* q, int rows, int cols) {
     return dst;
 }
 
+// int4: codes row-major [rows][cols] + sz [rows][cols / gs] -> the packed GEMV stream and its
+// (scale, zero) table; none (the bf16 dequantised copy serves every kernel) unless the group size
+// and K are whole 128-k units
+static fm_llm::QInfo pack_q4_dev(fm_llm* m, const void* q, const void* sz, int rows, int cols) {
+    if (m->q4_gs % 128 || cols % 128) return fm_llm::QInfo{};
+    const size_t tiles = (size_t)(rows + 15) / 16;
+    void* dq = nullptr;
+    void* ds = nullptr;
+    HIPCHK(hipMalloc(&dq, tiles * 16 * cols / 2));
+    HIPCHK(hipMalloc(&ds, tiles * (cols / 128) * 16 * 4));
+    launch_pack_q4(m->stream, (const uint8_t*)q, rows, cols, (uint8_t*)dq);
+    launch_pack_sz4(m->stream, (const uint32_t*)sz, rows, cols, m->q4_gs, (uint32_t*)ds);
+    HIPCHK(hipGetLastError());
+    m->allocs.push_back(dq);
+    m->allocs.push_back(ds);
+    return fm_llm::QInfo{(const unsigned char*)dq, nullptr, (const uint32_t*)ds};
+}
+
 // int8 mode, before packing: every quantized linear ends with t.p = T(q) row-major (what the
 // T-fragment kernels read), t.q = int8 row-major, t.s = row scales.  int8 checkpoints supply q and
 // "<name>.scales"; float weights are quantized here with quantize.py's per-channel rule.
 static void quantize_linears(fm_llm* m) {
+    if (m->quant == FM_QUANT_INT4) {  // every linear: codes, group (scale, zero), dequantised bf16 in place
+        for (auto& kv : m->w) {
+            if (!is_quant_linear(kv.first)) continue;
+            DTensor& t = kv.second;
+            const size_t rp = (size_t)(t.rows + 15) / 16 * 16;
+            HIPCHK(hipMalloc(&t.q, rp * t.cols));
+            HIPCHK(hipMemsetAsync(t.q, 8, rp * t.cols, m->stream));
+            void* sz = nullptr;
+            HIPCHK(hipMalloc(&sz, rp * (t.cols / m->q4_gs) * 4));
+            HIPCHK(hipMemsetAsync(sz, 0, rp * (t.cols / m->q4_gs) * 4, m->stream));
+            t.s = sz;
+            launch_quant4(m->stream, (bf16_t*)t.p, (int)t.rows, (int)t.cols, m->q4_gs, (uint8_t*)t.q, (uint32_t*)sz);
+            HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipStreamSynchronize(m->stream));
+        return;
+    }
     for (auto& kv : m->w) {
         if (!is_quant_linear(kv.first)) continue;
         DTensor& t = kv.second;
@@ -1380,7 +1427,26 @@ static void* pack_w13(fm_llm* m, const std::string& p, int inter, int dim) {
     HIPCHK(hipMemcpy2DAsync((char*)tmp + 8 * rb, 16 * rb, t3.p, 8 * rb, 8 * rb, inter / 8, hipMemcpyDeviceToDevice,
                             m->stream));
     void* pk = pack_dev(m, tmp, 2 * inter, dim);
-    if (m->quant) {  // the same interleave of the int8 rows and of the row scales
+    if (m->quant == FM_QUANT_INT4) {  // the same interleave of the code rows and of the (scale, zero) rows
+        const size_t gb = (size_t)(dim / m->q4_gs) * 4;
+        void* qt = nullptr;
+        void* st = nullptr;
+        HIPCHK(hipMalloc(&qt, 2 * (size_t)inter * dim));
+        HIPCHK(hipMalloc(&st, 2 * (size_t)inter * gb));
+        HIPCHK(hipMemcpy2DAsync(qt, 16 * (size_t)dim, t1.q, 8 * (size_t)dim, 8 * (size_t)dim, inter / 8,
+                                hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpy2DAsync((char*)qt + 8 * (size_t)dim, 16 * (size_t)dim, t3.q, 8 * (size_t)dim,
+                                8 * (size_t)dim, inter / 8, hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpy2DAsync(st, 16 * gb, t1.s, 8 * gb, 8 * gb, inter / 8, hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpy2DAsync((char*)st + 8 * gb, 16 * gb, t3.s, 8 * gb, 8 * gb, inter / 8, hipMemcpyDeviceToDevice,
+                                m->stream));
+        const fm_llm::QInfo qi = pack_q4_dev(m, qt, st, 2 * inter, dim);
+        if (qi.q8) m->qmap[pk] = qi;
+        HIPCHK(hipStreamSynchronize(m->stream));
+        for (void* p : {qt, st, t1.q, t3.q, t1.s, t3.s}) HIPCHK(hipFree(p));
+        t1.q = t3.q = nullptr;
+        t1.s = t3.s = nullptr;
+    } else if (m->quant) {  // the same interleave of the int8 rows and of the row scales
         void* qt = nullptr;
         HIPCHK(hipMalloc(&qt, 2 * (size_t)inter * dim));
         HIPCHK(hipMemcpy2DAsync(qt, 16 * (size_t)dim, t1.q, 8 * (size_t)dim, 8 * (size_t)dim, inter / 8,
@@ -1489,7 +1555,15 @@ static void finalize(fm_llm* m) {
         if (!is_linear_weight(kv.first) || is_ffn_w13(kv.first)) continue;  // W1/W3: pack_w13 below
         DTensor& t = kv.second;
         void* pk = pack_dev(m, t.p, (int)t.rows, (int)t.cols);
-        if (m->quant) {
+        if (m->quant == FM_QUANT_INT4) {
+            const fm_llm::QInfo qi = pack_q4_dev(m, t.q, t.s, (int)t.rows, (int)t.cols);
+            if (qi.q8) m->qmap[pk] = qi;
+            HIPCHK(hipStreamSynchronize(m->stream));
+            HIPCHK(hipFree(t.q));
+            HIPCHK(hipFree(const_cast<void*>(t.s)));
+            t.q = nullptr;
+            t.s = nullptr;
+        } else if (m->quant) {
             m->qmap[pk] = fm_llm::QInfo{(const unsigned char*)pack_q8_dev(m, t.q, (int)t.rows, (int)t.cols), t.s};
             HIPCHK(hipStreamSynchronize(m->stream));
             HIPCHK(hipFree(t.q));
@@ -1546,7 +1620,27 @@ static void finalize(fm_llm* m) {
                           m->stream));
     m->head_c = pack_dev(m, head_rm, m->Nhead, c.dim);
     m->allocs.push_back(m->head_c);
-    if (m->quant && !c.tie_word_embeddings) {  // the same compact rows of the int8 head and its scales
+    if (m->quant == FM_QUANT_INT4 && !c.tie_word_embeddings) {  // the compact rows of the codes and groups
+        DTensor& o = m->w.at("output.weight");
+        const size_t gb = (size_t)(c.dim / m->q4_gs) * 4;
+        void* hq = nullptr;
+        void* hs = nullptr;
+        HIPCHK(hipMalloc(&hq, (size_t)(m->Nhead + 15) / 16 * 16 * c.dim));
+        HIPCHK(hipMalloc(&hs, (size_t)(m->Nhead + 15) / 16 * 16 * gb));
+        HIPCHK(hipMemcpyAsync(hq, (const char*)o.q + (size_t)c.semantic_begin_id * c.dim, (size_t)m->nsem * c.dim,
+                              hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpyAsync((char*)hq + (size_t)m->nsem * c.dim, (const char*)o.q + (size_t)c.im_end_id * c.dim,
+                              c.dim, hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpyAsync(hs, (const char*)o.s + (size_t)c.semantic_begin_id * gb, (size_t)m->nsem * gb,
+                              hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpyAsync((char*)hs + (size_t)m->nsem * gb, (const char*)o.s + (size_t)c.im_end_id * gb, gb,
+                              hipMemcpyDeviceToDevice, m->stream));
+        const fm_llm::QInfo qi = pack_q4_dev(m, hq, hs, m->Nhead, c.dim);
+        if (qi.q8) m->qmap[m->head_c] = qi;
+        HIPCHK(hipStreamSynchronize(m->stream));
+        for (void* p : {hq, hs, o.q, o.s}) HIPCHK(hipFree(p));
+        o.q = o.s = nullptr;
+    } else if (m->quant && !c.tie_word_embeddings) {  // the same compact rows of the int8 head and its scales
         DTensor& o = m->w.at("output.weight");
         void* hq = m->dalloc((size_t)(m->Nhead + 15) / 16 * 16 * c.dim);
         HIPCHK(hipMemcpyAsync(hq, (const char*)o.q + (size_t)c.semantic_begin_id * c.dim, (size_t)m->nsem * c.dim,
@@ -1789,7 +1883,31 @@ int fm_llm_open(const fm_model_config* cfg, int device, int precision, int max_s
     });
 }
 
+int fm_llm_set_quant_int4(fm_llm* m, int groupsize) {
+    return fm_guard([&] {
+        FMCHECK(m && (groupsize == 32 || groupsize == 64 || groupsize == 128 || groupsize == 256),
+                "int4: groupsize must be 32, 64, 128 or 256 (WeightOnlyInt4QuantHandler, quantize.py:366)");
+        FMCHECK(!m->finalized, "weights are frozen after finalize");
+        for (auto& kv : m->w) FMCHECK(!kv.second.set, "set the quantization mode before any tensor");
+        FMCHECK(m->quant == FM_QUANT_NONE, "quantization mode already set");
+        FMCHECK(m->prec == FM_PREC_BF16, "int4: bf16 precision only (the reference quantizes the bf16 weights)");
+        const fm_model_config& c = m->c;
+        // create_quantized_state_dict asserts bias-free linears (quantize.py:371)
+        FMCHECK(!c.qkv_bias && !c.o_bias && !c.fast_qkv_bias && !c.fast_o_bias,
+                "int4: the linears must be bias-free (quantize.py:371)");
+        for (auto& kv : m->w) {
+            if (!is_quant_linear(kv.first)) continue;
+            FMCHECK(kv.second.cols % groupsize == 0, "int4: in_features must be a multiple of the group size: " + kv.first);
+            FMCHECK(m->w.find(base_of(kv.first) + ".bias") == m->w.end(),
+                    "int4: the linears must be bias-free (quantize.py:371): " + kv.first);
+        }
+        m->quant = FM_QUANT_INT4;
+        m->q4_gs = groupsize;
+    });
+}
+
 int fm_llm_set_quant(fm_llm* m, int mode) {
+    if (mode == FM_QUANT_INT4) return fm_llm_set_quant_int4(m, 128);
     return fm_guard([&] {
         FMCHECK(m && (mode == FM_QUANT_NONE || mode == FM_QUANT_INT8), "bad arguments");
         FMCHECK(!m->finalized, "weights are frozen after finalize");
@@ -2164,20 +2282,24 @@ int64_t fm_llm_frame_bytes(fm_llm* m, int n, int pos) {
     if (!m) return -1;
     const fm_model_config& c = m->c;
     const int64_t E = (int64_t)m->esz;
-    // weight-only int8: one byte per linear weight plus one T scale per output row
-    const int64_t WE = m->quant ? 1 : E, SE = m->quant ? E : 0;
-    const bool hq = m->quant && !c.tie_word_embeddings;
+    // weight-only int8: one byte per linear weight plus one T scale per output row; int4 (streamed
+    // form): half a byte per weight plus one (scale, zero) word per row and 128-k unit
+    const bool q4 = m->quant == FM_QUANT_INT4 && m->q4_gs % 128 == 0;
+    auto lin = [&](int64_t N, int64_t K) -> int64_t {
+        if (q4 && K % 128 == 0) return N * K / 2 + N * (K / 128) * 4;
+        if (m->quant == FM_QUANT_INT8) return N * K + N * E;
+        return N * K * E;
+    };
     auto stack_bytes = [&](const StackDims& d) {
-        const int64_t lin = (int64_t)d.nqkv() * d.dim + (int64_t)d.dim * d.nq() + 3LL * d.inter * d.dim;
-        const int64_t rows = (int64_t)d.nqkv() + d.dim + 3LL * d.inter;
-        int64_t per = lin * WE + rows * SE + 2LL * d.dim * E;
+        int64_t per = lin(d.nqkv(), d.dim) + lin(d.dim, d.nq()) + lin(2LL * d.inter, d.dim) + lin(d.dim, d.inter) +
+                      2LL * d.dim * E;
         if (d.qk_norm) per += 2LL * d.hd * E;
         return per * d.n_layer;
     };
-    int64_t b = stack_bytes(m->sd) + (int64_t)m->Nhead * (c.dim * (hq ? 1 : E) + (hq ? E : 0)) + (int64_t)c.dim * E;
-    b += (int64_t)m->C * stack_bytes(m->fdm) +
-         (int64_t)(m->C - 1) * ((int64_t)m->cb * (c.fast_dim * WE + SE) + (int64_t)c.fast_dim * E);
-    if (m->fproj_w) b += (int64_t)c.fast_dim * (c.dim * WE + SE);
+    int64_t b = stack_bytes(m->sd) + (c.tie_word_embeddings ? (int64_t)m->Nhead * c.dim * E : lin(m->Nhead, c.dim)) +
+                (int64_t)c.dim * E;
+    b += (int64_t)m->C * stack_bytes(m->fdm) + (int64_t)(m->C - 1) * (lin(m->cb, c.fast_dim) + (int64_t)c.fast_dim * E);
+    if (m->fproj_w) b += lin(c.fast_dim, c.dim);
     // per-stream: KV reads (+ the row written), embeddings
     int64_t per_stream = 2LL * m->sd.n_layer * m->sd.nkv * m->sd.hd * E * (pos + 1);
     for (int cc = 0; cc < m->C; ++cc) per_stream += 2LL * m->fdm.n_layer * m->fdm.nkv * m->fdm.hd * E * (cc + 1);
@@ -2300,6 +2422,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "bstream_nw") {
             FMCHECK(value >= 0 && value <= 16, "bstream_nw must be in [0, 16]");
             t.bstream_nw = value;
+        } else if (k == "int4_stream") {
+            t.int4_stream = value != 0;
         } else if (k == "pass_fast") {
             t.pass_fast = value != 0;
         } else if (k == "pass_cfg") {

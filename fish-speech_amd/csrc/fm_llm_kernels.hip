@@ -246,6 +246,81 @@ void launch_pack_q8(hipStream_t s, const int8_t* src, int N, int K, int8_t* dst)
     const int64_t n = (int64_t)((N + 15) / 16) * (K / 64) * 64;
     pack_q8_kernel<<<(int)std::min<int64_t>(FM_CEIL(n, 256), 16384), 256, 0, s>>>(src, N, K, dst);
 }
+// ---- weight-only int4 (tools/llama/quantize.py:57-160) --------------------------------------
+// one thread per (row, group): get_group_qparams + group_quantize_tensor_from_qparams in torch's bf16
+// arithmetic (fp32 op, bf16 rounding after every op), then the dequantised bf16 weight in place
+__global__ void quant4_kernel(bf16_t* __restrict__ w, int N, int K, int gs, uint8_t* __restrict__ q,
+                              uint32_t* __restrict__ sz) {
+    const int ng = K / gs;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)N * ng) return;
+    const int n = (int)(idx / ng), gi = (int)(idx - (int64_t)n * ng);
+    bf16_t* p = w + (size_t)n * K + (size_t)gi * gs;
+    uint8_t* qp = q + (size_t)n * K + (size_t)gi * gs;
+    auto rb = [](float x) { return bf2f(f2bf(x)); };
+    float mn = INFINITY, mx = -INFINITY;
+    for (int k = 0; k < gs; ++k) {
+        const float v = bf2f(p[k]);
+        mn = fminf(mn, v);
+        mx = fmaxf(mx, v);
+    }
+    const float d = fmaxf(rb(mx - mn), rb(1e-6f));  // (max - min).clamp(min=1e-6) in bf16
+    const float sc = rb(d / 15.f);                   // / max_int
+    const float s8 = rb(sc * 8.f);
+    const float zr = rb(mn + s8);                    // zeros = min + scales * 2^(n_bit - 1)
+    const float lo = rb(zr - s8);                    // min_val of from_qparams
+    for (int k = 0; k < gs; ++k) {
+        const float x = rb(rb(bf2f(p[k]) - lo) / sc);
+        const float qv = fminf(fmaxf(rintf(x), 0.f), 15.f);
+        qp[k] = (uint8_t)qv;
+        p[k] = f2bf(__fmaf_rn(qv - 8.f, sc, zr));
+    }
+    sz[idx] = (uint32_t)__builtin_bit_cast(uint16_t, f2bf(sc)) | ((uint32_t)__builtin_bit_cast(uint16_t, f2bf(zr)) << 16);
+}
+void launch_quant4(hipStream_t s, bf16_t* w, int N, int K, int gs, uint8_t* q, uint32_t* sz) {
+    const int64_t n = (int64_t)N * (K / gs);
+    quant4_kernel<<<(int)FM_CEIL(n, 256), 256, 0, s>>>(w, N, K, gs, q, sz);
+}
+// one thread per (unit, lane): word j of its 16 bytes = the 8 codes of k-step j (nibble e = k e)
+__global__ void pack_q4_kernel(const uint8_t* __restrict__ q, int N, int K, uint8_t* __restrict__ dst) {
+    const int U = K >> 7;
+    const int64_t n = (int64_t)((N + 15) / 16) * U * 64;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t unit = i >> 6;
+        const int l = (int)(i & 63);
+        const int t = (int)(unit / U), u = (int)(unit - (int64_t)t * U);
+        const int row = 16 * t + (l & 15);
+        uint32_t wd[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                v |= (uint32_t)(row < N ? q[(size_t)row * K + 128 * u + 32 * j + 8 * (l >> 4) + e] & 15 : 8) << (4 * e);
+            wd[j] = v;
+        }
+        *reinterpret_cast<u32x4_t*>(dst + i * 16) = (u32x4_t){wd[0], wd[1], wd[2], wd[3]};
+    }
+}
+void launch_pack_q4(hipStream_t s, const uint8_t* q, int N, int K, uint8_t* dst) {
+    const int64_t n = (int64_t)((N + 15) / 16) * (K / 128) * 64;
+    pack_q4_kernel<<<(int)std::min<int64_t>(FM_CEIL(n, 256), 16384), 256, 0, s>>>(q, N, K, dst);
+}
+__global__ void pack_sz4_kernel(const uint32_t* __restrict__ sz, int N, int K, int gs, uint32_t* __restrict__ dst) {
+    const int U = K >> 7, ng = K / gs;
+    const int64_t n = (int64_t)((N + 15) / 16) * U * 16;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t tu = i >> 4;
+        const int r = (int)(i & 15);
+        const int t = (int)(tu / U), u = (int)(tu - (int64_t)t * U);
+        const int row = 16 * t + r;
+        dst[i] = row < N ? sz[(size_t)row * ng + (128 * u) / gs] : 0u;
+    }
+}
+void launch_pack_sz4(hipStream_t s, const uint32_t* sz, int N, int K, int gs, uint32_t* dst) {
+    const int64_t n = (int64_t)((N + 15) / 16) * (K / 128) * 16;
+    pack_sz4_kernel<<<(int)std::min<int64_t>(FM_CEIL(n, 256), 16384), 256, 0, s>>>(sz, N, K, gs, dst);
+}
 template void launch_quant_rows<bf16_t>(hipStream_t, bf16_t*, int, int, int8_t*, bf16_t*);
 template void launch_quant_rows<float>(hipStream_t, float*, int, int, int8_t*, float*);
 template void launch_i8_to<bf16_t>(hipStream_t, const int8_t*, int64_t, bf16_t*);

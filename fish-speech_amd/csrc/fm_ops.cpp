@@ -18,6 +18,7 @@
 // caller's business: pass bf16-valued floats for bit-level comparisons).
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <string.h>
 
 #include <algorithm>
 #include <vector>
@@ -395,6 +396,78 @@ int fm_op_embed(int device, int precision, const int32_t* tok, int R, const floa
         else
             embed_t<float>(g.s, tok, R, emb, vocab, cbemb, dim, num_codebooks, codebook_size, semantic_begin_id,
                            semantic_end_id, scale_codebook_embeddings, x);
+    });
+}
+
+// weight-only int4: the device quantizer (launch_quant4) on a caller bf16 matrix, then the decode
+// GEMV on R rows of x three ways: the streamed int4 codes (when gs % 128 == 0), the bf16 weights it
+// dequantised to, and (for reference) nothing else -- y_q4 / y_bf16 are [R][N] fp32 (EPI_F32)
+int fm_op_quant4(int device, const float* w, int N, int K, int gs, uint8_t* q, float* scale, float* zero,
+                 float* w_deq, const float* x, int R, float* y_q4, float* y_bf16) {
+    return fm_guard([&] {
+        FMCHECK(w && q && scale && zero && w_deq && N >= 1 && gs >= 2 && K % gs == 0, "bad arguments");
+        FMCHECK(!x || (R >= 1 && R <= 8 && K % 32 == 0 && y_bf16), "bad GEMV arguments");
+        StreamGuard g(device);
+        DevBufs b(g.s);
+        const int Np = (N + 15) / 16 * 16;
+        bf16_t* dw = (bf16_t*)b.alloc((size_t)Np * K * 2);
+        {
+            bf16_t* t = b.upload<bf16_t>(w, (size_t)N * K);
+            HIPCHK(hipMemcpyAsync(dw, t, (size_t)N * K * 2, hipMemcpyDeviceToDevice, g.s));
+        }
+        uint8_t* dq = (uint8_t*)b.alloc((size_t)Np * K);
+        uint32_t* dsz = (uint32_t*)b.alloc((size_t)Np * (K / gs) * 4);
+        launch_quant4(g.s, dw, N, K, gs, dq, dsz);
+        HIPCHK(hipGetLastError());
+        std::vector<uint16_t> hw((size_t)N * K);
+        std::vector<uint32_t> hs((size_t)N * (K / gs));
+        HIPCHK(hipMemcpyAsync(q, dq, (size_t)N * K, hipMemcpyDeviceToHost, g.s));
+        HIPCHK(hipMemcpyAsync(hw.data(), dw, hw.size() * 2, hipMemcpyDeviceToHost, g.s));
+        HIPCHK(hipMemcpyAsync(hs.data(), dsz, hs.size() * 4, hipMemcpyDeviceToHost, g.s));
+        HIPCHK(hipStreamSynchronize(g.s));
+        for (size_t i = 0; i < hw.size(); ++i) {
+            const uint32_t u = (uint32_t)hw[i] << 16;
+            memcpy(&w_deq[i], &u, 4);
+        }
+        for (size_t i = 0; i < hs.size(); ++i) {
+            const uint32_t us = hs[i] << 16, uz = hs[i] & 0xffff0000u;
+            memcpy(&scale[i], &us, 4);
+            memcpy(&zero[i], &uz, 4);
+        }
+        if (!x) return;
+        // the decode GEMV: packed bf16 fragments of the dequantised weights, and the int4 stream
+        bf16_t* pk = (bf16_t*)b.alloc((size_t)Np * K * 2);
+        launch_pack<bf16_t>(g.s, dw, N, K, pk);
+        bf16_t* dx = b.upload<bf16_t>(x, (size_t)R * K);
+        float* dy = (float*)b.alloc((size_t)R * N * 4);
+        int* tk = (int*)b.alloc((size_t)(Np / 16 + 16) * 4);
+        GemvArgs<bf16_t> a{};
+        a.W = pk;
+        a.X = dx;
+        a.ldx = K;
+        a.R = R;
+        a.N = N;
+        a.K = K;
+        a.Yf = dy;
+        a.ldy = N;
+        a.tickets = tk;
+        a.eps = 1e-6f;
+        launch_gemv<bf16_t>(g.s, a, PRO_PLAIN, EPI_F32, 1);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(y_bf16, dy, (size_t)R * N * 4, hipMemcpyDeviceToHost, g.s));
+        HIPCHK(hipStreamSynchronize(g.s));
+        if (y_q4 && gs % 128 == 0 && K % 128 == 0) {
+            uint8_t* q4 = (uint8_t*)b.alloc((size_t)Np * K / 2);
+            uint32_t* sz4 = (uint32_t*)b.alloc((size_t)(Np / 16) * (K / 128) * 16 * 4);
+            launch_pack_q4(g.s, dq, N, K, q4);
+            launch_pack_sz4(g.s, dsz, N, K, gs, sz4);
+            a.Wq = q4;
+            a.wsz = sz4;
+            launch_gemv<bf16_t>(g.s, a, PRO_PLAIN, EPI_F32, 1);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(y_q4, dy, (size_t)R * N * 4, hipMemcpyDeviceToHost, g.s));
+            HIPCHK(hipStreamSynchronize(g.s));
+        }
     });
 }
 

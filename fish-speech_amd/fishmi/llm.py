@@ -45,7 +45,7 @@ def resolve_im_end_id(path) -> Optional[int]:
 
 class DualARModel:
     def __init__(self, cfg: DualARConfig, device: int = 0, precision: str = "bf16",
-                 max_slots: int = 1, quant: Optional[str] = None):
+                 max_slots: int = 1, quant: Optional[str] = None, groupsize: int = 128):
         if cfg.im_end_id < 0:
             raise ValueError("config.im_end_id must be set (tokenizer's <|im_end|> id)")
         self.cfg = cfg
@@ -61,18 +61,23 @@ class DualARModel:
         prec = native.FM_PREC_BF16 if precision == "bf16" else native.FM_PREC_FP32
         native.check(L.fm_llm_open(ctypes.byref(self._c), device, prec, max_slots, ctypes.byref(h)))
         self.h = h
-        if quant not in (None, "int8"):
-            raise ValueError(f"quant must be None or 'int8', got {quant!r}")
+        if quant not in (None, "int8", "int4"):
+            raise ValueError(f"quant must be None, 'int8' or 'int4', got {quant!r}")
         self.quant = quant
         if quant == "int8":  # WeightOnlyInt8QuantHandler.convert_for_runtime (llama.py:528-535)
             native.check(L.fm_llm_set_quant(h, native.FM_QUANT_INT8))
+        elif quant == "int4":  # WeightOnlyInt4QuantHandler(model, groupsize) (llama.py:537-543), bf16 weights
+            native.check(L.fm_llm_set_quant_int4(h, int(groupsize)))
         self._finalized = False
         self.tokenizer = None  # FishTokenizer when loaded from a checkpoint with tokenizer.json
 
     # ---- construction --------------------------------------------------------------
     @classmethod
     def from_pretrained(cls, path, device: int = 0, precision: str = "bf16", max_slots: int = 1,
-                        max_length: Optional[int] = None, im_end_id: Optional[int] = None):
+                        max_length: Optional[int] = None, im_end_id: Optional[int] = None,
+                        quant: Optional[str] = None, groupsize: int = 128):
+        """quant="int4": quantize the bf16 checkpoint's linears at load (the reference's quantize.py
+        --mode int4 --groupsize g, then its int4 runtime); int8 checkpoints are detected."""
         cfg = DualARConfig.from_pretrained(path)
         if max_length is not None:
             cfg.max_seq_len = max_length
@@ -89,8 +94,14 @@ class DualARModel:
             raise ValueError(f"cannot resolve <|im_end|> id: no tokenizer.json in {path}; pass im_end_id")
         cfg.im_end_id = im
         weights = load_llm_weights(path)
-        quant = "int8" if any(t.int8 for t in weights.values()) else None
-        m = cls(cfg, device, precision, max_slots, quant)
+        if any(k.endswith("scales_and_zeros") for k in weights):
+            raise ValueError("int4 checkpoints hold torch's _convert_weight_to_int4pack tiles (quantize.py:239-247), "
+                             "which this build does not read: load the bf16 checkpoint with quant='int4'")
+        if any(t.int8 for t in weights.values()):
+            if quant == "int4":
+                raise ValueError("int4 quantization needs a float checkpoint, this one is int8")
+            quant = "int8"
+        m = cls(cfg, device, precision, max_slots, quant, groupsize)
         m.load_weights(weights)
         m.finalize()
         m.tokenizer = tok
@@ -98,10 +109,11 @@ class DualARModel:
 
     @classmethod
     def synthetic(cls, cfg: DualARConfig, seed: int, log2_half: int = 5, device: int = 0,
-                  precision: str = "bf16", max_slots: int = 1, quant: Optional[str] = None):
+                  precision: str = "bf16", max_slots: int = 1, quant: Optional[str] = None,
+                  groupsize: int = 128):
         """Seeded weights at cfg's shapes; quant="int8" quantizes the linears at finalize with
-        quantize.py's per-channel rule."""
-        m = cls(cfg, device, precision, max_slots, quant)
+        quantize.py's per-channel rule, quant="int4" with its groupwise rule (groupsize)."""
+        m = cls(cfg, device, precision, max_slots, quant, groupsize)
         m.synth(seed, log2_half)
         m.finalize()
         return m

@@ -15,13 +15,13 @@ LIB_PATH = os.path.join(HERE, "libfishmi.so")
 
 FM_PREC_BF16, FM_PREC_FP32 = 0, 1
 FM_DT_F32, FM_DT_BF16, FM_DT_I8 = 0, 1, 2
-FM_QUANT_NONE, FM_QUANT_INT8 = 0, 1
+FM_QUANT_NONE, FM_QUANT_INT8, FM_QUANT_INT4 = 0, 1, 2
 
 _lib = None
 
 # every symbol include/fishmi.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = [
-    "fm_device_count", "fm_last_error", "fm_llm_open", "fm_llm_set_quant", "fm_llm_set_tensor", "fm_llm_synth_tensor",
+    "fm_device_count", "fm_last_error", "fm_stream_peak", "fm_llm_open", "fm_llm_set_quant", "fm_llm_set_quant_int4", "fm_llm_set_tensor", "fm_llm_synth_tensor",
     "fm_llm_finalize", "fm_llm_prefill", "fm_llm_prefill_batch", "fm_llm_decode", "fm_llm_decode_frames", "fm_llm_generate", "fm_llm_generate_at", "fm_llm_prefill_at", "fm_llm_slot_pos", "fm_llm_teacher_step",
     "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph", "fm_llm_debug_vec", "fm_tune", "fm_debug_ts_read",
     "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
@@ -29,7 +29,7 @@ ABI_SYMBOLS = [
     "fm_codec_stream_open", "fm_codec_stream_decode", "fm_codec_stream_close",
     "fm_codec_profile_read", "fm_codec_debug_read", "fm_codec_enable_encoder", "fm_codec_encode",
     "fm_codec_close", "fm_llm_force", "fm_llm_read_logits", "fm_op_rmsnorm", "fm_op_qk_rope", "fm_op_decode_attn", "fm_op_prompt_attn",
-    "fm_op_embed", "fm_rope_table",
+    "fm_op_embed", "fm_op_quant4", "fm_rope_table",
 ]
 
 
@@ -65,8 +65,10 @@ def lib():
     pf32 = ctypes.POINTER(ctypes.c_float)
     L.fm_last_error.restype = ctypes.c_char_p
     L.fm_device_count.restype = i32
+    L.fm_stream_peak.argtypes = [i32, i64, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
     L.fm_llm_open.argtypes = [vp, i32, i32, i32, ctypes.POINTER(vp)]
     L.fm_llm_set_quant.argtypes = [vp, i32]
+    L.fm_llm_set_quant_int4.argtypes = [vp, i32]
     L.fm_llm_set_tensor.argtypes = [vp, ctypes.c_char_p, vp, i32, i64]
     L.fm_llm_synth_tensor.argtypes = [vp, ctypes.c_char_p, i64, u64, f32, i32]
     L.fm_llm_finalize.argtypes = [vp]
@@ -101,6 +103,8 @@ def lib():
     L.fm_op_decode_attn.argtypes = [i32, i32, i32, pf32, i32, i32, i32, i32, pf32, pf32, i32, f32, f32, pi32, pf32,
                                     pf32, i32, i32, pf32, pf32, pf32]
     L.fm_op_embed.argtypes = [i32, i32, pi32, i32, pf32, i32, pf32, i32, i32, i32, i32, i32, i32, pf32]
+    L.fm_op_quant4.argtypes = [i32, pf32, i32, i32, i32, ctypes.POINTER(ctypes.c_uint8), pf32, pf32, pf32, pf32, i32,
+                               pf32, pf32]
     L.fm_rope_table.argtypes = [i32, i32, f32, pf32]
     if hasattr(L, "fm_codec_open"):
         L.fm_codec_open.argtypes = [vp, i32, i32, i32, ctypes.POINTER(vp)]
@@ -132,6 +136,13 @@ def check(rc: int):
 
 def device_count() -> int:
     return lib().fm_device_count()
+
+
+def stream_peak(device: int = 0, nbytes: int = 2 << 30, reps: int = 10):
+    """(read GB/s, copy GB/s) of the measured HBM stream peak (fm_stream_peak)."""
+    r, c = ctypes.c_double(), ctypes.c_double()
+    check(lib().fm_stream_peak(int(device), int(nbytes), int(reps), ctypes.byref(r), ctypes.byref(c)))
+    return r.value, c.value
 
 
 def i32p(a: np.ndarray):

@@ -10,6 +10,8 @@ Reference semantics pinned (file:line in PoTaTo-Mika/fish-speech):
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
 from . import native
@@ -114,3 +116,29 @@ def rope_table(seq_len, head_dim, base):
     out = np.zeros((seq_len, head_dim // 2, 2), np.float32)
     native.check(native.lib().fm_rope_table(seq_len, head_dim, float(base), native.f32p(out)))
     return out
+
+
+def quant4(w, gs, x=None, device=0):
+    """fm_op_quant4: (q [N][K] uint8, scale [N][K/gs], zero [N][K/gs], dequantised w [N][K]) from the
+    device int4 quantizer, and with x ([R][K]) the decode GEMV on the dequantised bf16 weights and on
+    the streamed 4-bit codes: (..., y_bf16 [R][N], y_q4 [R][N] or None)."""
+    w = np.ascontiguousarray(w, np.float32)
+    N, K = w.shape
+    q = np.zeros((N, K), np.uint8)
+    sc = np.zeros((N, K // gs), np.float32)
+    zr = np.zeros((N, K // gs), np.float32)
+    wd = np.zeros((N, K), np.float32)
+    if x is None:
+        native.check(native.lib().fm_op_quant4(device, native.f32p(w), N, K, gs,
+                                               q.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                               native.f32p(sc), native.f32p(zr), native.f32p(wd), None, 0, None, None))
+        return q, sc, zr, wd
+    x = np.ascontiguousarray(x, np.float32).reshape(-1, K)
+    R = x.shape[0]
+    yb = np.zeros((R, N), np.float32)
+    y4 = np.zeros((R, N), np.float32) if (gs % 128 == 0 and K % 128 == 0) else None
+    native.check(native.lib().fm_op_quant4(device, native.f32p(w), N, K, gs,
+                                           q.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), native.f32p(sc),
+                                           native.f32p(zr), native.f32p(wd), native.f32p(x), R,
+                                           native.f32p(y4) if y4 is not None else None, native.f32p(yb)))
+    return q, sc, zr, wd, yb, y4

@@ -58,6 +58,7 @@ extern "C" {
 /* weight-only quantization of the Dual-AR linears (fm_llm_set_quant) */
 #define FM_QUANT_NONE 0
 #define FM_QUANT_INT8 1
+#define FM_QUANT_INT4 2  /* groupwise int4, group size 128 (fm_llm_set_quant_int4 for others) */
 
 /* == DualARModelArgs after from_pretrained (llama.py:27-193); im_end_id from the tokenizer. */
 typedef struct fm_model_config {
@@ -86,6 +87,11 @@ typedef struct fm_llm fm_llm;
 
 int fm_device_count(void);
 const char* fm_last_error(void);
+/* Measured HBM stream peak of `device` (no reference counterpart: SURVEY.md §8d's STREAM-like
+   figure beside the vendor peak): a non-temporal float4 read stream (GB/s read) and a float4 copy
+   (GB/s read + written) over `bytes`-sized buffers (>= 64 MiB; use >> 256 MiB to defeat the MALL),
+   `reps` timed launches each. */
+int fm_stream_peak(int device, int64_t bytes, int reps, double* read_gbps, double* copy_gbps);
 
 int fm_llm_open(const fm_model_config* cfg, int device, int precision, int max_slots,
                 fm_llm** out);
@@ -99,6 +105,15 @@ int fm_llm_open(const fm_model_config* cfg, int device, int precision, int max_s
    (that module has none).  Off the bf16 parity contract: parity is against the reference's own
    int8 model. */
 int fm_llm_set_quant(fm_llm* h, int mode);
+/* Weight-only int4, groupwise affine (replaces tools/llama/quantize.py WeightOnlyInt4QuantHandler
+   .create_quantized_state_dict + convert_for_runtime and the int4 branch of from_pretrained,
+   llama.py:537-543; quantize.py:57-160, 239-418).  bf16 only; bias-free linears (quantize.py:371);
+   groupsize 32, 64, 128 or 256 dividing every in_features.  Every nn.Linear takes float weights, quantized at
+   finalize with the reference's group_quantize_tensor (bit-exact, in its bf16 arithmetic); each
+   then computes with the weights bf16(fma(q - 8, scale, zero)), and the batch <= 8 decode GEMVs
+   stream the 4-bit codes (group size a multiple of 128).  The reference's packed checkpoint format
+   (_convert_weight_to_int4pack tiles) is not read: quantize from the bf16 checkpoint instead. */
+int fm_llm_set_quant_int4(fm_llm* h, int groupsize);
 /* name = reference state_dict key after remap (e.g. "layers.3.attention.wqkv.weight") */
 int fm_llm_set_tensor(fm_llm* h, const char* name, const void* host_data, int src_dtype,
                       int64_t numel);
@@ -228,6 +243,13 @@ int fm_op_prompt_attn(int device, int precision, int kernel, const float* q, int
 int fm_op_embed(int device, int precision, const int32_t* tok, int R, const float* emb, int vocab,
                 const float* cbemb, int dim, int num_codebooks, int codebook_size, int semantic_begin_id,
                 int semantic_end_id, int scale_codebook_embeddings, float* x);
+/* Weight-only int4 (fm_llm_set_quant_int4): the device quantizer on a bf16-valued w [N][K] with group
+   size gs (quantize.py:57-160 in its bf16 arithmetic): codes q [N][K] (0..15), group scale / zero
+   [N][K/gs] and the dequantised weights bf16(fma(q - 8, scale, zero)) [N][K].  With x (R <= 8 rows
+   of K), also the decode GEMV y = x . w_deq^T ([R][N] fp32) on the dequantised bf16 weights (y_bf16)
+   and, when gs and K are multiples of 128 and y_q4 is given, on the streamed 4-bit codes (y_q4). */
+int fm_op_quant4(int device, const float* w, int N, int K, int gs, uint8_t* q, float* scale, float* zero,
+                 float* w_deq, const float* x, int R, float* y_q4, float* y_bf16);
 /* the RoPE cos/sin table the library builds on the host (precompute_freqs_cis, llama.py:1003-1022):
    out [seq_len][head_dim/2][2], bf16-valued floats.  No device needed. */
 int fm_rope_table(int seq_len, int head_dim, float base, float* out);

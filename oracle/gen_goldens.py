@@ -678,7 +678,9 @@ def _bf16_bits(x: np.ndarray) -> np.ndarray:
     return b
 
 
-def _timed_case(out_name, config, T, n_new, prompt_seed):
+def _timed_case(out_name, config, T, n_new, prompt_seed, fast_last_only=False):
+    """fast_last_only: keep the fast logits of the last codebook only (long runs: its pass reads
+    every fast cache position), as fast_last_bits / fast_last_f32."""
     from fish_speech.models.text2semantic import inference
 
     t0 = time.time()
@@ -697,12 +699,13 @@ def _timed_case(out_name, config, T, n_new, prompt_seed):
     s32, f32, _ = teacher_forced(m32, seq, T, n, torch.float32)
     del m32
     keep = np.r_[IM_END_ID, cfg.semantic_begin_id:cfg.semantic_end_id + 1]
+    fast_fields = dict(fast_last_bits=_bf16_bits(fast[:, -1]), fast_last_f32=f32[:, -1]) if fast_last_only else \
+        dict(fast_logits_bits=_bf16_bits(fast), fast_logits_f32=f32)
     np.savez_compressed(os.path.join(GOLD, f"{out_name}.npz"), config=np.array(json.dumps(config)),
                         prompt=prompt.numpy().astype(np.int32), seq=seq.numpy().astype(np.int32),
                         slow_rows=keep.astype(np.int32), slow_logits_bits=_bf16_bits(slow[:, keep]),
-                        fast_logits_bits=_bf16_bits(fast), slow_logits_f32=s32[:, keep], fast_logits_f32=f32,
-                        synth_seed=41, log2_half=5, torch_version=torch.__version__,
-                        threads=torch.get_num_threads())
+                        slow_logits_f32=s32[:, keep], synth_seed=41, log2_half=5,
+                        torch_version=torch.__version__, threads=torch.get_num_threads(), **fast_fields)
     e_s = np.abs(slow[:, keep] - s32[:, keep])
     print(f"{out_name}: T={T}, {n} frames in {time.time() - t0:.0f}s; reference bf16-vs-fp32 slow logits max "
           f"{e_s.max():.4g} rms {np.sqrt((e_s ** 2).mean()):.4g}; first cols", seq[:, T:T + 2].T.tolist())
@@ -713,10 +716,29 @@ def cmd_llm_full():
     _timed_case("llm_full_bf16", _wide_config(36, 4, 128), T=64, n_new=9, prompt_seed=3)
 
 
+def cmd_llm_full64():
+    """Config 2 at full depth over 64 decode frames (positions 64..128): prefill + 64 frames,
+    every frame's slow logits and the last codebook's fast logits."""
+    _timed_case("llm_full64_bf16", _wide_config(36, 4, 160), T=64, n_new=65, prompt_seed=7, fast_last_only=True)
+
+
+def cmd_llm_long4():
+    """A 3000-token context through 4 slow layers (+ 1 fast) at S2-Pro widths."""
+    _timed_case("llm_long4_bf16", _wide_config(4, 1, 3072), T=3000, n_new=7, prompt_seed=9)
+
+
 def cmd_llm_long():
     """A 3000-token context at S2-Pro widths (2 slow + 1 fast layers): every decode frame's slow
     attention spans many flash-decode splits."""
     _timed_case("llm_long_bf16", _wide_config(2, 1, 3072), T=3000, n_new=7, prompt_seed=5)
+
+
+def cmd_llm_ragged64():
+    """Config 3's ragged batch over 64 decode frames (positions up to 256 + 64): the same 32
+    prompt lengths as llm_ragged, each run by the reference at batch 1; greedy columns for all 65
+    frames, teacher-forced logits (slow rows + the last codebook's fast logits) kept at frames 0,
+    32 and 64 (the file stays small; the GPU run teacher-forces every frame in between)."""
+    _ragged_case("llm_ragged64_bf16", n_new=65, keep_frames=(0, 32, 64), max_seq_len=336, prompt_seed0=200)
 
 
 def cmd_llm_ragged():
@@ -724,10 +746,14 @@ def cmd_llm_ragged():
     uniform over 16..256 (seed 2), each run by the reference at batch 1 (its only
     mode): greedy columns + teacher-forced logits for the prefill frame and 2 decode frames.  Fast
     logits are kept for the last codebook only (its pass reads every fast cache position)."""
+    _ragged_case("llm_ragged_bf16", n_new=3, keep_frames=(0, 1, 2), max_seq_len=272, prompt_seed0=100)
+
+
+def _ragged_case(out_name, n_new, keep_frames, max_seq_len, prompt_seed0):
     from fish_speech.models.text2semantic import inference
 
-    B, n_new = 32, 3
-    config = _wide_config(2, 1, 272)
+    B = 32
+    config = _wide_config(2, 1, max_seq_len)
     lens = np.random.default_rng(2).integers(16, 257, B)
     t0 = time.time()
     cfg, state = _llm_state(config, 41, 5)
@@ -735,11 +761,12 @@ def cmd_llm_ragged():
     m32 = _llm_from_state(cfg, state, torch.float32)
     del state
     keep = np.r_[IM_END_ID, cfg.semantic_begin_id:cfg.semantic_end_id + 1]
+    kf = list(keep_frames)
     res = {k: [] for k in ("seq", "slow_bits", "fast_bits", "slow_f32", "fast_f32")}
     prompts = {}
     for i, T in enumerate(lens):
         T = int(T)
-        prompt = make_prompt(cfg, T, 100 + i)
+        prompt = make_prompt(cfg, T, prompt_seed0 + i)
         prompts[f"prompt_{i}"] = prompt.numpy().astype(np.int32)
         seq = inference.generate(model=model, prompt=prompt.clone(), max_new_tokens=n_new, audio_masks=None,
                                  audio_parts=None, temperature=0.7, top_p=0.9, top_k=1)
@@ -747,17 +774,19 @@ def cmd_llm_ragged():
         slow, fast, _ = teacher_forced(model, seq, T, n_new, torch.bfloat16)
         s32, f32, _ = teacher_forced(m32, seq, T, n_new, torch.float32)
         res["seq"].append(seq[:, T:].numpy().astype(np.int32))
-        res["slow_bits"].append(_bf16_bits(slow[:, keep]))
-        res["fast_bits"].append(_bf16_bits(fast[:, -1]))
-        res["slow_f32"].append(s32[:, keep])
-        res["fast_f32"].append(f32[:, -1])
-    np.savez_compressed(os.path.join(GOLD, "llm_ragged_bf16.npz"), config=np.array(json.dumps(config)),
+        res["slow_bits"].append(_bf16_bits(slow[kf][:, keep]))
+        res["fast_bits"].append(_bf16_bits(fast[kf][:, -1]))
+        res["slow_f32"].append(s32[kf][:, keep])
+        res["fast_f32"].append(f32[kf][:, -1])
+        print(f"{out_name}: prompt {i} (T={T}) done at {time.time() - t0:.0f}s", flush=True)
+    np.savez_compressed(os.path.join(GOLD, f"{out_name}.npz"), config=np.array(json.dumps(config)),
                         lens=lens.astype(np.int32), cols=np.stack(res["seq"]), slow_rows=keep.astype(np.int32),
+                        keep_frames=np.array(kf, np.int32),
                         slow_logits_bits=np.stack(res["slow_bits"]), fast_last_bits=np.stack(res["fast_bits"]),
                         slow_logits_f32=np.stack(res["slow_f32"]), fast_last_f32=np.stack(res["fast_f32"]),
                         synth_seed=41, log2_half=5, torch_version=torch.__version__,
                         threads=torch.get_num_threads(), **prompts)
-    print(f"llm_ragged: {B} prompts (lens {lens.min()}..{lens.max()}) x {n_new} frames in {time.time() - t0:.0f}s")
+    print(f"{out_name}: {B} prompts (lens {lens.min()}..{lens.max()}) x {n_new} frames in {time.time() - t0:.0f}s")
 
 
 # --------------------------------------------------------------------------------------
@@ -791,6 +820,33 @@ def _quantize_module():
     from tools.llama import quantize
 
     return quantize
+
+
+def cmd_int4_quant():
+    """Weight-only int4 groupwise quantization (the int4 half): the reference's
+    own group_quantize_tensor / group_dequantize_tensor (tools/llama/quantize.py:57-160) on seeded
+    bf16 matrices, every group size the handler accepts (quantize.py:366), with rows that hit the
+    clamp (a constant row: max == min), wide and tiny magnitudes.  Its packed matmul
+    (_weight_int4pack_mm, quantize.py:249-257) does not run on this CPU: the build is pinned here at
+    the quantizer, not at the packed-matmul level."""
+    q = _quantize_module()
+    out = {}
+    rng = np.random.default_rng(17)
+    for gs, (N, K) in ((32, (24, 256)), (64, (24, 512)), (128, (48, 1024)), (256, (32, 1024))):
+        w = rng.standard_normal((N, K)).astype(np.float32) * 0.05
+        w[1] = 0.0371  # constant row: scales clamp to 1e-6
+        w[2] *= 400.0  # wide range
+        w[3] *= 1e-4  # tiny range
+        w[4, ::7] = 3.5  # outliers
+        wb = torch.from_numpy(w).to(torch.bfloat16)
+        w_int32, sz = q.group_quantize_tensor(wb, n_bit=4, groupsize=gs)
+        wdq = q.group_dequantize_tensor(w_int32, sz.float(), n_bit=4, groupsize=gs)
+        out[f"w_bits_g{gs}"] = synth.f32_to_bf16_bits(wb.float().numpy())
+        out[f"q_g{gs}"] = w_int32.numpy().astype(np.uint8)
+        out[f"sz_bits_g{gs}"] = synth.f32_to_bf16_bits(sz.float().numpy())  # [K/gs][N][2] (scale, zero)
+        out[f"dq_g{gs}"] = wdq.float().numpy()
+    np.savez_compressed(os.path.join(GOLD, "int4_quant.npz"), torch_version=torch.__version__, **out)
+    print("int4_quant:", {k: v.shape for k, v in out.items() if k.startswith("q_")})
 
 
 def int8_model(config, qsd, seed, log2_half, dtype):

@@ -245,3 +245,31 @@ def op_rope(x, tab_rows, bf16=True):
     y = np.zeros_like(x)
     L.orc_op_rope(_f32p(x), _f32p(tabs), rows, hd, int(bf16), _f32p(y))
     return y
+
+
+# ---- weight-only int4 (tools/llama/quantize.py:57-160), numpy restatement -------------------
+def _bf16r(x):
+    """round-to-nearest-even to bf16, as float32 values (torch's bf16 op results)."""
+    b = np.ascontiguousarray(x, np.float32).view(np.uint32)
+    r = ((b + 0x7FFF + ((b >> 16) & 1)) & 0xFFFF0000).astype(np.uint32)
+    return r.view(np.float32)
+
+
+def int4_group_quantize(w, gs):
+    """get_group_qparams + group_quantize_tensor_from_qparams (quantize.py:57-127) on bf16-valued w
+    [N][K], in torch's bf16 arithmetic (fp32 op, bf16 result): (q [N][K] uint8, scale, zero [N][K/gs]
+    as float32 of bf16 values), and the affine dequantisation (q - 8) * scale + zero in fp32
+    (group_dequantize_tensor_from_qparams, quantize.py:130-152 with float scales)."""
+    w = np.ascontiguousarray(w, np.float32)
+    N, K = w.shape
+    g = w.reshape(N, K // gs, gs)
+    mx, mn = g.max(-1), g.min(-1)
+    d = np.maximum(_bf16r(mx - mn), _bf16r(np.float32(1e-6)))
+    sc = _bf16r(d / np.float32(15))
+    s8 = _bf16r(sc * np.float32(8))
+    zr = _bf16r(mn + s8)
+    lo = _bf16r(zr - s8)
+    x = _bf16r(_bf16r(g - lo[..., None]) / sc[..., None])
+    q = np.clip(np.rint(x), 0, 15).astype(np.uint8)
+    dq = ((q.astype(np.float64) - 8) * sc[..., None].astype(np.float64) + zr[..., None]).astype(np.float32)
+    return q.reshape(N, K), sc, zr, dq.reshape(N, K)

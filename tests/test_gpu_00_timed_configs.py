@@ -59,6 +59,45 @@ def test_long_context_bf16_vs_reference(golden):
     _teacher_case("llm_long_bf16.npz", golden)
 
 
+def _golden_or_skip(golden, name):
+    import os
+
+    from conftest import GOLDEN
+
+    if not os.path.exists(os.path.join(GOLDEN, name)):
+        pytest.skip(f"{name} not generated (oracle/gen_goldens.py)")
+    return golden(name)
+
+
+def test_config2_full_depth_64_frames_bf16_vs_reference(golden):
+    """Config 2 at full depth over 64 decode frames (positions 64..128) through the production
+    decode graph, teacher-forced with the reference's columns: every frame's slow logits and the
+    last codebook's fast logits within BF16_RATIO x the reference's own bf16 error."""
+    from fishmi.llm import DualARModel
+
+    g = _golden_or_skip(golden, "llm_full64_bf16.npz")
+    cfg = _cfg(g)
+    T = g["prompt"].shape[1]
+    assert g["seq"].shape[1] - T >= 65
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 1)
+    try:
+        slow, fast = m.teacher_decode(g["prompt"], g["seq"][:, T:])
+    finally:
+        m.close()
+    rows = g["slow_rows"]
+    st = bf16_vs_reference(slow[:, rows], fast[:, -1:], bits_to_f32(g["slow_logits_bits"]),
+                           bits_to_f32(g["fast_last_bits"])[:, None], g["slow_logits_f32"],
+                           g["fast_last_f32"][:, None])
+    assert st["top1_checked"] >= 40
+
+
+def test_long_context_4_layers_bf16_vs_reference(golden):
+    """3000-token prompt through 4 slow layers: the long-context error growth over depth."""
+    g = _golden_or_skip(golden, "llm_long4_bf16.npz")
+    assert g["prompt"].shape[1] >= 3000 and _cfg(g).n_layer == 4
+    _teacher_case("llm_long4_bf16.npz", golden)
+
+
 @pytest.fixture
 def knob():
     from fishmi import native
@@ -123,6 +162,51 @@ def test_config3_ragged_32_slots_bf16_vs_reference(prefill, chain, slab, golden,
                            bits_to_f32(g["slow_logits_bits"]).reshape(B * n, -1),
                            bits_to_f32(g["fast_last_bits"]).reshape(B * n, 1, -1),
                            g["slow_logits_f32"].reshape(B * n, -1), g["fast_last_f32"].reshape(B * n, 1, -1))
+    assert st["top1_checked"] >= B
+
+
+def test_config3_ragged_32_slots_64_frames_bf16_vs_reference(golden):
+    """Config 3's ragged batch over 64 decode frames (positions up to 320): 32 prompts in permuted
+    slots, prefill_batch then 64 batched frames, all teacher-forced with each prompt's reference
+    columns; logits checked at the golden's kept frames (0, 32, 64)."""
+    from fishmi.llm import DualARModel
+
+    g = _golden_or_skip(golden, "llm_ragged64_bf16.npz")
+    cfg = _cfg(g)
+    B = int(g["lens"].size)
+    cols = g["cols"]
+    n = cols.shape[2]
+    kf = [int(k) for k in g["keep_frames"]]
+    assert B == 32 and n >= 65 and kf[-1] == n - 1
+    prompts = [g[f"prompt_{i}"] for i in range(B)]
+    slot_of = np.random.default_rng(6).permutation(B)
+    order = [int(slot_of[i]) for i in np.random.default_rng(7).permutation(B)]
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", B)
+    slow = np.zeros((B, len(kf), len(g["slow_rows"])), np.float32)
+    fast = np.zeros((B, len(kf), 1, cfg.codebook_size), np.float32)
+    sp = DualARModel.sampling(top_k=1)
+    try:
+        for k in range(n):
+            for i in range(B):
+                m.force(int(slot_of[i]), cols[i, :, k])
+            if k == 0:
+                m.prefill_batch([int(s) for s in slot_of], prompts, [sp] * B)
+            else:
+                m.decode(order)
+            if k in kf:
+                for i in range(B):
+                    s_, f_ = m.read_logits(int(slot_of[i]))
+                    slow[i, kf.index(k)] = s_[g["slow_rows"]]
+                    fast[i, kf.index(k), 0] = f_[-1]
+    finally:
+        for s in range(B):
+            m.force(s, None)
+        m.close()
+    nk = len(kf)
+    st = bf16_vs_reference(slow.reshape(B * nk, -1), fast.reshape(B * nk, 1, -1),
+                           bits_to_f32(g["slow_logits_bits"]).reshape(B * nk, -1),
+                           bits_to_f32(g["fast_last_bits"]).reshape(B * nk, 1, -1),
+                           g["slow_logits_f32"].reshape(B * nk, -1), g["fast_last_f32"].reshape(B * nk, 1, -1))
     assert st["top1_checked"] >= B
 
 

@@ -1,0 +1,97 @@
+"""Weight-only int4 (fm_llm_set_quant_int4; tools/llama/quantize.py WeightOnlyInt4QuantHandler,
+llama.py:537-543) on the GPU.  The device quantizer is pinned bit-exact to the reference's own
+group_quantize_tensor (tests/golden/int4_quant.npz).  The reference's packed matmul
+(_weight_int4pack_mm) does not run on this CPU, so the matmul is parity-unpinned: it is held to the
+same linear on the dequantised bf16 weights (every other kernel's operand) instead.  Run on the
+MI355X box: pytest -m gpu."""
+import json
+
+import numpy as np
+import pytest
+
+from parity_util import bits_to_f32
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf16r(x):
+    b = np.ascontiguousarray(x, np.float32).view(np.uint32)
+    return ((b + 0x7FFF + ((b >> 16) & 1)) & 0xFFFF0000).astype(np.uint32).view(np.float32)
+
+
+@pytest.mark.parametrize("gs", [32, 64, 128, 256])
+def test_device_quantizer_matches_reference(golden, gs):
+    """launch_quant4: codes, scales and zeros bit-exact with group_quantize_tensor; the dequantised
+    weights are bf16 of group_dequantize_tensor's values."""
+    from fishmi import ops
+
+    g = golden("int4_quant.npz")
+    w = bits_to_f32(g[f"w_bits_g{gs}"])
+    q, sc, zr, wd = ops.quant4(w, gs)
+    sz = bits_to_f32(g[f"sz_bits_g{gs}"])
+    np.testing.assert_array_equal(q, g[f"q_g{gs}"])
+    np.testing.assert_array_equal(sc, sz[..., 0].T)
+    np.testing.assert_array_equal(zr, sz[..., 1].T)
+    np.testing.assert_array_equal(wd, _bf16r(g[f"dq_g{gs}"]))
+
+
+@pytest.mark.parametrize("R", [1, 4])
+def test_q4_gemv_equals_dequantized_linear(R):
+    """The streamed int4 GEMV (4-bit codes + group (scale, zero), dequantised in registers) against
+    the bf16 GEMV on the dequantised weights: the same products, only the fp32 summation grouping
+    differs; both against a float64 x . w_deq^T."""
+    from fishmi import ops
+
+    rng = np.random.default_rng(3)
+    N, K = 1040, 2560
+    w = _bf16r(rng.standard_normal((N, K)).astype(np.float32) * 0.03)
+    x = _bf16r(rng.standard_normal((R, K)).astype(np.float32))
+    q, sc, zr, wd, yb, y4 = ops.quant4(w, 128, x)
+    ref = x.astype(np.float64) @ wd.astype(np.float64).T
+    scale = np.abs(ref).max()
+    assert np.abs(yb - ref).max() <= 1e-5 * scale * np.sqrt(K) and np.abs(y4 - ref).max() <= 1e-5 * scale * np.sqrt(K)
+    np.testing.assert_allclose(y4, yb, rtol=0, atol=2e-6 * scale * np.sqrt(K))
+
+
+def test_int4_model_stream_matches_dequantized_model(golden):
+    """S2-Pro widths (llm_wide: 2 slow + 1 fast layers), int4 with group size 128, teacher-forced
+    frames through the production decode graph: the streamed 4-bit GEMVs (fm_tune int4_stream 1)
+    against the same model on its dequantised bf16 weights (int4_stream 0) -- logits equal up to
+    fp32 summation order; and the int4 model tracks the bf16 model (quantization error only)."""
+    from fishmi import native
+    from fishmi.config import DualARConfig
+    from fishmi.llm import DualARModel
+
+    g = golden("llm_wide_bf16.npz")
+    cfg = DualARConfig._from_fish_qwen3_omni(json.loads(str(g["config"])))
+    cfg.im_end_id = 4
+    T = g["prompt"].shape[1]
+    cols = g["seq"][:, T:T + 5]
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 1, quant="int4",
+                              groupsize=128)
+    out = {}
+    try:
+        for st in (1, 0):
+            native.tune("int4_stream", st)
+            m.use_graph(True)
+            out[st] = m.teacher_decode(g["prompt"], cols)
+    finally:
+        native.tune("int4_stream", 1)
+        m.close()
+    mb = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 1)
+    try:
+        sb, fb = mb.teacher_decode(g["prompt"], cols)
+    finally:
+        mb.close()
+    rows = g["slow_rows"]
+    for k in (0, 1):  # slow, fast
+        a, b = out[1][k], out[0][k]
+        if k == 0:
+            a, b = a[:, rows], b[:, rows]
+        fin = np.isfinite(b)
+        rel = np.sqrt(np.mean((a[fin] - b[fin]) ** 2)) / np.sqrt(np.mean(b[fin] ** 2))
+        assert rel < 5e-3, (k, rel)
+        assert np.array_equal(np.isfinite(a), fin)
+    # against the bf16 model: correlated, not equal (the int4 quantisation error)
+    f4, fbf = out[1][1].ravel(), fb.ravel()
+    assert np.corrcoef(f4, fbf)[0, 1] > 0.8

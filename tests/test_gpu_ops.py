@@ -193,3 +193,12 @@ def test_prompt_attention(kernel, R, pos0):
     scale = np.abs(ref).max(axis=-1, keepdims=True)
     err = np.abs(out - ref) / scale
     assert err.max() <= 2.0 ** -8 + 4e-3, (kernel, R, pos0, float(err.max()))
+
+
+def test_stream_peak_is_plausible():
+    """fm_stream_peak (the bench line's measured stream peak): the read stream and the copy land
+    between 3 TB/s and the 8 TB/s vendor figure."""
+    from fishmi import native
+
+    r, c = native.stream_peak(0, 1 << 30, 4)
+    assert 3000 < r < 8000 and 3000 < c < 8000, (r, c)
