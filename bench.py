@@ -307,14 +307,16 @@ def longform_leg(ccfg, device, turns, frames_per_turn, seed):
             "turn_first_chunk_ms_p90": round(float(np.percentile(f, 90)), 2)}
 
 
-def int8_leg(cfg, codec, args, local):
-    """Config 2 with weight-only int8 linears (opt-in; tools/llama/quantize.py's
-    per-channel rule applied on the device to the same synthetic weights): the same utterance loop,
-    and the int8 decode GEMV's roofline at its own algorithmic bytes (1 byte per weight)."""
+def quant_leg(cfg, codec, args, local, quant):
+    """Config 2 with weight-only int8 / int4 linears (opt-in; tools/llama/
+    quantize.py's per-channel int8 rule or groupwise int4 rule (group 128) applied on the device to the
+    same synthetic weights): the same utterance loop, and the quantized decode GEMV's roofline at its
+    own algorithmic bytes (int8: 1 byte per weight + row scales; int4: half a byte + a (scale, zero)
+    word per row and 128-k unit)."""
     from fishmi.llm import DualARModel
 
     llm = DualARModel.synthetic(cfg, seed=args.seed, log2_half=5, device=local, precision="bf16",
-                                max_slots=1, quant="int8")
+                                max_slots=1, quant=quant)
     def go(step):
         sp = DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30, seed=7919 * step, mask_im_end=True)
         return utterance(llm, codec, make_prompt(cfg, args.prompt_len, 1000 * step), sp, args.frames,
@@ -336,8 +338,11 @@ def int8_leg(cfg, codec, args, local):
     fb = llm.frame_bytes(1, pos)
     llm.close()
     ach = b / n / (avg_us * 1e-6) / 1e9
-    return {"workload": "config 2 as above with weight-only int8 linears (round(round(x.q) * scale), "
-                        "biases dropped, as WeightOnlyInt8Linear); opt-in, off the bf16 parity contract",
+    what = ("weight-only int8 linears (round(round(x.q) * scale), biases dropped, as WeightOnlyInt8Linear)"
+            if quant == "int8" else
+            "weight-only int4 linears, group 128 (quantize.py's group_quantize_tensor on the device, bit-exact; "
+            "weights bf16(fma(q - 8, scale, zero)), 4-bit codes streamed by the batch-1 GEMVs)")
+    return {"workload": f"config 2 as above with {what}; opt-in, off the bf16 parity contract",
             "value": round(args.steps * args.frames / FRAME_RATE / el, 4), "unit": "audio-sec/wall-sec",
             "ms_per_frame": round(dec_s * 1e3, 4), "bytes_per_frame": int(fb),
             "frame_frac": round(fb / dec_s / 1e9 / HBM_PEAK_GBPS, 4),
@@ -595,10 +600,11 @@ def main():
     longf = longform_leg(ccfg, local, args.longform_turns, args.longform_frames, args.seed) \
         if args.longform_turns > 0 and rank == 0 else None
 
-    q8 = None
+    q8 = q4 = None
     if rank == 0 and not args.no_int8:
         llm.close()
-        q8 = int8_leg(cfg, codec, args, local)
+        q8 = quant_leg(cfg, codec, args, local, "int8")
+        q4 = quant_leg(cfg, codec, args, local, "int4")
     stream_gbps = stream_peak_gbps() if rank == 0 else (None, None)
     box = box_identity() if rank == 0 else None
     traffic, traffic_note = None, "not measured (--no-pmc or N>1)"
@@ -663,6 +669,7 @@ def main():
             "encode": enc,
             "longform": longf,
             "int8": q8,
+            "int4": q4,
             "cpu_baseline": cpu,
             "box": box,
         }

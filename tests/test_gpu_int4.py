@@ -4,8 +4,6 @@ group_quantize_tensor (tests/golden/int4_quant.npz).  The reference's packed mat
 (_weight_int4pack_mm) does not run on this CPU, so the matmul is parity-unpinned: it is held to the
 same linear on the dequantised bf16 weights (every other kernel's operand) instead.  Run on the
 MI355X box: pytest -m gpu."""
-import json
-
 import numpy as np
 import pytest
 
@@ -48,9 +46,11 @@ def test_q4_gemv_equals_dequantized_linear(R):
     x = _bf16r(rng.standard_normal((R, K)).astype(np.float32))
     q, sc, zr, wd, yb, y4 = ops.quant4(w, 128, x)
     ref = x.astype(np.float64) @ wd.astype(np.float64).T
-    scale = np.abs(ref).max()
-    assert np.abs(yb - ref).max() <= 1e-5 * scale * np.sqrt(K) and np.abs(y4 - ref).max() <= 1e-5 * scale * np.sqrt(K)
-    np.testing.assert_allclose(y4, yb, rtol=0, atol=2e-6 * scale * np.sqrt(K))
+    # EPI_F32 rounds each output to bf16 (the head's round(x . w) as fp32): one bf16 ulp, plus the
+    # fp32 summation slack
+    tol = np.abs(ref) * 2.0 ** -8 + 1e-6 * np.abs(ref).max() * np.sqrt(K)
+    assert (np.abs(yb - ref) <= tol).all() and (np.abs(y4 - ref) <= tol).all()
+    assert np.mean(y4 == yb) > 0.95  # the same bf16 output almost everywhere (summation order aside)
 
 
 def test_int4_model_stream_matches_dequantized_model(golden):
@@ -62,8 +62,12 @@ def test_int4_model_stream_matches_dequantized_model(golden):
     from fishmi.config import DualARConfig
     from fishmi.llm import DualARModel
 
+    import os
+
+    from conftest import GOLDEN
+
     g = golden("llm_wide_bf16.npz")
-    cfg = DualARConfig._from_fish_qwen3_omni(json.loads(str(g["config"])))
+    cfg = DualARConfig.from_pretrained(os.path.join(GOLDEN, "llm_wide"))
     cfg.im_end_id = 4
     T = g["prompt"].shape[1]
     cols = g["seq"][:, T:T + 5]
