@@ -551,6 +551,8 @@ static BstreamPlan bsacc_plan(int N, int K, int R, int epi, size_t esz) {
             }
         }
         kparts = best;
+        const int fk = fm_tuning().bsacc_kparts;  // developer override (subject to the same limits)
+        if (fk > 0 && S % fk == 0 && S / fk >= 8 && ((tiles * fk + G - 1) / G) <= 6) kparts = fk;
     }
     const int Sp = S / kparts, NW = std::min(8, Sp);
     const int ntm = (tiles * kparts + G - 1) / G;

@@ -61,9 +61,11 @@ constexpr int gemv_wpe(int pro, int epi) { return pro == PRO_PRENORM && epi == E
 // as a T fragment is), dequantised exactly to two T fragments in registers; each output is
 // round(round(acc) * wscale[row]) (WeightOnlyInt8Linear.forward, quantize.py:228-229).
 // QM 2 (weight-only int4, bf16): one ring slot = one 128-k unit of 4-bit codes (1 KiB per wave) plus
-// the lane's row (scale, zero) of that unit's group (a.wsz, group size a multiple of 128), each code
-// dequantised to bf16(fma(q - 8, scale, zero)) -- the value the int4 model's bf16 weight copy holds
-// (launch_quant4), so the GEMV computes the same linear the T-fragment kernels do.
+// the (scale, zero) of that unit's group for the lane's four accumulator rows (a.wsz, group size a
+// multiple of 128).  No per-weight dequantisation: each code becomes the exact bf16 128 + q by one
+// mask-and-or per pair (0x4300 | q), the unit's four MFMAs give B = sum x (128 + q) per (row, x row),
+// and the unit adds s * B + (z - 136 s) * X_u, X_u = sum x over the unit (staged in LDS by the
+// prologue) -- the group's affine map sum x ((q - 8) s + z) applied exactly in fp32.
 // ---- chain hand-off (one launch, stages in sequence; cdna_hip_programming.md §6 Guideline 16,
 // write-through form): every byte a later stage of the launch reads is stored sc1 and drained
 // (s_waitcnt vmcnt(0)) by its storing wave before the block's one arrival on a sharded counter;
@@ -219,7 +221,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
     const int wa = (wave * Sb) / WPB, wb = ((wave + 1) * Sb) / WPB, nmy = wb - wa;
     typename G::f fa[QQ ? 1 : U], fb[NACC == 2 ? U : 1];
     u32x4_t fq[QQ ? U : 1];
-    uint32_t fz[Q4 ? U : 1];  // int4: the lane's row (scale, zero) per ring slot
+    u32x4_t fz[Q4 ? U : 1];  // int4: (scale, zero) of the lane's 4 accumulator rows per ring slot
     // Fragment i of the run into ring slot u.  Branch-free on purpose: a load under a branch makes
     // the compiler drain vmcnt(0) before every MFMA (no pipelining at all), so tail slots load a
     // fixed fragment (fm_tune gemv_dummy: one per (block, wave), a cache hit) instead of being
@@ -229,7 +231,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
     const T* wrun = QQ ? nullptr : a.W + run0;
     const T* wrun2 = (EPI == EPI_SWIGLU) ? a.W2 + run0 : nullptr;
     const unsigned char* qrun = QQ ? a.Wq + run0 : nullptr;
-    const uint32_t* zrun = Q4 ? a.wsz + (run0 >> 10) * 16 + (lane & 15) : nullptr;
+    const uint32_t* zrun = Q4 ? a.wsz + (run0 >> 10) * 16 + 4 * (lane >> 4) : nullptr;
     const bool dtail = a.dummy_tail != 0;
     // dummy_tail 2: the fixed fragment differs per (block, wave) over 256 fragments (no hot line)
     // (bounded by the matrix's own fragment count: ceil(N / 16) tiles x S k-steps)
@@ -241,7 +243,8 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
             const u32x4_t* p = reinterpret_cast<const u32x4_t*>((past ? a.Wq + dfr * 1024 : qrun + ii * 1024) + lane * 16);
             if constexpr (NT) fq[u] = __builtin_nontemporal_load(p);
             else fq[u] = *p;
-            if constexpr (Q4) fz[u] = past ? a.wsz[dfr * 16 + (lane & 15)] : zrun[ii * 16];
+            if constexpr (Q4)
+                fz[u] = *reinterpret_cast<const u32x4_t*>(past ? a.wsz + dfr * 16 + 4 * (lane >> 4) : zrun + ii * 16);
         } else {
             fa[u] = G::template load_w<NT>(past ? a.W + dfr * 512 : wrun + ii * 512, lane);
             if constexpr (NACC == 2) fb[u] = G::template load_w<NT>(past ? a.W + dfr * 512 : wrun2 + ii * 512, lane);
@@ -476,6 +479,19 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
         }
     }
     lds_barrier();  // X' staged; the weight ring stays in flight (each MFMA waits for its own fragment)
+    // int4: X_u = sum of each staged x row over each 128-k unit (one wave per (unit, row), 2 k per lane)
+    float* xsum = reinterpret_cast<float*>(smem + a.q4_xsum_off);
+    if constexpr (Q4) {
+        const int nu = Kb >> 7;
+        for (int pr = wave; pr < nu * R; pr += WPB) {
+            const int uu = pr / R, rr = pr - uu * R;
+            const T* xr = xs + (size_t)rr * xstride + uu * 128 + 2 * lane;
+            float v = ld(xr, 0) + ld(xr, 1);
+            v = wave_sum(v);
+            if (lane == 0) xsum[pr] = v;
+        }
+        lds_barrier();
+    }
 
     const unsigned long long ts1 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     // ---------------- main loop: ring of U fragments per wave ------------------------------------
@@ -486,10 +502,21 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
         for (int u = 0; u < U; ++u) {
             if (i + u < nmy) {
                 if constexpr (Q4) {
-                    const float zs = __uint_as_float(fz[u] << 16), zz = __uint_as_float(fz[u] & 0xffff0000u);
+                    f32x4_t b = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc0 = G::mma(G::dq4(fq[u][j], zs, zz), G::load(xp + (size_t)(i + u) * 128 + 32 * j), acc0);
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t w = fq[u][j];
+                        typename G::f A;
+#pragma unroll
+                        for (int p = 0; p < 4; ++p) A[p] = ((w >> (4 * p)) & 0x000F000Fu) | 0x43004300u;
+                        b = G::mma(A, G::load(xp + (size_t)(i + u) * 128 + 32 * j), b);
+                    }
+                    const float xu = xsum[(wa + i + u) * R + (r < R ? r : 0)];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float sc = __uint_as_float(fz[u][e] << 16), zr = __uint_as_float(fz[u][e] & 0xffff0000u);
+                        acc0[e] += sc * b[e] + (zr - 136.f * sc) * xu;
+                    }
                 } else if constexpr (Q8) {
                     typename G::f w0, w1;
                     G::dq8(fq[u], w0, w1);
@@ -757,11 +784,16 @@ static void gemv_go(hipStream_t s, const GemvArgs<T>& a, int ksb) {
         gemv_go_u<T, PRO, EPI, false>(s, b, grid, lds);
 }
 
-// weight-only int8: one configuration (non-temporal, 8 units in flight per wave, 4 waves)
+// weight-only int8: non-temporal, fm_tune q_u units in flight per wave (default 4), 4 waves
 template <typename T, int PRO, int EPI>
 static void gemv_go_q8(hipStream_t s, const GemvArgs<T>& a, int ksb) {
     FMCHECK(a.K % (64 * ksb) == 0 && a.wscale, "int8 GEMV: K slices must be whole 64-k units, scales set");
-    gemv_launch<T, PRO, EPI, true, 8, 4, 1>(s, a, dim3(FM_CEIL(a.N, 16), ksb), gemv_lds_bytes(a.R, a.K / ksb, sizeof(T)));
+    const dim3 grid(FM_CEIL(a.N, 16), ksb);
+    const size_t lds = gemv_lds_bytes(a.R, a.K / ksb, sizeof(T));
+    if (fm_tuning().q_u == 16) gemv_launch<T, PRO, EPI, true, 16, 4, 1>(s, a, grid, lds);
+    else if (fm_tuning().q_u == 8) gemv_launch<T, PRO, EPI, true, 8, 4, 1>(s, a, grid, lds);
+    else if (fm_tuning().q_u == 2) gemv_launch<T, PRO, EPI, true, 2, 4, 1>(s, a, grid, lds);
+    else gemv_launch<T, PRO, EPI, true, 4, 4, 1>(s, a, grid, lds);
 }
 
 // weight-only int4 (bf16): the same configuration over 128-k units
@@ -769,7 +801,14 @@ template <typename T, int PRO, int EPI>
 static void gemv_go_q4(hipStream_t s, const GemvArgs<T>& a, int ksb) {
     if constexpr (sizeof(T) == 2) {
         FMCHECK(a.K % (128 * ksb) == 0 && a.wsz && !a.wscale, "int4 GEMV: K slices must be whole 128-k units, (scale, zero) set");
-        gemv_launch<T, PRO, EPI, true, 8, 4, 2>(s, a, dim3(FM_CEIL(a.N, 16), ksb), gemv_lds_bytes(a.R, a.K / ksb, sizeof(T)));
+        const dim3 grid(FM_CEIL(a.N, 16), ksb);
+        GemvArgs<T> b = a;
+        b.q4_xsum_off = (int)((gemv_lds_bytes(a.R, a.K / ksb, sizeof(T)) + 15) & ~(size_t)15);
+        const size_t lds = b.q4_xsum_off + (size_t)(a.K / ksb / 128) * a.R * 4;
+        if (fm_tuning().q_u == 16) gemv_launch<T, PRO, EPI, true, 16, 4, 2>(s, b, grid, lds);
+        else if (fm_tuning().q_u == 8) gemv_launch<T, PRO, EPI, true, 8, 4, 2>(s, b, grid, lds);
+        else if (fm_tuning().q_u == 2) gemv_launch<T, PRO, EPI, true, 2, 4, 2>(s, b, grid, lds);
+        else gemv_launch<T, PRO, EPI, true, 4, 4, 2>(s, b, grid, lds);
     } else {
         FMCHECK(false, "int4 GEMV: bf16 only");
     }

@@ -32,10 +32,11 @@ void launch_pack_q8(hipStream_t s, const int8_t* src, int N, int K, int8_t* dst)
 // with bf16(fma(q - 8, scale, zero)) (the dequantised weight every bf16 kernel then reads).
 void launch_quant4(hipStream_t s, bf16_t* w, int N, int K, int gs, uint8_t* q, uint32_t* sz);
 // codes row-major [N][K] -> the int4 decode-GEMV layout: [ceil(N/16)][K/128] units of 1 KiB, lane l
-// (row l & 15, k-offset 8 * (l >> 4)) holding word j = the 8 codes of k-step j of the unit (nibble e:
-// k = 128 u + 32 j + 8 (l >> 4) + e)
-void launch_pack_q4(hipStream_t s, const uint8_t* q, int N, int K, uint8_t* dst);
+// (row l & 15, k-offset 8 * (l >> 4)) holding word j = the 8 codes of k-step j of the unit, k =
+// 128 u + 32 j + 8 (l >> 4) + e: even e at bits 2e (e / 2 nibbles up), odd e at bits 16 + 2(e - 1),
+// so (word >> 4p) & 0x000F000F is the pair (e = 2p, 2p + 1) in bf16 mantissa position
 // sz [N][K/gs] -> [ceil(N/16)][K/128][16 rows] (gs a multiple of 128: one group per unit)
+void launch_pack_q4(hipStream_t s, const uint8_t* q, int N, int K, uint8_t* dst);
 void launch_pack_sz4(hipStream_t s, const uint32_t* sz, int N, int K, int gs, uint32_t* dst);
 
 template <typename T> struct LinearArgs {
@@ -218,6 +219,7 @@ template <typename T> struct GemvArgs {
     // weight-only int4 (bf16): Wq holds 4-bit codes ([tiles][K/128][64 lanes][16 B], launch_pack_q4)
     // and wsz each (tile, 128-k unit, row)'s group (scale, zero) as bf16 pairs (launch_pack_sz4)
     const uint32_t* wsz;
+    int q4_xsum_off;  // int4: LDS byte offset of the per-(128-k unit, x row) sums (launcher)
     // optional KV prefetch (batch-1 QKV GEMV, fm_tune kv_prefetch): while the weights stream, the
     // cached K / V rows the next attention launch reads (positions 0 .. pos of row 0's slot) are
     // pulled into L2: block b loads kv head b % pf_nkv, which under round-robin workgroup placement
@@ -274,6 +276,8 @@ struct FmTuning {
     int chain_max = 4;       // gemv_chain: GEMVs per launch at most (2..4)
     int chain_sleep = 4;     // gemv_chain: s_sleep argument between a waiting block's polls (1, 4 or 16)
     int gemv_chain = 0;      // 1: batch-1 decode runs wo -> w1||w3 -> w2 -> next qkv as one launch (gemv_chain_kernel)
+    int bsacc_kparts = 0;    // developer: force the K parts of the batched split-K (slab) linears (0: bsacc_plan's pick)
+    int q_u = 4;             // int8 / int4 decode GEMV: ring units in flight per wave (2, 4, 8, 16; int8 frame 3.79 -> 3.59 ms at 8 -> 4)
     int int4_stream = 1;     // weight-only int4: 1 the batch <= 8 GEMVs stream the 4-bit codes, 0 the dequantised bf16 copy
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
     int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1)

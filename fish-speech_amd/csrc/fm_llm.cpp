@@ -2422,6 +2422,12 @@ int fm_tune(const char* key, int value) {
         } else if (k == "bstream_nw") {
             FMCHECK(value >= 0 && value <= 16, "bstream_nw must be in [0, 16]");
             t.bstream_nw = value;
+        } else if (k == "bsacc_kparts") {
+            FMCHECK(value == 0 || value == 1 || value == 2 || value == 4 || value == 8, "bsacc_kparts must be 0, 1, 2, 4 or 8");
+            t.bsacc_kparts = value;
+        } else if (k == "q_u") {
+            FMCHECK(value == 2 || value == 4 || value == 8 || value == 16, "q_u must be 2, 4, 8 or 16");
+            t.q_u = value;
         } else if (k == "int4_stream") {
             t.int4_stream = value != 0;
         } else if (k == "pass_fast") {
@@ -2533,8 +2539,10 @@ int fm_llm_force(fm_llm* m, int slot, const int32_t* col) {
         const int on = col != nullptr;
         if (on) {
             const fm_model_config& c = m->c;
-            FMCHECK((col[0] >= c.semantic_begin_id && col[0] <= c.semantic_end_id) || col[0] == c.im_end_id,
-                    "forced token is outside the sampler's support (semantic ids + <|im_end|>)");
+            // any vocabulary id: the reference's bf16 multinomial draw can emit ids outside the
+            // semantic support (torch.rand_like in bf16 yields 0 or 1, and argmax over an all-zero
+            // or NaN row is id 0: inference.py:43-46), and teacher forcing replays its streams
+            FMCHECK(col[0] >= 0 && col[0] < c.vocab_size, "forced token outside the vocabulary");
             for (int q = 1; q < m->C1; ++q)
                 FMCHECK(col[q] >= 0 && col[q] < m->cb, "forced codebook token out of range");
             HIPCHK(hipMemcpyAsync(m->force_cols + (size_t)slot * m->C1, col, (size_t)m->C1 * 4,

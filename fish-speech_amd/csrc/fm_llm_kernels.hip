@@ -281,7 +281,8 @@ void launch_quant4(hipStream_t s, bf16_t* w, int N, int K, int gs, uint8_t* q, u
     const int64_t n = (int64_t)N * (K / gs);
     quant4_kernel<<<(int)FM_CEIL(n, 256), 256, 0, s>>>(w, N, K, gs, q, sz);
 }
-// one thread per (unit, lane): word j of its 16 bytes = the 8 codes of k-step j (nibble e = k e)
+// one thread per (unit, lane): word j of its 16 bytes = the 8 codes of k-step j (even e in the low
+// half at nibble e / 2, odd e in the high half at nibble (e - 1) / 2)
 __global__ void pack_q4_kernel(const uint8_t* __restrict__ q, int N, int K, uint8_t* __restrict__ dst) {
     const int U = K >> 7;
     const int64_t n = (int64_t)((N + 15) / 16) * U * 64;
@@ -296,7 +297,8 @@ __global__ void pack_q4_kernel(const uint8_t* __restrict__ q, int N, int K, uint
             uint32_t v = 0;
 #pragma unroll
             for (int e = 0; e < 8; ++e)
-                v |= (uint32_t)(row < N ? q[(size_t)row * K + 128 * u + 32 * j + 8 * (l >> 4) + e] & 15 : 8) << (4 * e);
+                v |= (uint32_t)(row < N ? q[(size_t)row * K + 128 * u + 32 * j + 8 * (l >> 4) + e] & 15 : 8)
+                     << ((e & 1) ? 16 + 4 * (e >> 1) : 4 * (e >> 1));
             wd[j] = v;
         }
         *reinterpret_cast<u32x4_t*>(dst + i * 16) = (u32x4_t){wd[0], wd[1], wd[2], wd[3]};
