@@ -700,8 +700,97 @@ void bsacc_init() {
     (void)hipGetLastError();  // an attribute the runtime declines must not linger as the sticky error
 }
 
+// The same finalise + RMSNorm with each row split over `ch` blocks (R * ch blocks: 256 CUs busy at
+// R = 32, ch = 8, instead of 32): every block loads only its chunk's K-part slabs, residual and norm
+// weights (one round trip), writes x, and publishes its chunk's sum of squares write-through; the
+// row's ch blocks then meet on an arrival counter (all resident: R * ch <= 1024 small blocks), read
+// the ch partial sums in chunk order (a fixed fp32 order) and normalise their chunk.  The last block
+// of a row to read resets the row's two counters, so the next launch starts from zero.
+constexpr int FS_THREADS = 64;
+template <typename T>
+__global__ __launch_bounds__(FS_THREADS) void finalize_split_kernel(FinalizeArgs<T> a) {
+    typedef __attribute__((address_space(1))) int g_i32;
+    typedef __attribute__((address_space(1))) float g_f32;
+    const int r = blockIdx.x / a.ch, c = blockIdx.x - r * a.ch;
+    const int per = (a.d / 8 + a.ch - 1) / a.ch;  // 8-element items per chunk
+    const int it = c * per + (int)threadIdx.x;    // this thread's item (one per thread: per <= 64)
+    const bool live = (int)threadIdx.x < per && it < a.d / 8;
+    const int i = 8 * (live ? it : 0);
+    float wn[8], x[8], y[8], b[8], v[8];
+    if (a.nw) load8(a.nw + i, wn);
+    load8(a.res + (size_t)r * a.ldr + i, x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] = 0.f;
+    for (int q = 0; q < a.kparts; ++q) {  // K parts in order (the restatement's fp32 add order)
+        const float* sp = a.slab + ((size_t)q * a.R + r) * a.lds + i;
+        const f32x4_t p0 = *reinterpret_cast<const f32x4_t*>(sp);
+        const f32x4_t p1 = *reinterpret_cast<const f32x4_t*>(sp + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            y[j] += p0[j];
+            y[4 + j] += p1[j];
+        }
+    }
+    if (a.bias) {
+        load8(a.bias + i, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] += b[j];
+    }
+    if (a.wscale) {
+        float sc[8];
+        load8(a.wscale + i, sc);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = rnd<T>(rnd<T>(y[j]) * sc[j]);
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        v[j] = rnd<T>(x[j] + rnd<T>(y[j]));
+        ss += v[j] * v[j];
+    }
+    if (live) {
+        T* xo = a.x_out + (size_t)r * a.ldx + i;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) st(xo, j, v[j]);
+    }
+    if (!a.nw) return;
+    ss = wave_sum(live ? ss : 0.f);
+    int* arrive = a.cnt + 2 * r;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store((g_f32*)(a.ss_part + (size_t)r * a.ch + c), ss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add((g_i32*)arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (unsigned spin = 0;; ++spin) {  // bounded: every block of the row is resident
+            if (__hip_atomic_load((g_i32*)arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.ch) break;
+            if (spin > (1u << 22)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    float tot = 0.f;
+    for (int q = 0; q < a.ch; ++q)  // chunk order: the same sum in every block of the row
+        tot += __hip_atomic_load((g_f32*)(a.ss_part + (size_t)r * a.ch + q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float rs = 1.0f / sqrtf(tot / (float)a.d + a.eps);
+    if (live) {
+        T* xn = a.xn_out + (size_t)r * a.ldxn + i;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) st(xn, j, rnd<T>(rnd<T>(v[j] * rs) * wn[j]));
+    }
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (__hip_atomic_fetch_add((g_i32*)(arrive + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.ch - 1) {
+            __hip_atomic_store((g_i32*)arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((g_i32*)(arrive + 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 template <typename T> void launch_finalize_norm(hipStream_t s, const FinalizeArgs<T>& a) {
     FMCHECK(a.d % 8 == 0 && a.d <= 8 * FN_THREADS * FN_CPT && a.lds % 4 == 0, "finalize_norm: bad row width");
+    if (a.ch > 1 && a.cnt && a.ss_part && a.R * a.ch <= 1024 && (a.d / 8 + a.ch - 1) / a.ch <= FS_THREADS) {
+        finalize_split_kernel<T><<<a.R * a.ch, FS_THREADS, 0, s>>>(a);
+        return;
+    }
     finalize_norm_kernel<T><<<a.R, FN_THREADS, 0, s>>>(a);
 }
 

@@ -278,6 +278,7 @@ struct FmTuning {
     int gemv_chain = 0;      // 1: batch-1 decode runs wo -> w1||w3 -> w2 -> next qkv as one launch (gemv_chain_kernel)
     int bsacc_kparts = 0;    // developer: force the K parts of the batched split-K (slab) linears (0: bsacc_plan's pick)
     int q_u = 4;             // int8 / int4 decode GEMV: ring units in flight per wave (2, 4, 8, 16; int8 frame 3.79 -> 3.59 ms at 8 -> 4)
+    int fin_split = 0;       // batched finalize_norm: each row over this many blocks (0 / 1: one block per row)
     int int4_stream = 1;     // weight-only int4: 1 the batch <= 8 GEMVs stream the 4-bit codes, 0 the dequantised bf16 copy
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
     int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1)
@@ -429,6 +430,11 @@ template <typename T> struct FinalizeArgs {
     T* xn_out;          // [R][ldxn]
     int ldxn, d, R;
     const T* wscale = nullptr;  // weight-only int8: round(res + round(round(sum) * wscale[n]))
+    // split form (fm_tune fin_split = ch > 1): each row over ch blocks that meet on cnt[2 r .. 2 r + 1]
+    // (zero between launches) after publishing their chunk's sum of squares to ss_part[r][ch]
+    int ch = 0;
+    int* cnt = nullptr;
+    float* ss_part = nullptr;
 };
 template <typename T> void launch_finalize_norm(hipStream_t s, const FinalizeArgs<T>& a);
 

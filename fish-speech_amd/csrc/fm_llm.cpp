@@ -181,6 +181,8 @@ struct fm_llm {
     // weight-only int8 (fm_llm_set_quant): packed T pointer of a linear -> its int8 form
     int quant = FM_QUANT_NONE;
     int q4_gs = 0;  // int4: group size along K
+    int* fin_cnt = nullptr;   // split finalize_norm: [max rows][2] counters (zero between launches)
+    float* fin_ss = nullptr;  //                      [max rows][16] chunk sums of squares
     struct QInfo {
         const unsigned char* q8 = nullptr;  // packed int8 (int4: 4-bit codes) decode-GEMV layout
         const void* scale = nullptr;        // int8: [rows padded to 16] in packed row order
@@ -453,6 +455,11 @@ template <typename T> struct Run {
                        void* xn, int d, int R, const void* sc) {
         FinalizeArgs<T> f{slab, kparts, d, (const T*)bias, (const T*)res, d, (T*)out, d, (const T*)nw,
                           m->c.norm_eps, (T*)xn, d, d, R, (const T*)sc};
+        if (fm_tuning().fin_split > 1 && m->fin_cnt) {
+            f.ch = fm_tuning().fin_split;
+            f.cnt = m->fin_cnt;
+            f.ss_part = m->fin_ss;
+        }
         run_("norm", 0, 0, [&] { launch_finalize_norm<T>(s, f); });
     }
     // finalise a W2 left pending by the last block of a stack (no norm)
@@ -1711,6 +1718,8 @@ static void finalize(fm_llm* m) {
         // arrival counters: one per 16-row tile of the largest decode GEMV (the slow head / W13)
         const int maxn = std::max({m->Nhead, 2 * c.intermediate_size, 2 * c.fast_intermediate_size, qkvmax, dmax, m->cb});  // W1||W3 is one 2*I-row linear on the batched path
         m->tickets = (int*)m->dalloc((size_t)(maxn / 16 + 16) * sizeof(int));
+        m->fin_cnt = (int*)m->dalloc((size_t)std::max(m->max_slots, 64) * 2 * sizeof(int));
+        m->fin_ss = (float*)m->dalloc((size_t)std::max(m->max_slots, 64) * 16 * sizeof(float));
         m->skpart_cap = 16ll << 20;  // 64 MiB of partial tiles (prompt GEMM slabs: 256 rows x 2 x 19456)
         m->skpart = (float*)m->dalloc((size_t)m->skpart_cap * sizeof(float), false);
     }
@@ -2428,6 +2437,9 @@ int fm_tune(const char* key, int value) {
         } else if (k == "q_u") {
             FMCHECK(value == 2 || value == 4 || value == 8 || value == 16, "q_u must be 2, 4, 8 or 16");
             t.q_u = value;
+        } else if (k == "fin_split") {
+            FMCHECK(value >= 0 && value <= 16, "fin_split must be 0..16");
+            t.fin_split = value;
         } else if (k == "int4_stream") {
             t.int4_stream = value != 0;
         } else if (k == "pass_fast") {
