@@ -11,6 +11,7 @@ per-launch HBM traffic of that kernel is added, FETCH_SIZE doubled per the gfx95
 MI355X_MICROARCH.md §HBM (wide coalesced reads are tallied at half their bytes).
 """
 import argparse
+import re
 import csv
 import json
 import os
@@ -76,7 +77,9 @@ def main():
         by[name][1] += ns
     total = sum(v[1] for v in by.values())
     rows = sorted(by.items(), key=lambda kv: -kv[1][1])
-    gemv = [(n, ns) for n, ns, _ in d if n.startswith("void gemv_kernel")]
+    # the bench's roofline kernel is the bf16 decode GEMV: gemv_kernel<..., QM = 0> (the int8 / int4
+    # legs' instantiations end in 1> / 2> and are reported apart)
+    gemv = [(n, ns) for n, ns, _ in d if n.startswith("void gemv_kernel") and re.search(r", 0>\(", n)]
     g_n = len(gemv)
     g_avg_us = sum(ns for _, ns in gemv) / max(g_n, 1) / 1e3
     summary = {"trace": os.path.basename(a.trace), "total_kernel_ms": total / 1e6,
@@ -92,13 +95,13 @@ def main():
             summary["gemv_kernel"]["bench_event_avg_us"] = bench["roofline"]["avg_launch_us"]
     if a.pmc_fetch:
         f = load_pmc(a.pmc_fetch, "FETCH_SIZE")
-        fv = [v for n, vs in f.items() if n.startswith("void gemv_kernel") for v in vs]
+        fv = [v for n, vs in f.items() if n.startswith("void gemv_kernel") and re.search(r", 0>\(", n) for v in vs]
         if fv:
             # rocprofv3 reports FETCH_SIZE in KB; x2 = gfx950 wide-read correction
             summary["gemv_kernel"]["fetch_bytes_per_launch"] = 2 * 1024 * sum(fv) / len(fv)
     if a.pmc_write:
         w = load_pmc(a.pmc_write, "WRITE_SIZE")
-        wv = [v for n, vs in w.items() if n.startswith("void gemv_kernel") for v in vs]
+        wv = [v for n, vs in w.items() if n.startswith("void gemv_kernel") and re.search(r", 0>\(", n) for v in vs]
         if wv:
             summary["gemv_kernel"]["write_bytes_per_launch"] = 1024 * sum(wv) / len(wv)
     g = summary["gemv_kernel"]
@@ -119,7 +122,7 @@ def main():
         fh.write("| % time | launches | avg us | total ms | kernel |\n|---:|---:|---:|---:|---|\n")
         for name, (n, ns) in rows[:30]:
             fh.write(f"| {100 * ns / total:.1f} | {n} | {ns / n / 1e3:.2f} | {ns / 1e6:.1f} | `{short(name)}` |\n")
-        fh.write(f"\n`gemv_kernel` (all instantiations): {g_n} launches, average {g_avg_us:.3f} us")
+        fh.write(f"\n`gemv_kernel` (bf16 instantiations, QM = 0): {g_n} launches, average {g_avg_us:.3f} us")
         if bench:
             fh.write(f"; bench.py HIP-event average in the same run: {bench['roofline']['avg_launch_us']} us")
         fh.write("\n")

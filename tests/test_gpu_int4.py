@@ -63,7 +63,8 @@ def test_int4_model_stream_matches_dequantized_model(golden):
     """S2-Pro widths (llm_wide: 2 slow + 1 fast layers), int4 with group size 128, teacher-forced
     frames through the production decode graph: the streamed 4-bit GEMVs (fm_tune int4_stream 1)
     against the same model on its dequantised bf16 weights (int4_stream 0) -- logits equal up to
-    fp32 summation order; and the int4 model tracks the bf16 model (quantization error only)."""
+    the rounding of the dequantised weights (the streamed form applies the affine map exactly, the
+    copy holds it rounded to bf16); and the int4 model tracks the bf16 model (quantization error only)."""
     from fishmi import native
     from fishmi.config import DualARConfig
     from fishmi.llm import DualARModel
@@ -100,7 +101,7 @@ def test_int4_model_stream_matches_dequantized_model(golden):
             a, b = a[:, rows], b[:, rows]
         fin = np.isfinite(b)
         rel = np.sqrt(np.mean((a[fin] - b[fin]) ** 2)) / np.sqrt(np.mean(b[fin] ** 2))
-        assert rel < 5e-3, (k, rel)
+        assert rel < 2e-2, (k, rel)  # (exact vs bf16-rounded dequantised weights)
         assert np.array_equal(np.isfinite(a), fin)
     # against the bf16 model: correlated, not equal (the int4 quantisation error)
     f4, fbf = out[1][1].ravel(), fb.ravel()

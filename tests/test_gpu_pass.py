@@ -58,8 +58,14 @@ def test_pass_matches_launch_path_and_replays(golden, pass_on):
     from fishmi import native
     from fishmi.llm import DualARModel
 
+    import os
+
+    from conftest import GOLDEN
+    from fishmi.config import DualARConfig
+
     g = golden("llm_wide_bf16.npz")
-    cfg = _cfg(g)
+    cfg = DualARConfig.from_pretrained(os.path.join(GOLDEN, "llm_wide"))
+    cfg.im_end_id = IM_END
     m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 2)
     T = g["prompt"].shape[1]
     cols = g["seq"][:, T:T + 6]
