@@ -2,7 +2,7 @@
 // runtime, for kernels shaped like libfishmi's (by-value argument structs of 64 B .. 2 KiB, dynamic
 // LDS past 64 KiB)?  hipcc --offload-arch=gfx950 -O2 scripts/graph_trace_probe.hip -o scripts/graph_trace_probe
 // Usage: graph_trace_probe [variant]  (0 all kernels, 1 small args only, 2 big args, 3 big LDS,
-// 4 a device-to-device copy node, 5 a memset node, 6 a copy into pinned host memory)
+// 4 a device-to-device copy node, 5 a memset node, 6 a copy into pinned host memory) [graph launches]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -68,7 +68,8 @@ int main(int argc, char** argv) {
     }
     CK(hipStreamEndCapture(s, &g));
     CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-    for (int r = 0; r < 3; ++r) CK(hipGraphLaunch(ge, s));
+    const int launches = argc > 2 ? atoi(argv[2]) : 3;
+    for (int r = 0; r < launches; ++r) CK(hipGraphLaunch(ge, s));
     CK(hipStreamSynchronize(s));
     float h[2];
     CK(hipMemcpy(h, d, 8, hipMemcpyDeviceToHost));
