@@ -82,6 +82,7 @@ struct fm_codec {
     void *z = nullptr, *xn = nullptr, *qkv = nullptr, *att = nullptr, *g1 = nullptr, *g3 = nullptr;
     void *u0 = nullptr, *u1 = nullptr, *hh = nullptr, *gb = nullptr;
     void *xb = nullptr, *A = nullptr, *B = nullptr, *Cb = nullptr;
+    void* zeros = nullptr;  // 256 zero bytes (resunit_kernel's DMA source outside the input rows)
     float* wave = nullptr;
     // stream state: carried rows per causal site (zeros at a stream start == causal padding)
     float* ksp = nullptr;                   // split-K workspace (conv_gemm_kernel slabs)
@@ -643,7 +644,12 @@ static void finalize(fm_codec* m) {
         auto& c0 = m->sctx[0];
         for (auto& pb : m->st_all) c0.bufs.push_back(pb.first);
     }
-    m->Cb = m->dalloc(Tm * maxact * E);
+    // the k7 output of the two-launch ResidualUnit, or (prefixed: it is a k7 input then) the third
+    // buffer the fused units ping-pong with
+    m->Cb = m->dalloc_prefixed(Tm * maxact * E, (size_t)CODEC_HALO * std::max(ch, D) * E);
+    m->zeros = m->dalloc(256);
+    HIPCHK(hipMemset(m->zeros, 0, 256));
+    resunit_init();
     m->ksp_cap = (size_t)16 << 20;  // split-K partial slabs of the small-grid codec GEMMs (64 MB)
     m->ksp = (float*)m->dalloc(m->ksp_cap * 4);
     m->wave = (float*)m->dalloc(Tm * 2048 * 4);
@@ -697,6 +703,46 @@ template <typename T> struct CRun {
         launch_conv_gemm<T>(s, a);
         m->flops += 2.0 * Lq * W.nphase * (double)W.Co * W.ntaps * W.Ci;
         m->launches++;
+    }
+
+    // one decoder ResidualUnit (modded_dac.py:599-620) as resunit_kernel (bf16, 96 / 192 channels):
+    // x = snake_a0 of the unit input in `x`, the residual in m->xb, snake_an of the output -> out2.
+    // false: not covered (fp32, other widths, fm_tune codec_fuse 0) -- the caller runs the two GEMMs
+    bool resunit(const RU& R, int dil, const void* x, int L, int lo, bool store_res, const void* an, void* out2,
+                 int C) {
+        if constexpr (sizeof(T) != 2) {
+            return false;
+        } else {
+            if (!R.c7.bias || !R.c1.bias || R.c7.ntaps != 7 || R.c7.Ci != C || R.c7.Co != C || R.c1.Ci != C ||
+                R.c1.Co != C || R.c7.ks != 1)
+                return false;
+            auto ia = [&](const void* al) {
+                auto it = m->ialpha.find(al);
+                FMCHECK(it != m->ialpha.end(), "codec: Snake alpha without reciprocals");
+                return (const float*)it->second;
+            };
+            ResUnitArgs a{};
+            a.x = (const bf16_t*)x;
+            a.L = L;
+            a.lo = lo;
+            a.dil = dil;
+            a.w7 = (const bf16_t*)R.c7.w;
+            a.b7 = (const bf16_t*)R.c7.bias;
+            a.a2 = (const bf16_t*)R.a2;
+            a.ia2 = ia(R.a2);
+            a.w1 = (const bf16_t*)R.c1.w;
+            a.b1 = (const bf16_t*)R.c1.bias;
+            a.res = (bf16_t*)m->xb;
+            a.store_res = store_res;
+            a.an = (const bf16_t*)an;
+            a.ian = ia(an);
+            a.out2 = (bf16_t*)out2;
+            a.zeros = (const bf16_t*)m->zeros;
+            if (!launch_resunit(s, a, C)) return false;
+            m->flops += 2.0 * L * (double)C * 8 * C;  // k7 (K = 7 C) + k1 (K = C)
+            m->launches++;
+            return true;
+        }
     }
 
     // WindowLimitedTransformer.forward (modded_dac.py:418-439) on z [Tn][Dm] in place; the final
@@ -836,6 +882,7 @@ template <typename T> struct CRun {
         site_out(stream, xin, D, 6, L, m->st_c0);
         void* in = m->A;
         void* alt = m->B;
+        void* spare = m->Cb;  // fused units: alt -> spare, then the two swap
         int cin = ch;
         const int rates[4] = {8, 8, 4, 2};
         for (int b = 0; b < 4; ++b) {
@@ -850,10 +897,15 @@ template <typename T> struct CRun {
             for (int r = 0; r < 3; ++r) {
                 const RU& R = Bk.ru[r];
                 const int hr = 6 * dl[r];
+                const void* an = r < 2 ? Bk.ru[r + 1].a0 : (b < 3 ? m->blk[b + 1].alpha : m->falpha);
                 site_in(stream, alt, cout, hr, m->st_c7[b][r]);
+                if (resunit(R, dl[r], alt, L, stream ? -hr : 0, r < 2, an, spare, cout)) {
+                    site_out(stream, alt, cout, hr, L, m->st_c7[b][r]);
+                    std::swap(alt, spare);
+                    continue;
+                }
                 gemm(R.c7, alt, cout, L, L, nullptr, 0, 0, nullptr, 0, nullptr, R.a2, m->Cb, cout, stream ? -hr : 0);
                 site_out(stream, alt, cout, hr, L, m->st_c7[b][r]);
-                const void* an = r < 2 ? Bk.ru[r + 1].a0 : (b < 3 ? m->blk[b + 1].alpha : m->falpha);
                 gemm(R.c1, m->Cb, cout, L, L, m->xb, cout, (r < 2 ? CE_STORE : 0) | CE_RES, m->xb, cout, nullptr,
                      an, alt, cout);
             }

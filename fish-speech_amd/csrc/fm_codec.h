@@ -43,6 +43,34 @@ template <typename T> struct ConvArgs {
     int ksplit;                // set by the launcher
 };
 
+// One decoder ResidualUnit (modded_dac.py:599-620) in one launch, bf16, C in {96, 192}:
+//   h   = round(snake_a2(round(conv7_dil(x) + b7)))            (the k7 conv's output, LDS only)
+//   y   = round(res + round(conv1(h) + b1))                    (res: stored back when store_res)
+//   out2 = round(snake_an(y))                                  (the next unit's / stage's input)
+// x = snake_a0 of the unit input, time-major [t][C], rows [lo, 0) the carried context of a streamed
+// chunk (buffer prefix), rows < lo causal zeros.  out2 must not alias x (neighbour tiles read x's
+// rows behind them).  The k-steps and their fp32 accumulation order are conv_gemm2_kernel's, so
+// the result is bit-identical to the two-launch form.
+struct ResUnitArgs {
+    const bf16_t* x;
+    int L, lo, dil;
+    const bf16_t* w7;    // packed k7 weights (fm_kernels.h fragment order, K = 7 C as [tap][ci])
+    const bf16_t* b7;
+    const bf16_t* a2;
+    const float* ia2;
+    const bf16_t* w1;    // packed k1 weights (K = C)
+    const bf16_t* b1;
+    bf16_t* res;         // residual [L][C], read, and written back when store_res
+    int store_res;
+    const bf16_t* an;
+    const float* ian;
+    bf16_t* out2;        // [L][C]
+    const bf16_t* zeros; // >= 16 zero bytes: the LDS-DMA source of rows outside [lo, L)
+};
+// false: shape not covered (C not 96 / 192, dil > 9) -- the caller runs the two-launch form
+bool launch_resunit(hipStream_t s, const ResUnitArgs& a, int C);
+void resunit_init();
+
 struct RvqPtrs {
     const float* cb[16];  // codebooks [size][cd]
     const float* w[16];   // folded out_proj [D][cd]

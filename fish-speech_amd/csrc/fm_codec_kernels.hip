@@ -778,6 +778,220 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0
     conv_gemm_kernel<T><<<g, 256, 0, s>>>(b);
 }
 
+// ---------------------------------------------------------------------------------------
+// resunit_kernel: a decoder ResidualUnit (ResUnitArgs, fm_codec.h) per launch.  Block tile: BM
+// output times x all C channels; wave (wt, wc) owns times [128 wt, +128) x channels [48 wc, +48),
+// 8 x 3 MFMA tiles (24 accumulators), so a k-step costs a wave 8 X fragments from LDS and 3 weight
+// fragments from L2 (the k7 weights, 7 C^2 x 2 B <= 516 KB, stay L2-resident).
+//  1. the input window (rows t0 - 6 dil .. t0 + BM) lands in LDS once by LDS-DMA (16-B slots of a
+//     padded row, out-of-range rows from a zero block): every tap reads it at a row offset, so X
+//     costs HBM its bytes once instead of once per tap and channel tile;
+//  2. k7: k-steps in conv_gemm2_kernel's order (tap-major, 32 channels each), the weights through a
+//     three-step register ring;
+//  3. h = round(snake(round(acc + b7))) overwrites the window in LDS (bf16 [BM][C + 8]);
+//  4. k1 over h, weights again from L2;
+//  5. round(acc + b1) parked in LDS, then 16-B chunks: + residual, store, next Snake.
+// LDS <= 72 KB and 4 waves: two blocks per CU, one block's window DMA under the other's MFMAs.
+namespace {
+__device__ __forceinline__ uint32_t ru_lds_off(const void* p) {
+    return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+// one 16-B slot per lane by LDS-DMA: lane l's 16 bytes at gsrc -> LDS lds_base + 16 l (M0 saved
+// and restored in the statement; the DMA is invisible to hipcc's waitcnt bookkeeping, so the wait
+// for it is an explicit s_waitcnt vmcnt)
+__device__ __forceinline__ void ru_glds16(const void* gsrc, uint32_t lds_base) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_base)
+        : "memory");
+}
+constexpr int RU_MAXDIL = 9;
+template <int C, int BM> constexpr int ru_nw() { return (BM / 128) * (C / 48); }
+template <int C, int BM> constexpr size_t ru_lds() {
+    constexpr size_t slots = (size_t)(BM + 6 * RU_MAXDIL) * ((C + 8) / 8);
+    constexpr size_t win = (slots + 63) / 64 * 1024;  // whole 64-slot DMA instructions
+    constexpr size_t h = (size_t)BM * (C + 8) * 2;
+    return win > h ? win : h;
+}
+}  // namespace
+
+template <int C, int BM>
+__global__ __launch_bounds__((ru_nw<C, BM>() * 64)) __attribute__((amdgpu_waves_per_eu(2))) void resunit_kernel(
+    ResUnitArgs a) {
+    using F = Frag<bf16_t>;
+    constexpr int NW = ru_nw<C, BM>(), NT = NW * 64, WCN = C / 48;
+    constexpr int XS = C + 8;     // LDS row stride (elements): 16-B reads of 16 rows spread over the banks
+    constexpr int SPR = XS / 8;   // 16-B slots per LDS row (C / 8 data + 1 pad)
+    constexpr int SK = C / 32;    // k-steps per tap
+    constexpr int S7 = 7 * SK, S1 = SK;
+    static_assert(C % 48 == 0 && BM % 128 == 0 && S7 % 3 == 0 && S1 % 3 == 0, "resunit tiling");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_ru[];
+    bf16_t* xw = reinterpret_cast<bf16_t*>(smem_ru);
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int wt = wave / WCN, wc = wave - wt * WCN;
+    const int t0 = blockIdx.x * BM;
+    const int hal = 6 * a.dil, nslot = (BM + hal) * SPR;
+
+    // 1. window -> LDS (wave-uniform instruction bases; lanes past the window write the tail of the
+    //    last 1 KiB, which ru_lds reserves)
+    {
+        const uint32_t x0 = __builtin_amdgcn_readfirstlane(ru_lds_off(xw));
+        for (int i0 = wave * 64; i0 < nslot; i0 += NT) {
+            const int i = i0 + lane;
+            const int r = i / SPR, c = i - r * SPR;
+            const int tin = t0 - hal + r;
+            const bool ok = i < nslot && c < C / 8 && tin >= a.lo && tin < a.L;
+            ru_glds16(ok ? (const void*)(a.x + (ptrdiff_t)tin * C + 8 * c) : (const void*)a.zeros,
+                      __builtin_amdgcn_readfirstlane(x0 + 16u * i0));
+        }
+    }
+    // weight ring: fragments (channel tile 3 wc + ct, k-step s), 3 k-steps deep
+    const bf16_t* w7 = a.w7 + (size_t)(3 * wc) * S7 * 512;
+    const bf16_t* w1 = a.w1 + (size_t)(3 * wc) * S1 * 512;
+    u32x4_t wr0[3], wr1[3], wr2[3];
+    auto wload = [&](u32x4_t (&w)[3], const bf16_t* base, int S, int s) {
+        s = s < S ? s : S - 1;
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) w[ct] = F::load_w(base + ((size_t)ct * S + s) * 512, lane);
+    };
+    wload(wr0, w7, S7, 0);
+    wload(wr1, w7, S7, 1);
+    wload(wr2, w7, S7, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    f32x4_t acc[8][3];
+#pragma unroll
+    for (int tt = 0; tt < 8; ++tt)
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) acc[tt][ct] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int xr = 128 * wt + (lane & 15), xk = 8 * (lane >> 4);
+    // one k-step: 8 X fragments (rows xr + 16 tt + row offset) x the ring's 3 weight fragments
+    auto mma8 = [&](const bf16_t* xb, const u32x4_t (&w)[3]) {
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+            const F::f xf = F::load(xb + (size_t)16 * tt * XS);
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct) acc[tt][ct] = F::mma(w[ct], xf, acc[tt][ct]);
+        }
+    };
+    // 2. k7: k-step s = tap j, channels [32 q, 32 q + 32); tap j reads input row t - (6 - j) dil =
+    //    window row (t - t0) + j dil
+    auto step7 = [&](int s, const u32x4_t (&w)[3]) {
+        const int j = s / SK, q = s - j * SK;
+        mma8(xw + (size_t)(xr + j * a.dil) * XS + 32 * q + xk, w);
+    };
+    for (int s = 0; s < S7; s += 3) {
+        step7(s, wr0);
+        wload(wr0, w7, S7, s + 3);
+        step7(s + 1, wr1);
+        wload(wr1, w7, S7, s + 4);
+        step7(s + 2, wr2);
+        wload(wr2, w7, S7, s + 5);
+    }
+    // the k1 ring goes out before the epilogue (its loads overlap it)
+    wload(wr0, w1, S1, 0);
+    wload(wr1, w1, S1, 1);
+    wload(wr2, w1, S1, 2);
+    // 3. h = round(snake_a2(round(acc + b7))) -> LDS over the window (every wave is past its reads)
+    const int cl = 48 * wc + 4 * (lane >> 4);  // + 16 ct + i: the lane's accumulator channels
+    auto park = [&](const bf16_t* bias, const bf16_t* al, const float* ia) {
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) {
+            float bv[4], av[4], iv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int co = cl + 16 * ct + i;
+                bv[i] = bf2f(bias[co]);
+                av[i] = al ? bf2f(al[co]) : 0.f;
+                iv[i] = al ? ia[co] : 0.f;
+            }
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) {
+                float y[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    y[i] = bfround(acc[tt][ct][i] + bv[i]);
+                    if (al) y[i] = bfround(snake_fi(y[i], av[i], iv[i]));
+                }
+                const uint32_t w0 = (__float_as_uint(y[0]) >> 16) | (__float_as_uint(y[1]) & 0xffff0000u);
+                const uint32_t w1v = (__float_as_uint(y[2]) >> 16) | (__float_as_uint(y[3]) & 0xffff0000u);
+                *reinterpret_cast<uint2*>(xw + (size_t)(xr + 16 * tt) * XS + cl + 16 * ct) = make_uint2(w0, w1v);
+            }
+        }
+    };
+    __syncthreads();
+    park(a.b7, a.a2, a.ia2);
+    __syncthreads();
+    // 4. k1 over h
+#pragma unroll
+    for (int tt = 0; tt < 8; ++tt)
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) acc[tt][ct] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const bf16_t* hb = xw + (size_t)xr * XS + xk;
+    for (int s = 0; s < S1; s += 3) {
+        mma8(hb + 32 * s, wr0);
+        wload(wr0, w1, S1, s + 3);
+        mma8(hb + 32 * (s + 1), wr1);
+        wload(wr1, w1, S1, s + 4);
+        mma8(hb + 32 * (s + 2), wr2);
+        wload(wr2, w1, S1, s + 5);
+    }
+    // 5. round(acc + b1) parked over h, then per 16-B chunk: residual, store, next Snake
+    __syncthreads();
+    park(a.b1, nullptr, nullptr);
+    __syncthreads();
+    for (int q = threadIdx.x; q < BM * (C / 8); q += NT) {
+        const int row = q / (C / 8), cc = q - row * (C / 8);
+        const int t = t0 + row;
+        if (t >= a.L) continue;
+        const int co = 8 * cc;
+        float y[8], rv[8], al[8], sn[8];
+        load8(xw + (size_t)row * XS + co, y);
+        load8(a.res + (size_t)t * C + co, rv);
+        load8(a.an + co, al);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = bfround(rv[j] + y[j]);
+        if (a.store_res) store8(a.res + (size_t)t * C + co, y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sn[j] = bfround(snake_fi(y[j], al[j], a.ian[co + j]));
+        store8(a.out2 + (size_t)t * C + co, sn);
+    }
+}
+
+void resunit_init() {
+    static bool done = false;
+    if (done) return;
+    done = true;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&resunit_kernel<192, 128>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ru_lds<192, 128>());
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&resunit_kernel<96, 256>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ru_lds<96, 256>());
+    (void)hipGetLastError();
+}
+
+bool launch_resunit(hipStream_t s, const ResUnitArgs& a, int C) {
+    if (!fm_tuning().codec_fuse || a.dil < 1 || a.dil > RU_MAXDIL || a.L < 1 || a.lo > 0) return false;
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    FMCHECK(a.x && a.w7 && a.b7 && a.a2 && a.ia2 && a.w1 && a.b1 && a.res && a.an && a.ian && a.out2 && a.zeros &&
+                al16(a.x) && al16(a.res) && al16(a.out2) && a.out2 != a.x,
+            "resunit: operands");
+    if (C == 192) {
+        resunit_kernel<192, 128><<<FM_CEIL(a.L, 128), ru_nw<192, 128>() * 64, ru_lds<192, 128>(), s>>>(a);
+    } else if (C == 96) {
+        resunit_kernel<96, 256><<<FM_CEIL(a.L, 256), ru_nw<96, 256>() * 64, ru_lds<96, 256>(), s>>>(a);
+    } else {
+        return false;
+    }
+    return true;
+}
+
 template <typename T> void launch_snake_inv(hipStream_t s, const T* alpha, int64_t n, float* ialpha) {
     snake_inv_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(alpha, n, ialpha);
 }

@@ -19,14 +19,18 @@ def run():
     ccfg = CodecConfig()
     codec = FishMICodec.synthetic(ccfg, 1, 0, "bf16", max_frames=216)
     codes = np.random.default_rng(0).integers(0, 1024, (ccfg.n_codebooks + 1, 216)).astype(np.int32)
-    for conv2 in (1, 1):
-        native.tune("conv2", conv2)
+    ref = None
+    for fuse in (0, 1, 0, 1):  # fused decoder ResidualUnits (resunit_kernel) off / on
+        native.tune("codec_fuse", fuse)
         for _ in range(3):
-            codec.decode_codes(codes)
+            w = codec.decode_codes(codes)
         ms0, n0, f0 = codec.profile()
         codec.decode_codes(codes)
         ms1, n1, f1 = codec.profile()
-        print(f"conv2={conv2}: {ms1 - ms0:.2f} ms, {(f1 - f0) / ((ms1 - ms0) * 1e-3) / 1e12:.1f} TFLOP/s", flush=True)
+        same = "" if ref is None else f", bit-identical to fuse=0: {bool(np.array_equal(w, ref))}"
+        ref = w if ref is None else ref
+        print(f"codec_fuse={fuse}: {ms1 - ms0:.2f} ms, {n1 - n0} GEMM launches, "
+              f"{(f1 - f0) / ((ms1 - ms0) * 1e-3) / 1e12:.1f} TFLOP/s{same}", flush=True)
 
 
 def sequence(db, n_decodes):

@@ -1,0 +1,77 @@
+"""GPU: the fused decoder ResidualUnit (resunit_kernel, fm_tune codec_fuse) against the two-launch
+form (k7 conv_gemm2 + k1 conv_gemm2).
+
+The fused kernel runs the same k-steps (tap-major, 32 channels each) through the same MFMA into
+the same fp32 accumulators, and rounds h, y and both Snakes exactly as the two epilogues do, so
+the bound is bit-for-bit equality of the waveform: one-shot at config-2 length (216 frames, the
+reference's own codes), streamed in config 2's growing chunks (carried causal context through the
+fused units' input prefix), and 300 random frames in ragged chunks.  Stages at 96 and 192
+channels are fused; the 768 / 384 stages keep the two launches in both modes.
+"""
+import json
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _codec(golden, max_frames):
+    from fishmi.codec import FishMICodec
+    from fishmi.config import CodecConfig
+
+    g = golden("codec_long.npz")
+    cfg = CodecConfig.from_spec(json.loads(str(g["spec"])))
+    return FishMICodec.synthetic(cfg, int(g["synth_seed"]), 0, "bf16", max_frames), g
+
+
+def _both(m, f):
+    from fishmi import native
+
+    native.tune("codec_fuse", 0)
+    try:
+        two = f()
+    finally:
+        native.tune("codec_fuse", 1)
+    return f(), two
+
+
+def _stream(m, codes, sizes):
+    m.stream_reset()
+    out, t = [], 0
+    for n in sizes:
+        out.append(m.decode_chunk(np.ascontiguousarray(codes[:, t:t + n])))
+        t += n
+    assert t == codes.shape[1]
+    return np.concatenate(out)
+
+
+def test_fused_equals_two_launch_one_shot(golden):
+    m, g = _codec(golden, 216)
+    codes = g["codes"][0]
+    fused, two = _both(m, lambda: m.decode_codes(codes))
+    assert fused.shape == (codes.shape[1] * 2048,)
+    np.testing.assert_array_equal(fused, two)
+    m.close()
+
+
+def test_fused_equals_two_launch_streamed(golden):
+    m, g = _codec(golden, 216)
+    codes = g["codes"][0]
+    fused, two = _both(m, lambda: _stream(m, codes, (1, 4, 16, 64, 131)))
+    np.testing.assert_array_equal(fused, two)
+    np.testing.assert_array_equal(fused, m.decode_codes(codes))
+    m.close()
+
+
+def test_fused_random_ragged(golden):
+    m, _ = _codec(golden, 320)
+    rng = np.random.default_rng(11)
+    C1, T = m.cfg.n_codebooks + 1, 300
+    codes = np.zeros((C1, T), np.int32)
+    codes[0] = rng.integers(0, m.cfg.semantic_codebook_size, T)
+    codes[1:] = rng.integers(0, m.cfg.codebook_size, (C1 - 1, T))
+    fused, two = _both(m, lambda: _stream(m, codes, (3, 9, 22, 100, 166)))
+    np.testing.assert_array_equal(fused, two)
+    assert np.abs(fused).max() <= 1.0
+    m.close()
