@@ -705,7 +705,7 @@ template <typename T> struct CRun {
         m->launches++;
     }
 
-    // one decoder ResidualUnit (modded_dac.py:599-620) as resunit_kernel (bf16, 96 / 192 channels):
+    // one decoder ResidualUnit (modded_dac.py:599-620) as resunit_kernel (bf16, 96 / 192 / 384 channels):
     // x = snake_a0 of the unit input in `x`, the residual in m->xb, snake_an of the output -> out2.
     // false: not covered (fp32, other widths, fm_tune codec_fuse 0) -- the caller runs the two GEMMs
     bool resunit(const RU& R, int dil, const void* x, int L, int lo, bool store_res, const void* an, void* out2,

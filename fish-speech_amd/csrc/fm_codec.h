@@ -43,7 +43,7 @@ template <typename T> struct ConvArgs {
     int ksplit;                // set by the launcher
 };
 
-// One decoder ResidualUnit (modded_dac.py:599-620) in one launch, bf16, C in {96, 192}:
+// One decoder ResidualUnit (modded_dac.py:599-620) in one launch, bf16, C in {96, 192, 384}:
 //   h   = round(snake_a2(round(conv7_dil(x) + b7)))            (the k7 conv's output, LDS only)
 //   y   = round(res + round(conv1(h) + b1))                    (res: stored back when store_res)
 //   out2 = round(snake_an(y))                                  (the next unit's / stage's input)
@@ -67,7 +67,7 @@ struct ResUnitArgs {
     bf16_t* out2;        // [L][C]
     const bf16_t* zeros; // >= 16 zero bytes: the LDS-DMA source of rows outside [lo, L)
 };
-// false: shape not covered (C not 96 / 192, dil > 9) -- the caller runs the two-launch form
+// false: shape not covered (C not 96 / 192 / 384, dil > 9) -- the caller runs the two-launch form
 bool launch_resunit(hipStream_t s, const ResUnitArgs& a, int C);
 void resunit_init();
 

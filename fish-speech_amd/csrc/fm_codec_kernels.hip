@@ -19,19 +19,14 @@
 #include "fm_runtime.h"
 #include "fm_frag.h"
 
-// sin^2(x) without the library sinf's wide-range machinery (the epilogues apply it to every output
-// element): Cody-Waite reduction by pi/2 in three fmas (x = n pi/2 + r, |r| <= pi/4, good to
-// |x| ~ 1e4), the Cephes sin polynomial on r, and sin^2(x) = sin^2(r) for even n, 1 - sin^2(r) for
-// odd n (sin^2(r) <= 1/2 there, so no cancellation).  Within a few fp32 ulp of sinf(x)^2.
+// sin^2(x) for the Snake epilogues (descript Snake1d: x + (a+1e-9)^-1 sin^2(a x)), applied to every
+// output element, twice per ResidualUnit: the hardware sine (v_sin_f32, argument in revolutions) of
+// the fractional revolution x / 2 pi -- three VALU slots and one transcendental instead of a
+// Cody-Waite reduction and a polynomial (the epilogues, not the MFMAs, bound the narrow decoder
+// stages).  The reduction to [0, 1) keeps the argument inside v_sin_f32's domain at any |x|.
 __device__ __forceinline__ float sin2_f(float x) {
-    const float n = rintf(x * 0.636619772367581343f);
-    float r = fmaf(-n, 1.5703125f, x);
-    r = fmaf(-n, 4.837512969970703125e-4f, r);
-    r = fmaf(-n, 7.54978995489188216e-8f, r);
-    const float z = r * r;
-    const float sr = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
-    const float s2 = sr * sr;
-    return (((int)n) & 1) ? 1.0f - s2 : s2;
+    const float s = __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(x * 0.159154943091895336f));
+    return s * s;
 }
 __device__ __forceinline__ float snake_f(float y, float al) {
     return y + (1.0f / (al + 1e-9f)) * sin2_f(al * y);
@@ -812,7 +807,7 @@ __device__ __forceinline__ void ru_glds16(const void* gsrc, uint32_t lds_base) {
         : "memory");
 }
 constexpr int RU_MAXDIL = 9;
-template <int C, int BM> constexpr int ru_nw() { return (BM / 128) * (C / 48); }
+template <int C, int BM, int TT> constexpr int ru_nw() { return (BM / (16 * TT)) * (C / 48); }
 template <int C, int BM> constexpr size_t ru_lds() {
     constexpr size_t slots = (size_t)(BM + 6 * RU_MAXDIL) * ((C + 8) / 8);
     constexpr size_t win = (slots + 63) / 64 * 1024;  // whole 64-slot DMA instructions
@@ -821,16 +816,16 @@ template <int C, int BM> constexpr size_t ru_lds() {
 }
 }  // namespace
 
-template <int C, int BM>
-__global__ __launch_bounds__((ru_nw<C, BM>() * 64)) __attribute__((amdgpu_waves_per_eu(2))) void resunit_kernel(
+template <int C, int BM, int TT, int WPE>
+__global__ __launch_bounds__((ru_nw<C, BM, TT>() * 64)) __attribute__((amdgpu_waves_per_eu(WPE))) void resunit_kernel(
     ResUnitArgs a) {
     using F = Frag<bf16_t>;
-    constexpr int NW = ru_nw<C, BM>(), NT = NW * 64, WCN = C / 48;
+    constexpr int NW = ru_nw<C, BM, TT>(), NT = NW * 64, WCN = C / 48;
     constexpr int XS = C + 8;     // LDS row stride (elements): 16-B reads of 16 rows spread over the banks
     constexpr int SPR = XS / 8;   // 16-B slots per LDS row (C / 8 data + 1 pad)
     constexpr int SK = C / 32;    // k-steps per tap
     constexpr int S7 = 7 * SK, S1 = SK;
-    static_assert(C % 48 == 0 && BM % 128 == 0 && S7 % 3 == 0 && S1 % 3 == 0, "resunit tiling");
+    static_assert(C % 48 == 0 && BM % (16 * TT) == 0 && S7 % 3 == 0 && S1 % 3 == 0, "resunit tiling");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_ru[];
     bf16_t* xw = reinterpret_cast<bf16_t*>(smem_ru);
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -866,16 +861,16 @@ __global__ __launch_bounds__((ru_nw<C, BM>() * 64)) __attribute__((amdgpu_waves_
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    f32x4_t acc[8][3];
+    f32x4_t acc[TT][3];
 #pragma unroll
-    for (int tt = 0; tt < 8; ++tt)
+    for (int tt = 0; tt < TT; ++tt)
 #pragma unroll
         for (int ct = 0; ct < 3; ++ct) acc[tt][ct] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    const int xr = 128 * wt + (lane & 15), xk = 8 * (lane >> 4);
+    const int xr = 16 * TT * wt + (lane & 15), xk = 8 * (lane >> 4);
     // one k-step: 8 X fragments (rows xr + 16 tt + row offset) x the ring's 3 weight fragments
     auto mma8 = [&](const bf16_t* xb, const u32x4_t (&w)[3]) {
 #pragma unroll
-        for (int tt = 0; tt < 8; ++tt) {
+        for (int tt = 0; tt < TT; ++tt) {
             const F::f xf = F::load(xb + (size_t)16 * tt * XS);
 #pragma unroll
             for (int ct = 0; ct < 3; ++ct) acc[tt][ct] = F::mma(w[ct], xf, acc[tt][ct]);
@@ -887,13 +882,18 @@ __global__ __launch_bounds__((ru_nw<C, BM>() * 64)) __attribute__((amdgpu_waves_
         const int j = s / SK, q = s - j * SK;
         mma8(xw + (size_t)(xr + j * a.dil) * XS + 32 * q + xk, w);
     };
+    // (sched_barrier: each refill stays right behind the step that freed its slot; left to itself
+    // the compiler sinks all three to the end of the trip and the ring's lookahead is gone)
     for (int s = 0; s < S7; s += 3) {
         step7(s, wr0);
         wload(wr0, w7, S7, s + 3);
+        __builtin_amdgcn_sched_barrier(0);
         step7(s + 1, wr1);
         wload(wr1, w7, S7, s + 4);
+        __builtin_amdgcn_sched_barrier(0);
         step7(s + 2, wr2);
         wload(wr2, w7, S7, s + 5);
+        __builtin_amdgcn_sched_barrier(0);
     }
     // the k1 ring goes out before the epilogue (its loads overlap it)
     wload(wr0, w1, S1, 0);
@@ -913,7 +913,7 @@ __global__ __launch_bounds__((ru_nw<C, BM>() * 64)) __attribute__((amdgpu_waves_
                 iv[i] = al ? ia[co] : 0.f;
             }
 #pragma unroll
-            for (int tt = 0; tt < 8; ++tt) {
+            for (int tt = 0; tt < TT; ++tt) {
                 float y[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -931,17 +931,20 @@ __global__ __launch_bounds__((ru_nw<C, BM>() * 64)) __attribute__((amdgpu_waves_
     __syncthreads();
     // 4. k1 over h
 #pragma unroll
-    for (int tt = 0; tt < 8; ++tt)
+    for (int tt = 0; tt < TT; ++tt)
 #pragma unroll
         for (int ct = 0; ct < 3; ++ct) acc[tt][ct] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     const bf16_t* hb = xw + (size_t)xr * XS + xk;
     for (int s = 0; s < S1; s += 3) {
         mma8(hb + 32 * s, wr0);
         wload(wr0, w1, S1, s + 3);
+        __builtin_amdgcn_sched_barrier(0);
         mma8(hb + 32 * (s + 1), wr1);
         wload(wr1, w1, S1, s + 4);
+        __builtin_amdgcn_sched_barrier(0);
         mma8(hb + 32 * (s + 2), wr2);
         wload(wr2, w1, S1, s + 5);
+        __builtin_amdgcn_sched_barrier(0);
     }
     // 5. round(acc + b1) parked over h, then per 16-B chunk: residual, store, next Snake
     __syncthreads();
@@ -965,14 +968,19 @@ __global__ __launch_bounds__((ru_nw<C, BM>() * 64)) __attribute__((amdgpu_waves_
     }
 }
 
+// tile variants (fm_tune resunit_cfg): {C, BM, time tiles per wave, waves per SIMD}
+#define RU_VARIANTS(X) \
+    X(192, 128, 8, 2) X(96, 256, 8, 2) X(192, 64, 4, 3) X(96, 128, 4, 4) X(192, 128, 4, 4) X(96, 128, 8, 2) \
+    X(384, 64, 4, 2)
 void resunit_init() {
     static bool done = false;
     if (done) return;
     done = true;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&resunit_kernel<192, 128>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ru_lds<192, 128>());
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&resunit_kernel<96, 256>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ru_lds<96, 256>());
+#define RU_ATTR(C, BM, TT, WPE)                                                                     \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&resunit_kernel<C, BM, TT, WPE>),       \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ru_lds<C, BM>());
+    RU_VARIANTS(RU_ATTR)
+#undef RU_ATTR
     (void)hipGetLastError();
 }
 
@@ -982,14 +990,23 @@ bool launch_resunit(hipStream_t s, const ResUnitArgs& a, int C) {
     FMCHECK(a.x && a.w7 && a.b7 && a.a2 && a.ia2 && a.w1 && a.b1 && a.res && a.an && a.ian && a.out2 && a.zeros &&
                 al16(a.x) && al16(a.res) && al16(a.out2) && a.out2 != a.x,
             "resunit: operands");
-    if (C == 192) {
-        resunit_kernel<192, 128><<<FM_CEIL(a.L, 128), ru_nw<192, 128>() * 64, ru_lds<192, 128>(), s>>>(a);
-    } else if (C == 96) {
-        resunit_kernel<96, 256><<<FM_CEIL(a.L, 256), ru_nw<96, 256>() * 64, ru_lds<96, 256>(), s>>>(a);
-    } else {
-        return false;
-    }
+    const int cfg = fm_tuning().resunit_cfg;
+#define RU_GO(CC, BM, TT, WPE)                                                                            \
+    resunit_kernel<CC, BM, TT, WPE><<<FM_CEIL(a.L, BM), ru_nw<CC, BM, TT>() * 64, ru_lds<CC, BM>(), s>>>(a); \
     return true;
+    if (C == 192) {
+        if (cfg == 1) { RU_GO(192, 64, 4, 3) }
+        if (cfg == 2) { RU_GO(192, 128, 4, 4) }
+        RU_GO(192, 128, 8, 2)
+    }
+    if (C == 384 && fm_tuning().resunit_384) { RU_GO(384, 64, 4, 2) }
+    if (C == 96) {
+        if (cfg == 1) { RU_GO(96, 128, 4, 4) }
+        if (cfg == 2) { RU_GO(96, 128, 8, 2) }
+        RU_GO(96, 256, 8, 2)
+    }
+#undef RU_GO
+    return false;
 }
 
 template <typename T> void launch_snake_inv(hipStream_t s, const T* alpha, int64_t n, float* ialpha) {

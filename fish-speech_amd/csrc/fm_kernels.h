@@ -258,7 +258,9 @@ struct FmTuning {
     int prompt_gemm = 1;     // 1: prompt-chunk linears (R > 32) on the codec's LDS-tiled GEMM kernels
     int conv2 = 1;           // 1: codec GEMMs on the LDS-staged conv_gemm2_kernel, 0: conv_gemm_kernel
     int conv_splitk = 1;     // 1: small-grid codec GEMMs split K into fp32 slabs + a reduce/epilogue kernel
-    int codec_fuse = 1;      // 1: decoder ResidualUnits at 96 / 192 channels as one resunit_kernel launch (k7 + k1)
+    int resunit_cfg = 1;     // resunit_kernel tile at 192 / 96 channels: 0 (BM 128 / 256, 8 time tiles per wave), 1 (BM 64 / 128, 4 tiles), 2 (128 / 128)
+    int resunit_384 = 1;     // 1: the 384-channel stage's units fused too (BM 64, 8 waves)
+    int codec_fuse = 1;      // 1: decoder ResidualUnits at 96 / 192 / 384 channels as one resunit_kernel launch (k7 + k1)
     int bstream = 1;         // 1: batched decode linears (8 < R <= 32) on bstream_kernel (fm_bstream.hip)
     int bstream_kparts = 0;  // bstream EPI_SLAB K parts (0: by K)
     int bstream_nw = 0;      // bstream waves per block (0: 16 whole-K, 8 split-K)

@@ -2360,6 +2360,11 @@ int fm_tune(const char* key, int value) {
             t.conv_splitk = value != 0;
         } else if (k == "codec_fuse") {
             t.codec_fuse = value != 0;
+        } else if (k == "resunit_384") {
+            t.resunit_384 = value != 0;
+        } else if (k == "resunit_cfg") {
+            FMCHECK(value >= 0 && value <= 2, "resunit_cfg must be 0..2");
+            t.resunit_cfg = value;
         } else if (k == "attn_wo") {
             t.attn_wo = value != 0;
         } else if (k == "gemv_wpb") {

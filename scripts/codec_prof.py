@@ -20,8 +20,10 @@ def run():
     codec = FishMICodec.synthetic(ccfg, 1, 0, "bf16", max_frames=216)
     codes = np.random.default_rng(0).integers(0, 1024, (ccfg.n_codebooks + 1, 216)).astype(np.int32)
     ref = None
-    for fuse in (0, 1, 0, 1):  # fused decoder ResidualUnits (resunit_kernel) off / on
+    # fused decoder ResidualUnits (resunit_kernel) off / on, and its tile variants (resunit_cfg)
+    for fuse, cfg in ((0, 0), (1, 0), (1, 1), (1, 2), (0, 0), (1, 0), (1, 1), (1, 2)):
         native.tune("codec_fuse", fuse)
+        native.tune("resunit_cfg", cfg)
         for _ in range(3):
             w = codec.decode_codes(codes)
         ms0, n0, f0 = codec.profile()
@@ -29,7 +31,7 @@ def run():
         ms1, n1, f1 = codec.profile()
         same = "" if ref is None else f", bit-identical to fuse=0: {bool(np.array_equal(w, ref))}"
         ref = w if ref is None else ref
-        print(f"codec_fuse={fuse}: {ms1 - ms0:.2f} ms, {n1 - n0} GEMM launches, "
+        print(f"codec_fuse={fuse} resunit_cfg={cfg}: {ms1 - ms0:.2f} ms, {n1 - n0} GEMM launches, "
               f"{(f1 - f0) / ((ms1 - ms0) * 1e-3) / 1e12:.1f} TFLOP/s{same}", flush=True)
 
 
@@ -52,7 +54,7 @@ def summarise(db):
     rows = c.execute("select name, start, end, grid_x, grid_y, grid_z, workgroup_x from kernels order by start").fetchall()
     agg = defaultdict(lambda: [0, 0.0])
     for r in rows:
-        if "conv_gemm" not in r[0]:
+        if "conv_gemm" not in r[0] and "resunit" not in r[0]:
             continue
         k = (r[0].split("(")[0].replace("void ", "")[:40], r[3] // r[6], r[4], r[5])
         agg[k][0] += 1

@@ -7,5 +7,5 @@ mkdir -p gpurun_out
 timeout -k 10 200 rocprofv3 --kernel-trace -d /tmp/prof_$TAG -o run -- python3 scripts/codec_prof.py \
     > gpurun_out/prof_$TAG.log 2>&1 &&
 python3 scripts/codec_prof.py $(find /tmp/prof_$TAG -name '*results.db' -print -quit) >> gpurun_out/prof_$TAG.log 2>&1 &&
-python3 scripts/codec_prof.py $(find /tmp/prof_$TAG -name "*results.db" -print -quit) 16 > gpurun_out/seq_$TAG.log 2>&1 &&
+python3 scripts/codec_prof.py $(find /tmp/prof_$TAG -name "*results.db" -print -quit) 32 > gpurun_out/seq_$TAG.log 2>&1 &&
 echo PROF_DONE
