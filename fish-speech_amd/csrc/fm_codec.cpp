@@ -236,6 +236,7 @@ static void build_inventory(fm_codec* m) {
 
 // encode-side keys (mirrors fishmi/checkpoint.codec_encoder_tensor_shapes)
 static const int ENC_RATES[4] = {2, 4, 8, 8};
+static const int ENC_DILS[3] = {1, 3, 9};  // the three ResidualUnits of an EncoderBlock
 static constexpr int ENC_WINDOW = 512;  // EncoderBlock transformer: getattr(partial, "window_size", 512)
 static void add_tlayers(fm_codec* m, const std::string& pre, int dim, int layers, int HD, int I) {
     for (int l = 0; l < layers; ++l) {
@@ -706,10 +707,10 @@ template <typename T> struct CRun {
     }
 
     // one decoder ResidualUnit (modded_dac.py:599-620) as resunit_kernel (bf16, 96 / 192 / 384 channels):
-    // x = snake_a0 of the unit input in `x`, the residual in m->xb, snake_an of the output -> out2.
+    // x = snake_a0 of the unit input in `x`, the residual in `res`, snake_an of the output -> out2.
     // false: not covered (fp32, other widths, fm_tune codec_fuse 0) -- the caller runs the two GEMMs
     bool resunit(const RU& R, int dil, const void* x, int L, int lo, bool store_res, const void* an, void* out2,
-                 int C) {
+                 int C, void* res) {
         if constexpr (sizeof(T) != 2) {
             return false;
         } else {
@@ -732,7 +733,7 @@ template <typename T> struct CRun {
             a.ia2 = ia(R.a2);
             a.w1 = (const bf16_t*)R.c1.w;
             a.b1 = (const bf16_t*)R.c1.bias;
-            a.res = (bf16_t*)m->xb;
+            a.res = (bf16_t*)res;
             a.store_res = store_res;
             a.an = (const bf16_t*)an;
             a.ian = ia(an);
@@ -790,8 +791,12 @@ template <typename T> struct CRun {
             const int st = ENC_RATES[b], d = 2 * h;
             for (int r = 0; r < 3; ++r) {  // ResidualUnit (modded_dac.py:600-620)
                 const RU& R = B.ru[r];
-                gemm(R.c7, alt, h, L, L, nullptr, 0, 0, nullptr, 0, nullptr, R.a2, spare, h);
                 const void* an = r < 2 ? B.ru[r + 1].a0 : B.a3;
+                if (resunit(R, ENC_DILS[r], alt, L, 0, r < 2, an, spare, h, m->e_x)) {
+                    std::swap(alt, spare);  // (the unit's output Snake is in `spare` now)
+                    continue;
+                }
+                gemm(R.c7, alt, h, L, L, nullptr, 0, 0, nullptr, 0, nullptr, R.a2, spare, h);
                 gemm(R.c1, spare, h, L, L, m->e_x, h, (r < 2 ? CE_STORE : 0) | CE_RES, m->e_x, h, nullptr, an, alt, h);
             }
             const int Lo = L / st;
@@ -899,7 +904,7 @@ template <typename T> struct CRun {
                 const int hr = 6 * dl[r];
                 const void* an = r < 2 ? Bk.ru[r + 1].a0 : (b < 3 ? m->blk[b + 1].alpha : m->falpha);
                 site_in(stream, alt, cout, hr, m->st_c7[b][r]);
-                if (resunit(R, dl[r], alt, L, stream ? -hr : 0, r < 2, an, spare, cout)) {
+                if (resunit(R, dl[r], alt, L, stream ? -hr : 0, r < 2, an, spare, cout, m->xb)) {
                     site_out(stream, alt, cout, hr, L, m->st_c7[b][r]);
                     std::swap(alt, spare);
                     continue;

@@ -807,7 +807,7 @@ __device__ __forceinline__ void ru_glds16(const void* gsrc, uint32_t lds_base) {
         : "memory");
 }
 constexpr int RU_MAXDIL = 9;
-template <int C, int BM, int TT> constexpr int ru_nw() { return (BM / (16 * TT)) * (C / 48); }
+template <int C, int BM, int TT, int CT> constexpr int ru_nw() { return (BM / (16 * TT)) * (C / (16 * CT)); }
 template <int C, int BM> constexpr size_t ru_lds() {
     constexpr size_t slots = (size_t)(BM + 6 * RU_MAXDIL) * ((C + 8) / 8);
     constexpr size_t win = (slots + 63) / 64 * 1024;  // whole 64-slot DMA instructions
@@ -816,16 +816,16 @@ template <int C, int BM> constexpr size_t ru_lds() {
 }
 }  // namespace
 
-template <int C, int BM, int TT, int WPE>
-__global__ __launch_bounds__((ru_nw<C, BM, TT>() * 64)) __attribute__((amdgpu_waves_per_eu(WPE))) void resunit_kernel(
+template <int C, int BM, int TT, int WPE, int CT>
+__global__ __launch_bounds__((ru_nw<C, BM, TT, CT>() * 64)) __attribute__((amdgpu_waves_per_eu(WPE))) void resunit_kernel(
     ResUnitArgs a) {
     using F = Frag<bf16_t>;
-    constexpr int NW = ru_nw<C, BM, TT>(), NT = NW * 64, WCN = C / 48;
+    constexpr int NW = ru_nw<C, BM, TT, CT>(), NT = NW * 64, WCN = C / (16 * CT);
     constexpr int XS = C + 8;     // LDS row stride (elements): 16-B reads of 16 rows spread over the banks
     constexpr int SPR = XS / 8;   // 16-B slots per LDS row (C / 8 data + 1 pad)
     constexpr int SK = C / 32;    // k-steps per tap
     constexpr int S7 = 7 * SK, S1 = SK;
-    static_assert(C % 48 == 0 && BM % (16 * TT) == 0 && S7 % 3 == 0 && S1 % 3 == 0, "resunit tiling");
+    static_assert(C % (16 * CT) == 0 && C % 32 == 0 && BM % (16 * TT) == 0, "resunit tiling");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_ru[];
     bf16_t* xw = reinterpret_cast<bf16_t*>(smem_ru);
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -847,13 +847,13 @@ __global__ __launch_bounds__((ru_nw<C, BM, TT>() * 64)) __attribute__((amdgpu_wa
         }
     }
     // weight ring: fragments (channel tile 3 wc + ct, k-step s), 3 k-steps deep
-    const bf16_t* w7 = a.w7 + (size_t)(3 * wc) * S7 * 512;
-    const bf16_t* w1 = a.w1 + (size_t)(3 * wc) * S1 * 512;
-    u32x4_t wr0[3], wr1[3], wr2[3];
-    auto wload = [&](u32x4_t (&w)[3], const bf16_t* base, int S, int s) {
+    const bf16_t* w7 = a.w7 + (size_t)(CT * wc) * S7 * 512;
+    const bf16_t* w1 = a.w1 + (size_t)(CT * wc) * S1 * 512;
+    u32x4_t wr0[CT], wr1[CT], wr2[CT];
+    auto wload = [&](u32x4_t (&w)[CT], const bf16_t* base, int S, int s) {
         s = s < S ? s : S - 1;
 #pragma unroll
-        for (int ct = 0; ct < 3; ++ct) w[ct] = F::load_w(base + ((size_t)ct * S + s) * 512, lane);
+        for (int ct = 0; ct < CT; ++ct) w[ct] = F::load_w(base + ((size_t)ct * S + s) * 512, lane);
     };
     wload(wr0, w7, S7, 0);
     wload(wr1, w7, S7, 1);
@@ -861,38 +861,44 @@ __global__ __launch_bounds__((ru_nw<C, BM, TT>() * 64)) __attribute__((amdgpu_wa
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    f32x4_t acc[TT][3];
+    f32x4_t acc[TT][CT];
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt)
 #pragma unroll
-        for (int ct = 0; ct < 3; ++ct) acc[tt][ct] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        for (int ct = 0; ct < CT; ++ct) acc[tt][ct] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     const int xr = 16 * TT * wt + (lane & 15), xk = 8 * (lane >> 4);
     // one k-step: 8 X fragments (rows xr + 16 tt + row offset) x the ring's 3 weight fragments
-    auto mma8 = [&](const bf16_t* xb, const u32x4_t (&w)[3]) {
+    auto mma8 = [&](const bf16_t* xb, const u32x4_t (&w)[CT]) {
 #pragma unroll
         for (int tt = 0; tt < TT; ++tt) {
             const F::f xf = F::load(xb + (size_t)16 * tt * XS);
 #pragma unroll
-            for (int ct = 0; ct < 3; ++ct) acc[tt][ct] = F::mma(w[ct], xf, acc[tt][ct]);
+            for (int ct = 0; ct < CT; ++ct) acc[tt][ct] = F::mma(w[ct], xf, acc[tt][ct]);
         }
     };
     // 2. k7: k-step s = tap j, channels [32 q, 32 q + 32); tap j reads input row t - (6 - j) dil =
     //    window row (t - t0) + j dil
-    auto step7 = [&](int s, const u32x4_t (&w)[3]) {
+    auto step7 = [&](int s, const u32x4_t (&w)[CT]) {
         const int j = s / SK, q = s - j * SK;
         mma8(xw + (size_t)(xr + j * a.dil) * XS + 32 * q + xk, w);
     };
     // (sched_barrier: each refill stays right behind the step that freed its slot; left to itself
     // the compiler sinks all three to the end of the trip and the ring's lookahead is gone)
+    // (a trip count that is not a multiple of 3 ends in a guarded partial trip; the guards fold
+    // away when it is)
     for (int s = 0; s < S7; s += 3) {
         step7(s, wr0);
         wload(wr0, w7, S7, s + 3);
         __builtin_amdgcn_sched_barrier(0);
-        step7(s + 1, wr1);
-        wload(wr1, w7, S7, s + 4);
+        if (S7 % 3 == 0 || s + 1 < S7) {
+            step7(s + 1, wr1);
+            wload(wr1, w7, S7, s + 4);
+        }
         __builtin_amdgcn_sched_barrier(0);
-        step7(s + 2, wr2);
-        wload(wr2, w7, S7, s + 5);
+        if (S7 % 3 == 0 || s + 2 < S7) {
+            step7(s + 2, wr2);
+            wload(wr2, w7, S7, s + 5);
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
     // the k1 ring goes out before the epilogue (its loads overlap it)
@@ -900,10 +906,10 @@ __global__ __launch_bounds__((ru_nw<C, BM, TT>() * 64)) __attribute__((amdgpu_wa
     wload(wr1, w1, S1, 1);
     wload(wr2, w1, S1, 2);
     // 3. h = round(snake_a2(round(acc + b7))) -> LDS over the window (every wave is past its reads)
-    const int cl = 48 * wc + 4 * (lane >> 4);  // + 16 ct + i: the lane's accumulator channels
+    const int cl = 16 * CT * wc + 4 * (lane >> 4);  // + 16 ct + i: the lane's accumulator channels
     auto park = [&](const bf16_t* bias, const bf16_t* al, const float* ia) {
 #pragma unroll
-        for (int ct = 0; ct < 3; ++ct) {
+        for (int ct = 0; ct < CT; ++ct) {
             float bv[4], av[4], iv[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -933,17 +939,21 @@ __global__ __launch_bounds__((ru_nw<C, BM, TT>() * 64)) __attribute__((amdgpu_wa
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt)
 #pragma unroll
-        for (int ct = 0; ct < 3; ++ct) acc[tt][ct] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        for (int ct = 0; ct < CT; ++ct) acc[tt][ct] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     const bf16_t* hb = xw + (size_t)xr * XS + xk;
     for (int s = 0; s < S1; s += 3) {
         mma8(hb + 32 * s, wr0);
         wload(wr0, w1, S1, s + 3);
         __builtin_amdgcn_sched_barrier(0);
-        mma8(hb + 32 * (s + 1), wr1);
-        wload(wr1, w1, S1, s + 4);
+        if (S1 % 3 == 0 || s + 1 < S1) {
+            mma8(hb + 32 * (s + 1), wr1);
+            wload(wr1, w1, S1, s + 4);
+        }
         __builtin_amdgcn_sched_barrier(0);
-        mma8(hb + 32 * (s + 2), wr2);
-        wload(wr2, w1, S1, s + 5);
+        if (S1 % 3 == 0 || s + 2 < S1) {
+            mma8(hb + 32 * (s + 2), wr2);
+            wload(wr2, w1, S1, s + 5);
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
     // 5. round(acc + b1) parked over h, then per 16-B chunk: residual, store, next Snake
@@ -968,16 +978,18 @@ __global__ __launch_bounds__((ru_nw<C, BM, TT>() * 64)) __attribute__((amdgpu_wa
     }
 }
 
-// tile variants (fm_tune resunit_cfg): {C, BM, time tiles per wave, waves per SIMD}
-#define RU_VARIANTS(X) \
-    X(192, 128, 8, 2) X(96, 256, 8, 2) X(192, 64, 4, 3) X(96, 128, 4, 4) X(192, 128, 4, 4) X(96, 128, 8, 2) \
-    X(384, 64, 4, 2)
+// tile variants: {C, BM, time tiles per wave, waves per SIMD, channel tiles per wave}; decoder
+// (fm_tune resunit_cfg picks among the 192 / 96 ones), then encoder widths
+#define RU_VARIANTS(X)                                                                                  \
+    X(192, 128, 8, 2, 3) X(96, 256, 8, 2, 3) X(192, 64, 4, 3, 3) X(96, 128, 4, 4, 3) X(192, 128, 4, 4, 3) \
+    X(96, 128, 8, 2, 3) X(384, 64, 4, 2, 3) X(64, 256, 4, 3, 4) X(128, 128, 4, 3, 4) X(256, 64, 4, 3, 4)  \
+    X(512, 64, 4, 2, 4)
 void resunit_init() {
     static bool done = false;
     if (done) return;
     done = true;
-#define RU_ATTR(C, BM, TT, WPE)                                                                     \
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&resunit_kernel<C, BM, TT, WPE>),       \
+#define RU_ATTR(C, BM, TT, WPE, CT)                                                                 \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&resunit_kernel<C, BM, TT, WPE, CT>),   \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)ru_lds<C, BM>());
     RU_VARIANTS(RU_ATTR)
 #undef RU_ATTR
@@ -991,19 +1003,26 @@ bool launch_resunit(hipStream_t s, const ResUnitArgs& a, int C) {
                 al16(a.x) && al16(a.res) && al16(a.out2) && a.out2 != a.x,
             "resunit: operands");
     const int cfg = fm_tuning().resunit_cfg;
-#define RU_GO(CC, BM, TT, WPE)                                                                            \
-    resunit_kernel<CC, BM, TT, WPE><<<FM_CEIL(a.L, BM), ru_nw<CC, BM, TT>() * 64, ru_lds<CC, BM>(), s>>>(a); \
+#define RU_GO(CC, BM, TT, WPE, CT)                                                                   \
+    resunit_kernel<CC, BM, TT, WPE, CT>                                                                \
+        <<<FM_CEIL(a.L, BM), ru_nw<CC, BM, TT, CT>() * 64, ru_lds<CC, BM>(), s>>>(a);                   \
     return true;
+    if (C == 384 && fm_tuning().resunit_384) { RU_GO(384, 64, 4, 2, 3) }
     if (C == 192) {
-        if (cfg == 1) { RU_GO(192, 64, 4, 3) }
-        if (cfg == 2) { RU_GO(192, 128, 4, 4) }
-        RU_GO(192, 128, 8, 2)
+        if (cfg == 0) { RU_GO(192, 128, 8, 2, 3) }
+        if (cfg == 2) { RU_GO(192, 128, 4, 4, 3) }
+        RU_GO(192, 64, 4, 3, 3)
     }
-    if (C == 384 && fm_tuning().resunit_384) { RU_GO(384, 64, 4, 2) }
     if (C == 96) {
-        if (cfg == 1) { RU_GO(96, 128, 4, 4) }
-        if (cfg == 2) { RU_GO(96, 128, 8, 2) }
-        RU_GO(96, 256, 8, 2)
+        if (cfg == 0) { RU_GO(96, 256, 8, 2, 3) }
+        if (cfg == 2) { RU_GO(96, 128, 8, 2, 3) }
+        RU_GO(96, 128, 4, 4, 3)
+    }
+    if (fm_tuning().resunit_enc) {  // encoder widths (EncoderBlock's units, modded_dac.py:623-667)
+        if (C == 64) { RU_GO(64, 256, 4, 3, 4) }
+        if (C == 128) { RU_GO(128, 128, 4, 3, 4) }
+        if (C == 256) { RU_GO(256, 64, 4, 3, 4) }
+        if (C == 512) { RU_GO(512, 64, 4, 2, 4) }
     }
 #undef RU_GO
     return false;

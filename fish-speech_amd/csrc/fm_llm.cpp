@@ -2360,6 +2360,8 @@ int fm_tune(const char* key, int value) {
             t.conv_splitk = value != 0;
         } else if (k == "codec_fuse") {
             t.codec_fuse = value != 0;
+        } else if (k == "resunit_enc") {
+            t.resunit_enc = value != 0;
         } else if (k == "resunit_384") {
             t.resunit_384 = value != 0;
         } else if (k == "resunit_cfg") {

@@ -75,3 +75,33 @@ def test_fused_random_ragged(golden):
     np.testing.assert_array_equal(fused, two)
     assert np.abs(fused).max() <= 1.0
     m.close()
+
+
+def test_fused_encoder_units_equal_two_launch(golden):
+    """The encoder's ResidualUnits (64 / 128 / 256 / 512 channels at codec_enc_full's widths) run
+    the same fused kernel: z_enc and the codes bit-identical to the two-launch form, bf16."""
+    from fishmi import native
+    from fishmi.codec import FishMICodec
+    from fishmi.config import CodecConfig
+
+    g = golden("codec_enc_full.npz")
+    spec = json.loads(str(g["spec"]))
+    m = FishMICodec(CodecConfig.from_spec(spec), 0, "bf16", max_frames=16)
+    m.enable_encoder(spec["encoder_dim"], [int(v) for v in g["enc_layers"]])
+    m.synth(int(g["synth_seed"]))
+    m.synth_encoder(int(g["synth_seed"]))
+    m.finalize()
+
+    def run():
+        codes = m.encode_audio(g["audio"])
+        return codes, m.debug_read(10, codes.shape[1])
+
+    native.tune("resunit_enc", 0)
+    try:
+        c0, z0 = run()
+    finally:
+        native.tune("resunit_enc", 1)
+    c1, z1 = run()
+    np.testing.assert_array_equal(z1, z0)
+    np.testing.assert_array_equal(c1, c0)
+    m.close()
