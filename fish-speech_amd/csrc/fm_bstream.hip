@@ -413,8 +413,9 @@ __global__ __launch_bounds__(FN_THREADS) void finalize_norm_kernel(FinalizeArgs<
         const int i = 8 * (threadIdx.x + FN_THREADS * c);
         if (i < a.d) load8(a.res + (size_t)r * a.ldr + i, x[c]);
     }
-    // slab sums, K parts in order (fp32 add order = the reference restatement's), four parts'
-    // loads for both chunks issued before the adds that consume them
+    // slab sums, K parts in order (fp32 add order = the reference restatement's); eight (then
+    // four) parts' loads issued before the adds that consume them -- at 8 K parts (the S2-Pro
+    // slab linears) one round trip instead of two.  Chunk c = 1 only exists for d > 8 * FN_THREADS.
     float y[FN_CPT][8];
 #pragma unroll
     for (int c = 0; c < FN_CPT; ++c)
@@ -422,27 +423,51 @@ __global__ __launch_bounds__(FN_THREADS) void finalize_norm_kernel(FinalizeArgs<
         for (int j = 0; j < 8; ++j) y[c][j] = 0.f;
     {
         int q = 0;
-        for (; q + 4 <= a.kparts; q += 4) {
-            f32x4_t p[4][FN_CPT][2];
+        auto batch = [&](auto NB) {
+            constexpr int B = decltype(NB)::value;
+            for (; q + B <= a.kparts; q += B) {
+                f32x4_t p[B][FN_CPT][2];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+                for (int u = 0; u < B; ++u)
 #pragma unroll
-                for (int c = 0; c < FN_CPT; ++c) {
-                    const int i = 8 * (threadIdx.x + FN_THREADS * c);
+                    for (int c = 0; c < FN_CPT; ++c) {
+                        const int i = 8 * (threadIdx.x + FN_THREADS * c);
+                        const float* sp = a.slab + ((size_t)(q + u) * a.R + r) * a.lds + (i < a.d ? i : 0);
+                        p[u][c][0] = *reinterpret_cast<const f32x4_t*>(sp);
+                        p[u][c][1] = *reinterpret_cast<const f32x4_t*>(sp + 4);
+                    }
+#pragma unroll
+                for (int u = 0; u < B; ++u)
+#pragma unroll
+                    for (int c = 0; c < FN_CPT; ++c)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            y[c][j] += p[u][c][0][j];
+                            y[c][4 + j] += p[u][c][1][j];
+                        }
+            }
+        };
+        if (a.d <= 8 * FN_THREADS && a.fin8) {
+            // one chunk per thread: the eight parts' 16 loads fit the register budget
+            for (; q + 8 <= a.kparts; q += 8) {
+                f32x4_t p[8][2];
+                const int i = 8 * (int)threadIdx.x;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
                     const float* sp = a.slab + ((size_t)(q + u) * a.R + r) * a.lds + (i < a.d ? i : 0);
-                    p[u][c][0] = *reinterpret_cast<const f32x4_t*>(sp);
-                    p[u][c][1] = *reinterpret_cast<const f32x4_t*>(sp + 4);
+                    p[u][0] = *reinterpret_cast<const f32x4_t*>(sp);
+                    p[u][1] = *reinterpret_cast<const f32x4_t*>(sp + 4);
                 }
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int c = 0; c < FN_CPT; ++c)
+                for (int u = 0; u < 8; ++u)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        y[c][j] += p[u][c][0][j];
-                        y[c][4 + j] += p[u][c][1][j];
+                        y[0][j] += p[u][0][j];
+                        y[0][4 + j] += p[u][1][j];
                     }
+            }
         }
+        batch(std::integral_constant<int, 4>{});
         for (; q < a.kparts; ++q) {
 #pragma unroll
             for (int c = 0; c < FN_CPT; ++c) {
@@ -791,7 +816,9 @@ template <typename T> void launch_finalize_norm(hipStream_t s, const FinalizeArg
         finalize_split_kernel<T><<<a.R * a.ch, FS_THREADS, 0, s>>>(a);
         return;
     }
-    finalize_norm_kernel<T><<<a.R, FN_THREADS, 0, s>>>(a);
+    FinalizeArgs<T> b = a;
+    b.fin8 = fm_tuning().fin8;
+    finalize_norm_kernel<T><<<a.R, FN_THREADS, 0, s>>>(b);
 }
 
 template bool launch_bstream<bf16_t>(hipStream_t, const BstreamArgs<bf16_t>&, int, const BstreamPlan&);

@@ -282,6 +282,7 @@ struct FmTuning {
     int gemv_chain = 0;      // 1: batch-1 decode runs wo -> w1||w3 -> w2 -> next qkv as one launch (gemv_chain_kernel)
     int bsacc_kparts = 0;    // developer: force the K parts of the batched split-K (slab) linears (0: bsacc_plan's pick)
     int q_u = 4;             // int8 / int4 decode GEMV: ring units in flight per wave (2, 4, 8, 16; int8 frame 3.79 -> 3.59 ms at 8 -> 4)
+    int fin8 = 1;            // finalize_norm: all eight K parts' slab loads in one round trip (0: two batches of four)
     int fin_split = 0;       // batched finalize_norm: each row over this many blocks (0 / 1: one block per row)
     int int4_stream = 1;     // weight-only int4: 1 the batch <= 8 GEMVs stream the 4-bit codes, 0 the dequantised bf16 copy
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
@@ -439,6 +440,7 @@ template <typename T> struct FinalizeArgs {
     int ch = 0;
     int* cnt = nullptr;
     float* ss_part = nullptr;
+    int fin8 = 0;       // set by the launcher (fm_tune fin8): eight K parts' slab loads in one round trip
 };
 template <typename T> void launch_finalize_norm(hipStream_t s, const FinalizeArgs<T>& a);
 

@@ -2446,6 +2446,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "q_u") {
             FMCHECK(value == 2 || value == 4 || value == 8 || value == 16, "q_u must be 2, 4, 8 or 16");
             t.q_u = value;
+        } else if (k == "fin8") {
+            t.fin8 = value != 0;
         } else if (k == "fin_split") {
             FMCHECK(value >= 0 && value <= 16, "fin_split must be 0..16");
             t.fin_split = value;
