@@ -30,9 +30,14 @@ static void small_m(PackedW& W) {
     W.ks = W.Co % 8 == 0 ? ks : 1;
 }
 
+// [A rows | B rows] of two packed one-tap linears over the same input as one PackedW (the packed
+// layout is 16-row tile-major, so it is the two buffers back to back)
+static PackedW concat_rows(fm_codec* m, const PackedW& A, const PackedW& B);
+
 struct TLayer {
     void *an, *fn, *ag, *fg;
     PackedW wqkv, wo, w1, w3, w2;
+    PackedW w13;  // [W1 rows | W3 rows] as one GEMM (CE_SWIGLU split-K epilogue); w null: not built
 };
 struct RU {
     void *a0, *a2;
@@ -335,6 +340,20 @@ static void* as_snake(fm_codec* m, const float* src, int64_t n) {
 }
 
 // prepare a GEMM weight: kind per conv_weight_kernel; returns phases packed
+static PackedW concat_rows(fm_codec* m, const PackedW& A, const PackedW& B) {
+    FMCHECK(A.Ci == B.Ci && A.ntaps == 1 && B.ntaps == 1 && A.nphase == 1 && B.nphase == 1 && A.Co % 16 == 0 &&
+                A.Co == B.Co && !A.bias && !B.bias && A.ks == B.ks && A.wphase == B.wphase,
+            "codec: W1 / W3 concatenation needs two bias-free one-tap linears of one shape");
+    PackedW p = A;
+    p.Co = A.Co + B.Co;
+    p.wphase = A.wphase + B.wphase;
+    p.w = m->dalloc(p.wphase * m->esz);
+    HIPCHK(hipMemcpyAsync(p.w, A.w, A.wphase * m->esz, hipMemcpyDeviceToDevice, m->stream));
+    HIPCHK(hipMemcpyAsync((char*)p.w + A.wphase * m->esz, B.w, B.wphase * m->esz, hipMemcpyDeviceToDevice, m->stream));
+    HIPCHK(hipStreamSynchronize(m->stream));
+    return p;
+}
+
 static PackedW prep(fm_codec* m, const float* w, int kind, int Ci, int Co, int k, int s, int dil,
                     const float* bias) {
     PackedW p;
@@ -551,6 +570,7 @@ static void finalize(fm_codec* m) {
         L.w3 = prep(m, raw(m, p + "feed_forward.w3.weight"), 3, D, I, 1, 1, 1, nullptr);
         L.w2 = prep(m, raw(m, p + "feed_forward.w2.weight"), 3, I, D, 1, 1, 1, nullptr);
         for (PackedW* W : {&L.wqkv, &L.wo, &L.w1, &L.w3, &L.w2}) small_m(*W);
+        L.w13 = concat_rows(m, L.w1, L.w3);
     }
     m->tnorm = as_T(m, raw(m, "quantizer.post_module.norm.weight"), D);
     for (int u = 0; u < 2; ++u) {
@@ -746,6 +766,19 @@ template <typename T> struct CRun {
         }
     }
 
+    // FeedForward's silu(w1 x) * w3 x (modded_dac.py:316-317) into g3: one GEMM over [W1 | W3] with
+    // the SwiGLU split-K epilogue when the layer splits K (bit-identical), else w1, w3, silu_mul
+    void ffn13(const TLayer& L, const void* xn, int Dm, int Tn, int I, void* g1, void* g3) {
+        const FmTuning& tu = fm_tuning();
+        if (L.w13.w && tu.codec_swiglu && tu.conv_splitk && L.w13.ks > 1) {
+            gemm(L.w13, xn, Dm, Tn, Tn, g3, I, CE_STORE | CE_SWIGLU);
+            return;
+        }
+        gemm(L.w1, xn, Dm, Tn, Tn, g1, I, CE_STORE);
+        gemm(L.w3, xn, Dm, Tn, Tn, g3, I, CE_STORE);
+        launch_silu_mul<T>(s, (const T*)g1, (T*)g3, (size_t)Tn * I);
+    }
+
     // WindowLimitedTransformer.forward (modded_dac.py:418-439) on z [Tn][Dm] in place; the final
     // norm goes to xn
     void transformer(const std::vector<TLayer>& tl, const void* norm, int Tn, int Dm, int H, int hd, int I,
@@ -758,9 +791,7 @@ template <typename T> struct CRun {
             launch_window_attn<T>(s, (const T*)qkv, Tn, H, hd, window, (T*)att, 0);
             gemm(L.wo, att, H * hd, Tn, Tn, z, Dm, CE_STORE | CE_RES | CE_GAMMA, z, Dm, L.ag);
             launch_rmsnorm<T>(s, (const T*)z, Dm, (const T*)L.fn, Dm, eps, (T*)xn, Dm, Tn);
-            gemm(L.w1, xn, Dm, Tn, Tn, g1, I, CE_STORE);
-            gemm(L.w3, xn, Dm, Tn, Tn, g3, I, CE_STORE);
-            launch_silu_mul<T>(s, (const T*)g1, (T*)g3, (size_t)Tn * I);
+            ffn13(L, xn, Dm, Tn, I, g1, g3);
             gemm(L.w2, g3, I, Tn, Tn, z, Dm, CE_STORE | CE_RES | CE_GAMMA, z, Dm, L.fg);
         }
         launch_rmsnorm<T>(s, (const T*)z, Dm, (const T*)norm, Dm, eps, (T*)xn, Dm, Tn);
@@ -858,9 +889,7 @@ template <typename T> struct CRun {
             site_out(stream, m->qkv, 3 * H * hd, W1, Tn, m->st_kv[l]);
             gemm(L.wo, m->att, H * hd, Tn, Tn, m->z, D, CE_STORE | CE_RES | CE_GAMMA, m->z, D, L.ag);
             launch_rmsnorm<T>(s, (const T*)m->z, D, (const T*)L.fn, D, c.norm_eps, (T*)m->xn, D, Tn);
-            gemm(L.w1, m->xn, D, Tn, Tn, m->g1, I, CE_STORE);
-            gemm(L.w3, m->xn, D, Tn, Tn, m->g3, I, CE_STORE);
-            launch_silu_mul<T>(s, (const T*)m->g1, (T*)m->g3, (size_t)Tn * I);
+            ffn13(L, m->xn, D, Tn, I, m->g1, m->g3);
             gemm(L.w2, m->g3, I, Tn, Tn, m->z, D, CE_STORE | CE_RES | CE_GAMMA, m->z, D, L.fg);
         }
         launch_rmsnorm<T>(s, (const T*)m->z, D, (const T*)m->tnorm, D, c.norm_eps, (T*)m->xn, D, Tn);

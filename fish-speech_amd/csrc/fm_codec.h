@@ -12,6 +12,8 @@ enum {
     CE_SNAKE = 32,    // store snake(y, alpha2) to out2 (the next stage's input)
     CE_TANH = 64,     // y = tanh(y) (decoder output, modded_dac.py:795)
     CE_F32OUT = 128,  // out is fp32 (final waveform)
+    CE_SWIGLU = 256,  // split-K epilogue only: out[t][n] = round(round(silu(y[n])) * y[Co/2 + n]) for
+                      // n < Co/2 (W1 and W3 of a FeedForward as one GEMM, modded_dac.py:316-317)
 };
 
 // out[t_out][co] (time-major, ld = ldo) with t_out = tq * stride + phase, tq in [0, Lq):

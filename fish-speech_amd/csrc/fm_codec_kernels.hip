@@ -144,17 +144,22 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
 
 // split-K reduction + the conv epilogue on 8 consecutive channels per thread (16-B accesses):
 // y = round(sum_kz partial + bias) -> GELU -> residual / LayerScale -> tanh -> store / Snake
+// CE_SWIGLU: the GEMM's channels are [W1 rows | W3 rows]; thread (t, n) also sums the partials of
+// channel Co/2 + n and writes round(round(silu(g1)) * g3), g = round(sum) -- silu_mul_kernel's
+// roundings on the two GEMMs' stored outputs, so the result is bit-identical to the three launches.
 template <typename T>
 __global__ __launch_bounds__(256) void conv_splitk_epi_kernel(ConvArgs<T> a) {
-    const int cpr = a.Co >> 3;
-    const size_t n = (size_t)a.nphase * a.Lq * cpr;
     const int fl = a.flags;
+    const int half = (fl & CE_SWIGLU) ? a.Co >> 1 : 0;
+    const int cpr = (half ? half : a.Co) >> 3;
+    const size_t n = (size_t)a.nphase * a.Lq * cpr;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
         const int cc = (int)(i % cpr);
         const size_t pt = i / cpr;  // phase * Lq + t
         const int t = (int)(pt % a.Lq), phase = (int)(pt / a.Lq);
         const int co = 8 * cc;
         float y[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        float u[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         for (int kz = 0; kz < a.ksplit; ++kz) {
             const float* p = a.slab + ((size_t)kz * a.nphase * a.Lq + pt) * a.Co + co;
             const f32x4_t p0 = *reinterpret_cast<const f32x4_t*>(p), p1 = *reinterpret_cast<const f32x4_t*>(p + 4);
@@ -163,6 +168,25 @@ __global__ __launch_bounds__(256) void conv_splitk_epi_kernel(ConvArgs<T> a) {
                 y[j] += p0[j];
                 y[4 + j] += p1[j];
             }
+            if (half) {
+                const f32x4_t q0 = *reinterpret_cast<const f32x4_t*>(p + half);
+                const f32x4_t q1 = *reinterpret_cast<const f32x4_t*>(p + half + 4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    u[j] += q0[j];
+                    u[4 + j] += q1[j];
+                }
+            }
+        }
+        if (half) {  // (no bias: the FeedForward linears have none)
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float g = rnd<T>(y[j]);
+                o[j] = rnd<T>(rnd<T>(g / (1.0f + expf(-g))) * rnd<T>(u[j]));
+            }
+            store8(reinterpret_cast<T*>(a.out) + ((size_t)t * a.stride + phase) * a.ldo + co, o);
+            continue;
         }
         float b[8];
         if (fl & CE_BIAS) load8(a.bias + co, b);
@@ -734,7 +758,7 @@ template <typename T> static void conv_splitk_go(hipStream_t s, const ConvArgs<T
             dim3 g(FM_CEIL(b.Lq, 64), FM_CEIL(b.Co, 64), b.nphase * b.ksplit);
             conv_gemm_kernel<T><<<g, 256, 0, s>>>(b);
         }
-        const size_t n = (size_t)b.nphase * b.Lq * (b.Co / 8);
+        const size_t n = (size_t)b.nphase * b.Lq * (((b.flags & CE_SWIGLU) ? b.Co / 2 : b.Co) / 8);
         conv_splitk_epi_kernel<T><<<(int)std::min<size_t>(FM_CEIL(n, 256), 4096), 256, 0, s>>>(b);
     }
 }
@@ -755,6 +779,7 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0
         conv_splitk_go<T>(s, a);
         return;
     }
+    FMCHECK(!(a.flags & CE_SWIGLU), "conv: the SwiGLU epilogue runs on the split-K path only");
     // LDS tiles once they give the chip >= 256 blocks (the 128-row tile, 96-128 channels)
     const long long cg2_blocks = (long long)FM_CEIL(a.Lq, CG2_BM) * FM_CEIL(a.Co, 128) * a.nphase;
     if (fm_tuning().conv2 && vec_ok && a.Ci % 8 == 0 && a.Ci >= 32 && a.Co % 16 == 0 && a.Co >= 96 &&

@@ -25,14 +25,14 @@ def _codec(golden, max_frames):
     return FishMICodec.synthetic(cfg, int(g["synth_seed"]), 0, "bf16", max_frames), g
 
 
-def _both(m, f):
+def _both(m, f, knob="codec_fuse"):
     from fishmi import native
 
-    native.tune("codec_fuse", 0)
+    native.tune(knob, 0)
     try:
         two = f()
     finally:
-        native.tune("codec_fuse", 1)
+        native.tune(knob, 1)
     return f(), two
 
 
@@ -104,4 +104,17 @@ def test_fused_encoder_units_equal_two_launch(golden):
     c1, z1 = run()
     np.testing.assert_array_equal(z1, z0)
     np.testing.assert_array_equal(c1, c0)
+    m.close()
+
+
+def test_feedforward_swiglu_gemm_equals_three_launches(golden):
+    """The codec transformer's FeedForward (modded_dac.py:316-317) as one split-K GEMM over
+    [W1 | W3] with the SwiGLU epilogue (fm_tune codec_swiglu) equals w1, w3 and silu_mul bit for
+    bit, one-shot and streamed."""
+    m, g = _codec(golden, 216)
+    codes = g["codes"][0]
+    fused, three = _both(m, lambda: m.decode_codes(codes), "codec_swiglu")
+    np.testing.assert_array_equal(fused, three)
+    fused, three = _both(m, lambda: _stream(m, codes, (1, 4, 16, 64, 131)), "codec_swiglu")
+    np.testing.assert_array_equal(fused, three)
     m.close()
