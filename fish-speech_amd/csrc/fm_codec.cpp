@@ -685,6 +685,7 @@ template <typename T> struct CRun {
     fm_codec* m;
     hipStream_t s;
     explicit CRun(fm_codec* mm) : m(mm), s(mm->stream) {}
+    int rope_pos0_ = 0, rope_nqk_ = 0, rope_hd_ = 0;  // CE_ROPE operands of the next gemm()
 
     void gemm(const PackedW& W, const void* x, int ldx, int Lq, int Lx, void* out, int ldo, int flags,
               const void* res = nullptr, int ldr = 0, const void* gamma = nullptr, const void* alpha2 = nullptr,
@@ -721,6 +722,12 @@ template <typename T> struct CRun {
         a.slab = m->ksp;
         a.slab_cap = m->ksp_cap;
         a.ksplit = fm_tuning().conv_splitk ? W.ks : 1;
+        if (flags & CE_ROPE) {
+            a.rope = m->rope;
+            a.rope_pos0 = rope_pos0_;
+            a.rope_nqk = rope_nqk_;
+            a.rope_hd = rope_hd_;
+        }
         launch_conv_gemm<T>(s, a);
         m->flops += 2.0 * Lq * W.nphase * (double)W.Co * W.ntaps * W.Ci;
         m->launches++;
@@ -882,8 +889,16 @@ template <typename T> struct CRun {
         for (int l = 0; l < c.t_layers; ++l) {
             const TLayer& L = m->tl[l];
             launch_rmsnorm<T>(s, (const T*)m->z, D, (const T*)L.an, D, c.norm_eps, (T*)m->xn, D, Tn);
-            gemm(L.wqkv, m->xn, D, Tn, Tn, m->qkv, 3 * H * hd, CE_STORE);
-            launch_rope_qk<T>(s, (T*)m->qkv, Tn, H, hd, m->rope, pos0);
+            if (fm_tuning().codec_rope && fm_tuning().conv_splitk && L.wqkv.ks > 1 && hd % 8 == 0) {
+                // RoPE in the projection's split-K epilogue (rope_qk_kernel's arithmetic)
+                rope_pos0_ = pos0;
+                rope_nqk_ = 2 * H * hd;
+                rope_hd_ = hd;
+                gemm(L.wqkv, m->xn, D, Tn, Tn, m->qkv, 3 * H * hd, CE_STORE | CE_ROPE);
+            } else {
+                gemm(L.wqkv, m->xn, D, Tn, Tn, m->qkv, 3 * H * hd, CE_STORE);
+                launch_rope_qk<T>(s, (T*)m->qkv, Tn, H, hd, m->rope, pos0);
+            }
             site_in(stream, m->qkv, 3 * H * hd, W1, m->st_kv[l]);
             launch_window_attn<T>(s, (const T*)m->qkv, Tn, H, hd, c.window, (T*)m->att, npre);
             site_out(stream, m->qkv, 3 * H * hd, W1, Tn, m->st_kv[l]);

@@ -14,6 +14,8 @@ enum {
     CE_F32OUT = 128,  // out is fp32 (final waveform)
     CE_SWIGLU = 256,  // split-K epilogue only: out[t][n] = round(round(silu(y[n])) * y[Co/2 + n]) for
                       // n < Co/2 (W1 and W3 of a FeedForward as one GEMM, modded_dac.py:316-317)
+    CE_ROPE = 512,    // split-K epilogue only: RoPE on channels [0, rope_nqk) (q and k heads of a wqkv
+                      // output) at position t + rope_pos0, as rope_qk_kernel does it
 };
 
 // out[t_out][co] (time-major, ld = ldo) with t_out = tq * stride + phase, tq in [0, Lq):
@@ -43,6 +45,8 @@ template <typename T> struct ConvArgs {
     float* slab;               // split-K workspace (launcher): fp32 partials [ksplit][nphase][Lq][Co]
     size_t slab_cap;           // its capacity in floats (0: no split-K)
     int ksplit;                // set by the launcher
+    const float* rope = nullptr;  // CE_ROPE: the (cos, sin) table [pos][hd / 2][2]
+    int rope_pos0 = 0, rope_nqk = 0, rope_hd = 0;
 };
 
 // One decoder ResidualUnit (modded_dac.py:599-620) in one launch, bf16, C in {96, 192, 384}:

@@ -198,6 +198,16 @@ __global__ __launch_bounds__(256) void conv_splitk_epi_kernel(ConvArgs<T> a) {
             if (fl & CE_GELU) v = rnd<T>(0.5f * v * (1.0f + erff(v * 0.70710678118654752f)));
             y[j] = v;
         }
+        if ((fl & CE_ROPE) && co < a.rope_nqk) {  // the 8 channels are 4 (even, odd) pairs of one head
+            const int half = a.rope_hd >> 1, p0 = (co % a.rope_hd) >> 1;
+            const float* cs = a.rope + ((size_t)(t + a.rope_pos0) * half + p0) * 2;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float c = cs[2 * j], sn = cs[2 * j + 1], x0 = y[2 * j], x1 = y[2 * j + 1];
+                y[2 * j] = rnd<T>(x0 * c - x1 * sn);
+                y[2 * j + 1] = rnd<T>(x1 * c + x0 * sn);
+            }
+        }
         const size_t tout = (size_t)t * a.stride + phase;
         if (fl & CE_RES) {
             float rv[8], gm[8];
@@ -744,6 +754,7 @@ template <typename T> static void conv_splitk_go(hipStream_t s, const ConvArgs<T
         b.x = a.x + (ptrdiff_t)r0 * a.ldx;
         b.Lx = a.Lx - r0;
         b.lo = a.lo - r0;
+        b.rope_pos0 = a.rope_pos0 + r0;  // (CE_ROPE: row r0 of the segment is position r0)
         const size_t o = (size_t)r0 * a.stride;
         if (a.out) b.out = (char*)a.out + o * a.ldo * sizeof(T);
         if (a.res) b.res = a.res + o * a.ldr;
@@ -779,7 +790,7 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0
         conv_splitk_go<T>(s, a);
         return;
     }
-    FMCHECK(!(a.flags & CE_SWIGLU), "conv: the SwiGLU epilogue runs on the split-K path only");
+    FMCHECK(!(a.flags & (CE_SWIGLU | CE_ROPE)), "conv: the SwiGLU / RoPE epilogues run on the split-K path only");
     // LDS tiles once they give the chip >= 256 blocks (the 128-row tile, 96-128 channels)
     const long long cg2_blocks = (long long)FM_CEIL(a.Lq, CG2_BM) * FM_CEIL(a.Co, 128) * a.nphase;
     if (fm_tuning().conv2 && vec_ok && a.Ci % 8 == 0 && a.Ci >= 32 && a.Co % 16 == 0 && a.Co >= 96 &&

@@ -118,3 +118,15 @@ def test_feedforward_swiglu_gemm_equals_three_launches(golden):
     fused, three = _both(m, lambda: _stream(m, codes, (1, 4, 16, 64, 131)), "codec_swiglu")
     np.testing.assert_array_equal(fused, three)
     m.close()
+
+
+def test_rope_in_projection_epilogue_equals_rope_kernel(golden):
+    """The codec transformer's RoPE applied in the wqkv split-K epilogue (fm_tune codec_rope)
+    equals the separate rope_qk_kernel bit for bit, one-shot and streamed (absolute positions)."""
+    m, g = _codec(golden, 216)
+    codes = g["codes"][0]
+    fused, two = _both(m, lambda: m.decode_codes(codes), "codec_rope")
+    np.testing.assert_array_equal(fused, two)
+    fused, two = _both(m, lambda: _stream(m, codes, (1, 4, 16, 64, 131)), "codec_rope")
+    np.testing.assert_array_equal(fused, two)
+    m.close()
