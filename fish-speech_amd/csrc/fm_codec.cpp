@@ -686,6 +686,21 @@ template <typename T> struct CRun {
     hipStream_t s;
     explicit CRun(fm_codec* mm) : m(mm), s(mm->stream) {}
     int rope_pos0_ = 0, rope_nqk_ = 0, rope_hd_ = 0;  // CE_ROPE operands of the next gemm()
+    const void* norm_w_ = nullptr;                     // CE_NORM: the norm weight of the next gemm()
+
+    // out = res + gamma * (W x) (the transformer's residual linears), then xn = RMSNorm(out, nw) --
+    // in the split-K epilogue when the layer splits K (fm_tune codec_norm), else a rmsnorm launch
+    void res_linear_norm(const PackedW& W, const void* x, int ldx, int Tn, void* z, int D, const void* gamma,
+                         const void* nw, void* xn) {
+        if (fm_tuning().codec_norm && fm_tuning().conv_splitk && W.ks > 1 && W.Co == D && D % 512 == 0 &&
+            D <= 2048 && W.nphase == 1) {
+            norm_w_ = nw;
+            gemm(W, x, ldx, Tn, Tn, z, D, CE_STORE | CE_RES | CE_GAMMA | CE_NORM, z, D, gamma, nullptr, xn, D);
+            return;
+        }
+        gemm(W, x, ldx, Tn, Tn, z, D, CE_STORE | CE_RES | CE_GAMMA, z, D, gamma);
+        launch_rmsnorm<T>(s, (const T*)z, D, (const T*)nw, D, m->c.norm_eps, (T*)xn, D, Tn);
+    }
 
     void gemm(const PackedW& W, const void* x, int ldx, int Lq, int Lx, void* out, int ldo, int flags,
               const void* res = nullptr, int ldr = 0, const void* gamma = nullptr, const void* alpha2 = nullptr,
@@ -717,7 +732,11 @@ template <typename T> struct CRun {
         a.ldo = ldo;
         a.out2 = (T*)out2;
         a.ldo2 = ldo2;
-        a.flags = flags | (W.bias ? CE_BIAS : 0) | (out2 ? CE_SNAKE : 0);
+        a.flags = flags | (W.bias ? CE_BIAS : 0) | ((out2 && !(flags & CE_NORM)) ? CE_SNAKE : 0);
+        if (flags & CE_NORM) {
+            a.normw = (const T*)norm_w_;
+            a.norm_eps = m->c.norm_eps;
+        }
         a.lo = lo;
         a.slab = m->ksp;
         a.slab_cap = m->ksp_cap;
@@ -886,9 +905,12 @@ template <typename T> struct CRun {
         const int W1 = c.window - 1, pos0 = stream ? m->spos : 0, npre = stream ? std::min(m->spos, W1) : 0;
         launch_rvq_decode<T>(s, m->d_codes, Tn, c.n_codebooks + 1, c.semantic_codebook_size, c.codebook_size,
                              c.codebook_dim, m->rvq, D, (T*)m->z);
+        // each layer's two norms come out of the residual linears before them (res_linear_norm);
+        // only the first attention_norm runs on its own
+        if (c.t_layers > 0)
+            launch_rmsnorm<T>(s, (const T*)m->z, D, (const T*)m->tl[0].an, D, c.norm_eps, (T*)m->xn, D, Tn);
         for (int l = 0; l < c.t_layers; ++l) {
             const TLayer& L = m->tl[l];
-            launch_rmsnorm<T>(s, (const T*)m->z, D, (const T*)L.an, D, c.norm_eps, (T*)m->xn, D, Tn);
             if (fm_tuning().codec_rope && fm_tuning().conv_splitk && L.wqkv.ks > 1 && hd % 8 == 0) {
                 // RoPE in the projection's split-K epilogue (rope_qk_kernel's arithmetic)
                 rope_pos0_ = pos0;
@@ -902,12 +924,13 @@ template <typename T> struct CRun {
             site_in(stream, m->qkv, 3 * H * hd, W1, m->st_kv[l]);
             launch_window_attn<T>(s, (const T*)m->qkv, Tn, H, hd, c.window, (T*)m->att, npre);
             site_out(stream, m->qkv, 3 * H * hd, W1, Tn, m->st_kv[l]);
-            gemm(L.wo, m->att, H * hd, Tn, Tn, m->z, D, CE_STORE | CE_RES | CE_GAMMA, m->z, D, L.ag);
-            launch_rmsnorm<T>(s, (const T*)m->z, D, (const T*)L.fn, D, c.norm_eps, (T*)m->xn, D, Tn);
+            res_linear_norm(L.wo, m->att, H * hd, Tn, m->z, D, L.ag, L.fn, m->xn);
             ffn13(L, m->xn, D, Tn, I, m->g1, m->g3);
-            gemm(L.w2, m->g3, I, Tn, Tn, m->z, D, CE_STORE | CE_RES | CE_GAMMA, m->z, D, L.fg);
+            res_linear_norm(L.w2, m->g3, I, Tn, m->z, D, L.fg, l + 1 < c.t_layers ? m->tl[l + 1].an : m->tnorm,
+                            m->xn);
         }
-        launch_rmsnorm<T>(s, (const T*)m->z, D, (const T*)m->tnorm, D, c.norm_eps, (T*)m->xn, D, Tn);
+        if (c.t_layers == 0)
+            launch_rmsnorm<T>(s, (const T*)m->z, D, (const T*)m->tnorm, D, c.norm_eps, (T*)m->xn, D, Tn);
         // upsample x2 x2: CausalTransConvNet(k2 s2) + ConvNeXt
         const void* xin = m->xn;
         int L = Tn;

@@ -16,6 +16,8 @@ enum {
                       // n < Co/2 (W1 and W3 of a FeedForward as one GEMM, modded_dac.py:316-317)
     CE_ROPE = 512,    // split-K epilogue only: RoPE on channels [0, rope_nqk) (q and k heads of a wqkv
                       // output) at position t + rope_pos0, as rope_qk_kernel does it
+    CE_NORM = 1024,   // split-K epilogue only (one phase, Co % 512 == 0, Co <= 2048): out2 = RMSNorm(y)
+                      // with weight normw, the next layer's / stage's norm, as rmsnorm_wave_kernel does it
 };
 
 // out[t_out][co] (time-major, ld = ldo) with t_out = tq * stride + phase, tq in [0, Lq):
@@ -47,6 +49,8 @@ template <typename T> struct ConvArgs {
     int ksplit;                // set by the launcher
     const float* rope = nullptr;  // CE_ROPE: the (cos, sin) table [pos][hd / 2][2]
     int rope_pos0 = 0, rope_nqk = 0, rope_hd = 0;
+    const T* normw = nullptr;     // CE_NORM: the RMSNorm weight [Co] and eps
+    float norm_eps = 0.f;
 };
 
 // One decoder ResidualUnit (modded_dac.py:599-620) in one launch, bf16, C in {96, 192, 384}:

@@ -231,6 +231,69 @@ __global__ __launch_bounds__(256) void conv_splitk_epi_kernel(ConvArgs<T> a) {
     }
 }
 
+// The split-K epilogue of a layer whose output row feeds an RMSNorm (CE_NORM: the transformer's wo
+// and w2, modded_dac.py:349-439): 256 / (Co / 8) whole rows per block, y = round(sum + bias) ->
+// residual / LayerScale -> store as conv_splitk_epi_kernel, the rounded rows parked in LDS, then the
+// first wave of each row sums the squares in rmsnorm_wave_kernel's order (lane l: 8-channel chunks
+// l, l + 64, ... in sequence, then wave_sum) and every thread writes round(round(y * rs) * w) to
+// out2 -- bit-identical to the rmsnorm launch it replaces.
+template <typename T>
+__global__ __launch_bounds__(256) void conv_splitk_epi_norm_kernel(ConvArgs<T> a) {
+    __shared__ float zrow[256 * 8];
+    __shared__ float rss[4];
+    const int fl = a.flags;
+    const int cpr = a.Co >> 3, rpb = 256 / cpr;  // host: Co % 512 == 0, Co <= 2048
+    const int rl = threadIdx.x / cpr, cc = threadIdx.x - rl * cpr, co = 8 * cc;
+    const int t = blockIdx.x * rpb + rl;
+    const bool live = t < a.Lq;
+    const int tt = live ? t : a.Lq - 1;
+    float y[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int kz = 0; kz < a.ksplit; ++kz) {
+        const float* p = a.slab + ((size_t)kz * a.Lq + tt) * a.Co + co;
+        const f32x4_t p0 = *reinterpret_cast<const f32x4_t*>(p), p1 = *reinterpret_cast<const f32x4_t*>(p + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            y[j] += p0[j];
+            y[4 + j] += p1[j];
+        }
+    }
+    float b[8];
+    if (fl & CE_BIAS) load8(a.bias + co, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] = rnd<T>((fl & CE_BIAS) ? y[j] + b[j] : y[j]);
+    if (fl & CE_RES) {
+        float rv[8], gm[8];
+        load8(a.res + (size_t)tt * a.ldr + co, rv);
+        if (fl & CE_GAMMA) load8(a.gamma + co, gm);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = (fl & CE_GAMMA) ? rnd<T>(rv[j] + rnd<T>(gm[j] * y[j])) : rnd<T>(rv[j] + y[j]);
+    }
+    if ((fl & CE_STORE) && live) store8(reinterpret_cast<T*>(a.out) + (size_t)t * a.ldo + co, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zrow[threadIdx.x * 8 + j] = y[j];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpr = cpr >> 6;  // waves per row
+    if (wv % wpr == 0) {  // the row's first wave: rmsnorm_wave_kernel's sum order
+        const float* zr = zrow + (size_t)rl * a.Co;
+        float ss = 0.f;
+        for (int c = 0; c < wpr; ++c) {
+            const float* v = zr + 8 * (c * 64 + lane);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+        }
+        ss = wave_sum(ss);
+        if (lane == 0) rss[rl] = 1.0f / sqrtf(ss / (float)a.Co + a.norm_eps);
+    }
+    __syncthreads();
+    if (!live) return;
+    const float rs = rss[rl];
+    float g[8], o[8];
+    load8(a.normw + co, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = rnd<T>(rnd<T>(y[j] * rs) * g[j]);
+    store8(a.out2 + (size_t)t * a.ldo2 + co, o);
+}
+
 // SwiGLU helper epilogue: out = silu(round(g)) * y   (modded_dac.py:316-317) -- done by a tiny
 // elementwise kernel after the w3 GEMM to keep conv_gemm_kernel's epilogue set small.
 template <typename T>
@@ -769,6 +832,13 @@ template <typename T> static void conv_splitk_go(hipStream_t s, const ConvArgs<T
             dim3 g(FM_CEIL(b.Lq, 64), FM_CEIL(b.Co, 64), b.nphase * b.ksplit);
             conv_gemm_kernel<T><<<g, 256, 0, s>>>(b);
         }
+        if (b.flags & CE_NORM) {
+            FMCHECK(b.nphase == 1 && b.Co % 512 == 0 && b.Co <= 2048 && b.normw && b.out2,
+                    "conv: the norm epilogue needs one phase, Co a multiple of 512 up to 2048, weight and out2");
+            const int rpb = 256 / (b.Co / 8);
+            conv_splitk_epi_norm_kernel<T><<<FM_CEIL(b.Lq, rpb), 256, 0, s>>>(b);
+            continue;
+        }
         const size_t n = (size_t)b.nphase * b.Lq * (((b.flags & CE_SWIGLU) ? b.Co / 2 : b.Co) / 8);
         conv_splitk_epi_kernel<T><<<(int)std::min<size_t>(FM_CEIL(n, 256), 4096), 256, 0, s>>>(b);
     }
@@ -790,7 +860,7 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0
         conv_splitk_go<T>(s, a);
         return;
     }
-    FMCHECK(!(a.flags & (CE_SWIGLU | CE_ROPE)), "conv: the SwiGLU / RoPE epilogues run on the split-K path only");
+    FMCHECK(!(a.flags & (CE_SWIGLU | CE_ROPE | CE_NORM)), "conv: the SwiGLU / RoPE / norm epilogues run on the split-K path only");
     // LDS tiles once they give the chip >= 256 blocks (the 128-row tile, 96-128 channels)
     const long long cg2_blocks = (long long)FM_CEIL(a.Lq, CG2_BM) * FM_CEIL(a.Co, 128) * a.nphase;
     if (fm_tuning().conv2 && vec_ok && a.Ci % 8 == 0 && a.Ci >= 32 && a.Co % 16 == 0 && a.Co >= 96 &&

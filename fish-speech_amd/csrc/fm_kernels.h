@@ -261,6 +261,7 @@ struct FmTuning {
     int resunit_cfg = 1;     // resunit_kernel tile at 192 / 96 channels: 0 (BM 128 / 256, 8 time tiles per wave), 1 (BM 64 / 128, 4 tiles), 2 (128 / 128)
     int resunit_enc = 1;     // 1: the encoder's units (64 / 128 / 256 / 512 channels) fused as well
     int resunit_384 = 1;     // 1: the 384-channel stage's units fused too (BM 64, 8 waves)
+    int codec_norm = 1;      // 1: the codec transformer's RMSNorms in the wo / w2 split-K epilogues (no rmsnorm launch)
     int codec_rope = 1;      // 1: the codec transformer's RoPE in the wqkv split-K epilogue (no rope_qk launch)
     int codec_swiglu = 1;    // 1: codec FeedForward W1 | W3 as one split-K GEMM with the SwiGLU epilogue
     int codec_fuse = 1;      // 1: decoder ResidualUnits at 96 / 192 / 384 channels as one resunit_kernel launch (k7 + k1)

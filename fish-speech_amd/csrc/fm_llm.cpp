@@ -2358,6 +2358,8 @@ int fm_tune(const char* key, int value) {
             t.conv2 = value != 0;
         } else if (k == "conv_splitk") {
             t.conv_splitk = value != 0;
+        } else if (k == "codec_norm") {
+            t.codec_norm = value != 0;
         } else if (k == "codec_rope") {
             t.codec_rope = value != 0;
         } else if (k == "codec_swiglu") {

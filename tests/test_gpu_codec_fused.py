@@ -130,3 +130,16 @@ def test_rope_in_projection_epilogue_equals_rope_kernel(golden):
     fused, two = _both(m, lambda: _stream(m, codes, (1, 4, 16, 64, 131)), "codec_rope")
     np.testing.assert_array_equal(fused, two)
     m.close()
+
+
+def test_norm_in_residual_epilogue_equals_rmsnorm_kernel(golden):
+    """The codec transformer's ffn_norm / next attention_norm / final norm computed in the wo and
+    w2 split-K epilogues (fm_tune codec_norm), with rmsnorm_wave_kernel's sum order, equal the
+    separate rmsnorm launches bit for bit, one-shot and streamed."""
+    m, g = _codec(golden, 216)
+    codes = g["codes"][0]
+    fused, two = _both(m, lambda: m.decode_codes(codes), "codec_norm")
+    np.testing.assert_array_equal(fused, two)
+    fused, two = _both(m, lambda: _stream(m, codes, (1, 4, 16, 64, 131)), "codec_norm")
+    np.testing.assert_array_equal(fused, two)
+    m.close()
