@@ -880,10 +880,10 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0
 }
 
 // ---------------------------------------------------------------------------------------
-// resunit_kernel: a decoder ResidualUnit (ResUnitArgs, fm_codec.h) per launch.  Block tile: BM
-// output times x all C channels; wave (wt, wc) owns times [128 wt, +128) x channels [48 wc, +48),
-// 8 x 3 MFMA tiles (24 accumulators), so a k-step costs a wave 8 X fragments from LDS and 3 weight
-// fragments from L2 (the k7 weights, 7 C^2 x 2 B <= 516 KB, stay L2-resident).
+// resunit_kernel: one ResidualUnit (ResUnitArgs, fm_codec.h; decoder and encoder) per launch.
+// Block tile: BM output times x all C channels; wave (wt, wc) owns times [16 TT wt, +16 TT) x
+// channels [16 CT wc, +16 CT), TT x CT MFMA tiles, so a k-step costs a wave TT X fragments from LDS
+// and CT weight fragments from L2 (the k7 weights, 7 C^2 x 2 B, stay L2-resident up to C = 512).
 //  1. the input window (rows t0 - 6 dil .. t0 + BM) lands in LDS once by LDS-DMA (16-B slots of a
 //     padded row, out-of-range rows from a zero block): every tap reads it at a row offset, so X
 //     costs HBM its bytes once instead of once per tap and channel tile;
@@ -892,7 +892,8 @@ template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0
 //  3. h = round(snake(round(acc + b7))) overwrites the window in LDS (bf16 [BM][C + 8]);
 //  4. k1 over h, weights again from L2;
 //  5. round(acc + b1) parked in LDS, then 16-B chunks: + residual, store, next Snake.
-// LDS <= 72 KB and 4 waves: two blocks per CU, one block's window DMA under the other's MFMAs.
+// The variants (RU_VARIANTS) keep LDS and registers at 2-3 blocks per CU, so one block's window
+// DMA runs under another's MFMAs (the 384 / 512-channel tiles: one 8-wave block per CU).
 namespace {
 __device__ __forceinline__ uint32_t ru_lds_off(const void* p) {
     return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
