@@ -143,3 +143,20 @@ def test_norm_in_residual_epilogue_equals_rmsnorm_kernel(golden):
     fused, two = _both(m, lambda: _stream(m, codes, (1, 4, 16, 64, 131)), "codec_norm")
     np.testing.assert_array_equal(fused, two)
     m.close()
+
+
+@pytest.mark.parametrize("cfg", [0, 2])
+def test_fused_tile_variants_equal_two_launch(cfg, golden):
+    """The non-default resunit tile variants (fm_tune resunit_cfg 0: BM 128 / 256 with 8 time tiles
+    per wave; 2: BM 128 at both widths) are bit-identical to the two-launch form as well."""
+    from fishmi import native
+
+    m, g = _codec(golden, 216)
+    codes = g["codes"][0]
+    native.tune("resunit_cfg", cfg)
+    try:
+        fused, two = _both(m, lambda: m.decode_codes(codes))
+    finally:
+        native.tune("resunit_cfg", 1)
+    np.testing.assert_array_equal(fused, two)
+    m.close()
