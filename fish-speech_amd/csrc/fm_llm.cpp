@@ -2462,7 +2462,7 @@ int fm_tune(const char* key, int value) {
         } else if (k == "pass_fast") {
             t.pass_fast = value != 0;
         } else if (k == "pass_cfg") {
-            FMCHECK(value >= 0 && value <= 4, "pass_cfg must be 0..4");
+            FMCHECK(value >= 0 && value <= 5, "pass_cfg must be 0..5");
             t.pass_cfg = value;
         } else if (k == "pass_mode") {
             FMCHECK(value >= 0 && value <= 15, "pass_mode must be 0..15");

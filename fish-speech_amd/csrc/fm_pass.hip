@@ -268,6 +268,7 @@ typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
 struct AttnLds {
     uint32_t raw, kvs, qn, kn, tab, out;
 };
+template <bool KVG>
 __device__ __forceinline__ void pass_attn4(int nh, int nkv, int hd, int cpos, int qk_norm, float eps, float scale,
                                            int hbase, int lane, AttnLds o, bf16_t* kc_base, bf16_t* vc_base,
                                            size_t kv_head_stride, bool store_kv) {
@@ -319,11 +320,15 @@ __device__ __forceinline__ void pass_attn4(int nh, int nkv, int hd, int cpos, in
     // scores: position j's 16 partial dots summed across the head's row (DPP), kept by lane j
     const lds_u32x4_t* K = kvs + (size_t)(2 * kvh) * cpos * nck;
     const lds_u32x4_t* V = K + (size_t)cpos * nck;
+    // KVG: the cached rows straight from the cache in HBM / L2 (no LDS copy; pass_cfg 5)
+    const u32x4_t* Kg = reinterpret_cast<const u32x4_t*>(kc_base + (size_t)kvh * kv_head_stride) + cc;
+    const u32x4_t* Vg = reinterpret_cast<const u32x4_t*>(vc_base + (size_t)kvh * kv_head_stride) + cc;
     float sc = -INFINITY;
     for (int jb = 0; jb <= cpos; jb += 4) {  // four positions' rows in flight at once
         u32x4_t kk[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) kk[u] = jb + u < cpos ? K[(jb + u) * nck + cc] : kp;
+        for (int u = 0; u < 4; ++u)
+            kk[u] = jb + u < cpos ? (KVG ? Kg[(size_t)(jb + u) * nck] : (u32x4_t)K[(jb + u) * nck + cc]) : kp;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const float d = row_sum16(dot8(kk[u], qp, 0.f));
@@ -341,7 +346,8 @@ __device__ __forceinline__ void pass_attn4(int nh, int nkv, int hd, int cpos, in
     for (int jb = 0; jb <= cpos; jb += 4) {
         u32x4_t vv[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) vv[u] = jb + u < cpos ? V[(jb + u) * nck + cc] : vw;
+        for (int u = 0; u < 4; ++u)
+            vv[u] = jb + u < cpos ? (KVG ? Vg[(size_t)(jb + u) * nck] : (u32x4_t)V[(jb + u) * nck + cc]) : vw;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int j = jb + u;
@@ -370,14 +376,14 @@ __device__ __forceinline__ void pass_attn4(int nh, int nkv, int hd, int cpos, in
 }  // namespace
 
 // LDS words of the role hand-offs (u32 offsets inside the flag block)
-enum { F_FULL = 0, F_FREE = 8, F_A = 16, F_B = 17, F_X = 18, F_R = 19, F_AT = 20, F_WORDS = 32 };
+enum { F_FULL = 0, F_FREE = 16, F_A = 32, F_B = 33, F_X = 34, F_R = 35, F_AT = 36, F_WORDS = 48 };
 // F_R: layers whose q|k|v row is in raw (the attention may start); F_AT: consumer waves' attention
 // calls done
 
 // NC consumer waves, a ring of NSLOT slots of PS_FILL 1 KiB fragments, PS_INFL fills in flight
-template <int NC, int NSLOT, int PS_FILL, int PS_INFL>
+template <int NC, int NSLOT, int PS_FILL, int PS_INFL, bool KVG = false>
 __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassArgs a) {
-    static_assert(NSLOT <= 8 && NSLOT > PS_INFL, "ring slots");
+    static_assert(NSLOT <= 16 && NSLOT > PS_INFL, "ring slots");
     auto nfills = [](int nfr) { return (nfr + PS_FILL - 1) / PS_FILL; };
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     bf16_t* xbuf = reinterpret_cast<bf16_t*>(smem + a.off_xbuf);    // the current op's input row
@@ -428,7 +434,7 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
         const size_t cb = (size_t)a.row_slot[0] * a.slot_stride + (size_t)layer * a.layer_stride;
         for (int hb = 4 * w8; hb < a.nh; hb += 4 * nw8) {
             AttnLds ao{lds_off(raw), lds_off(kvs), lds_off(aqn), lds_off(akn), lds_off(atab), lds_off(xbuf + (size_t)hb * a.hd)};
-            pass_attn4(a.nh, a.nkv, a.hd, a.cpos, a.qk_norm, a.eps, a.scale, hb, lane, ao, a.kc + cb, a.vc + cb,
+            pass_attn4<KVG>(a.nh, a.nkv, a.hd, a.cpos, a.qk_norm, a.eps, a.scale, hb, lane, ao, a.kc + cb, a.vc + cb,
                        (size_t)a.S * a.hd, store_kv);
         }
     };
@@ -643,7 +649,7 @@ __global__ __launch_bounds__((1 + NC + PASS_NWM) * 64, 1) void pass_kernel(PassA
     auto load_kvs = [&](int layer) {
         int t = t_;
         asm volatile("" : "+v"(t));
-        const int cpos = a.cpos, rc = hd / 8, n2 = a.nkv * 2 * cpos * rc;
+        const int cpos = a.cpos, rc = hd / 8, n2 = KVG ? 0 : a.nkv * 2 * cpos * rc;
         const size_t cbase = (size_t)slot * a.slot_stride + (size_t)layer * a.layer_stride;
         for (int i = t; i < n2; i += 256) {
             const int row = i / rc, cc = i - row * rc;
@@ -796,8 +802,9 @@ PassLds pass_lds(int kmax, int dim, int nqkv, int nkv, int S, int hd, int maxrow
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
     PassLds L;
     size_t o = 0;
+    const bool kvg = fm_tuning().pass_cfg == 5;  // K / V read from the cache, the ring takes their LDS
     L.ring = (int)o;
-    o = al(o + (size_t)PASS_RING_KB * 1024);
+    o = al(o + (size_t)(kvg ? 96 : PASS_RING_KB) * 1024);
     L.xbuf = (int)o;
     o = al(o + (size_t)kmax * 2);
     L.resx = (int)o;
@@ -807,7 +814,7 @@ PassLds pass_lds(int kmax, int dim, int nqkv, int nkv, int S, int hd, int maxrow
     L.raw = (int)o;
     o = al(o + (size_t)nqkv * 2);
     L.kvs = (int)o;
-    o = al(o + (size_t)nkv * 2 * (S > 1 ? S - 1 : 1) * hd * 2);
+    o = al(o + (kvg ? (size_t)16 : (size_t)nkv * 2 * (S > 1 ? S - 1 : 1) * hd * 2));
     o += 16 * 4;  // the exchange waves' sums of squares, just below red
     L.red = (int)o;
     o = al(o + (size_t)maxrows * PASS_NC * 4);  // [rows][NC]
@@ -847,7 +854,8 @@ void pass_init() {
                        reinterpret_cast<const void*>(&pass_kernel<PASS_NC, 4, 16, 2>),
                        reinterpret_cast<const void*>(&pass_kernel<PASS_NC, 8, 8, 5>),
                        reinterpret_cast<const void*>(&pass_kernel<PASS_NC, 8, 8, 3>),
-                       reinterpret_cast<const void*>(&pass_kernel<PASS_NC, 4, 16, 1>)};
+                       reinterpret_cast<const void*>(&pass_kernel<PASS_NC, 4, 16, 1>),
+                       reinterpret_cast<const void*>(&pass_kernel<PASS_NC, 12, 8, 4, true>)};
     for (const void* f : k) HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 }
 
@@ -874,6 +882,7 @@ void launch_pass(hipStream_t s, const PassArgs& a) {
         case 2: pass_kernel<PASS_NC, 8, 8, 5><<<grid, block, L.bytes, s>>>(a); break;
         case 3: pass_kernel<PASS_NC, 8, 8, 3><<<grid, block, L.bytes, s>>>(a); break;
         case 4: pass_kernel<PASS_NC, 4, 16, 1><<<grid, block, L.bytes, s>>>(a); break;
+        case 5: pass_kernel<PASS_NC, 12, 8, 4, true><<<grid, block, L.bytes, s>>>(a); break;  // 96 KiB ring
         default: pass_kernel<PASS_NC, 8, 8, 4><<<grid, block, L.bytes, s>>>(a); break;
     }
 }
