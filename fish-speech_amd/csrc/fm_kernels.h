@@ -289,7 +289,7 @@ struct FmTuning {
     int fin_split = 0;       // batched finalize_norm: each row over this many blocks (0 / 1: one block per row)
     int int4_stream = 1;     // weight-only int4: 1 the batch <= 8 GEMVs stream the 4-bit codes, 0 the dequantised bf16 copy
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
-    int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1), 5 (12 x 8, 4: K / V from the cache, 96 KiB ring)
+    int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1), 5 (12 x 8, 4: K / V from the cache, 96 KiB ring), 6 (no loader: stream waves with PASS_SR-fragment register rings)
     int pass_mode = 0;       // developer: PassArgs::mode
     int pass_nap = 2;        // PassArgs::sweep_nap
     int pass_prefetch = 12;  // PassArgs::prefetch
@@ -371,14 +371,15 @@ struct PassArgs {
                               // input-row wait, 2 consumers skip the dot products too
     unsigned long long* dbg;  // developer phase stamps (fm_tune debug_ts) or null
     int off_ring, off_xbuf, off_resx, off_resh, off_raw, off_kvs, off_red, off_sc, off_opt, off_lyt, off_attc,
-        off_flg, off_junk, off_dbg;  // LDS byte offsets (pass_lds)
+        off_flg, off_junk, off_dbg, off_wtab;  // LDS byte offsets (pass_lds)
     int prefetch;  // fills past the ring pulled into L2 while the ring is full (0: none)
 };
 constexpr int PASS_NWM = 4;    // exchange waves per workgroup
 constexpr int PASS_NC = 4;     // consumer waves per workgroup (plus one loader wave)
 constexpr int PASS_RING_KB = 64;  // LDS weight ring (fm_tune pass_cfg picks its slots x fill size)
+constexpr int PASS_SR = 48;       // pass_cfg 6: register-ring fragments per stream wave
 struct PassLds {
-    int ring, xbuf, resx, resh, raw, kvs, red, sc, opt, lyt, attc, flg, junk, dbg;
+    int ring, xbuf, resx, resh, raw, kvs, red, sc, opt, lyt, attc, flg, junk, dbg, wtab;
     size_t bytes;
 };
 PassLds pass_lds(int kmax, int dim, int nqkv, int nkv, int S, int hd, int maxrows, int nop);

@@ -1035,6 +1035,7 @@ template <typename T> struct Run {
         a.off_junk = L.junk;
         a.prefetch = fm_tuning().pass_prefetch;
         a.off_dbg = L.dbg;
+        a.off_wtab = L.wtab;
         int64_t bytes = 0;  // weight bytes streamed
         for (int o = 0; o < a.nop; ++o) {
             const int k = o >= 4 * f.n_layer ? 4 : (o & 3);
@@ -2462,7 +2463,7 @@ int fm_tune(const char* key, int value) {
         } else if (k == "pass_fast") {
             t.pass_fast = value != 0;
         } else if (k == "pass_cfg") {
-            FMCHECK(value >= 0 && value <= 5, "pass_cfg must be 0..5");
+            FMCHECK(value >= 0 && value <= 9, "pass_cfg must be 0..9");
             t.pass_cfg = value;
         } else if (k == "pass_mode") {
             FMCHECK(value >= 0 && value <= 15, "pass_mode must be 0..15");

@@ -31,7 +31,7 @@ def _cfg(g):
     return cfg
 
 
-@pytest.mark.parametrize("ring", [0, 1, 4, 5])
+@pytest.mark.parametrize("ring", [0, 1, 4, 5, 6, 7])
 def test_pass_full_depth_bf16_vs_reference(golden, pass_on, ring):
     """Config 2 at full depth (4 fast layers per pass, 10 passes per frame), graph-replayed frames,
     every ring configuration (fm_tune pass_cfg): within the bf16 bound of the reference."""
