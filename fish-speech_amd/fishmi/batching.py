@@ -223,9 +223,12 @@ class BatchedWorker:
                 for f in range(k):
                     self._take(st, out[f, j])
                 st.frames += k
-                self._stream(s)
+                try:  # a response queue that raises fails its own request only
+                    self._stream(s)
+                except Exception as e:
+                    self._fail(s, e)
             for s in live:
-                if self.active[s].done:
+                if s in self.active and self.active[s].done:
                     try:
                         if self._finish(s):
                             self._prefill_later(s)

@@ -45,6 +45,7 @@ import dataclasses
 import logging
 import queue
 import threading
+import time
 from typing import Deque, Dict, List, Optional, Tuple
 
 import numpy as np
@@ -134,34 +135,115 @@ class _Outbox:
         self.sink.append((self.rid, w))
 
 
-class _Vocoding:
-    """A request's response queue on the rank that decodes it, with a vocoder: each "sample" response
-    gets its PCM here (VQManager.decode_vq_tokens, vq_manager.py:16-21, or the request's own causal
-    stream for latency="balanced" chunks) before it moves on."""
+class _Vocoder:
+    """This rank's vocoder, off the tick's critical path: one FIFO of (request queue, response) items
+    served by a thread of its own, so a rank that finishes a long request does not hold every rank's
+    next all_gather while it vocodes (tools/vqgan/extract_vq.py:150-197 runs its codec beside the
+    loader the same way).  One FIFO keeps each request's responses in order; results go back to the
+    tick thread through `ready`, which the tick drains into its outbox (the outbox stays
+    single-threaded).  A codec call that raises answers its request with the error and drops that
+    request's later samples; every other request keeps being served."""
 
-    def __init__(self, inner, vocoder):
-        self.inner, self.voc, self.ctx = inner, vocoder, None
+    def __init__(self, codec, device=None):
+        self.codec, self.device = codec, device
+        self.fifo: "queue.Queue" = queue.Queue()
+        self.ready: "queue.Queue" = queue.Queue()
+        self.backlog = 0  # items put and not yet drained back (read by the tick thread)
+        self._lock = threading.Lock()
+        self.th = threading.Thread(target=self._run, daemon=True)
+        self.th.start()
+
+    def submit(self, v: "_Vocoding", w, done: bool = False):
+        with self._lock:
+            self.backlog += 1
+        self.fifo.put((v, w, done))
+
+    def drain(self, deliver) -> int:
+        """Hand every finished item to deliver(v, w) (tick thread); returns how many are still in
+        flight."""
+        n = 0
+        while True:
+            try:
+                v, w = self.ready.get_nowait()
+            except queue.Empty:
+                break
+            deliver(v, w)
+            n += 1
+        with self._lock:
+            self.backlog -= n
+            return self.backlog
+
+    def close(self):
+        self.fifo.put(None)
+
+    def _run(self):
+        if self.device is not None and getattr(self.device, "type", None) == "cuda":
+            import torch
+
+            torch.cuda.set_device(self.device)  # the current device is per thread
+        while True:
+            it = self.fifo.get()
+            if it is None:
+                return
+            v, w, done = it
+            if done:
+                v.close()
+                self.ready.put((v, None))
+                continue
+            self.ready.put((v, v.vocode(self.codec, w)))
+
+
+class _Vocoding:
+    """A request's response queue on the rank that decodes it, with a vocoder: each "sample"
+    response gets its PCM (VQManager.decode_vq_tokens, vq_manager.py:16-21, or the request's own
+    causal stream for latency="balanced" chunks) on this rank's vocoder thread before it moves on."""
+
+    def __init__(self, inner, vocoder: _Vocoder, item=None):
+        self.inner, self.voc, self.ctx, self.item = inner, vocoder, None, item
+        self.failed = False
 
     def put(self, w):
-        if w is not None and w.status == "success" and isinstance(w.response, GenerateResponse) \
-                and w.response.action == "sample" and w.response.codes is not None:
-            r = w.response
+        self.voc.submit(self, w)
+
+    def vocode(self, codec, w):
+        """(vocoder thread) the response with its PCM; after a codec error, the error once and the
+        request's later samples dropped (its caller has its answer)"""
+        if w is None or w.status != "success" or not isinstance(w.response, GenerateResponse) \
+                or w.response.action != "sample" or w.response.codes is None:
+            return w
+        if self.failed:
+            return _DROP
+        r = w.response
+        try:
             codes = np.asarray(r.codes)
             if r.stream is not None:  # chunk k of one text batch's stream: this request's codec state
                 if r.stream == 0 or self.ctx is None:
                     self.close()
-                    self.ctx = self.voc.open_stream()
+                    self.ctx = codec.open_stream()
                 pcm = self.ctx.decode_chunk(codes)
             else:
-                pcm = self.voc.decode_codes(codes)
-            w = WrappedGenerateResponse(status="success", response=dataclasses.replace(
-                r, audio=np.ascontiguousarray(pcm, dtype=np.float32)))
-        self.inner.put(w)
+                pcm = codec.decode_codes(codes)
+        except Exception as e:
+            log.error("vocoding failed: %r", e)
+            self.failed = True
+            self.close()
+            return WrappedGenerateResponse(status="error", response=e)
+        return WrappedGenerateResponse(status="success", response=dataclasses.replace(
+            r, audio=np.ascontiguousarray(pcm, dtype=np.float32)))
 
     def close(self):
         if self.ctx is not None:
-            self.ctx.close()
-            self.ctx = None
+            try:
+                self.ctx.close()
+            finally:
+                self.ctx = None
+
+
+class _Drop:
+    """Marks a response the vocoder dropped (a sample after its request's codec error)."""
+
+
+_DROP = _Drop()
 
 
 # ---- the worker ---------------------------------------------------------------------------------
@@ -174,7 +256,8 @@ class DistributedWorker:
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
         # the collectives' device: explicit (the caller's GPU), never this thread's current device
         self.dev = device if device is not None else _device()
-        self.vocoder = vocoder  # a FishMICodec on this rank's GPU: vocode where the codes are decoded
+        # a FishMICodec on this rank's GPU: vocode where the codes are decoded, on a thread of its own
+        self.vocoder = _Vocoder(vocoder, self.dev) if vocoder is not None else None
         self.w = BatchedWorker(model, max_slots, tick_frames)
         self.w.on_done = self._done
         self.idle_wait = idle_wait
@@ -191,21 +274,37 @@ class DistributedWorker:
     def _wrap(self, item: GenerateRequest) -> GenerateRequest:
         if self.vocoder is None:
             return item
-        w = GenerateRequest(request=item.request, response_queue=_Vocoding(item.response_queue, self.vocoder))
+        v = _Vocoding(item.response_queue, self.vocoder)
+        w = GenerateRequest(request=item.request, response_queue=v)
         if hasattr(item, "_rid"):
             w._rid = item._rid
+        v.item = w
         return w
+
+    def _deliver(self, v: _Vocoding, w):
+        """(tick thread) a vocoded response, or the request's done marker, in the request's order"""
+        if w is _DROP:
+            return
+        if w is None:
+            self._finished(v.item, v.inner)
+        else:
+            v.inner.put(w)
 
     def _done(self, item: GenerateRequest):
         q = item.response_queue
-        if isinstance(q, _Vocoding):
-            q.close()
-            q = q.inner
+        if isinstance(q, _Vocoding):  # behind the request's samples still being vocoded
+            q.voc.submit(q, None, done=True)
+            self.stats["served"] += 1
+            return
+        self._finished(item, q)
+
+    def _finished(self, item: GenerateRequest, q):
         if isinstance(q, _Outbox):
             q.put(None)
         else:
             self.routes.pop(getattr(item, "_rid", None), None)
-        self.stats["served"] += 1
+        if not isinstance(item.response_queue, _Vocoding):
+            self.stats["served"] += 1
 
     # ---- collectives ----------------------------------------------------------------------------
     def _tensor(self, b: bytes, n: int):
@@ -297,11 +396,23 @@ class DistributedWorker:
 
         dist = _dist()
         self.stats["ticks"] += 1
+        t0 = time.perf_counter()
+        try:
+            return self._tick(dist)
+        finally:  # (straggler check: a tick that waits on another rank's slow step shows here)
+            dt = time.perf_counter() - t0
+            self.stats["tick_max_s"] = max(self.stats.get("tick_max_s", 0.0), dt)
+
+    def _tick(self, dist) -> bool:
+        import torch
+
         if self.rank == 0:
             self._intake()
         wk = self.w
         free = wk.max_slots - len(wk.active) - len(wk.pending)
         busy = len(wk.active) + len(wk.pending)
+        if self.vocoder is not None:  # vocoded since the last tick -> outbox / callers
+            busy += self.vocoder.drain(self._deliver)
         if self.rank != 0 and self.outbox:  # this tick ships everything produced so far
             self._blob = pack([[rid, response_to_wire(w)] for rid, w in self.outbox])
             self.outbox.clear()  # _Outbox proxies hold this list: clear it in place
@@ -332,6 +443,10 @@ class DistributedWorker:
         err = e if isinstance(e, Exception) else RuntimeError(repr(e))
         log.error("rank %d: serving loop failed: %r", self.rank, e)
         self.w.fail_all(err)  # active + pending (their queues: callers, outboxes)
+        if self.vocoder is not None:  # their errors and done markers pass the vocoder's FIFO
+            self.vocoder.close()
+            self.vocoder.th.join(timeout=60)
+            self.vocoder.drain(self._deliver)
         if self.rank == 0:
             for rid, item in list(self.routes.items()):  # queued here or decoding on another rank
                 item.response_queue.put(WrappedGenerateResponse(status="error", response=err))
@@ -345,7 +460,10 @@ class DistributedWorker:
     def run(self):
         try:
             while self.tick():
-                pass
+                if self.vocoder is not None and self.vocoder.backlog and not (self.w.active or self.w.pending):
+                    time.sleep(0.001)  # only vocoding left on this rank: let it run, then tick again
+            if self.vocoder is not None:
+                self.vocoder.close()
         except BaseException as e:
             self._fail_everything(e)
             self.failed = e
@@ -398,4 +516,5 @@ def launch_distributed_queue(checkpoint_path, device, precision, max_slots: int 
     if failure:
         raise failure[0]
     holder["w"].thread = th
+    th.worker = holder["w"]
     return holder["w"].input, th

@@ -61,14 +61,20 @@ def _collect(q, n_final):
 
 class ScriptedVocoder:
     """Stands in for FishMICodec: PCM is a per-column function of the codes (HOP samples a column),
-    so a causal stream of chunks vocodes to the one-shot decode of their concatenation."""
+    so a causal stream of chunks vocodes to the one-shot decode of their concatenation.  delay: seconds
+    each call takes (a slow vocoder); fail_at: the call that raises (a codec error)."""
     HOP = 4
 
-    def __init__(self):
+    def __init__(self, delay=0.0, fail_at=None):
         self.calls = 0
+        self.delay, self.fail_at = delay, fail_at
 
     def decode_codes(self, codes):
         self.calls += 1
+        if self.delay:
+            time.sleep(self.delay)
+        if self.fail_at is not None and self.calls == self.fail_at:
+            raise RuntimeError("injected codec failure")
         c = np.asarray(codes, np.int64)
         col = (c * np.arange(1, c.shape[0] + 1)[:, None]).sum(0) % 997
         return np.repeat(col.astype(np.float32) / 997.0, self.HOP)
@@ -97,7 +103,13 @@ def _worker(rank, world, port, out_q, slots, tick, mode="plain"):
         from test_batching import ScriptedModel, _requests
 
         model = ScriptedModel(slots)
-        voc = ScriptedVocoder() if mode == "vocode" else None
+        voc = None
+        if mode == "vocode":
+            voc = ScriptedVocoder()
+        elif mode == "slowvoc":  # rank 1 vocodes slowly: rank 0's ticks must not wait for it
+            voc = ScriptedVocoder(delay=0.25 if rank == 1 else 0.0)
+        elif mode == "badvoc":  # rank 1's codec raises once: that request fails, the rest are served
+            voc = ScriptedVocoder(fail_at=2 if rank == 1 else None)
         if mode == "fail" and rank == 1:  # a tick that raises outside every per-request guard
             orig = DistributedWorker.tick
 
@@ -130,6 +142,17 @@ def _worker(rank, world, port, out_q, slots, tick, mode="plain"):
                 late = queue.Queue()  # a request after the failure is answered too
                 q_in.put(engine.GenerateRequest(request=reqs[0], response_queue=late))
                 assert late.get(timeout=30).status == "error"
+            elif mode == "badvoc":
+                failed = 0
+                for i, (q, rf) in enumerate(zip(qs, ref)):
+                    n_final = 0 if rf[-1].status == "error" else sum(w.response.action == "next" for w in rf)
+                    got = _collect(q, max(n_final, 1))
+                    if got[-1].status == "error" and rf[-1].status != "error":
+                        assert "injected codec failure" in str(got[-1].response), got[-1].response
+                        failed += 1
+                        continue
+                    _check(got, rf, i)
+                assert failed == 1, failed  # exactly the request whose samples hit the failing call
             else:
                 for i, (q, rf) in enumerate(zip(qs, ref)):
                     n_final = 0 if rf[-1].status == "error" else sum(w.response.action == "next" for w in rf)
@@ -144,6 +167,10 @@ def _worker(rank, world, port, out_q, slots, tick, mode="plain"):
             q_in.put(None)
         th.join(timeout=120)
         assert not th.is_alive()
+        if mode == "slowvoc" and rank == 0:
+            # rank 1 spends 0.25 s per vocoder call on its vocoder thread; rank 0's ticks (each an
+            # all_gather with rank 1) never waited for one of them
+            assert th.worker.stats["tick_max_s"] < 0.15, th.worker.stats
         decoded = [c for c in model.calls if c[0] in ("prefill", "prefill_batch")]
         if voc is not None:
             assert voc.calls > 0, f"rank {rank} vocoded nothing"
@@ -188,6 +215,19 @@ def test_distributed_worker_world2_vocodes_per_rank():
     """Each rank vocodes the samples it decoded; every response's PCM equals the one-shot decode of
     its codes (streamed chunks included), and both ranks' vocoders ran."""
     _run(slots=2, tick=3, mode="vocode")
+
+
+def test_distributed_worker_world2_slow_vocoder_does_not_stall_ticks():
+    """Rank 1's vocoder takes 0.25 s a call: it runs on the rank's vocoder thread, so the
+    synchronous ticks (all_gather across the ranks) are not held by it -- rank 0's longest tick stays
+    under 0.15 s -- and every response still arrives in order with its PCM."""
+    _run(slots=2, tick=3, mode="slowvoc")
+
+
+def test_distributed_worker_world2_codec_error_fails_one_request():
+    """Rank 1's codec raises on one call: that request is answered with the error, every other
+    request (on both ranks) gets exactly its serial responses, and the ranks keep serving."""
+    _run(slots=2, tick=3, mode="badvoc")
 
 
 def test_distributed_worker_world2_tick_failure_fails_requests():
