@@ -467,9 +467,10 @@ def pmc_gemv_traffic(timeout_s=150):
 
 def stream_peak_gbps(nbytes=2 << 30, reps=10):
     """Measured HBM stream peak (SURVEY.md §8d's STREAM-like figure beside the vendor 8 TB/s):
-    libfishmi's fm_stream_peak, a non-temporal float4 read stream and a float4 copy over 2 GiB
-    buffers (far past the 256 MiB MALL), HIP events.  The read stream is the ceiling a weight
-    stream can reach; the copy counts read + written bytes."""
+    libfishmi's fm_stream_peak: the best of several non-temporal read streams (register float4 and
+    LDS-DMA forms) and of two float4 copies over 2 GiB buffers (far past the 256 MiB MALL), HIP
+    events.  The read stream is the ceiling a weight stream can reach; the copy counts read +
+    written bytes."""
     from fishmi import native
 
     r, c = native.stream_peak(0, nbytes, reps)
@@ -651,9 +652,12 @@ def main():
                          "stream_peak_measured": {"read": stream_gbps[0], "copy": stream_gbps[1], "unit": "GB/s",
                                                   "frac_of_read_peak": round(achieved / stream_gbps[0], 4)
                                                   if stream_gbps[0] else None,
-                                                  "method": "fm_stream_peak: non-temporal float4 read "
-                                                            "stream / float4 copy (read + write bytes), "
-                                                            "2 GiB buffers, 10 launches, HIP events"},
+                                                  "method": "fm_stream_peak: best of non-temporal float4 "
+                                                            "read streams (4 / 8 in flight per thread, 8 / 16 "
+                                                            "blocks per CU) and non-temporal LDS-DMA streams "
+                                                            "(16 / 32 KiB in flight per wave); best of two "
+                                                            "float4 copies (read + write bytes); 2 GiB "
+                                                            "buffers, 10 launches each, HIP events"},
                          "bytes_per_launch": int(per_launch),
                          "avg_launch_us": round(avg_us, 3), "launches_per_frame": int(lin_n),
                          "method": "one frame's GEMV launches replayed x20 as a graph, HIP events on "

@@ -787,7 +787,10 @@ __global__ __launch_bounds__(FS_THREADS) void finalize_split_kernel(FinalizeArgs
         __hip_atomic_fetch_add((g_i32*)arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (unsigned spin = 0;; ++spin) {  // bounded: every block of the row is resident
             if (__hip_atomic_load((g_i32*)arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.ch) break;
-            if (spin > (1u << 22)) break;
+            if (spin > (1u << 22)) {  // reported (the host throws and resets the counters), never silent
+                if (a.err) __hip_atomic_store((g_i32*)a.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
         }
     }

@@ -976,9 +976,12 @@ template <typename T> struct CRun {
                     std::swap(alt, spare);
                     continue;
                 }
-                gemm(R.c7, alt, cout, L, L, nullptr, 0, 0, nullptr, 0, nullptr, R.a2, m->Cb, cout, stream ? -hr : 0);
+                // two launches: the k7 output goes to `spare` (never alt: after fused units swapped
+                // the pair, alt may be m->Cb itself)
+                FMCHECK(spare != alt && spare != in, "codec: ResidualUnit scratch aliases its input");
+                gemm(R.c7, alt, cout, L, L, nullptr, 0, 0, nullptr, 0, nullptr, R.a2, spare, cout, stream ? -hr : 0);
                 site_out(stream, alt, cout, hr, L, m->st_c7[b][r]);
-                gemm(R.c1, m->Cb, cout, L, L, m->xb, cout, (r < 2 ? CE_STORE : 0) | CE_RES, m->xb, cout, nullptr,
+                gemm(R.c1, spare, cout, L, L, m->xb, cout, (r < 2 ? CE_STORE : 0) | CE_RES, m->xb, cout, nullptr,
                      an, alt, cout);
             }
             std::swap(in, alt);

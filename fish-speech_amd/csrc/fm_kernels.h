@@ -289,6 +289,7 @@ struct FmTuning {
     int fin_split = 0;       // batched finalize_norm: each row over this many blocks (0 / 1: one block per row)
     int int4_stream = 1;     // weight-only int4: 1 the batch <= 8 GEMVs stream the 4-bit codes, 0 the dequantised bf16 copy
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
+    int pass_prepare = 0;    // 1: build the persistent pass's weight copy at finalize even with pass_fast 0
     int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1), 5 (12 x 8, 4: K / V from the cache, 96 KiB ring), 6 (no loader: stream waves with PASS_SR-fragment register rings)
     int pass_mode = 0;       // developer: PassArgs::mode
     int pass_nap = 2;        // PassArgs::sweep_nap
@@ -445,6 +446,7 @@ template <typename T> struct FinalizeArgs {
     int* cnt = nullptr;
     float* ss_part = nullptr;
     int fin8 = 0;       // set by the launcher (fm_tune fin8): eight K parts' slab loads in one round trip
+    int* err = nullptr; // split form: set when a row's blocks timed out waiting for each other
 };
 template <typename T> void launch_finalize_norm(hipStream_t s, const FinalizeArgs<T>& a);
 

@@ -459,6 +459,7 @@ template <typename T> struct Run {
             f.ch = fm_tuning().fin_split;
             f.cnt = m->fin_cnt;
             f.ss_part = m->fin_ss;
+            f.err = m->chain_err;
         }
         run_("norm", 0, 0, [&] { launch_finalize_norm<T>(s, f); });
     }
@@ -1501,6 +1502,9 @@ static bool pass_eligible(fm_llm* m, int* nwg_out) {
 }
 
 static void pass_prepare(fm_llm* m) {
+    // the row-major copy of the fast stack (~0.8 GB at S2-Pro) only for a model that may run the
+    // persistent pass: pass_fast (or pass_prepare) set when the model is finalised
+    if (!fm_tuning().pass_fast && !fm_tuning().pass_prepare) return;
     int nwg = 0;
     if (!pass_eligible(m, &nwg)) return;
     const StackDims& f = m->fdm;
@@ -1816,7 +1820,7 @@ static void upload_frame_rows(fm_llm* m, const int32_t* slots, int n) {
 // gemv chain health: the error word travels to pinned memory behind the frames; after the
 // host's stream sync, a timed-out hand-off wait (a hang avoided) resets the counters and fails
 static void chain_err_async(fm_llm* m) {
-    if (fm_tuning().gemv_chain || m->pass_ok)
+    if (fm_tuning().gemv_chain || (m->pass_ok && fm_tuning().pass_fast) || fm_tuning().fin_split > 1)
         HIPCHK(hipMemcpyAsync(m->h_chain_err, m->chain_err, sizeof(int), hipMemcpyDeviceToHost, m->stream));
 }
 static void chain_err_check(fm_llm* m) {
@@ -1824,7 +1828,9 @@ static void chain_err_check(fm_llm* m) {
     m->h_chain_err[0] = 0;
     HIPCHK(hipMemset(m->chain_cnt, 0, GEMV_CHAIN_WORDS * sizeof(unsigned)));
     HIPCHK(hipMemset(m->chain_err, 0, 16 * sizeof(int)));
-    throw FmError{FM_ERR_STATE, "in-launch hand-off wait timed out (gemv chain / persistent pass; counters reset)"};
+    if (m->fin_cnt) HIPCHK(hipMemset(m->fin_cnt, 0, (size_t)std::max(m->max_slots, 64) * 2 * sizeof(int)));
+    throw FmError{FM_ERR_STATE,
+                  "in-launch hand-off wait timed out (gemv chain / persistent pass / split finalize; counters reset)"};
 }
 
 // one decode frame for the uploaded rows (graph replay when enabled), async
@@ -2462,11 +2468,13 @@ int fm_tune(const char* key, int value) {
             t.int4_stream = value != 0;
         } else if (k == "pass_fast") {
             t.pass_fast = value != 0;
+        } else if (k == "pass_prepare") {
+            t.pass_prepare = value != 0;
         } else if (k == "pass_cfg") {
             FMCHECK(value >= 0 && value <= 9, "pass_cfg must be 0..9");
             t.pass_cfg = value;
         } else if (k == "pass_mode") {
-            FMCHECK(value >= 0 && value <= 15, "pass_mode must be 0..15");
+            FMCHECK(value >= 0 && value <= 31, "pass_mode must be 0..31");
             t.pass_mode = value;
         } else if (k == "pass_nap") {
             FMCHECK(value >= 1 && value <= 32, "pass_nap must be 1..32");

@@ -572,6 +572,10 @@ __global__ __launch_bounds__((SR ? 0 : 1) * 64 + (NC + PASS_NWM) * 64, SR ? 2 : 
             const int row0 = f0 / g.fpr;
             wt[o] = make_int4((int)(uint32_t)p, (int)(uint32_t)(p >> 32), m, (f0 - row0 * g.fpr) | (g.fpr << 8) | (row0 << 16));
         }
+        if (a.dbg) {
+            dbg_t[(NC + c) * 64 + lane] = 0;
+            dbg_t[(2 * NC + c) * 64 + lane] = 0;
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         auto went = [&](int o, const bf16_t*& p, int& m, int& w) {
             const int4 e = wt[o];
@@ -624,6 +628,7 @@ __global__ __launch_bounds__((SR ? 0 : 1) * 64 + (NC + PASS_NWM) * 64, SR ? 2 : 
         });
         // consume cursor: op co, row / fragment-in-row of the next fragment, fragments left
         int co = -1, cleft = 0, row = 0, kc = 0, fpr = 1;
+        int cdone = 0;  // fragments of op co consumed (developer stamps)
         f32x4_t acc4 = {0.f, 0.f, 0.f, 0.f};
         const int dsel = (lane & 15) - 4 * (lane >> 4);  // this lane's diagonal element of C, if any
         bool failed = false;
@@ -669,6 +674,8 @@ __global__ __launch_bounds__((SR ? 0 : 1) * 64 + (NC + PASS_NWM) * 64, SR ? 2 : 
                     kc = w & 255;
                     fpr = (w >> 8) & 255;
                     row = w >> 16;
+                    cdone = 0;
+                    if (a.dbg && lane == 0) dbg_t[(NC + c) * 64 + (co & 63)] = __builtin_amdgcn_s_memrealtime();
                     return;
                 }
                 arrive(co);
@@ -712,6 +719,8 @@ __global__ __launch_bounds__((SR ? 0 : 1) * 64 + (NC + PASS_NWM) * 64, SR ? 2 : 
                         : [xa] "v"(xaddr()), [vo] "v"(voff), [sb] "s"(gbase()), [nv] "n"(SR - 1), [nl] "n"(XR - 1)
                         : "memory");
                     iadv();
+                    if (a.dbg && ++cdone == 32 && lane == 0)  // developer: 32 fragments into the op
+                        dbg_t[(2 * NC + c) * 64 + (co & 63)] = __builtin_amdgcn_s_memrealtime();
                     if (++kc == fpr) {
                         flush();
                         ++row;
@@ -728,6 +737,12 @@ __global__ __launch_bounds__((SR ? 0 : 1) * 64 + (NC + PASS_NWM) * 64, SR ? 2 : 
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the ring's tail loads: none left in flight)
         if (failed && lane == 0) __hip_atomic_store((g_i32*)a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.dbg && lane == 0)  // per op: opened (input row seen), 32 fragments in, arrived
+            for (int o = 0; o < nop && o < 64; ++o) {
+                const unsigned long long t[7] = {dbg_t[(NC + c) * 64 + o], dbg_t[(2 * NC + c) * 64 + o],
+                                                 dbg_t[c * 64 + o], 0, 0, 0, 0};
+                dbg_record(a.dbg, 0xFB000000u | ((unsigned)wg << 12) | ((unsigned)c << 8) | (unsigned)o, gen, t);
+            }
         return;
     }
 
@@ -872,6 +887,10 @@ __global__ __launch_bounds__((SR ? 0 : 1) * 64 + (NC + PASS_NWM) * 64, SR ? 2 : 
     };
     auto set_ready = [&](int nready) {  // ops [0, nready) have their input row staged
         ex_sync();
+        if ((a.mode & 16) && t == 0) {  // developer: a 20 us seam (the weight rings land meanwhile)
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < 2000) __builtin_amdgcn_s_sleep(8);
+        }
         if (t == 0) flg[F_B] = (unsigned)nready;
     };
 
@@ -1042,7 +1061,7 @@ PassLds pass_lds(int kmax, int dim, int nqkv, int nkv, int S, int hd, int maxrow
     L.junk = (int)o;
     o = al(o + 1024);  // the prefetch DMAs' landing slot
     L.dbg = (int)o;
-    o = al(o + (size_t)PASS_NC * 64 * 8);  // developer stamps
+    o = al(o + (size_t)PASS_NC * 64 * 8 * (stream ? 3 : 1));  // developer stamps (stream: arrive, open, mid)
     L.wtab = (int)o;
     L.bytes = al(o + (stream ? (size_t)PASS_NC * nop * 16 : 0));  // stream waves' per-op shares
     return L;

@@ -4,6 +4,8 @@
 #include "fm_common.h"
 #include "fm_runtime.h"
 
+#include <algorithm>
+
 namespace {
 typedef __attribute__((ext_vector_type(4))) float f4_t;
 
@@ -25,6 +27,33 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const f4_t* __restrict
         acc += (v.x + v.y) + (v.z + v.w);
     }
     if (acc == 1234.5f) out[blockIdx.x] = acc;  // (keeps the loads; never true for the zeroed input)
+}
+
+// non-temporal LDS-DMA read stream (global_load_lds_dwordx4 nt, the decode pass's loader form):
+// every wave moves 1 KiB chunks into its own LDS slot, INF chunks in flight (vmcnt-throttled)
+template <int INF>
+__global__ __launch_bounds__(256) void stream_ldsdma_kernel(const char* __restrict__ a, int64_t nchunks) {
+    __shared__ __attribute__((aligned(16))) unsigned char slot[4][1024];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const uint32_t dst = (uint32_t)(size_t)(const __attribute__((address_space(3))) unsigned char*)slot[wave];
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(dst);
+    int n = 0;
+    for (int64_t c = (int64_t)blockIdx.x * 4 + wave; c < nchunks; c += nw) {
+        const char* src = a + c * 1024 + lane * 16;
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off nt\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src), "s"(m0)
+            : "memory");
+        if (++n >= INF) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INF - 1) : "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 __global__ __launch_bounds__(256) void stream_copy_kernel(const f4_t* __restrict__ a, f4_t* __restrict__ b, int64_t n4) {
@@ -60,12 +89,29 @@ extern "C" int fm_stream_peak(int device, int64_t bytes, int reps, double* read_
             HIPCHK(hipEventElapsedTime(&ms, e0, e1));
             return (double)ms * 1e-3;
         };
-        const double tr = time([&] {
+        // the best of several forms, so the quoted peak is what the part does, not what one kernel
+        // shape reaches: register float4 streams (4 / 8 in flight per thread, 8 / 16 blocks per CU)
+        // and non-temporal LDS-DMA streams (16 / 32 KiB in flight per wave)
+        double tr = 1e30, tc = 1e30;
+        tr = std::min(tr, time([&] {
             stream_read_kernel<4><<<grid, 256>>>(reinterpret_cast<const f4_t*>(a), n4, reinterpret_cast<float*>(o));
-        });
-        const double tc = time([&] {
+        }));
+        tr = std::min(tr, time([&] {
+            stream_read_kernel<8><<<ncu * 16, 256>>>(reinterpret_cast<const f4_t*>(a), n4, reinterpret_cast<float*>(o));
+        }));
+        const int64_t nch = bytes / 1024;
+        tr = std::min(tr, time([&] {
+            stream_ldsdma_kernel<16><<<ncu * 2, 256>>>(reinterpret_cast<const char*>(a), nch);
+        }));
+        tr = std::min(tr, time([&] {
+            stream_ldsdma_kernel<32><<<ncu * 2, 256>>>(reinterpret_cast<const char*>(a), nch);
+        }));
+        tc = std::min(tc, time([&] {
             stream_copy_kernel<<<grid, 256>>>(reinterpret_cast<const f4_t*>(a), reinterpret_cast<f4_t*>(b), n4);
-        });
+        }));
+        tc = std::min(tc, time([&] {
+            stream_copy_kernel<<<ncu * 16, 256>>>(reinterpret_cast<const f4_t*>(a), reinterpret_cast<f4_t*>(b), n4);
+        }));
         HIPCHK(hipGetLastError());
         if (read_gbps) *read_gbps = (double)bytes * reps / tr / 1e9;
         if (copy_gbps) *copy_gbps = 2.0 * (double)bytes * reps / tc / 1e9;

@@ -24,7 +24,7 @@ ABI_SYMBOLS = [
     "fm_device_count", "fm_last_error", "fm_stream_peak", "fm_llm_open", "fm_llm_set_quant", "fm_llm_set_quant_int4", "fm_llm_set_tensor", "fm_llm_synth_tensor",
     "fm_llm_finalize", "fm_llm_prefill", "fm_llm_prefill_batch", "fm_llm_decode", "fm_llm_decode_frames", "fm_llm_generate", "fm_llm_generate_at", "fm_llm_prefill_at", "fm_llm_slot_pos", "fm_llm_teacher_step",
     "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph", "fm_llm_debug_vec", "fm_tune", "fm_debug_ts_read",
-    "fm_llm_close", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
+    "fm_llm_close", "fm_source_hash", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
     "fm_codec_finalize", "fm_codec_decode", "fm_codec_stream_reset", "fm_codec_decode_chunk",
     "fm_codec_stream_open", "fm_codec_stream_decode", "fm_codec_stream_close",
     "fm_codec_profile_read", "fm_codec_debug_read", "fm_codec_enable_encoder", "fm_codec_encode",
@@ -35,6 +35,24 @@ ABI_SYMBOLS = [
 
 class FishMIError(RuntimeError):
     pass
+
+
+def tree_source_hash() -> str:
+    """sha256 (first 16 hex digits) over the files fish-speech_amd/Makefile's HASHED names, in its
+    order: the compiled sources (SRCS), the csrc headers sorted by name, include/fishmi.h."""
+    import hashlib
+    import re
+
+    pkg = os.path.dirname(HERE)
+    mk = open(os.path.join(pkg, "Makefile")).read()
+    srcs = re.search(r"^SRCS\s*=\s*(.+)$", mk, re.M).group(1).split()
+    heads = sorted(f for f in os.listdir(os.path.join(pkg, "csrc")) if f.endswith(".h"))
+    files = srcs + [os.path.join("csrc", h) for h in heads] + [os.path.join("..", "include", "fishmi.h")]
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(pkg, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 class SamplingC(ctypes.Structure):
@@ -59,6 +77,12 @@ def lib():
         except ImportError:
             pass
     L = ctypes.CDLL(LIB_PATH)
+    # build provenance: the library must have been compiled from the sources in this tree
+    L.fm_source_hash.restype = ctypes.c_char_p
+    built, tree = L.fm_source_hash().decode(), tree_source_hash()
+    if built != tree and not os.environ.get("FISHMI_ALLOW_STALE"):
+        raise FishMIError(f"{LIB_PATH} was built from other sources (hash {built}, tree {tree}): "
+                          "rebuild it with `make -C fish-speech_amd`")
     vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64
     f32 = ctypes.c_float
     pi32 = ctypes.POINTER(ctypes.c_int32)

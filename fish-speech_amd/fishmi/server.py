@@ -276,6 +276,10 @@ def create_app(engine: "TTS.TTSInferenceEngine", max_text_length: int = 0, api_k
             log.error("renaming reference %r: %s", old, e)
             return ref_reply(request, False, "File system error occurred", 500,
                              old_reference_id=old, new_reference_id=new)
+        except Exception as e:  # the reference's update route answers these too (views.py:472-480)
+            log.error("renaming reference %r: %s", old, e)
+            return ref_reply(request, False, "Internal server error occurred", 500,
+                             old_reference_id=old, new_reference_id=new)
 
     return app
 

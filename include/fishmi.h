@@ -87,6 +87,11 @@ typedef struct fm_llm fm_llm;
 
 int fm_device_count(void);
 const char* fm_last_error(void);
+
+/* Build provenance: the first 16 hex digits of sha256 over the sources and headers the library was
+ * compiled from (fish-speech_amd/Makefile HASHED); fishmi.native.lib() refuses a library whose hash
+ * differs from the tree's, so a stale prebuilt libfishmi.so cannot run. */
+const char* fm_source_hash(void);
 /* Measured HBM stream peak of `device` (no reference counterpart: SURVEY.md §8d's STREAM-like
    figure beside the vendor peak): a non-temporal float4 read stream (GB/s read) and a float4 copy
    (GB/s read + written) over `bytes`-sized buffers (>= 64 MiB; use >> 256 MiB to defeat the MALL),

@@ -722,6 +722,12 @@ def cmd_llm_full64():
     _timed_case("llm_full64_bf16", _wide_config(36, 4, 160), T=64, n_new=65, prompt_seed=7, fast_last_only=True)
 
 
+def cmd_llm_full216():
+    """Config 2's bench run at full depth: prefill + 216 decode frames (positions 64..280, the
+    positions bench.py decodes to), every frame's slow logits and the last codebook's fast logits."""
+    _timed_case("llm_full216_bf16", _wide_config(36, 4, 296), T=64, n_new=217, prompt_seed=11, fast_last_only=True)
+
+
 def cmd_llm_long4():
     """A 3000-token context through 4 slow layers (+ 1 fast) at S2-Pro widths."""
     _timed_case("llm_long4_bf16", _wide_config(4, 1, 3072), T=3000, n_new=7, prompt_seed=9)
@@ -741,6 +747,13 @@ def cmd_llm_ragged64():
     _ragged_case("llm_ragged64_bf16", n_new=65, keep_frames=(0, 32, 64), max_seq_len=336, prompt_seed0=200)
 
 
+def cmd_llm_ragged_full():
+    """Config 3's ragged batch at FULL depth (36 slow + 4 fast layers): the 32 prompt lengths of
+    llm_ragged, prefill + 8 decode frames, logits kept at frames 0, 4 and 8."""
+    _ragged_case("llm_ragged_full_bf16", n_new=9, keep_frames=(0, 4, 8), max_seq_len=272, prompt_seed0=300,
+                 n_layer=36, n_fast_layer=4)
+
+
 def cmd_llm_ragged():
     """Config 3's ragged batch at S2-Pro widths (2 slow + 1 fast layers): 32 prompts with lengths
     uniform over 16..256 (seed 2), each run by the reference at batch 1 (its only
@@ -749,11 +762,11 @@ def cmd_llm_ragged():
     _ragged_case("llm_ragged_bf16", n_new=3, keep_frames=(0, 1, 2), max_seq_len=272, prompt_seed0=100)
 
 
-def _ragged_case(out_name, n_new, keep_frames, max_seq_len, prompt_seed0):
+def _ragged_case(out_name, n_new, keep_frames, max_seq_len, prompt_seed0, n_layer=2, n_fast_layer=1):
     from fish_speech.models.text2semantic import inference
 
     B = 32
-    config = _wide_config(2, 1, max_seq_len)
+    config = _wide_config(n_layer, n_fast_layer, max_seq_len)
     lens = np.random.default_rng(2).integers(16, 257, B)
     t0 = time.time()
     cfg, state = _llm_state(config, 41, 5)

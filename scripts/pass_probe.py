@@ -16,6 +16,7 @@ from fishmi.llm import DualARModel  # noqa: E402
 
 args = [x for x in sys.argv[1:] if "=" not in x]
 frames = int(args[0]) if args else 32
+native.tune("pass_prepare", 1)  # the pass weights are built at finalize only when asked for
 for kv in (x for x in sys.argv[1:] if "=" in x):
     k, v = kv.split("=")
     native.tune(k, int(v))
@@ -92,6 +93,7 @@ if os.environ.get("STAMPS"):
     m2.decode([0])
     rec = native.debug_ts_read().astype(np.int64)
     native.tune("debug_ts", 0)
+    rec_all = rec.copy()
     tag = (rec[:, 0] >> 32) & 0xFFFFFFFF
     rec = rec[(tag >> 24) == 0xFA]
     wg = (rec[:, 0] >> 40) & 0xFF
@@ -114,6 +116,20 @@ if os.environ.get("STAMPS"):
               f"{np.median(d(4, 5)):5.2f} | {np.median(d(5, 6)):5.2f} ({np.median(q[:, 7] & 0xFFFFFFFF) / 100.0:5.2f}) | {np.median(seam):6.2f} {seam.max():6.2f} | "
               f"{(q[:, 2].max() - q[:, 2].min()) / 100.0:5.2f} | {np.median(q[:, 7] >> 32) / 100.0:5.2f}")
     print(f"pass span {(r[:, 6].max() - r[:, 1].min()) / 100.0:.1f} us")
+    # stream waves (pass_cfg >= 6): per op, input seen -> 32 fragments consumed -> arrived
+    sr = rec_all[((rec_all[:, 0] >> 56) & 0xFF) == 0xFB] if rec_all is not None else np.zeros((0, 8), np.int64)
+    if len(sr):
+        sg = sr[:, 0] & 0xFFFFFFFF
+        sr = sr[sg == g1]
+        so = (sr[:, 0] >> 32) & 0xFF
+        print("op  stream: open->32 frags med/max | open->arrive med/max (us)")
+        for k in sorted(set(so.tolist())):
+            q = sr[so == k]
+            mid = q[:, 2] > 0
+            d1 = (q[mid, 2] - q[mid, 1]) / 100.0
+            d2 = (q[:, 3] - q[:, 1]) / 100.0
+            print(f"{k:2d}  {np.median(d1) if len(d1) else float('nan'):7.2f} {d1.max() if len(d1) else float('nan'):7.2f} | "
+                  f"{np.median(d2):7.2f} {d2.max():7.2f}")
     q = r[o == 0][:, 7] & 0xFFFFFFFF
     print(f"attention (exchange waves' share) {np.median(q) / 100.0:.2f} us")
     m2.close()

@@ -31,6 +31,20 @@ def test_library_exports_every_header_symbol():
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libfishmi.so not built")
+def test_library_built_from_this_tree():
+    """Build provenance: the loaded libfishmi.so carries the hash of the sources it was compiled
+    from (Makefile HASHED), and it equals the hash of the sources in this tree -- a stale prebuilt
+    library cannot pass (native.lib() refuses it)."""
+    import ctypes
+
+    from fishmi import native
+
+    L = ctypes.CDLL(native.LIB_PATH)
+    L.fm_source_hash.restype = ctypes.c_char_p
+    built = L.fm_source_hash().decode()
+    assert len(built) == 16 and built == native.tree_source_hash()
+
+
 def test_library_loads_without_gpu():
     from fishmi import native
 

@@ -10,8 +10,12 @@ under `pytest -x -m gpu` nothing else can hide a failure here.
   batched path, each slot's logits against the reference's batch-1 run of its own prompt (bf16),
   and each slot's greedy stream against its own batch-1 stream (fp32 validation mode).
 
-Goldens: oracle/gen_goldens.py llm_full / llm_long / llm_ragged (the reference run on CPU in the
-dev container; weights regenerate from the seed on the device).  Bound: tests/parity_util.py."""
+* Round 5: config 2 over all 216 bench frames (positions 64..280) and config 3's ragged batch at
+  full depth (36 + 4 layers), the depths and positions the bench actually runs.
+
+Goldens: oracle/gen_goldens.py llm_full / llm_long / llm_ragged / llm_full216 / llm_ragged_full (the
+reference run on CPU in the dev container; weights regenerate from the seed on the device).  Bound:
+tests/parity_util.py."""
 import json
 
 import numpy as np
@@ -89,6 +93,28 @@ def test_config2_full_depth_64_frames_bf16_vs_reference(golden):
                            bits_to_f32(g["fast_last_bits"])[:, None], g["slow_logits_f32"],
                            g["fast_last_f32"][:, None])
     assert st["top1_checked"] >= 30  # (36 of 130 clear margins at this seed)
+
+
+def test_config2_full_depth_216_frames_bf16_vs_reference(golden):
+    """Config 2 exactly as bench.py runs it: full depth, 64-token prompt, prefill + 216 decode frames
+    (positions 64..280), teacher-forced through the production decode graph; every frame's slow
+    logits and the last codebook's fast logits within BF16_RATIO x the reference's own bf16 error."""
+    from fishmi.llm import DualARModel
+
+    g = _golden_or_skip(golden, "llm_full216_bf16.npz")
+    cfg = _cfg(g)
+    T = g["prompt"].shape[1]
+    assert T == 64 and g["seq"].shape[1] - T >= 217 and cfg.n_layer == 36
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 1)
+    try:
+        slow, fast = m.teacher_decode(g["prompt"], g["seq"][:, T:])
+    finally:
+        m.close()
+    rows = g["slow_rows"]
+    st = bf16_vs_reference(slow[:, rows], fast[:, -1:], bits_to_f32(g["slow_logits_bits"]),
+                           bits_to_f32(g["fast_last_bits"])[:, None], g["slow_logits_f32"],
+                           g["fast_last_f32"][:, None])
+    assert st["top1_checked"] >= 60
 
 
 def test_long_context_4_layers_bf16_vs_reference(golden):
@@ -181,6 +207,53 @@ def test_config3_ragged_32_slots_64_frames_bf16_vs_reference(golden):
     prompts = [g[f"prompt_{i}"] for i in range(B)]
     slot_of = np.random.default_rng(6).permutation(B)
     order = [int(slot_of[i]) for i in np.random.default_rng(7).permutation(B)]
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", B)
+    slow = np.zeros((B, len(kf), len(g["slow_rows"])), np.float32)
+    fast = np.zeros((B, len(kf), 1, cfg.codebook_size), np.float32)
+    sp = DualARModel.sampling(top_k=1)
+    try:
+        for k in range(n):
+            for i in range(B):
+                m.force(int(slot_of[i]), cols[i, :, k])
+            if k == 0:
+                m.prefill_batch([int(s) for s in slot_of], prompts, [sp] * B)
+            else:
+                m.decode(order)
+            if k in kf:
+                for i in range(B):
+                    s_, f_ = m.read_logits(int(slot_of[i]))
+                    slow[i, kf.index(k)] = s_[g["slow_rows"]]
+                    fast[i, kf.index(k), 0] = f_[-1]
+    finally:
+        for s in range(B):
+            m.force(s, None)
+        m.close()
+    nk = len(kf)
+    st = bf16_vs_reference(slow.reshape(B * nk, -1), fast.reshape(B * nk, 1, -1),
+                           bits_to_f32(g["slow_logits_bits"]).reshape(B * nk, -1),
+                           bits_to_f32(g["fast_last_bits"]).reshape(B * nk, 1, -1),
+                           g["slow_logits_f32"].reshape(B * nk, -1), g["fast_last_f32"].reshape(B * nk, 1, -1))
+    assert st["top1_checked"] >= B
+
+
+def test_config3_ragged_32_slots_full_depth_bf16_vs_reference(golden):
+    """Config 3's ragged batch at FULL depth (36 + 4 layers): 32 prompts of 16..256 tokens in
+    permuted slots, prefill_batch then 8 batched frames (bsacc_kernel, finalize_norm, attn_fd at 32
+    positions through 36 layers), teacher-forced; logits at the golden's kept frames (0, 4, 8)
+    against each prompt's batch-1 reference run."""
+    from fishmi.llm import DualARModel
+
+    g = _golden_or_skip(golden, "llm_ragged_full_bf16.npz")
+    cfg = _cfg(g)
+    assert cfg.n_layer == 36
+    B = int(g["lens"].size)
+    cols = g["cols"]
+    n = cols.shape[2]
+    kf = [int(k) for k in g["keep_frames"]]
+    assert B == 32 and n >= 9 and kf[-1] == n - 1
+    prompts = [g[f"prompt_{i}"] for i in range(B)]
+    slot_of = np.random.default_rng(8).permutation(B)
+    order = [int(slot_of[i]) for i in np.random.default_rng(9).permutation(B)]
     m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", B)
     slow = np.zeros((B, len(kf), len(g["slow_rows"])), np.float32)
     fast = np.zeros((B, len(kf), 1, cfg.codebook_size), np.float32)

@@ -160,3 +160,31 @@ def test_fused_tile_variants_equal_two_launch(cfg, golden):
         native.tune("resunit_cfg", 1)
     np.testing.assert_array_equal(fused, two)
     m.close()
+
+
+def test_fused_then_fallback_stages_equal_two_launch(golden):
+    """decoder_dim 384: the 192- and 96-channel stages run fused, the 48- and 24-channel stages fall
+    back to two launches after them (the fallback's k7 scratch must not alias the rotated
+    activation buffers).  Fused == two-launch bit for bit, one-shot and streamed."""
+    import dataclasses
+
+    from fishmi.codec import FishMICodec
+    from fishmi.config import CodecConfig
+
+    g = golden("codec_long.npz")
+    cfg = dataclasses.replace(CodecConfig.from_spec(json.loads(str(g["spec"]))), decoder_dim=384)
+    m = FishMICodec.synthetic(cfg, int(g["synth_seed"]), 0, "bf16", 64)
+    try:
+        rng = np.random.default_rng(5)
+        C1, T = m.cfg.n_codebooks + 1, 48
+        codes = np.zeros((C1, T), np.int32)
+        codes[0] = rng.integers(0, m.cfg.semantic_codebook_size, T)
+        codes[1:] = rng.integers(0, m.cfg.codebook_size, (C1 - 1, T))
+        fused, two = _both(m, lambda: m.decode_codes(codes))
+        assert np.isfinite(fused).all()
+        np.testing.assert_array_equal(fused, two)
+        sf, st = _both(m, lambda: _stream(m, codes, (5, 11, 32)))
+        np.testing.assert_array_equal(sf, st)
+        np.testing.assert_array_equal(sf, fused)
+    finally:
+        m.close()

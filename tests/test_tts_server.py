@@ -198,6 +198,20 @@ def test_http_reference_management(tmp_path):
     assert r.status_code == 200 and not (tmp_path / "bob").exists()
     assert c.request("DELETE", "/v1/references/delete", json={"reference_id": "bob"}).status_code == 404
     assert c.get("/v1/references/list?format=json").json()["reference_ids"] == ["alicia", "carol"]
+    # an unexpected failure: the reference's 500 body, not FastAPI's plain-text error
+    orig = eng.rename_reference
+
+    def broken(old, new):
+        raise RuntimeError("disk on fire")
+
+    eng.rename_reference = broken
+    try:
+        r = c.post("/v1/references/update?format=json", json={"old_reference_id": "carol", "new_reference_id": "z"})
+        assert r.status_code == 500
+        assert r.json() == {"success": False, "message": "Internal server error occurred",
+                            "old_reference_id": "carol", "new_reference_id": "z"}
+    finally:
+        eng.rename_reference = orig
 
 
 def test_http_tts_wav_and_stream_json_and_msgpack():
