@@ -437,7 +437,7 @@ def pmc_gemv_traffic(timeout_s=150):
     import tempfile
 
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
-    from rocprof_summary import load_pmc
+    from rocprof_summary import is_decode_linear, load_pmc
 
     exe = shutil.which("rocprofv3")
     if exe is None:
@@ -453,16 +453,16 @@ def pmc_gemv_traffic(timeout_s=150):
             glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         if r.returncode != 0 or not dbs:
             return None, f"rocprofv3 --pmc {counter} failed (rc {r.returncode}): {r.stderr[-300:].decode(errors='replace')}"
-        v = [x for name, xs in load_pmc(dbs[0], counter).items() if name.startswith("void gemv_kernel") for x in xs]
+        v = [x for name, xs in load_pmc(dbs[0], counter).items() if is_decode_linear(name) for x in xs]
         shutil.rmtree(d, ignore_errors=True)
         if not v:
-            return None, f"no gemv_kernel dispatches in the {counter} pass"
+            return None, f"no decode-linear dispatches in the {counter} pass"
         vals[counter] = 1024.0 * sum(v) / len(v)
     fetch = 2.0 * vals["FETCH_SIZE"]
     return int(round(fetch + vals["WRITE_SIZE"])), (
         f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes over scripts/pmc_probe.py in this run: "
         f"{fetch / 1e6:.2f} MB fetched (FETCH_SIZE KB x1024 x2, gfx950 wide-read correction) + "
-        f"{vals['WRITE_SIZE'] / 1e6:.3f} MB written per gemv_kernel launch")
+        f"{vals['WRITE_SIZE'] / 1e6:.3f} MB written per decode-linear launch (gemv_kernel, rowgemv_kernel)")
 
 
 def stream_peak_gbps(nbytes=2 << 30, reps=10):
@@ -645,7 +645,9 @@ def main():
             "per_stream_rtf": round(args.frames / FRAME_RATE / np.mean([t["total"] for t in tms]), 4),
             "breakdown_ms": {k: round(float(np.mean([t[k] for t in tms])) * 1e3, 2)
                              for k in ("prefill", "head", "decode", "codec", "total")},
-            "roofline": {"kernel": "gemv_kernel (decode linear layers, fused norm/residual prologues)",
+            "roofline": {"kernel": "decode linear layers: gemv_kernel (16-row MFMA tiles: w1||w3, heads, first-layer "
+                                   "wqkv) + rowgemv_kernel (row blocks: wo / w2 with the residual epilogue, wqkv "
+                                   "with the RMSNorm prologue)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "traffic_source": traffic_note,

@@ -417,6 +417,31 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
             pf_issue();
         }
         if constexpr (PRO == PRO_PRENORM) {
+            float* rsw = rsl + wave * GEMV_RMAX;
+            if (!CH && a.ss_gran == 1) {
+                // one row, whole K staged in xc (host-checked): the statistic from the row itself,
+                // sum of x^2 per thread, per wave, then over the block's waves in a fixed order
+                // (the producer -- fm_rowgemv.hip -- wrote no tile sums)
+                float sl = 0.f;
+#pragma unroll
+                for (int q = 0; q < PRE_N; ++q) {
+                    const int it = threadIdx.x + NTH * q;
+                    if (it < nitem) {
+                        float xv[8];
+                        c8_to_f(xc[q], xv);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) sl += xv[u] * xv[u];
+                    }
+                }
+                sl = wave_sum(sl);
+                if (lane == 0) red[wave] = sl;
+                lds_barrier();
+                if (a.dbg) tsA = __builtin_amdgcn_s_memrealtime();
+                float tot = 0.f;
+#pragma unroll
+                for (int w = 0; w < WPB; ++w) tot += red[w];
+                if (lane == 0) rsw[0] = 1.0f / sqrtf(tot / (float)a.K + a.eps);
+            } else {
             // stage the tile sums in `red` (free until the cross-wave reduction), then every wave
             // reduces each row's sums itself: per-row 1/rms in the wave's LDS slot (a register
             // array indexed by the runtime row would be spilled to scratch)
@@ -430,7 +455,6 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
             __syncthreads();
             if (a.dbg) tsA = __builtin_amdgcn_s_memrealtime();
             const int nt = a.K >> 4;
-            float* rsw = rsl + wave * GEMV_RMAX;
 #pragma unroll
             for (int rr = 0; rr < GEMV_RMAX; ++rr) {
                 if (rr >= R) break;
@@ -438,6 +462,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs<T>& a, const int bxi, c
                 for (int t = lane; t < nt; t += 64) sl += red[t * R + rr];
                 const float v = 1.0f / sqrtf(wave_sum(sl) / (float)a.K + a.eps);
                 if (lane == 0) rsw[rr] = v;
+            }
             }
             __builtin_amdgcn_wave_barrier();
             const bool writer = bxi == 0 && ks == 0 && a.xn_out;
@@ -817,6 +842,9 @@ static void gemv_go_q4(hipStream_t s, const GemvArgs<T>& a, int ksb) {
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb) {
     // PRO_PRENORM stages the [K/16][R] tile sums in the 256 * R floats of the reduction buffer
     FMCHECK(pro != PRO_PRENORM || (a.K <= 4096 && a.R <= GEMV_RMAX), "PRO_PRENORM needs K <= 4096, R <= 8");
+    FMCHECK(pro != PRO_PRENORM || (a.ss_in && (a.ss_gran != 1 || (a.R == 1 && ksb == 1 && !a.Wq &&
+                                                                   a.K <= 3 * 8 * 256))),
+            "PRO_PRENORM: ss_in set (also with ss_gran 1: one row, whole K staged)");
     FMCHECK(pro != PRO_FATT || (a.R == 1 && a.att.cpos < FAST_ATTN_MAXJ && a.att.cpos < a.att.S &&
                                 (a.K / ksb) % a.att.hd == 0 && a.att.hd % 16 == 0 && a.att.hd <= 16 * FATT_MAXPP &&
                                 a.att.ldqkv % 8 == 0),

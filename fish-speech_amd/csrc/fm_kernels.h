@@ -197,6 +197,7 @@ template <typename T> struct GemvArgs {
     const T* res;            // EPI_SLABFIN residual [R][ldr]
     int ldr;
     const float* ss_in;      // PRO_PRENORM: per-16-column-tile sums of squares of X [K/16][R]
+    int ss_gran;             // PRO_PRENORM: 0 ss_in as above; 1 the statistic from the staged row itself (R == 1, whole K)
     const T* nw;             // norm weight [K]
     float eps;
     int R, N, K;
@@ -288,6 +289,7 @@ struct FmTuning {
     int fin8 = 1;            // finalize_norm: all eight K parts' slab loads in one round trip (0: two batches of four)
     int fin_split = 0;       // batched finalize_norm: each row over this many blocks (0 / 1: one block per row)
     int int4_stream = 1;     // weight-only int4: 1 the batch <= 8 GEMVs stream the 4-bit codes, 0 the dequantised bf16 copy
+    int rowgemv = 3;         // batch-1 bf16 on the row-block GEMV (fm_rowgemv.hip): bit 0 wo / w2, bit 1 wqkv (0: 16-row MFMA tiles)
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
     int pass_prepare = 0;    // 1: build the persistent pass's weight copy at finalize even with pass_fast 0
     int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1), 5 (12 x 8, 4: K / V from the cache, 96 KiB ring), 6 (no loader: stream waves with PASS_SR-fragment register rings)
@@ -307,6 +309,35 @@ inline size_t gemv_lds_bytes(int R, int Kb, size_t esz) {
            8 * 8 * sizeof(float);
 }
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb);
+// batch-1 row-block GEMV (fm_rowgemv.hip): row-major bf16 W [N][K], RP rows per 256-thread block.
+//   ROWGEMV_FIN        (wo / w2, RP 2): y = round(res + round(W x + bias)) into res_out (its RMSNorm
+//                      consumer: GemvArgs::ss_gran = 1)
+//   ROWGEMV_NORM_STORE (wqkv, RP 8): x' = RMSNorm(x) * nw in the prologue, y = round(W x' + bias) into
+//                      Y, optional KV prefetch (GemvArgs::pf_kc semantics)
+enum { ROWGEMV_FIN = 0, ROWGEMV_NORM_STORE = 1 };
+struct RowGemvArgs {
+    const bf16_t* W;
+    const bf16_t* X;          // [K]
+    const bf16_t* bias;       // [N] or null
+    const bf16_t* nw;         // NORM: norm weight [K]
+    float eps;
+    const bf16_t* res;        // FIN: residual table [.][ldr] (row 0, or residx[res_col] clamped to res_rows)
+    int ldr;
+    const int32_t* residx;
+    int res_col, res_rows;
+    bf16_t* res_out;          // FIN: [N]
+    bf16_t* Y;                // STORE: [N]
+    int N, K;
+    const bf16_t* pf_kc;      // STORE: KV prefetch (null: off), as GemvArgs
+    const bf16_t* pf_vc;
+    const int32_t* pf_slot;
+    const int32_t* pf_pos;
+    size_t pf_slot_stride, pf_layer_off;
+    int pf_S, pf_nkv, pf_hd;
+    unsigned long long* dbg;  // developer timestamps (launcher: fm_tune debug_ts)
+};
+int rowgemv_u(int K);         // per-wave chunk depth for K (0: not eligible)
+void launch_rowgemv(hipStream_t s, const RowGemvArgs& a, int kind);
 // batch-1 GEMV chain (fm_gemv.hip gemv_chain_kernel): 2..GEMV_CHAIN_MAX dependent GEMVs in one launch,
 // whole K per block, one row.  Stage kinds: wo / w2 (PRO_PLAIN, EPI_SLABFIN; the residual may be a
 // gathered row), w1||w3 (PRO_PRENORM, EPI_SWIGLU8), qkv (PRO_PRENORM, EPI_STORE), and as the last

@@ -103,6 +103,7 @@ static int pick_ksb(int N, int K, int R, size_t esz) {
 struct LayerW {
     void *wqkv = nullptr, *bqkv = nullptr, *wo = nullptr, *bo = nullptr, *qn = nullptr, *kn = nullptr;
     void *w13 = nullptr, *w2 = nullptr, *an = nullptr, *fn = nullptr;  // w13: row-interleaved W1||W3
+    void *wo_rm = nullptr, *w2_rm = nullptr, *wqkv_rm = nullptr;  // bf16 row-major as well (fm_rowgemv.hip)
 };
 
 struct StackDims {
@@ -189,6 +190,9 @@ struct fm_llm {
         const uint32_t* sz = nullptr;       // int4: packed (scale, zero) per (tile, 128-k unit, row)
     };
     std::map<const void*, QInfo> qmap;
+    std::map<const void*, void*> rowmajor;  // packed wo / w2 -> their row-major bf16 copy (row-pair GEMV)
+    bool row_ok = false;                    // every layer of both stacks has wo / w2 row-major
+    bool row_qkv_ok = false;                //                         ... and wqkv
     const QInfo* qinfo(const void* W) const {
         auto it = qmap.find(W);
         return it == qmap.end() ? nullptr : &it->second;
@@ -737,6 +741,25 @@ template <typename T> struct Run {
         m->prof.record(cls, bytes, go);
         m->prof.run(s, cls, bytes, flops, go);
     }
+    // batch-1 bf16 wo / w2 on the row-block GEMV (fm_rowgemv.hip: one block per pair of rows, every
+    // CU busy); their RMSNorm consumers then take the statistic from the row they stage (ss_gran 1)
+    bool row_fin(int n) const {
+        const FmTuning& t = fm_tuning();
+        return sizeof(T) == 2 && n == 1 && m->row_ok && (t.rowgemv & 1) && !t.gemv_chain && !t.attn_wo;
+    }
+    // ... and wqkv (norm prologue, 8 rows per block)
+    bool row_qkv(int n) const {
+        const FmTuning& t = fm_tuning();
+        return sizeof(T) == 2 && n == 1 && m->row_qkv_ok && (t.rowgemv & 2) && !t.gemv_chain;
+    }
+    void rowgemv(const RowGemvArgs& a, int kind) {
+        chain_flush();
+        const int64_t bytes = (int64_t)a.N * a.K * 2 + (int64_t)a.K * 2;
+        hipStream_t st = s;
+        auto go = [st, a, kind] { launch_rowgemv(st, a, kind); };
+        m->prof.record("linear", bytes, go);
+        m->prof.run(s, "linear", bytes, 2.0 * a.N * a.K, go);
+    }
     template <typename F> void run_(const char* cls, int64_t bytes, double flops, F&& f) {
         chain_flush();
         m->prof.run(s, cls, bytes, flops, std::forward<F>(f));
@@ -779,6 +802,7 @@ template <typename T> struct Run {
         fa.dbg = fm_tuning().dbg;
         // fast model: attention recomputed by every block of the Wo GEMV (PRO_FATT, one row) --
         // no attention launch (fm_tune attn_wo; measured slower, kept under test)
+        const bool rf = row_fin(n);
         const bool att_wo = is_fast && fm_tuning().attn_wo && !m->quant && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
                             d.hd <= 128 && d.nh % d.nkv == 0 && (d.nq() / kp.wo) % d.hd == 0 && d.nqkv() % 8 == 0;
         // QKV (+ attention_norm)
@@ -812,10 +836,31 @@ template <typename T> struct Run {
                 a.xidx_col = xcol;
                 a.xidx_rows = xidx ? m->cb : 0;
                 gemv(a, PRO_NORM, epi, 1, "linear");
+            } else if (row_qkv(n)) {
+                RowGemvArgs r{};
+                r.W = (const bf16_t*)L.wqkv_rm;
+                r.X = (const bf16_t*)xb;
+                r.bias = (const bf16_t*)L.bqkv;
+                r.nw = (const bf16_t*)L.an;
+                r.eps = m->c.norm_eps;
+                r.Y = (bf16_t*)m->qkv;
+                r.N = d.nqkv();
+                r.K = d.dim;
+                r.pf_kc = (const bf16_t*)a.pf_kc;
+                r.pf_vc = (const bf16_t*)a.pf_vc;
+                r.pf_slot = a.pf_slot;
+                r.pf_pos = a.pf_pos;
+                r.pf_slot_stride = a.pf_slot_stride;
+                r.pf_layer_off = a.pf_layer_off;
+                r.pf_S = a.pf_S;
+                r.pf_nkv = a.pf_nkv;
+                r.pf_hd = a.pf_hd;
+                rowgemv(r, ROWGEMV_NORM_STORE);
             } else {
                 a.X = (const T*)xb;
                 a.ldx = d.dim;
                 a.ss_in = m->ssX;
+                a.ss_gran = rf ? 1 : 0;
                 gemv(a, PRO_PRENORM, epi, 1, "linear");
             }
         }
@@ -845,7 +890,26 @@ template <typename T> struct Run {
             });
         }
         // wo, split-K; the last block of each tile finalises h = x + wo(att) and its sums of squares
-        {
+        if (rf) {
+            RowGemvArgs r{};
+            r.W = (const bf16_t*)L.wo_rm;
+            r.X = (const bf16_t*)m->att;
+            r.bias = (const bf16_t*)L.bo;
+            if (first) {
+                r.res = (const bf16_t*)x_in;
+                r.ldr = ldx_in;
+                r.residx = xidx;
+                r.res_col = xcol;
+                r.res_rows = xidx ? m->cb : 0;
+            } else {
+                r.res = (const bf16_t*)xb;
+                r.ldr = d.dim;
+            }
+            r.res_out = (bf16_t*)hb;
+            r.N = d.dim;
+            r.K = d.nq();
+            rowgemv(r, ROWGEMV_FIN);
+        } else {
             GemvArgs<T> a = ga();
             a.W = (const T*)L.wo;
             a.bias = (const T*)L.bo;
@@ -889,12 +953,23 @@ template <typename T> struct Run {
             a.X = (const T*)hb;
             a.ldx = d.dim;
             a.ss_in = m->ssH;
+            a.ss_gran = rf ? 1 : 0;
             a.Y = (T*)m->act;
             a.ldy = d.inter;
             gemv(a, PRO_PRENORM, EPI_SWIGLU8, 1, "linear");
         }
         // W2, split-K; finalises the block output x = h + w2(act) into xb and its sums of squares
-        {
+        if (rf) {
+            RowGemvArgs r{};
+            r.W = (const bf16_t*)L.w2_rm;
+            r.X = (const bf16_t*)m->act;
+            r.res = (const bf16_t*)hb;
+            r.ldr = d.dim;
+            r.res_out = (bf16_t*)xo;
+            r.N = d.dim;
+            r.K = d.inter;
+            rowgemv(r, ROWGEMV_FIN);
+        } else {
             GemvArgs<T> a = ga();
             a.W = (const T*)L.w2;
             a.X = (const T*)m->act;
@@ -943,6 +1018,7 @@ template <typename T> struct Run {
             a.X = (const T*)xs;
             a.ldx = c.dim;
             a.ss_in = m->ssX;
+            a.ss_gran = row_fin(n) ? 1 : 0;
             gemv(a, PRO_PRENORM, EPI_F32, 1, "linear");
         } else {
             a.X = (const T*)xlast;
@@ -1074,6 +1150,7 @@ template <typename T> struct Run {
             a.X = (const T*)xbuf(m->fx, m->fx2, m->fdm.n_layer);
             a.ldx = c.fast_dim;
             a.ss_in = m->ssX;
+            a.ss_gran = row_fin(n) ? 1 : 0;
             gemv(a, PRO_PRENORM, EPI_F32, 1, "linear");
         }
     }
@@ -1413,6 +1490,18 @@ static void* pack_dev(fm_llm* m, const void* src, int rows, int cols) {
     return dst;
 }
 
+// bf16 wo / w2 / wqkv whose shapes the row-block GEMV takes keep their row-major copy
+// (fm_rowgemv.hip; ~3.7 GB at S2-Pro beside the packed tiles the batched paths read)
+static bool row_keep(fm_llm* m, const std::string& n, int rows, int cols) {
+    auto ends = [&](const char* suf) {
+        const size_t L = strlen(suf);
+        return n.size() >= L && n.compare(n.size() - L, L, suf) == 0;
+    };
+    if (m->prec != FM_PREC_BF16 || m->quant || rowgemv_u(cols) == 0) return false;
+    if (ends("attention.wo.weight") || ends("feed_forward.w2.weight")) return rows % 2 == 0;
+    return ends("attention.wqkv.weight") && rows % 8 == 0 && rowgemv_u(cols) <= 8;
+}
+
 static bool is_ffn_w13(const std::string& n) {
     auto ends = [&](const char* suf) {
         const size_t L = strlen(suf);
@@ -1582,7 +1671,12 @@ static void finalize(fm_llm* m) {
             t.q = nullptr;
         }
         HIPCHK(hipStreamSynchronize(m->stream));
-        HIPCHK(hipFree(t.p));
+        if (row_keep(m, kv.first, (int)t.rows, (int)t.cols)) {
+            m->rowmajor[pk] = t.p;  // kept for the batch-1 row-pair GEMV
+            m->allocs.push_back(t.p);
+        } else {
+            HIPCHK(hipFree(t.p));
+        }
         t.p = pk;
     }
     auto stack = [&](const std::string& pre, const StackDims& d, std::vector<LayerW>& out) {
@@ -1600,10 +1694,23 @@ static void finalize(fm_llm* m) {
             L.w2 = W(m, p + "feed_forward.w2.weight");
             L.an = W(m, p + "attention_norm.weight");
             L.fn = W(m, p + "ffn_norm.weight");
+            auto rm = [&](const void* pk) -> void* {
+                auto it = m->rowmajor.find(pk);
+                return it == m->rowmajor.end() ? nullptr : it->second;
+            };
+            L.wo_rm = rm(L.wo);
+            L.w2_rm = rm(L.w2);
+            L.wqkv_rm = rm(L.wqkv);
         }
     };
     stack("layers.", m->sd, m->slow);
     stack("fast_layers.", m->fdm, m->fast);
+    m->row_ok = m->row_qkv_ok = true;
+    for (auto* st : {&m->slow, &m->fast})
+        for (const LayerW& L : *st) {
+            m->row_ok = m->row_ok && L.wo_rm && L.w2_rm;
+            m->row_qkv_ok = m->row_qkv_ok && L.wqkv_rm;
+        }
     pass_tables(m);
     if (m->quant) {  // WeightOnlyInt8Linear has no bias (quantize.py:206-229): the checkpoint's are unused
         for (auto* st : {&m->slow, &m->fast})
@@ -2468,6 +2575,9 @@ int fm_tune(const char* key, int value) {
             t.int4_stream = value != 0;
         } else if (k == "pass_fast") {
             t.pass_fast = value != 0;
+        } else if (k == "rowgemv") {
+            FMCHECK(value >= 0 && value <= 3, "rowgemv must be 0..3 (bit 0 wo / w2, bit 1 wqkv)");
+            t.rowgemv = value;
         } else if (k == "pass_prepare") {
             t.pass_prepare = value != 0;
         } else if (k == "pass_cfg") {

@@ -4,8 +4,8 @@
 
     python scripts/rocprof_summary.py <db-or-csv> <out-prefix> [--bench <bench-json-log>]
 
-The JSON carries the aggregate of every `gemv_kernel<...>` dispatch (the bench's roofline
-kernel): launch count and average duration, to be checked against bench.py's HIP-event figure.
+The JSON carries the aggregate of every decode-linear dispatch (the bench's roofline kernel:
+the bf16 `gemv_kernel<..., QM = 0>` instantiations and `rowgemv_kernel<...>`): launch count and average duration, to be checked against bench.py's HIP-event figure.
 With --pmc-fetch/--pmc-write (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs, separate passes) the
 per-launch HBM traffic of that kernel is added, FETCH_SIZE doubled per the gfx950 correction in
 MI355X_MICROARCH.md §HBM (wide coalesced reads are tallied at half their bytes).
@@ -17,6 +17,12 @@ import json
 import os
 import sqlite3
 from collections import defaultdict
+
+
+def is_decode_linear(name):
+    """bench.py's roofline kernel family: the bf16 decode GEMVs (gemv_kernel QM = 0, rowgemv_kernel)."""
+    return (name.startswith("void gemv_kernel") and re.search(r", 0>\(", name) is not None) or \
+        name.startswith("void rowgemv_kernel")
 
 
 def load_dispatches(path):
@@ -77,9 +83,9 @@ def main():
         by[name][1] += ns
     total = sum(v[1] for v in by.values())
     rows = sorted(by.items(), key=lambda kv: -kv[1][1])
-    # the bench's roofline kernel is the bf16 decode GEMV: gemv_kernel<..., QM = 0> (the int8 / int4
-    # legs' instantiations end in 1> / 2> and are reported apart)
-    gemv = [(n, ns) for n, ns, _ in d if n.startswith("void gemv_kernel") and re.search(r", 0>\(", n)]
+    # the bench's roofline kernel is the bf16 decode linear: gemv_kernel<..., QM = 0> (the int8 / int4
+    # legs' instantiations end in 1> / 2> and are reported apart) and the row-block rowgemv_kernel
+    gemv = [(n, ns) for n, ns, _ in d if is_decode_linear(n)]
     g_n = len(gemv)
     g_avg_us = sum(ns for _, ns in gemv) / max(g_n, 1) / 1e3
     summary = {"trace": os.path.basename(a.trace), "total_kernel_ms": total / 1e6,
@@ -95,13 +101,13 @@ def main():
             summary["gemv_kernel"]["bench_event_avg_us"] = bench["roofline"]["avg_launch_us"]
     if a.pmc_fetch:
         f = load_pmc(a.pmc_fetch, "FETCH_SIZE")
-        fv = [v for n, vs in f.items() if n.startswith("void gemv_kernel") and re.search(r", 0>\(", n) for v in vs]
+        fv = [v for n, vs in f.items() if is_decode_linear(n) for v in vs]
         if fv:
             # rocprofv3 reports FETCH_SIZE in KB; x2 = gfx950 wide-read correction
             summary["gemv_kernel"]["fetch_bytes_per_launch"] = 2 * 1024 * sum(fv) / len(fv)
     if a.pmc_write:
         w = load_pmc(a.pmc_write, "WRITE_SIZE")
-        wv = [v for n, vs in w.items() if n.startswith("void gemv_kernel") and re.search(r", 0>\(", n) for v in vs]
+        wv = [v for n, vs in w.items() if is_decode_linear(n) for v in vs]
         if wv:
             summary["gemv_kernel"]["write_bytes_per_launch"] = 1024 * sum(wv) / len(wv)
     g = summary["gemv_kernel"]
@@ -122,12 +128,13 @@ def main():
         fh.write("| % time | launches | avg us | total ms | kernel |\n|---:|---:|---:|---:|---|\n")
         for name, (n, ns) in rows[:30]:
             fh.write(f"| {100 * ns / total:.1f} | {n} | {ns / n / 1e3:.2f} | {ns / 1e6:.1f} | `{short(name)}` |\n")
-        fh.write(f"\n`gemv_kernel` (bf16 instantiations, QM = 0): {g_n} launches, average {g_avg_us:.3f} us")
+        fh.write(f"\ndecode linears (`gemv_kernel` bf16 instantiations, QM = 0, and `rowgemv_kernel`): {g_n} "
+                 f"launches, average {g_avg_us:.3f} us")
         if bench:
             fh.write(f"; bench.py HIP-event average in the same run: {bench['roofline']['avg_launch_us']} us")
         fh.write("\n")
         if "hbm_bytes_per_launch" in g:
-            fh.write(f"\nPMC (separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes): per gemv_kernel launch "
+            fh.write(f"\nPMC (separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes): per decode-linear launch "
                      f"{g['fetch_bytes_per_launch'] / 1e6:.2f} MB fetched (FETCH_SIZE KB x1024 x2, gfx950 "
                      f"wide-read correction) + {g['write_bytes_per_launch'] / 1e6:.3f} MB written = "
                      f"{g['hbm_bytes_per_launch'] / 1e6:.2f} MB HBM traffic\n")

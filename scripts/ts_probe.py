@@ -20,7 +20,8 @@ for kv in sys.argv[2:]:
 cfg = DualARConfig._from_fish_qwen3_omni(S2_PRO_CONFIG)
 cfg.im_end_id = S2_PRO_IM_END_ID
 cfg.max_seq_len = 1024
-m = DualARModel.synthetic(cfg, seed=0, log2_half=5, device=0, precision="bf16", max_slots=1)
+quant = os.environ.get("TS_QUANT") or None  # int8 / int4 weight-only linears
+m = DualARModel.synthetic(cfg, seed=0, log2_half=5, device=0, precision="bf16", max_slots=1, quant=quant)
 p = np.zeros((cfg.num_codebooks + 1, 64), np.int32)
 p[0] = np.random.default_rng(1).integers(16, cfg.semantic_begin_id, 64)
 m.prefill(0, p, DualARModel.sampling(mask_im_end=True))
@@ -48,6 +49,21 @@ for tag, name, labels in ((0xFFFE, "fast_attn2", ("load", "prep", "scores", "pv+
         aux = a[:, 0].astype(np.int64) & 0xFFFFFFFF
         print(f"{name} phases (us):", " ".join(f"{l} {v:.2f}" for l, v in zip(labels, d)),
               "| blocks", len(a), "aux mean", round(float(aux.mean()), 1))
+rg = rec[(rec[:, 0] >> 32) == 0xFFFA].astype(np.float64)
+if len(rg):
+    # row-pair GEMV (fm_rowgemv.hip): launches split at gaps > 5 us between block starts
+    st = rg[np.argsort(rg[:, 1])]
+    cut = np.where(np.diff(st[:, 1]) > 500)[0] + 1
+    spans, blk, strm = [], [], []
+    for g in np.split(st, cut):
+        spans.append((g[:, 3].max() - g[:, 1].min()) / 100)
+        blk.append(np.mean(g[:, 3] - g[:, 1]) / 100)
+        strm.append(np.mean(g[:, 2] - g[:, 1]) / 100)
+    n = np.array([len(g) for g in np.split(st, cut)])
+    for nb in sorted(set(n.tolist())):
+        sel = n == nb
+        print(f"rowgemv {nb} blocks x {sel.sum()} launches: span {np.mean(np.array(spans)[sel]):.2f} us, "
+              f"block {np.mean(np.array(blk)[sel]):.2f} us (loads+dots {np.mean(np.array(strm)[sel]):.2f})")
 cmb = rec[(rec[:, 0] >> 32) == 0xFFFB].astype(np.float64)
 fd = rec[(rec[:, 0] >> 32) == 0xFFFC].astype(np.float64)
 if len(cmb) and len(fd):

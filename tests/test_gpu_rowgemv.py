@@ -1,0 +1,142 @@
+"""The batch-1 row-block GEMV (fm_rowgemv.hip: wo / w2 with the residual epilogue, wqkv with the
+RMSNorm prologue; fm_tune rowgemv bits 0 / 1) against the reference goldens at S2-Pro shapes and
+against the 16-row MFMA tile path on a model with qkv / o biases.  Run on the MI355X box:
+pytest -m gpu."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from parity_util import bf16_vs_golden
+
+pytestmark = pytest.mark.gpu
+
+IM_END = 4
+ROW_TAG = 0xFFFA  # fm_rowgemv.hip's debug_ts record tag
+
+
+@pytest.fixture
+def rowgemv_mode():
+    from fishmi import native
+
+    yield lambda v: native.tune("rowgemv", v)
+    native.tune("rowgemv", 3)
+
+
+def _row_blocks_ran(m, step):
+    """Number of row-GEMV block records of one eager step (debug_ts): proves the path ran."""
+    from fishmi import native
+
+    m.use_graph(False)
+    native.tune("debug_ts", 1)
+    try:
+        step()
+        rec = native.debug_ts_read().astype(np.int64)
+    finally:
+        native.tune("debug_ts", 0)
+        m.use_graph(True)
+    return int(((rec[:, 0] >> 32) == ROW_TAG).sum())
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_rowgemv_full_depth_bf16_vs_reference(golden, rowgemv_mode, mode):
+    """Config 2 at full depth (36 + 4 layers, S2-Pro shapes), graph-replayed frames, with wo / w2
+    (bit 0), wqkv (bit 1) or both on the row-block GEMV: within the bf16 bound of the reference."""
+    from fishmi.config import DualARConfig
+    from fishmi.llm import DualARModel
+
+    rowgemv_mode(mode)
+    g = golden("llm_full_bf16.npz")
+    cfg = DualARConfig._from_fish_qwen3_omni(json.loads(str(g["config"])))
+    cfg.im_end_id = IM_END
+    m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 1)
+    try:
+        T = g["prompt"].shape[1]
+        slow, fast = m.teacher_decode(g["prompt"], g["seq"][:, T:])
+        m.prefill(0, g["prompt"], DualARModel.sampling(top_k=1))
+        nrec = _row_blocks_ran(m, lambda: m.decode([0]))
+    finally:
+        m.close()
+    # per frame: wo + w2 of 36 slow layers and 10 x 4 fast layers at 1280 blocks each (bit 0);
+    # wqkv of 35 slow + 10 x 3 fast layers at 768 blocks (bit 1; first layers keep their gather)
+    want = (1280 * 2 * (36 + 40) if mode & 1 else 0) + (768 * (35 + 30) if mode & 2 else 0)
+    assert nrec == want, (nrec, want)
+    st = bf16_vs_golden(slow, fast, g, rows=g["slow_rows"])
+    assert st["top1_checked"] >= 9
+
+
+def _biased_cfg():
+    """llm_b's layout (qkv and o biases, no qk-norm, untied head) at widths the row path takes."""
+    from conftest import GOLDEN
+    from fishmi.config import DualARConfig
+
+    c = json.load(open(os.path.join(GOLDEN, "llm_b", "config.json")))
+    c.update(dim=512, n_head=8, n_local_heads=2, head_dim=64, intermediate_size=1024, n_layer=2,
+             max_seq_len=96)
+    c = {k: v for k, v in c.items() if k in DualARConfig.__dataclass_fields__}
+    for k in ("fast_dim", "fast_n_head", "fast_n_local_heads", "fast_head_dim", "fast_intermediate_size"):
+        c.pop(k, None)
+    cfg = DualARConfig(**c)
+    cfg.im_end_id = IM_END
+    return cfg
+
+
+def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
+    """Teacher-forced frames of a biased model, row-block GEMV (rowgemv 3) vs the 16-row MFMA tiles
+    (rowgemv 0): logits agree to bf16 rounding-order level (relative RMS < 2e-2, argmax equal where
+    the margin is clear), the row path really ran, and its graph replay equals its eager frame bit
+    for bit."""
+    from fishmi.llm import DualARModel
+
+    cfg = _biased_cfg()
+    m = DualARModel.synthetic(cfg, 11, 5, 0, "bf16", 2)
+    rng = np.random.default_rng(3)
+    C1 = cfg.num_codebooks + 1
+    prompt = np.zeros((C1, 12), np.int32)
+    prompt[0] = rng.integers(16, cfg.semantic_begin_id, 12)
+    cols = np.zeros((C1, 6), np.int32)
+    cols[0] = rng.integers(cfg.semantic_begin_id, cfg.semantic_end_id + 1, 6)
+    cols[1:] = rng.integers(0, cfg.codebook_size, (C1 - 1, 6))
+    sp = DualARModel.sampling(top_k=1)
+    try:
+        out = {}
+        for slot, mode in ((0, 0), (1, 3)):
+            rowgemv_mode(mode)
+            sl, fl = [], []
+            for k in range(cols.shape[1]):
+                m.force(slot, cols[:, k])
+                if k == 0:
+                    m.prefill(slot, prompt, sp)
+                else:
+                    m.decode([slot])
+                s, f = m.read_logits(slot)
+                sl.append(s)
+                fl.append(f)
+            out[mode] = (np.stack(sl), np.stack(fl))
+        for a, b in zip(out[0], out[3]):
+            fin = np.isfinite(a)  # (the constrained head's masked rows are -inf in both)
+            assert np.array_equal(fin, np.isfinite(b))
+            rel = np.sqrt(np.mean((a[fin] - b[fin]) ** 2)) / np.sqrt(np.mean(a[fin] ** 2))
+            assert rel < 2e-2, rel
+            srt = np.sort(a, axis=-1)
+            clear = (srt[..., -1] - srt[..., -2]) > 0.1
+            assert np.array_equal(np.argmax(a, -1)[clear], np.argmax(b, -1)[clear])
+        rowgemv_mode(3)
+        m.force(1, cols[:, 1])
+        assert _row_blocks_ran(m, lambda: m.decode([1])) > 0
+        res = {}
+        for graph in (False, True):
+            m.use_graph(graph)
+            m.force(0, cols[:, 0])
+            m.prefill(0, prompt, sp)
+            m.force(0, cols[:, 1])
+            m.decode([0])
+            res[graph] = m.read_logits(0)
+        for a, b in zip(res[False], res[True]):
+            np.testing.assert_array_equal(a, b)
+    finally:
+        for s in (0, 1):
+            m.force(s, None)
+        m.use_graph(True)
+        m.close()
