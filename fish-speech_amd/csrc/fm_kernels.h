@@ -289,6 +289,9 @@ struct FmTuning {
     int fin8 = 1;            // finalize_norm: all eight K parts' slab loads in one round trip (0: two batches of four)
     int fin_split = 0;       // batched finalize_norm: each row over this many blocks (0 / 1: one block per row)
     int int4_stream = 1;     // weight-only int4: 1 the batch <= 8 GEMVs stream the 4-bit codes, 0 the dequantised bf16 copy
+    int fw_delay = 0;        // fattn_wo: FattnWoArgs::delay
+    int fw_cheap = 0;        // fattn_wo: FattnWoArgs::cheap
+    int fattn_wo = 1;        // 1: batch-1 bf16 fast-model attention + wo as one launch (fm_rowgemv.hip fattn_wo_kernel)
     int rowgemv = 3;         // batch-1 bf16 on the row-block GEMV (fm_rowgemv.hip): bit 0 wo / w2, bit 1 wqkv (0: 16-row MFMA tiles)
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
     int pass_prepare = 0;    // 1: build the persistent pass's weight copy at finalize even with pass_fast 0
@@ -338,6 +341,22 @@ struct RowGemvArgs {
 };
 int rowgemv_u(int K);         // per-wave chunk depth for K (0: not eligible)
 void launch_rowgemv(hipStream_t s, const RowGemvArgs& a, int kind);
+// batch-1 bf16 fast-model attention + wo in one launch (fm_rowgemv.hip fattn_wo_kernel): the
+// attention blocks store their output as tagged words (bf16 << 16 | gen) into xt [nh * hd]; the wo
+// row-pair blocks (RowGemvArgs FIN; its X is unused) poll them.  gen: 1..65535, unique among
+// consecutive launches on the same xt; err: set when a wait timed out.
+struct FattnWoArgs {
+    FastFusedArgs<bf16_t> at;
+    RowGemvArgs wo;
+    uint32_t* xt;
+    int gen;
+    int* err;
+    int delay;                // wo blocks wait this many 10-ns ticks before their weight loads (fm_tune fw_delay)
+    int cheap;                // 1: poll one word per 32-element group before the full read (fm_tune fw_cheap)
+    unsigned long long* dbg;  // developer records (launcher: fm_tune debug_ts)
+};
+bool fattn_wo_ok(int nh, int nkv, int hd, int cpos, int N, int K);
+void launch_fattn_wo(hipStream_t s, const FattnWoArgs& a);
 // batch-1 GEMV chain (fm_gemv.hip gemv_chain_kernel): 2..GEMV_CHAIN_MAX dependent GEMVs in one launch,
 // whole K per block, one row.  Stage kinds: wo / w2 (PRO_PLAIN, EPI_SLABFIN; the residual may be a
 // gathered row), w1||w3 (PRO_PRENORM, EPI_SWIGLU8), qkv (PRO_PRENORM, EPI_STORE), and as the last

@@ -193,6 +193,7 @@ struct fm_llm {
     std::map<const void*, void*> rowmajor;  // packed wo / w2 -> their row-major bf16 copy (row-pair GEMV)
     bool row_ok = false;                    // every layer of both stacks has wo / w2 row-major
     bool row_qkv_ok = false;                //                         ... and wqkv
+    uint32_t* fxt = nullptr;                // fused fast attention + wo: tagged attention words [nh * hd]
     const QInfo* qinfo(const void* W) const {
         auto it = qmap.find(W);
         return it == qmap.end() ? nullptr : &it->second;
@@ -803,6 +804,9 @@ template <typename T> struct Run {
         // fast model: attention recomputed by every block of the Wo GEMV (PRO_FATT, one row) --
         // no attention launch (fm_tune attn_wo; measured slower, kept under test)
         const bool rf = row_fin(n);
+        // fast model, batch 1: attention and wo as one launch (fm_rowgemv.hip fattn_wo_kernel)
+        const bool fw = is_fast && rf && fm_tuning().fattn_wo && m->fxt && m->fdm.n_layer * m->C >= 2 &&
+                        fattn_wo_ok(d.nh, d.nkv, d.hd, cpos, d.dim, d.nq());
         const bool att_wo = is_fast && fm_tuning().attn_wo && !m->quant && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
                             d.hd <= 128 && d.nh % d.nkv == 0 && (d.nq() / kp.wo) % d.hd == 0 && d.nqkv() % 8 == 0;
         // QKV (+ attention_norm)
@@ -879,7 +883,7 @@ template <typename T> struct Run {
             auto go = [st, aa, n] { attn_slow_on(st, aa, n); };
             m->prof.record("attn_slow", 0, go);  // the slow model's launches alone (fm_llm_kernel_bench)
             run_rec("attn", go);
-        } else if (!att_wo) {
+        } else if (!att_wo && !fw) {
             hipStream_t st = s;
             const bool f2 = cpos < 16 && d.hd <= 256;
             run_rec("attn", [st, fa, n, f2] {
@@ -890,7 +894,39 @@ template <typename T> struct Run {
             });
         }
         // wo, split-K; the last block of each tile finalises h = x + wo(att) and its sums of squares
-        if (rf) {
+        if (fw) {
+            FattnWoArgs A{};
+            A.at = *reinterpret_cast<const FastFusedArgs<bf16_t>*>(&fa);
+            A.at.dbg = nullptr;
+            RowGemvArgs& r = A.wo;
+            r.W = (const bf16_t*)L.wo_rm;
+            r.X = (const bf16_t*)m->att;  // (unused: x comes from the tagged words)
+            r.bias = (const bf16_t*)L.bo;
+            if (first) {
+                r.res = (const bf16_t*)x_in;
+                r.ldr = ldx_in;
+                r.residx = xidx;
+                r.res_col = xcol;
+                r.res_rows = xidx ? m->cb : 0;
+            } else {
+                r.res = (const bf16_t*)xb;
+                r.ldr = d.dim;
+            }
+            r.res_out = (bf16_t*)hb;
+            r.N = d.dim;
+            r.K = d.nq();
+            A.xt = m->fxt;
+            A.gen = 1 + layer + m->fdm.n_layer * cpos;
+            A.err = m->chain_err;
+            A.delay = fm_tuning().fw_delay;
+            A.cheap = fm_tuning().fw_cheap;
+            chain_flush();
+            const int64_t bytes = (int64_t)r.N * r.K * 2;
+            hipStream_t st = s;
+            auto go = [st, A] { launch_fattn_wo(st, A); };
+            m->prof.record("attn_wo", bytes, go);  // (not "linear": attention + GEMV, reported apart)
+            m->prof.run(s, "attn", bytes, 2.0 * r.N * r.K, go);
+        } else if (rf) {
             RowGemvArgs r{};
             r.W = (const bf16_t*)L.wo_rm;
             r.X = (const bf16_t*)m->att;
@@ -1705,6 +1741,8 @@ static void finalize(fm_llm* m) {
     };
     stack("layers.", m->sd, m->slow);
     stack("fast_layers.", m->fdm, m->fast);
+    if (m->prec == FM_PREC_BF16 && !m->quant)
+        m->fxt = (uint32_t*)m->dalloc((size_t)m->fdm.nh * m->fdm.hd * sizeof(uint32_t));  // tags 0: never current
     m->row_ok = m->row_qkv_ok = true;
     for (auto* st : {&m->slow, &m->fast})
         for (const LayerW& L : *st) {
@@ -1927,7 +1965,8 @@ static void upload_frame_rows(fm_llm* m, const int32_t* slots, int n) {
 // gemv chain health: the error word travels to pinned memory behind the frames; after the
 // host's stream sync, a timed-out hand-off wait (a hang avoided) resets the counters and fails
 static void chain_err_async(fm_llm* m) {
-    if (fm_tuning().gemv_chain || (m->pass_ok && fm_tuning().pass_fast) || fm_tuning().fin_split > 1)
+    if (fm_tuning().gemv_chain || (m->pass_ok && fm_tuning().pass_fast) || fm_tuning().fin_split > 1 ||
+        (m->fxt && fm_tuning().fattn_wo))
         HIPCHK(hipMemcpyAsync(m->h_chain_err, m->chain_err, sizeof(int), hipMemcpyDeviceToHost, m->stream));
 }
 static void chain_err_check(fm_llm* m) {
@@ -1937,7 +1976,8 @@ static void chain_err_check(fm_llm* m) {
     HIPCHK(hipMemset(m->chain_err, 0, 16 * sizeof(int)));
     if (m->fin_cnt) HIPCHK(hipMemset(m->fin_cnt, 0, (size_t)std::max(m->max_slots, 64) * 2 * sizeof(int)));
     throw FmError{FM_ERR_STATE,
-                  "in-launch hand-off wait timed out (gemv chain / persistent pass / split finalize; counters reset)"};
+                  "in-launch hand-off wait timed out (gemv chain / persistent pass / split finalize / fused fast "
+                  "attention + wo; counters reset)"};
 }
 
 // one decode frame for the uploaded rows (graph replay when enabled), async
@@ -2575,6 +2615,13 @@ int fm_tune(const char* key, int value) {
             t.int4_stream = value != 0;
         } else if (k == "pass_fast") {
             t.pass_fast = value != 0;
+        } else if (k == "fw_delay") {
+            FMCHECK(value >= 0 && value <= 1000, "fw_delay must be 0..1000 (10-ns ticks)");
+            t.fw_delay = value;
+        } else if (k == "fw_cheap") {
+            t.fw_cheap = value != 0;
+        } else if (k == "fattn_wo") {
+            t.fattn_wo = value != 0;
         } else if (k == "rowgemv") {
             FMCHECK(value >= 0 && value <= 3, "rowgemv must be 0..3 (bit 0 wo / w2, bit 1 wqkv)");
             t.rowgemv = value;

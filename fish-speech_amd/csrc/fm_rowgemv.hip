@@ -42,6 +42,11 @@ __device__ __forceinline__ float dot4(u32x2_t w, u32x2_t x, float acc) {
 }
 __device__ __forceinline__ float lo16(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi16(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ void ld_pair_bf(const bf16_t* p, float& x0, float& x1) {
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
+    x0 = lo16(w);
+    x1 = hi16(w);
+}
 
 // G: the residual row is gathered (residx; the fast model's first layer), whose index load the
 // residual load must wait for -- the compiler hoists that pair ahead of the weight loads (one round
@@ -223,5 +228,293 @@ void launch_rowgemv(hipStream_t s, const RowGemvArgs& a0, int kind) {
     } else {
         FMCHECK(kind == ROWGEMV_NORM_STORE && a.N % 8 == 0 && a.nw && a.Y, "row GEMV (norm, store): N % 8 == 0, norm weight and output set");
         rowgemv_go<8, true, false>(s, a, U);
+    }
+}
+
+// =========================================================================================
+// Fast-model attention + wo in ONE launch (batch 1, bf16; fm_tune fattn_wo).
+//
+// The fast model's attention (llama.py:947-975, one query row at codebook position cpos < 16) is
+// latency-bound: ~4 us of dependent round trips on 32 of 256 CUs, while the wo GEMV that consumes
+// it is a 21 MB weight stream.  Here blocks 0 .. nkv-1 run the attention (one block per kv group,
+// one wave per q head, cached K / V rows staged in LDS) and blocks nkv .. nkv + N/2 - 1 are the
+// row-pair wo blocks of rowgemv_kernel, which issue their whole weight run first and only then
+// wait for the attention output.  The hand-off has no counters and no fences: each attention
+// output element is stored write-through (sc1) as one 32-bit word (bf16 value << 16 | gen), gen a
+// tag unique among consecutive launches (host: 1 + layer + n_layer * cpos), and a wo wave re-reads
+// its x words (sc1 loads) until every tag is current.  Deadlock-free by dispatch order: the
+// attention blocks have the lowest indices, so they are resident before any waiting block, and the
+// whole grid fits at once (<= 8 blocks of 4 waves per CU, 10 KiB LDS each).  Every wait is bounded
+// (FattnWoArgs::err set on timeout; the host throws and resets).
+constexpr int FW_MAXJ = 15;   // cached rows staged in LDS (cpos < 16)
+constexpr int FW_MAXHD = 128;
+
+template <int U, bool G>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6)))
+void fattn_wo_kernel(FattnWoArgs A) {
+    __shared__ __attribute__((aligned(16))) bf16_t kvs[2 * FW_MAXJ * FW_MAXHD];
+    __shared__ float red[8];
+    const FastFusedArgs<bf16_t>& at = A.at;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t gen = (uint32_t)A.gen;
+    const unsigned long long ts0 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    if ((int)blockIdx.x < at.nkv) {
+        // ---------------- attention: kv group kvh, q head kvh * g + wave ----------------------
+        const int kvh = blockIdx.x, hd = at.hd, g = at.nh / at.nkv, cpos = at.cpos, half = hd >> 1;
+        const int slot = at.row_slot[0];
+        const bool live = wave < g;
+        const int h = kvh * g + (live ? wave : 0);
+        const float* tab = at.rope + (size_t)cpos * hd;
+        float q0[2], q1[2], k0[2], k1[2], v0[2], v1[2], qw0[2], qw1[2], kw0[2], kw1[2], c_[2], s_[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            const int pp = p < half ? p : 0;
+            ld_pair_bf(at.qkv + (size_t)h * hd + 2 * pp, q0[u], q1[u]);
+            ld_pair_bf(at.qkv + (size_t)(at.nh + kvh) * hd + 2 * pp, k0[u], k1[u]);
+            ld_pair_bf(at.qkv + (size_t)(at.nh + at.nkv + kvh) * hd + 2 * pp, v0[u], v1[u]);
+            if (at.qk_norm) {
+                ld_pair_bf(at.qn + 2 * pp, qw0[u], qw1[u]);
+                ld_pair_bf(at.kn + 2 * pp, kw0[u], kw1[u]);
+            } else {
+                qw0[u] = qw1[u] = kw0[u] = kw1[u] = 1.f;
+            }
+            c_[u] = tab[2 * pp];
+            s_[u] = tab[2 * pp + 1];
+            if (p >= half) q0[u] = q1[u] = k0[u] = k1[u] = v0[u] = v1[u] = 0.f;
+        }
+        // the cached rows j < cpos of this kv head -> LDS (K rows, then V rows), 16 B per thread
+        const size_t base = (size_t)slot * at.slot_stride + at.layer_off + (size_t)kvh * at.S * hd;
+        const int nck = cpos * hd / 8;
+        for (int i = threadIdx.x; i < 2 * nck; i += 256) {
+            const bool isv = i >= nck;
+            const int c = isv ? i - nck : i;
+            const u32x4_t v = *reinterpret_cast<const u32x4_t*>((isv ? at.vc : at.kc) + base + (size_t)c * 8);
+            *reinterpret_cast<u32x4_t*>(kvs + (isv ? FW_MAXJ * FW_MAXHD : 0) + c * 8) = v;
+        }
+        // qk-norm (fp32 incl. weight, one rounding) + RoPE (bf16 table, rounded): fm_attn_dev.h
+        auto prep = [&](float (&x0)[2], float (&x1)[2], const float (&w0)[2], const float (&w1)[2]) {
+            if (at.qk_norm) {
+                float ss = 0.f;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) ss += x0[u] * x0[u] + x1[u] * x1[u];
+                ss = wave_sum(ss);
+                const float rs = 1.0f / sqrtf(ss / (float)hd + at.eps);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    x0[u] = bfround((x0[u] * rs) * w0[u]);
+                    x1[u] = bfround((x1[u] * rs) * w1[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const float y0 = bfround(x0[u] * c_[u] - x1[u] * s_[u]);
+                const float y1 = bfround(x1[u] * c_[u] + x0[u] * s_[u]);
+                x0[u] = y0;
+                x1[u] = y1;
+            }
+        };
+        prep(q0, q1, qw0, qw1);
+        prep(k0, k1, kw0, kw1);
+        if (wave == 0) {  // the group's new k / v of cpos into the fast cache
+            bf16_t* kd = at.kc + base + (size_t)cpos * hd;
+            bf16_t* vd = at.vc + base + (size_t)cpos * hd;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int p = lane + 64 * u;
+                if (p < half) {
+                    *reinterpret_cast<uint32_t*>(kd + 2 * p) = (uint32_t)f2bf(k0[u]) | ((uint32_t)f2bf(k1[u]) << 16);
+                    *reinterpret_cast<uint32_t*>(vd + 2 * p) = (uint32_t)f2bf(v0[u]) | ((uint32_t)f2bf(v1[u]) << 16);
+                }
+            }
+        }
+        __syncthreads();  // K / V rows staged
+        const unsigned long long ts1 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+        if (!live) return;
+        const bf16_t* Ks = kvs;
+        const bf16_t* Vs = kvs + FW_MAXJ * FW_MAXHD;
+        // scores round(round(q.k) * scale), softmax, probabilities rounded (fast SDPA path)
+        float sc[FW_MAXJ + 1];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j <= FW_MAXJ; ++j) {
+            if (j > cpos) break;
+            float d = 0.f;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int p = lane + 64 * u;
+                const int pp = p < half ? p : 0;
+                float a0 = k0[u], a1 = k1[u];
+                if (j < cpos) {
+                    const uint32_t w = *reinterpret_cast<const uint32_t*>(Ks + j * hd + 2 * pp);
+                    a0 = p < half ? lo16(w) : 0.f;
+                    a1 = p < half ? hi16(w) : 0.f;
+                }
+                d += q0[u] * a0 + q1[u] * a1;
+            }
+            d = wave_sum(d);
+            sc[j] = bfround(bfround(d) * at.scale);
+            mx = fmaxf(mx, sc[j]);
+        }
+        float den = 0.f;
+#pragma unroll
+        for (int j = 0; j <= FW_MAXJ; ++j) {
+            if (j > cpos) break;
+            sc[j] = expf(sc[j] - mx);
+            den += sc[j];
+        }
+        float o0[2] = {0.f, 0.f}, o1[2] = {0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j <= FW_MAXJ; ++j) {
+            if (j > cpos) break;
+            const float pj = bfround(sc[j] / den);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int p = lane + 64 * u;
+                const int pp = p < half ? p : 0;
+                float b0 = v0[u], b1 = v1[u];
+                if (j < cpos) {
+                    const uint32_t w = *reinterpret_cast<const uint32_t*>(Vs + j * hd + 2 * pp);
+                    b0 = lo16(w);
+                    b1 = hi16(w);
+                }
+                o0[u] += pj * b0;
+                o1[u] += pj * b1;
+            }
+        }
+        // tagged write-through store: word = bf16 << 16 | gen
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int p = lane + 64 * u;
+            if (p < half) {
+                const uint64_t w = (uint64_t)(((uint32_t)f2bf(o0[u]) << 16) | gen) |
+                                   ((uint64_t)(((uint32_t)f2bf(o1[u]) << 16) | gen) << 32);
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(A.xt + (size_t)h * hd + 2 * p), w, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (A.dbg && lane == 0) {  // developer record per attention wave (tag 0xFFF9): start, staged, stored
+            const unsigned long long t[7] = {ts0, ts1, __builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0};
+            dbg_record(A.dbg, 0xFFF9, (unsigned)h, t);
+        }
+        return;
+    }
+    // ---------------- wo rows 2p, 2p + 1 (rowgemv_kernel FIN, x from the tagged words) --------
+    const RowGemvArgs& a = A.wo;
+    const int p = blockIdx.x - at.nkv, n0 = 2 * p;
+    const int nch = a.K >> 8;
+    const int wa = (wave * nch) >> 2, nmy = (((wave + 1) * nch) >> 2) - wa;
+    const int last = nmy > 0 ? nmy - 1 : 0;
+    const int er = n0 + (int)(threadIdx.x & 1);
+    int ri = 0;
+    if constexpr (G) {
+        const int32_t iv = a.residx[a.res_col];
+        ri = iv < 0 ? 0 : (iv >= a.res_rows ? a.res_rows - 1 : iv);
+    }
+    const bf16_t rv = a.res[(size_t)ri * a.ldr + er];
+    const bf16_t bv = *(a.bias ? a.bias + er : a.res);
+    // optional head start for the attention's dependent round trips (FattnWoArgs::delay, 10-ns
+    // ticks): the weight flood otherwise queues ahead of them
+    if (A.delay > 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t < (unsigned long long)A.delay) __builtin_amdgcn_s_sleep(2);
+    }
+    asm volatile("" ::: "memory");
+    const u32x2_t* wp = reinterpret_cast<const u32x2_t*>(a.W + (size_t)n0 * a.K) + (size_t)wa * 64 + lane;
+    const size_t rs4 = (size_t)(a.K >> 2);
+    u32x2_t wv[U][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int j = (u < last ? u : last) * 64;
+        wv[u][0] = __builtin_nontemporal_load(wp + j);
+        wv[u][1] = __builtin_nontemporal_load(wp + rs4 + j);
+    }
+    asm volatile("" ::: "memory");
+    const unsigned long long ts1 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    // x: 4 tagged words per lane per chunk, sc1 loads, re-read until every tag is this launch's
+    // (FattnWoArgs::cheap: first poll one word per 32-element group until all are current)
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)A.xt, (short)0, a.K * 4, 0x00020000);
+    unsigned it = 0;
+    if (A.cheap) {
+        const int span = (last + 1) * 256;  // elements of the wave's run
+        const int pw = wa * 256 + ((lane * 32) % span) + 31;  // the last word of lane's 32-element group
+        for (;; ++it) {
+            const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(xr, pw * 4, 0, 16);
+            if (__all((w & 0xffffu) == gen) || it >= (1u << 14)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    const unsigned long long ts2 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    u32x4_t xw[U];
+    for (;; ++it) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = u < last ? u : last;
+            xw[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, ((wa + j) * 256 + 4 * lane) * 4, 0, 16);
+        }
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ok = ok && ((xw[u][e] & 0xffffu) == gen);
+        if (__all(ok)) break;
+        if (it >= (1u << 14)) {  // bounded: the host sees err and fails the frame
+            if (lane == 0) __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    const unsigned long long ts3 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (u < nmy) {
+            u32x2_t xv;
+            xv[0] = (xw[u][0] >> 16) | (xw[u][1] & 0xffff0000u);
+            xv[1] = (xw[u][2] >> 16) | (xw[u][3] & 0xffff0000u);
+            acc0 = dot4(wv[u][0], xv, acc0);
+            acc1 = dot4(wv[u][1], xv, acc1);
+        }
+    }
+    acc0 = wave_sum(acc0);
+    acc1 = wave_sum(acc1);
+    if (lane == 0) {
+        red[2 * wave] = acc0;
+        red[2 * wave + 1] = acc1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const int t = threadIdx.x;
+        float v = ((red[t] + red[2 + t]) + red[4 + t]) + red[6 + t];
+        if (a.bias) v += bf2f(bv);
+        a.res_out[er] = f2bf(bfround(bf2f(rv) + bfround(v)));
+    }
+    if (A.dbg && threadIdx.x == 0 && (p & 63) == 0) {  // sampled wo block (tag 0xFFF8)
+        const unsigned long long t[7] = {ts0, ts1, ts2, ts3, __builtin_amdgcn_s_memrealtime(), 0, 0};
+        dbg_record(A.dbg, 0xFFF8, it, t);
+    }
+}
+
+bool fattn_wo_ok(int nh, int nkv, int hd, int cpos, int N, int K) {
+    const int U = rowgemv_u(K);
+    return nkv > 0 && nh % nkv == 0 && nh / nkv <= 4 && hd % 2 == 0 && hd <= FW_MAXHD && cpos >= 0 &&
+           cpos < FW_MAXJ + 1 && K == nh * hd && N % 2 == 0 && U > 0 && U <= 8;
+}
+
+void launch_fattn_wo(hipStream_t s, const FattnWoArgs& A0) {
+    FattnWoArgs A = A0;
+    A.dbg = fm_tuning().dbg;
+    const FastFusedArgs<bf16_t>& at = A.at;
+    FMCHECK(fattn_wo_ok(at.nh, at.nkv, at.hd, at.cpos, A.wo.N, A.wo.K) && A.xt && A.err && A.gen > 0 && A.gen < 65536 &&
+                A.wo.res && A.wo.res_out && A.wo.W,
+            "fused fast attention + wo: shapes, tag and buffers");
+    const dim3 grid(at.nkv + A.wo.N / 2), block(256);
+    const bool G = A.wo.residx != nullptr;
+    switch (rowgemv_u(A.wo.K)) {
+#define FW(u) \
+    case u: (G ? fattn_wo_kernel<u, true> : fattn_wo_kernel<u, false>)<<<grid, block, 0, s>>>(A); break;
+        FW(2) FW(3) FW(4) FW(5) FW(6)
+        default: (G ? fattn_wo_kernel<8, true> : fattn_wo_kernel<8, false>)<<<grid, block, 0, s>>>(A); break;
+#undef FW
     }
 }

@@ -13,18 +13,24 @@ from parity_util import bf16_vs_golden
 pytestmark = pytest.mark.gpu
 
 IM_END = 4
-ROW_TAG = 0xFFFA  # fm_rowgemv.hip's debug_ts record tag
+ROW_TAG = 0xFFFA  # fm_rowgemv.hip's debug_ts record tags: row-block GEMV blocks
+FW_TAG = 0xFFF9   # fused fast attention + wo: attention waves
 
 
 @pytest.fixture
 def rowgemv_mode():
     from fishmi import native
 
-    yield lambda v: native.tune("rowgemv", v)
+    def set_(v, fused=1):
+        native.tune("rowgemv", v)
+        native.tune("fattn_wo", fused)
+
+    yield set_
     native.tune("rowgemv", 3)
+    native.tune("fattn_wo", 1)
 
 
-def _row_blocks_ran(m, step):
+def _row_blocks_ran(m, step, tag=ROW_TAG):
     """Number of row-GEMV block records of one eager step (debug_ts): proves the path ran."""
     from fishmi import native
 
@@ -36,17 +42,18 @@ def _row_blocks_ran(m, step):
     finally:
         native.tune("debug_ts", 0)
         m.use_graph(True)
-    return int(((rec[:, 0] >> 32) == ROW_TAG).sum())
+    return int(((rec[:, 0] >> 32) == tag).sum())
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3])
-def test_rowgemv_full_depth_bf16_vs_reference(golden, rowgemv_mode, mode):
+@pytest.mark.parametrize("mode,fused", [(1, 0), (2, 0), (3, 0), (1, 1), (3, 1)])
+def test_rowgemv_full_depth_bf16_vs_reference(golden, rowgemv_mode, mode, fused):
     """Config 2 at full depth (36 + 4 layers, S2-Pro shapes), graph-replayed frames, with wo / w2
-    (bit 0), wqkv (bit 1) or both on the row-block GEMV: within the bf16 bound of the reference."""
+    (bit 0), wqkv (bit 1) or both on the row-block GEMV, the fast model's attention + wo fused or
+    not: within the bf16 bound of the reference."""
     from fishmi.config import DualARConfig
     from fishmi.llm import DualARModel
 
-    rowgemv_mode(mode)
+    rowgemv_mode(mode, fused)
     g = golden("llm_full_bf16.npz")
     cfg = DualARConfig._from_fish_qwen3_omni(json.loads(str(g["config"])))
     cfg.im_end_id = IM_END
@@ -56,12 +63,17 @@ def test_rowgemv_full_depth_bf16_vs_reference(golden, rowgemv_mode, mode):
         slow, fast = m.teacher_decode(g["prompt"], g["seq"][:, T:])
         m.prefill(0, g["prompt"], DualARModel.sampling(top_k=1))
         nrec = _row_blocks_ran(m, lambda: m.decode([0]))
+        m.prefill(0, g["prompt"], DualARModel.sampling(top_k=1))
+        nfw = _row_blocks_ran(m, lambda: m.decode([0]), FW_TAG)
     finally:
         m.close()
-    # per frame: wo + w2 of 36 slow layers and 10 x 4 fast layers at 1280 blocks each (bit 0);
-    # wqkv of 35 slow + 10 x 3 fast layers at 768 blocks (bit 1; first layers keep their gather)
-    want = (1280 * 2 * (36 + 40) if mode & 1 else 0) + (768 * (35 + 30) if mode & 2 else 0)
+    # per frame: wo + w2 of 36 slow layers and 10 x 4 fast layers at 1280 blocks each (bit 0; the
+    # fast wo inside the fused launch when on); wqkv of 35 slow + 10 x 3 fast layers at 768 blocks
+    # (bit 1; first layers keep their gather); fused: 32 attention waves x 40 fast layers
+    fw = fused and (mode & 1)
+    want = (1280 * (2 * 36 + 40 + (0 if fw else 40)) if mode & 1 else 0) + (768 * (35 + 30) if mode & 2 else 0)
     assert nrec == want, (nrec, want)
+    assert nfw == (32 * 40 if fw else 0), nfw
     st = bf16_vs_golden(slow, fast, g, rows=g["slow_rows"])
     assert st["top1_checked"] >= 9
 
@@ -102,7 +114,7 @@ def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
     try:
         out = {}
         for slot, mode in ((0, 0), (1, 3)):
-            rowgemv_mode(mode)
+            rowgemv_mode(mode, 1 if mode else 0)
             sl, fl = [], []
             for k in range(cols.shape[1]):
                 m.force(slot, cols[:, k])
@@ -122,9 +134,11 @@ def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
             srt = np.sort(a, axis=-1)
             clear = (srt[..., -1] - srt[..., -2]) > 0.1
             assert np.array_equal(np.argmax(a, -1)[clear], np.argmax(b, -1)[clear])
-        rowgemv_mode(3)
+        rowgemv_mode(3, 1)
         m.force(1, cols[:, 1])
         assert _row_blocks_ran(m, lambda: m.decode([1])) > 0
+        m.force(1, cols[:, 2])
+        assert _row_blocks_ran(m, lambda: m.decode([1]), FW_TAG) > 0
         res = {}
         for graph in (False, True):
             m.use_graph(graph)
