@@ -26,13 +26,19 @@ def _cfg(g):
 
 @pytest.fixture
 def chain():
+    """gemv_chain on / off against the 16-row tile launch chain it replaces: the row-block GEMVs
+    (rowgemv) and the fused fast attention + wo (fattn_wo) are off in both runs."""
     from fishmi import native
 
     def put(on):
         native.tune("gemv_chain", int(on))
 
+    native.tune("rowgemv", 0)
+    native.tune("fattn_wo", 0)
     yield put
     native.tune("gemv_chain", 0)
+    native.tune("rowgemv", 3)
+    native.tune("fattn_wo", 1)
 
 
 def _prompt(cfg, T, seed):
