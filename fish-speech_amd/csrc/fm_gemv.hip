@@ -842,8 +842,7 @@ static void gemv_go_q4(hipStream_t s, const GemvArgs<T>& a, int ksb) {
 template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int pro, int epi, int ksb) {
     // PRO_PRENORM stages the [K/16][R] tile sums in the 256 * R floats of the reduction buffer
     FMCHECK(pro != PRO_PRENORM || (a.K <= 4096 && a.R <= GEMV_RMAX), "PRO_PRENORM needs K <= 4096, R <= 8");
-    FMCHECK(pro != PRO_PRENORM || (a.ss_in && (a.ss_gran != 1 || (a.R == 1 && ksb == 1 && !a.Wq &&
-                                                                   a.K <= 3 * 8 * 256))),
+    FMCHECK(pro != PRO_PRENORM || (a.ss_in && (a.ss_gran != 1 || (a.R == 1 && ksb == 1 && a.K <= 3 * 8 * 256))),
             "PRO_PRENORM: ss_in set (also with ss_gran 1: one row, whole K staged)");
     FMCHECK(pro != PRO_FATT || (a.R == 1 && a.att.cpos < FAST_ATTN_MAXJ && a.att.cpos < a.att.S &&
                                 (a.K / ksb) % a.att.hd == 0 && a.att.hd % 16 == 0 && a.att.hd <= 16 * FATT_MAXPP &&

@@ -276,6 +276,8 @@ struct FmTuning {
     int gemv_dummy = 2;
     int bs_qkv_slab = 1;     // batched frames: QKV as K-part slabs summed by the attention (balanced
                              // grid: 384 tiles x 2 K parts over 256 CUs; B=32 frame 6.48 -> 6.33 ms)
+    int fast_tail = 1;       // 1: codebook 0's fast pass stops its last layer after the K / V cache write (its output is discarded)
+    int fkv_prefetch = 0;    // 1: the batch-1 fast-model QKV GEMV pulls the fast attention's cached rows into L2 too
     int kv_prefetch = 1;     // 1: the batch-1 QKV GEMV pulls the next attention's K / V rows into L2
     int bstream_chain = 0;   // 1: bsacc SLABFIN / PRENORM chain instead of finalize_norm launches (measured 6.31 -> 6.75 ms per B=32 frame)
     int bstream_acc = 1;     // 1: bsacc_kernel (per-tile register accumulators, one reduction at the end, balanced K parts); 0: bstream_kernel
@@ -291,6 +293,7 @@ struct FmTuning {
     int int4_stream = 1;     // weight-only int4: 1 the batch <= 8 GEMVs stream the 4-bit codes, 0 the dequantised bf16 copy
     int fw_delay = 0;        // fattn_wo: FattnWoArgs::delay
     int fw_cheap = 0;        // fattn_wo: FattnWoArgs::cheap
+    int fw_prio = 0;         // fattn_wo: FattnWoArgs::prio
     int fattn_wo = 1;        // 1: batch-1 bf16 fast-model attention + wo as one launch (fm_rowgemv.hip fattn_wo_kernel)
     int rowgemv = 3;         // batch-1 bf16 on the row-block GEMV (fm_rowgemv.hip): bit 0 wo / w2, bit 1 wqkv (0: 16-row MFMA tiles)
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
@@ -320,6 +323,8 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
 enum { ROWGEMV_FIN = 0, ROWGEMV_NORM_STORE = 1 };
 struct RowGemvArgs {
     const bf16_t* W;
+    const int8_t* Wq;         // weight-only int8 (instead of W): row-major codes, output round(round(acc) * wscale)
+    const bf16_t* wscale;     // int8: per-row scales [N]
     const bf16_t* X;          // [K]
     const bf16_t* bias;       // [N] or null
     const bf16_t* nw;         // NORM: norm weight [K]
@@ -339,7 +344,7 @@ struct RowGemvArgs {
     int pf_S, pf_nkv, pf_hd;
     unsigned long long* dbg;  // developer timestamps (launcher: fm_tune debug_ts)
 };
-int rowgemv_u(int K);         // per-wave chunk depth for K (0: not eligible)
+int rowgemv_u(int K, int qm);  // per-wave chunk depth for K (qm 1: int8 codes; 0: not eligible)
 void launch_rowgemv(hipStream_t s, const RowGemvArgs& a, int kind);
 // batch-1 bf16 fast-model attention + wo in one launch (fm_rowgemv.hip fattn_wo_kernel): the
 // attention blocks store their output as tagged words (bf16 << 16 | gen) into xt [nh * hd]; the wo
@@ -353,6 +358,7 @@ struct FattnWoArgs {
     int* err;
     int delay;                // wo blocks wait this many 10-ns ticks before their weight loads (fm_tune fw_delay)
     int cheap;                // 1: poll one word per 32-element group before the full read (fm_tune fw_cheap)
+    int prio;                 // 1: attention waves at s_setprio 3 (fm_tune fw_prio)
     unsigned long long* dbg;  // developer records (launcher: fm_tune debug_ts)
 };
 bool fattn_wo_ok(int nh, int nkv, int hd, int cpos, int N, int K);

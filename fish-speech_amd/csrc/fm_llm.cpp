@@ -190,10 +190,11 @@ struct fm_llm {
         const uint32_t* sz = nullptr;       // int4: packed (scale, zero) per (tile, 128-k unit, row)
     };
     std::map<const void*, QInfo> qmap;
-    std::map<const void*, void*> rowmajor;  // packed wo / w2 -> their row-major bf16 copy (row-pair GEMV)
+    std::map<const void*, void*> rowmajor;  // packed wo / w2 / wqkv -> row-major bf16 copy (int8: codes)
     bool row_ok = false;                    // every layer of both stacks has wo / w2 row-major
     bool row_qkv_ok = false;                //                         ... and wqkv
     uint32_t* fxt = nullptr;                // fused fast attention + wo: tagged attention words [nh * hd]
+    int32_t* fiota = nullptr;               // [16]: fiota[c] = c - 1 (the fast KV prefetch's last cached row)
     const QInfo* qinfo(const void* W) const {
         auto it = qmap.find(W);
         return it == qmap.end() ? nullptr : &it->second;
@@ -751,11 +752,12 @@ template <typename T> struct Run {
     // ... and wqkv (norm prologue, 8 rows per block)
     bool row_qkv(int n) const {
         const FmTuning& t = fm_tuning();
-        return sizeof(T) == 2 && n == 1 && m->row_qkv_ok && (t.rowgemv & 2) && !t.gemv_chain;
+        // (int8: the tile kernel's wqkv measured as fast, 3.12 vs 3.14 ms per frame)
+        return sizeof(T) == 2 && n == 1 && m->row_qkv_ok && !m->quant && (t.rowgemv & 2) && !t.gemv_chain;
     }
     void rowgemv(const RowGemvArgs& a, int kind) {
         chain_flush();
-        const int64_t bytes = (int64_t)a.N * a.K * 2 + (int64_t)a.K * 2;
+        const int64_t bytes = (a.Wq ? (int64_t)a.N * a.K + (int64_t)a.N * 2 : (int64_t)a.N * a.K * 2) + (int64_t)a.K * 2;
         hipStream_t st = s;
         auto go = [st, a, kind] { launch_rowgemv(st, a, kind); };
         m->prof.record("linear", bytes, go);
@@ -793,7 +795,7 @@ template <typename T> struct Run {
     // xo: where W2 writes the block's output row (xb itself unless the chain alternates buffers)
     void block_small(const StackDims& d, const LayerW& L, int n, bool first, const void* x_in, int ldx_in,
                      const int32_t* xidx, int xcol, void* xb, void* hb, bool is_fast, int cpos, int layer,
-                     const KsbPlan& kp, void* xo) {
+                     const KsbPlan& kp, void* xo, bool kv_only = false) {
         const int C1 = m->C1;
         const float scale = 1.0f / sqrtf((float)d.hd);
         FastFusedArgs<T> fa{(const T*)m->qkv, d.nqkv(), m->frame_slot, d.nh, d.nkv, d.hd, d.qk_norm,
@@ -804,10 +806,19 @@ template <typename T> struct Run {
         // fast model: attention recomputed by every block of the Wo GEMV (PRO_FATT, one row) --
         // no attention launch (fm_tune attn_wo; measured slower, kept under test)
         const bool rf = row_fin(n);
+        // the row-block GEMV's weight: bf16 row-major, or (weight-only int8) the codes + row scales
+        auto row_w = [&](RowGemvArgs& r, void* rm, const void* packed) {
+            if (m->quant) {
+                r.Wq = (const int8_t*)rm;
+                r.wscale = (const bf16_t*)m->qinfo(packed)->scale;
+            } else {
+                r.W = (const bf16_t*)rm;
+            }
+        };
         // fast model, batch 1: attention and wo as one launch (fm_rowgemv.hip fattn_wo_kernel)
-        const bool fw = is_fast && rf && fm_tuning().fattn_wo && m->fxt && m->fdm.n_layer * m->C >= 2 &&
+        const bool fw = is_fast && !kv_only && rf && !m->quant && fm_tuning().fattn_wo && m->fxt && m->fdm.n_layer * m->C >= 2 &&
                         fattn_wo_ok(d.nh, d.nkv, d.hd, cpos, d.dim, d.nq());
-        const bool att_wo = is_fast && fm_tuning().attn_wo && !m->quant && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
+        const bool att_wo = is_fast && !kv_only && fm_tuning().attn_wo && !m->quant && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
                             d.hd <= 128 && d.nh % d.nkv == 0 && (d.nq() / kp.wo) % d.hd == 0 && d.nqkv() % 8 == 0;
         // QKV (+ attention_norm)
         {
@@ -830,6 +841,17 @@ template <typename T> struct Run {
                 a.pf_S = m->S;
                 a.pf_nkv = d.nkv;
                 a.pf_hd = d.hd;
+            } else if (is_fast && n == 1 && fm_tuning().fkv_prefetch && m->fiota && cpos < 16) {
+                // the fast attention's cached rows 0 .. cpos - 1 (fiota[cpos] = cpos - 1)
+                a.pf_kc = (const T*)m->fkc;
+                a.pf_vc = (const T*)m->fvc;
+                a.pf_slot = m->frame_slot;
+                a.pf_pos = m->fiota + cpos;
+                a.pf_slot_stride = m->fslot_stride;
+                a.pf_layer_off = (size_t)layer * m->flayer_stride;
+                a.pf_S = m->C;
+                a.pf_nkv = d.nkv;
+                a.pf_hd = d.hd;
             }
             const int epi = EPI_STORE;
             if (first) {
@@ -842,7 +864,7 @@ template <typename T> struct Run {
                 gemv(a, PRO_NORM, epi, 1, "linear");
             } else if (row_qkv(n)) {
                 RowGemvArgs r{};
-                r.W = (const bf16_t*)L.wqkv_rm;
+                row_w(r, L.wqkv_rm, L.wqkv);
                 r.X = (const bf16_t*)xb;
                 r.bias = (const bf16_t*)L.bqkv;
                 r.nw = (const bf16_t*)L.an;
@@ -893,6 +915,9 @@ template <typename T> struct Run {
                     launch_fast_attn_fused<T>(st, fa, n);
             });
         }
+        // kv_only: the layer's K / V rows at cpos are all a later launch reads (the attention above
+        // wrote them to the cache); its wo / feed-forward output would be discarded
+        if (kv_only) return;
         // wo, split-K; the last block of each tile finalises h = x + wo(att) and its sums of squares
         if (fw) {
             FattnWoArgs A{};
@@ -920,6 +945,7 @@ template <typename T> struct Run {
             A.err = m->chain_err;
             A.delay = fm_tuning().fw_delay;
             A.cheap = fm_tuning().fw_cheap;
+            A.prio = fm_tuning().fw_prio;
             chain_flush();
             const int64_t bytes = (int64_t)r.N * r.K * 2;
             hipStream_t st = s;
@@ -928,7 +954,7 @@ template <typename T> struct Run {
             m->prof.run(s, "attn", bytes, 2.0 * r.N * r.K, go);
         } else if (rf) {
             RowGemvArgs r{};
-            r.W = (const bf16_t*)L.wo_rm;
+            row_w(r, L.wo_rm, L.wo);
             r.X = (const bf16_t*)m->att;
             r.bias = (const bf16_t*)L.bo;
             if (first) {
@@ -997,7 +1023,7 @@ template <typename T> struct Run {
         // W2, split-K; finalises the block output x = h + w2(act) into xb and its sums of squares
         if (rf) {
             RowGemvArgs r{};
-            r.W = (const bf16_t*)L.w2_rm;
+            row_w(r, L.w2_rm, L.w2);
             r.X = (const bf16_t*)m->act;
             r.res = (const bf16_t*)hb;
             r.ldr = d.dim;
@@ -1171,8 +1197,11 @@ template <typename T> struct Run {
             const bool first = l == 0;
             const void* xin = cc == 0 ? hidden : m->femb;
             const int32_t* xidx = cc == 0 ? nullptr : m->cols;
+            // codebook 0's pass (no head: inference.py:148-149 discards its output) only fills the fast
+            // KV cache, so its last layer stops once its K / V rows are cached (fm_tune fast_tail)
+            const bool kv_only = !with_head && l == m->fdm.n_layer - 1 && fm_tuning().fast_tail;
             block_small(m->fdm, m->fast[l], n, first, xin, c.fast_dim, xidx, cc, xbuf(m->fx, m->fx2, l), m->fh, true,
-                        cc, l, kp, xbuf(m->fx, m->fx2, l + 1));
+                        cc, l, kp, xbuf(m->fx, m->fx2, l + 1), kv_only);
         }
         if (with_head) {
             GemvArgs<T> a = ga();
@@ -1533,9 +1562,11 @@ static bool row_keep(fm_llm* m, const std::string& n, int rows, int cols) {
         const size_t L = strlen(suf);
         return n.size() >= L && n.compare(n.size() - L, L, suf) == 0;
     };
-    if (m->prec != FM_PREC_BF16 || m->quant || rowgemv_u(cols) == 0) return false;
+    // bf16: the T row-major weight; weight-only int8: the int8 row-major codes (rowgemv QM 1)
+    const int qm = m->quant == FM_QUANT_INT8 ? 1 : 0;
+    if (m->prec != FM_PREC_BF16 || (m->quant && !qm) || rowgemv_u(cols, qm) == 0) return false;
     if (ends("attention.wo.weight") || ends("feed_forward.w2.weight")) return rows % 2 == 0;
-    return ends("attention.wqkv.weight") && rows % 8 == 0 && rowgemv_u(cols) <= 8;
+    return ends("attention.wqkv.weight") && rows % 8 == 0 && rowgemv_u(cols, qm) <= 8;
 }
 
 static bool is_ffn_w13(const std::string& n) {
@@ -1703,11 +1734,16 @@ static void finalize(fm_llm* m) {
         } else if (m->quant) {
             m->qmap[pk] = fm_llm::QInfo{(const unsigned char*)pack_q8_dev(m, t.q, (int)t.rows, (int)t.cols), t.s};
             HIPCHK(hipStreamSynchronize(m->stream));
-            HIPCHK(hipFree(t.q));
+            if (row_keep(m, kv.first, (int)t.rows, (int)t.cols)) {
+                m->rowmajor[pk] = t.q;  // the int8 codes, row-major, for the row-block GEMV
+                m->allocs.push_back(t.q);
+            } else {
+                HIPCHK(hipFree(t.q));
+            }
             t.q = nullptr;
         }
         HIPCHK(hipStreamSynchronize(m->stream));
-        if (row_keep(m, kv.first, (int)t.rows, (int)t.cols)) {
+        if (!m->quant && row_keep(m, kv.first, (int)t.rows, (int)t.cols)) {
             m->rowmajor[pk] = t.p;  // kept for the batch-1 row-pair GEMV
             m->allocs.push_back(t.p);
         } else {
@@ -1741,6 +1777,12 @@ static void finalize(fm_llm* m) {
     };
     stack("layers.", m->sd, m->slow);
     stack("fast_layers.", m->fdm, m->fast);
+    {
+        int32_t io[16];
+        for (int c = 0; c < 16; ++c) io[c] = c - 1;
+        m->fiota = (int32_t*)m->dalloc(sizeof(io), false);
+        HIPCHK(hipMemcpy(m->fiota, io, sizeof(io), hipMemcpyHostToDevice));
+    }
     if (m->prec == FM_PREC_BF16 && !m->quant)
         m->fxt = (uint32_t*)m->dalloc((size_t)m->fdm.nh * m->fdm.hd * sizeof(uint32_t));  // tags 0: never current
     m->row_ok = m->row_qkv_ok = true;
@@ -2586,6 +2628,10 @@ int fm_tune(const char* key, int value) {
             t.bs_dummy = value;
         } else if (k == "bs_qkv_slab") {
             t.bs_qkv_slab = value != 0;
+        } else if (k == "fast_tail") {
+            t.fast_tail = value != 0;
+        } else if (k == "fkv_prefetch") {
+            t.fkv_prefetch = value != 0;
         } else if (k == "kv_prefetch") {
             t.kv_prefetch = value != 0;
         } else if (k == "bstream") {
@@ -2618,6 +2664,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "fw_delay") {
             FMCHECK(value >= 0 && value <= 1000, "fw_delay must be 0..1000 (10-ns ticks)");
             t.fw_delay = value;
+        } else if (k == "fw_prio") {
+            t.fw_prio = value != 0;
         } else if (k == "fw_cheap") {
             t.fw_cheap = value != 0;
         } else if (k == "fattn_wo") {

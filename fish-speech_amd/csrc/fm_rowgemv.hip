@@ -27,6 +27,7 @@
 #include "fm_common.h"
 #include "fm_kernels.h"
 #include "fm_runtime.h"
+#include <type_traits>
 
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
@@ -50,19 +51,32 @@ __device__ __forceinline__ void ld_pair_bf(const bf16_t* p, float& x0, float& x1
 
 // G: the residual row is gathered (residx; the fast model's first layer), whose index load the
 // residual load must wait for -- the compiler hoists that pair ahead of the weight loads (one round
-// trip), so the plain form keeps it out of the kernel entirely
-template <int U, int RP, bool PRENORM, bool FIN, bool G>
+// trip), so the plain form keeps it out of the kernel entirely.
+// QM 1 (weight-only int8, WeightOnlyInt8Linear, /root/reference/tools/llama/quantize.py:212-240):
+// W is the int8 row-major matrix, a chunk is 512 k (8 codes = 8 B per lane per row, x 16 B), the
+// codes become floats exactly (byte ^ 0x80 -> v_cvt_f32_ubyte = q + 128, the 128 * sum(x) taken off
+// once at the end) and each output is round(round(acc) * scale[row]) (quantize.py:228-229).
+template <int QM> struct RowT {
+    static constexpr int EPL = QM ? 8 : 4;  // elements per lane per chunk
+    static constexpr int CE = 64 * EPL;     // k per chunk
+    using XV = typename std::conditional<QM != 0, u32x4_t, u32x2_t>::type;  // EPL bf16
+};
+
+template <int U, int RP, bool PRENORM, bool FIN, bool G, int QM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RP == 2 ? 5 : 3)))
 void rowgemv_kernel(RowGemvArgs a) {
-    __shared__ float red[4 * RP + 4];
+    using R = RowT<QM>;
+    using XV = typename R::XV;
+    constexpr int EPL = R::EPL, NW = EPL / 2;  // NW: 32-bit words of x per lane per chunk
+    __shared__ float red[4 * RP + 8];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n0 = blockIdx.x * RP;
-    const int nch = a.K >> 8;
+    const int nch = a.K / R::CE;
     const int wa = (wave * nch) >> 2, nmy = (((wave + 1) * nch) >> 2) - wa;
     const int last = nmy > 0 ? nmy - 1 : 0;
     const unsigned long long ts0 = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    // first round trip, unconditional (a load under a branch drains vmcnt): the epilogue's residual
-    // and bias elements of row n0 + (thread % RP), then x (and the norm weight) of the wave's chunks
+    // first round trip, unconditional (a load under a branch drains vmcnt): the epilogue's residual,
+    // bias and (int8) scale elements of row n0 + (thread % RP), then x (and the norm weight)
     const int er = n0 + (int)(threadIdx.x % RP);
     int ri = 0;
     if constexpr (G) {
@@ -72,9 +86,11 @@ void rowgemv_kernel(RowGemvArgs a) {
     bf16_t rv = 0;
     if constexpr (FIN) rv = a.res[(size_t)ri * a.ldr + er];
     const bf16_t bv = *(a.bias ? a.bias + er : a.X);
-    const u32x2_t* xp = reinterpret_cast<const u32x2_t*>(a.X) + (size_t)wa * 64 + lane;
-    const u32x2_t* gp = reinterpret_cast<const u32x2_t*>(PRENORM ? a.nw : a.X) + (size_t)wa * 64 + lane;
-    u32x2_t xv[U], gv[PRENORM ? U : 1];
+    bf16_t sv = 0;
+    if constexpr (QM == 1) sv = a.wscale[er];
+    const XV* xp = reinterpret_cast<const XV*>(a.X) + (size_t)wa * 64 + lane;
+    const XV* gp = reinterpret_cast<const XV*>(PRENORM ? a.nw : a.X) + (size_t)wa * 64 + lane;
+    XV xv[U], gv[PRENORM ? U : 1];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int j = (u < last ? u : last) * 64;
@@ -90,15 +106,17 @@ void rowgemv_kernel(RowGemvArgs a) {
         pf_p = *(pf_on ? a.pf_pos : reinterpret_cast<const int32_t*>(a.X));
     }
     asm volatile("" ::: "memory");  // keep the first round trip ahead of the weight loads
-    // the block's weights: RP rows of each chunk (tail slots re-load the run's last chunk)
-    const u32x2_t* wp = reinterpret_cast<const u32x2_t*>(a.W + (size_t)n0 * a.K) + (size_t)wa * 64 + lane;
-    const size_t rs4 = (size_t)(a.K >> 2);  // one row in u32x2 units
+    // the block's weights: RP rows of each chunk, 8 B per lane (tail slots re-load the run's last chunk)
+    const unsigned char* wb = QM ? reinterpret_cast<const unsigned char*>(a.Wq) : reinterpret_cast<const unsigned char*>(a.W);
+    const size_t rowb = (size_t)a.K * (QM ? 1 : 2);  // bytes per row
+    const u32x2_t* wp = reinterpret_cast<const u32x2_t*>(wb + (size_t)n0 * rowb) + (size_t)wa * 64 + lane;
+    const size_t rs8 = rowb / 8;  // one row in u32x2 units
     u32x2_t wv[U][RP];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int j = (u < last ? u : last) * 64;
 #pragma unroll
-        for (int r = 0; r < RP; ++r) wv[u][r] = __builtin_nontemporal_load(wp + r * rs4 + j);
+        for (int r = 0; r < RP; ++r) wv[u][r] = __builtin_nontemporal_load(wp + r * rs8 + j);
     }
     asm volatile("" ::: "memory");
     float pfw[PF];
@@ -130,8 +148,11 @@ void rowgemv_kernel(RowGemvArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (u < nmy) {
-                const float e0 = lo16(xv[u][0]), e1 = hi16(xv[u][0]), e2 = lo16(xv[u][1]), e3 = hi16(xv[u][1]);
-                sl += e0 * e0 + e1 * e1 + e2 * e2 + e3 * e3;
+#pragma unroll
+                for (int h = 0; h < NW; ++h) {
+                    const float e0 = lo16(xv[u][h]), e1 = hi16(xv[u][h]);
+                    sl += e0 * e0 + e1 * e1;
+                }
             }
         }
         sl = wave_sum(sl);
@@ -141,9 +162,9 @@ void rowgemv_kernel(RowGemvArgs a) {
         const float rs = 1.0f / sqrtf(tot / (float)a.K + a.eps);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            u32x2_t o;
+            XV o;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            for (int h = 0; h < NW; ++h) {
                 const float y0 = bfround(bfround(lo16(xv[u][h]) * rs) * lo16(gv[u][h]));
                 const float y1 = bfround(bfround(hi16(xv[u][h]) * rs) * hi16(gv[u][h]));
                 o[h] = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
@@ -154,11 +175,32 @@ void rowgemv_kernel(RowGemvArgs a) {
     float acc[RP];
 #pragma unroll
     for (int r = 0; r < RP; ++r) acc[r] = 0.f;
+    float xs = 0.f;  // int8: this lane's sum of x (the 128 offset of the codes)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         if (u < nmy) {
+            if constexpr (QM == 0) {
 #pragma unroll
-            for (int r = 0; r < RP; ++r) acc[r] = dot4(wv[u][r], xv[u], acc[r]);
+                for (int r = 0; r < RP; ++r) acc[r] = dot4(wv[u][r], xv[u], acc[r]);
+            } else {
+                float xf[8];
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    xf[2 * h] = lo16(xv[u][h]);
+                    xf[2 * h + 1] = hi16(xv[u][h]);
+                }
+                xs += ((xf[0] + xf[1]) + (xf[2] + xf[3])) + ((xf[4] + xf[5]) + (xf[6] + xf[7]));
+#pragma unroll
+                for (int r = 0; r < RP; ++r) {
+                    const uint32_t c0 = wv[u][r][0] ^ 0x80808080u, c1 = wv[u][r][1] ^ 0x80808080u;
+                    float t = acc[r];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) t = fmaf((float)((c0 >> (8 * e)) & 0xffu), xf[e], t);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) t = fmaf((float)((c1 >> (8 * e)) & 0xffu), xf[4 + e], t);
+                    acc[r] = t;
+                }
+            }
         }
     }
     if constexpr (!FIN) {  // keep the prefetch loads (retired with the weights)
@@ -171,10 +213,18 @@ void rowgemv_kernel(RowGemvArgs a) {
         const float v = wave_sum(acc[r]);
         if (lane == 0) red[wave * RP + r] = v;
     }
+    if constexpr (QM == 1) {
+        const float v = wave_sum(xs);
+        if (lane == 0) red[4 * RP + 4 + wave] = v;
+    }
     __syncthreads();
     if ((int)threadIdx.x < RP) {
         const int t = threadIdx.x;
         float v = ((red[t] + red[RP + t]) + red[2 * RP + t]) + red[3 * RP + t];
+        if constexpr (QM == 1) {
+            const float xt = ((red[4 * RP + 4] + red[4 * RP + 5]) + red[4 * RP + 6]) + red[4 * RP + 7];
+            v = bfround(bfround(v - 128.f * xt) * bf2f(sv));
+        }
         if (a.bias) v += bf2f(bv);
         if constexpr (FIN) {
             a.res_out[er] = f2bf(bfround(bf2f(rv) + bfround(v)));
@@ -189,21 +239,22 @@ void rowgemv_kernel(RowGemvArgs a) {
 }
 
 // smallest instantiated depth covering a wave's share of the K chunks (0: not eligible)
-int rowgemv_u(int K) {
-    if (K <= 0 || K % 256) return 0;
-    const int need = (K / 256 + 3) / 4;
+int rowgemv_u(int K, int qm) {
+    const int ce = qm ? 512 : 256;
+    if (K <= 0 || K % ce) return 0;
+    const int need = (K / ce + 3) / 4;
     for (int u : {2, 3, 4, 5, 6, 8, 10, 12})
         if (need <= u) return u;
     return 0;
 }
 
-template <int RP, bool PRENORM, bool FIN>
+template <int RP, bool PRENORM, bool FIN, int QM>
 static void rowgemv_go(hipStream_t s, const RowGemvArgs& a, int U) {
     const dim3 grid(a.N / RP), block(256);
     auto go = [&](void (*plain)(RowGemvArgs), void (*gathered)(RowGemvArgs)) {
         (FIN && a.residx ? gathered : plain)<<<grid, block, 0, s>>>(a);
     };
-#define RG(u) go(rowgemv_kernel<u, RP, PRENORM, FIN, false>, rowgemv_kernel<u, RP, PRENORM, FIN, FIN>)
+#define RG(u) go(rowgemv_kernel<u, RP, PRENORM, FIN, false, QM>, rowgemv_kernel<u, RP, PRENORM, FIN, FIN, QM>)
     switch (U) {
         case 2: RG(2); break;
         case 3: RG(3); break;
@@ -220,14 +271,19 @@ static void rowgemv_go(hipStream_t s, const RowGemvArgs& a, int U) {
 void launch_rowgemv(hipStream_t s, const RowGemvArgs& a0, int kind) {
     RowGemvArgs a = a0;
     a.dbg = fm_tuning().dbg;
-    const int U = rowgemv_u(a.K);
-    FMCHECK(U > 0 && a.W && a.X, "row GEMV: K % 256 == 0 and K <= 12288, operands set");
+    const int qm = a.Wq ? 1 : 0;
+    const int U = rowgemv_u(a.K, qm);
+    FMCHECK(U > 0 && (qm ? (a.Wq && a.wscale && !a.bias) : a.W != nullptr) && a.X,
+            "row GEMV: K a whole number of chunks (256 k, int8 512 k), at most 48 per wave; operands set");
     if (kind == ROWGEMV_FIN) {
         FMCHECK(a.N % 2 == 0 && a.res && a.res_out, "row GEMV (fin): N even, residual rows set");
-        rowgemv_go<2, false, true>(s, a, U);
+        if (qm) rowgemv_go<2, false, true, 1>(s, a, U);
+        else rowgemv_go<2, false, true, 0>(s, a, U);
     } else {
-        FMCHECK(kind == ROWGEMV_NORM_STORE && a.N % 8 == 0 && a.nw && a.Y, "row GEMV (norm, store): N % 8 == 0, norm weight and output set");
-        rowgemv_go<8, true, false>(s, a, U);
+        FMCHECK(kind == ROWGEMV_NORM_STORE && a.N % 8 == 0 && a.nw && a.Y && U <= 8,
+                "row GEMV (norm, store): N % 8 == 0, norm weight and output set");
+        if (qm) rowgemv_go<8, true, false, 1>(s, a, U);
+        else rowgemv_go<8, true, false, 0>(s, a, U);
     }
 }
 
@@ -260,6 +316,8 @@ void fattn_wo_kernel(FattnWoArgs A) {
     const unsigned long long ts0 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     if ((int)blockIdx.x < at.nkv) {
         // ---------------- attention: kv group kvh, q head kvh * g + wave ----------------------
+        // top issue priority: the wo waves sharing this CU queue their whole weight run at once
+        if (A.prio) __builtin_amdgcn_s_setprio(3);
         const int kvh = blockIdx.x, hd = at.hd, g = at.nh / at.nkv, cpos = at.cpos, half = hd >> 1;
         const int slot = at.row_slot[0];
         const bool live = wave < g;
@@ -496,7 +554,7 @@ void fattn_wo_kernel(FattnWoArgs A) {
 }
 
 bool fattn_wo_ok(int nh, int nkv, int hd, int cpos, int N, int K) {
-    const int U = rowgemv_u(K);
+    const int U = rowgemv_u(K, 0);
     return nkv > 0 && nh % nkv == 0 && nh / nkv <= 4 && hd % 2 == 0 && hd <= FW_MAXHD && cpos >= 0 &&
            cpos < FW_MAXJ + 1 && K == nh * hd && N % 2 == 0 && U > 0 && U <= 8;
 }
@@ -510,7 +568,7 @@ void launch_fattn_wo(hipStream_t s, const FattnWoArgs& A0) {
             "fused fast attention + wo: shapes, tag and buffers");
     const dim3 grid(at.nkv + A.wo.N / 2), block(256);
     const bool G = A.wo.residx != nullptr;
-    switch (rowgemv_u(A.wo.K)) {
+    switch (rowgemv_u(A.wo.K, 0)) {
 #define FW(u) \
     case u: (G ? fattn_wo_kernel<u, true> : fattn_wo_kernel<u, false>)<<<grid, block, 0, s>>>(A); break;
         FW(2) FW(3) FW(4) FW(5) FW(6)

@@ -67,13 +67,14 @@ def test_rowgemv_full_depth_bf16_vs_reference(golden, rowgemv_mode, mode, fused)
         nfw = _row_blocks_ran(m, lambda: m.decode([0]), FW_TAG)
     finally:
         m.close()
-    # per frame: wo + w2 of 36 slow layers and 10 x 4 fast layers at 1280 blocks each (bit 0; the
-    # fast wo inside the fused launch when on); wqkv of 35 slow + 10 x 3 fast layers at 768 blocks
-    # (bit 1; first layers keep their gather); fused: 32 attention waves x 40 fast layers
+    # per frame: wo + w2 of 36 slow layers and 10 x 4 - 1 fast layers at 1280 blocks each (bit 0;
+    # codebook 0's last fast layer stops after its K / V write, fm_tune fast_tail; the fast wo inside
+    # the fused launch when on); wqkv of 35 slow + 10 x 3 fast layers at 768 blocks (bit 1; first
+    # layers keep their gather); fused: 32 attention waves x 39 fast layers
     fw = fused and (mode & 1)
-    want = (1280 * (2 * 36 + 40 + (0 if fw else 40)) if mode & 1 else 0) + (768 * (35 + 30) if mode & 2 else 0)
+    want = (1280 * (2 * 36 + 39 + (0 if fw else 39)) if mode & 1 else 0) + (768 * (35 + 30) if mode & 2 else 0)
     assert nrec == want, (nrec, want)
-    assert nfw == (32 * 40 if fw else 0), nfw
+    assert nfw == (32 * 39 if fw else 0), nfw
     st = bf16_vs_golden(slow, fast, g, rows=g["slow_rows"])
     assert st["top1_checked"] >= 9
 
