@@ -37,6 +37,9 @@ void launch_quant4(hipStream_t s, bf16_t* w, int N, int K, int gs, uint8_t* q, u
 // so (word >> 4p) & 0x000F000F is the pair (e = 2p, 2p + 1) in bf16 mantissa position
 // sz [N][K/gs] -> [ceil(N/16)][K/128][16 rows] (gs a multiple of 128: one group per unit)
 void launch_pack_q4(hipStream_t s, const uint8_t* q, int N, int K, uint8_t* dst);
+// int4 codes (one per byte) [N][K] -> row-major words [N][K / 8]: word j = codes 8j .. 8j+7, the even
+// ones in the low half at nibble e / 2, the odd ones in the high half (fm_rowgemv.hip QM 2)
+void launch_pack_q4_rows(hipStream_t s, const uint8_t* q, int N, int K, uint32_t* dst);
 void launch_pack_sz4(hipStream_t s, const uint32_t* sz, int N, int K, int gs, uint32_t* dst);
 
 template <typename T> struct LinearArgs {
@@ -325,6 +328,9 @@ struct RowGemvArgs {
     const bf16_t* W;
     const int8_t* Wq;         // weight-only int8 (instead of W): row-major codes, output round(round(acc) * wscale)
     const bf16_t* wscale;     // int8: per-row scales [N]
+    const uint32_t* Wq4;      // weight-only int4 (instead of W): packed row-major codes [N][K / 8] (launch_pack_q4_rows)
+    const uint32_t* wsz;      // int4: (scale, zero) bf16 pairs [N][K / gs]
+    int gs;                   // int4: group size
     const bf16_t* X;          // [K]
     const bf16_t* bias;       // [N] or null
     const bf16_t* nw;         // NORM: norm weight [K]

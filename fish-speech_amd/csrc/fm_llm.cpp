@@ -190,7 +190,8 @@ struct fm_llm {
         const uint32_t* sz = nullptr;       // int4: packed (scale, zero) per (tile, 128-k unit, row)
     };
     std::map<const void*, QInfo> qmap;
-    std::map<const void*, void*> rowmajor;  // packed wo / w2 / wqkv -> row-major bf16 copy (int8: codes)
+    std::map<const void*, void*> rowmajor;  // packed wo / w2 / wqkv -> row-major bf16 copy (int8 / int4: codes)
+    std::map<const void*, const void*> rowsz;  // int4: packed -> its row-major (scale, zero) table
     bool row_ok = false;                    // every layer of both stacks has wo / w2 row-major
     bool row_qkv_ok = false;                //                         ... and wqkv
     uint32_t* fxt = nullptr;                // fused fast attention + wo: tagged attention words [nh * hd]
@@ -747,17 +748,21 @@ template <typename T> struct Run {
     // CU busy); their RMSNorm consumers then take the statistic from the row they stage (ss_gran 1)
     bool row_fin(int n) const {
         const FmTuning& t = fm_tuning();
-        return sizeof(T) == 2 && n == 1 && m->row_ok && (t.rowgemv & 1) && !t.gemv_chain && !t.attn_wo;
+        return sizeof(T) == 2 && n == 1 && m->row_ok && (t.rowgemv & 1) && !t.gemv_chain && !t.attn_wo &&
+               (m->quant != FM_QUANT_INT4 || t.int4_stream);
     }
     // ... and wqkv (norm prologue, 8 rows per block)
     bool row_qkv(int n) const {
         const FmTuning& t = fm_tuning();
         // (int8: the tile kernel's wqkv measured as fast, 3.12 vs 3.14 ms per frame)
-        return sizeof(T) == 2 && n == 1 && m->row_qkv_ok && !m->quant && (t.rowgemv & 2) && !t.gemv_chain;
+        return sizeof(T) == 2 && n == 1 && m->row_qkv_ok && m->quant != FM_QUANT_INT8 && (t.rowgemv & 2) &&
+               !t.gemv_chain && (m->quant != FM_QUANT_INT4 || t.int4_stream);
     }
     void rowgemv(const RowGemvArgs& a, int kind) {
         chain_flush();
-        const int64_t bytes = (a.Wq ? (int64_t)a.N * a.K + (int64_t)a.N * 2 : (int64_t)a.N * a.K * 2) + (int64_t)a.K * 2;
+        const int64_t wbytes = a.Wq4 ? (int64_t)a.N * a.K / 2 + (int64_t)a.N * (a.K / a.gs) * 4
+                               : (a.Wq ? (int64_t)a.N * a.K + (int64_t)a.N * 2 : (int64_t)a.N * a.K * 2);
+        const int64_t bytes = wbytes + (int64_t)a.K * 2;
         hipStream_t st = s;
         auto go = [st, a, kind] { launch_rowgemv(st, a, kind); };
         m->prof.record("linear", bytes, go);
@@ -808,7 +813,11 @@ template <typename T> struct Run {
         const bool rf = row_fin(n);
         // the row-block GEMV's weight: bf16 row-major, or (weight-only int8) the codes + row scales
         auto row_w = [&](RowGemvArgs& r, void* rm, const void* packed) {
-            if (m->quant) {
+            if (m->quant == FM_QUANT_INT4) {
+                r.Wq4 = (const uint32_t*)rm;
+                r.wsz = (const uint32_t*)m->rowsz.at(packed);
+                r.gs = m->q4_gs;
+            } else if (m->quant) {
                 r.Wq = (const int8_t*)rm;
                 r.wscale = (const bf16_t*)m->qinfo(packed)->scale;
             } else {
@@ -1563,8 +1572,9 @@ static bool row_keep(fm_llm* m, const std::string& n, int rows, int cols) {
         return n.size() >= L && n.compare(n.size() - L, L, suf) == 0;
     };
     // bf16: the T row-major weight; weight-only int8: the int8 row-major codes (rowgemv QM 1)
-    const int qm = m->quant == FM_QUANT_INT8 ? 1 : 0;
-    if (m->prec != FM_PREC_BF16 || (m->quant && !qm) || rowgemv_u(cols, qm) == 0) return false;
+    const int qm = m->quant == FM_QUANT_INT8 ? 1 : (m->quant == FM_QUANT_INT4 ? 2 : 0);
+    if (m->prec != FM_PREC_BF16 || rowgemv_u(cols, qm) == 0) return false;
+    if (qm == 2 && (m->q4_gs % 8 || cols % m->q4_gs)) return false;
     if (ends("attention.wo.weight") || ends("feed_forward.w2.weight")) return rows % 2 == 0;
     return ends("attention.wqkv.weight") && rows % 8 == 0 && rowgemv_u(cols, qm) <= 8;
 }
@@ -1726,9 +1736,18 @@ static void finalize(fm_llm* m) {
         if (m->quant == FM_QUANT_INT4) {
             const fm_llm::QInfo qi = pack_q4_dev(m, t.q, t.s, (int)t.rows, (int)t.cols);
             if (qi.q8) m->qmap[pk] = qi;
+            const bool keep = row_keep(m, kv.first, (int)t.rows, (int)t.cols);
+            if (keep) {  // the codes as packed row-major words + the row-major (scale, zero) table
+                void* rw = m->dalloc((size_t)t.rows * t.cols / 2, false);
+                launch_pack_q4_rows(m->stream, (const uint8_t*)t.q, (int)t.rows, (int)t.cols, (uint32_t*)rw);
+                HIPCHK(hipGetLastError());
+                m->rowmajor[pk] = rw;
+                m->rowsz[pk] = t.s;
+                m->allocs.push_back(const_cast<void*>(t.s));
+            }
             HIPCHK(hipStreamSynchronize(m->stream));
             HIPCHK(hipFree(t.q));
-            HIPCHK(hipFree(const_cast<void*>(t.s)));
+            if (!keep) HIPCHK(hipFree(const_cast<void*>(t.s)));
             t.q = nullptr;
             t.s = nullptr;
         } else if (m->quant) {

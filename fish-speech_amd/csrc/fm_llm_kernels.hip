@@ -304,6 +304,18 @@ __global__ void pack_q4_kernel(const uint8_t* __restrict__ q, int N, int K, uint
         *reinterpret_cast<u32x4_t*>(dst + i * 16) = (u32x4_t){wd[0], wd[1], wd[2], wd[3]};
     }
 }
+__global__ void pack_q4_rows_kernel(const uint8_t* __restrict__ q, int64_t nw, uint32_t* __restrict__ dst) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v |= (uint32_t)(q[i * 8 + e] & 15) << ((e & 1) ? 16 + 4 * (e >> 1) : 4 * (e >> 1));
+        dst[i] = v;
+    }
+}
+void launch_pack_q4_rows(hipStream_t s, const uint8_t* q, int N, int K, uint32_t* dst) {
+    const int64_t nw = (int64_t)N * (K / 8);
+    pack_q4_rows_kernel<<<(int)std::min<int64_t>(FM_CEIL(nw, 256), 16384), 256, 0, s>>>(q, nw, dst);
+}
 void launch_pack_q4(hipStream_t s, const uint8_t* q, int N, int K, uint8_t* dst) {
     const int64_t n = (int64_t)((N + 15) / 16) * (K / 128) * 64;
     pack_q4_kernel<<<(int)std::min<int64_t>(FM_CEIL(n, 256), 16384), 256, 0, s>>>(q, N, K, dst);

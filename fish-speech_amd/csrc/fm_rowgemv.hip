@@ -43,6 +43,19 @@ __device__ __forceinline__ float dot4(u32x2_t w, u32x2_t x, float acc) {
 }
 __device__ __forceinline__ float lo16(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi16(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+// acc += w . x over 8 bf16 pairs (v_dot2c_f32_bf16); whole-vector bit casts (fm_pass.hip dot8)
+__device__ __forceinline__ float dot8r(u32x4_t w, u32x4_t x, float acc) {
+    const bf16x8_t wb = __builtin_bit_cast(bf16x8_t, w), xb = __builtin_bit_cast(bf16x8_t, x);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(wb, wb, 0, 1), __builtin_shufflevector(xb, xb, 0, 1),
+                                          acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(wb, wb, 2, 3), __builtin_shufflevector(xb, xb, 2, 3),
+                                          acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(wb, wb, 4, 5), __builtin_shufflevector(xb, xb, 4, 5),
+                                          acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(wb, wb, 6, 7), __builtin_shufflevector(xb, xb, 6, 7),
+                                          acc, false);
+    return acc;
+}
 __device__ __forceinline__ void ld_pair_bf(const bf16_t* p, float& x0, float& x1) {
     const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
     x0 = lo16(w);
@@ -56,10 +69,17 @@ __device__ __forceinline__ void ld_pair_bf(const bf16_t* p, float& x0, float& x1
 // W is the int8 row-major matrix, a chunk is 512 k (8 codes = 8 B per lane per row, x 16 B), the
 // codes become floats exactly (byte ^ 0x80 -> v_cvt_f32_ubyte = q + 128, the 128 * sum(x) taken off
 // once at the end) and each output is round(round(acc) * scale[row]) (quantize.py:228-229).
+// QM 2 (weight-only int4, group size gs a multiple of 8; quantize.py:57-160 group quantization):
+// W is the packed row-major code matrix (one 32-bit word = 8 codes, the even ones in the low half),
+// a chunk is 512 k (one word per lane per row); each code pair becomes the exact bf16 pair
+// (128 + q) by one mask-and-or, two v_dot2c per word pair give B = sum x (128 + q) over the lane's
+// 8 k (inside one group), and the group's affine map is applied as s * B + (z - 136 s) * sum x,
+// i.e. sum x ((q - 8) s + z) in fp32 (the tile kernel's QM 2 form, fm_gemv.hip).
 template <int QM> struct RowT {
     static constexpr int EPL = QM ? 8 : 4;  // elements per lane per chunk
     static constexpr int CE = 64 * EPL;     // k per chunk
     using XV = typename std::conditional<QM != 0, u32x4_t, u32x2_t>::type;  // EPL bf16
+    static constexpr int WPL = QM == 2 ? 1 : 2;  // 32-bit words of weights per lane per row per chunk
 };
 
 template <int U, int RP, bool PRENORM, bool FIN, bool G, int QM>
@@ -106,17 +126,36 @@ void rowgemv_kernel(RowGemvArgs a) {
         pf_p = *(pf_on ? a.pf_pos : reinterpret_cast<const int32_t*>(a.X));
     }
     asm volatile("" ::: "memory");  // keep the first round trip ahead of the weight loads
-    // the block's weights: RP rows of each chunk, 8 B per lane (tail slots re-load the run's last chunk)
-    const unsigned char* wb = QM ? reinterpret_cast<const unsigned char*>(a.Wq) : reinterpret_cast<const unsigned char*>(a.W);
-    const size_t rowb = (size_t)a.K * (QM ? 1 : 2);  // bytes per row
-    const u32x2_t* wp = reinterpret_cast<const u32x2_t*>(wb + (size_t)n0 * rowb) + (size_t)wa * 64 + lane;
-    const size_t rs8 = rowb / 8;  // one row in u32x2 units
-    u32x2_t wv[U][RP];
+    // the block's weights: RP rows of each chunk, 8 B (int4: 4 B) per lane; int4: the lane's group
+    // (scale, zero) per row too (tail slots re-load the run's last chunk)
+    constexpr int WU = QM == 2 ? 1 : U, WR = QM == 2 ? 1 : RP;
+    constexpr int QU = QM == 2 ? U : 1, QR = QM == 2 ? RP : 1;
+    u32x2_t wv[WU][WR];
+    uint32_t w4[QU][QR], szv[QU][QR];
+    if constexpr (QM == 2) {
+        const size_t rw = (size_t)(a.K >> 3);  // one row in words
+        const int ng = a.K / a.gs;
+        const uint32_t* wp = a.Wq4 + (size_t)n0 * rw + (size_t)wa * 64 + lane;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int j = (u < last ? u : last) * 64;
+        for (int u = 0; u < U; ++u) {
+            const int jc = u < last ? u : last;
 #pragma unroll
-        for (int r = 0; r < RP; ++r) wv[u][r] = __builtin_nontemporal_load(wp + r * rs8 + j);
+            for (int r = 0; r < RP; ++r) {
+                w4[u][r] = __builtin_nontemporal_load(wp + r * rw + jc * 64);
+                szv[u][r] = a.wsz[(size_t)(n0 + r) * ng + ((wa + jc) * 512 + lane * 8) / a.gs];
+            }
+        }
+    } else {
+        const unsigned char* wb = QM ? reinterpret_cast<const unsigned char*>(a.Wq) : reinterpret_cast<const unsigned char*>(a.W);
+        const size_t rowb = (size_t)a.K * (QM ? 1 : 2);  // bytes per row
+        const u32x2_t* wp = reinterpret_cast<const u32x2_t*>(wb + (size_t)n0 * rowb) + (size_t)wa * 64 + lane;
+        const size_t rs8 = rowb / 8;  // one row in u32x2 units
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = (u < last ? u : last) * 64;
+#pragma unroll
+            for (int r = 0; r < RP; ++r) wv[u][r] = __builtin_nontemporal_load(wp + r * rs8 + j);
+        }
     }
     asm volatile("" ::: "memory");
     float pfw[PF];
@@ -182,6 +221,20 @@ void rowgemv_kernel(RowGemvArgs a) {
             if constexpr (QM == 0) {
 #pragma unroll
                 for (int r = 0; r < RP; ++r) acc[r] = dot4(wv[u][r], xv[u], acc[r]);
+            } else if constexpr (QM == 2) {
+                const u32x4_t ones = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+                const float xl = dot8r(ones, xv[u], 0.f);  // sum of the lane's 8 x
+#pragma unroll
+                for (int r = 0; r < RP; ++r) {
+                    const uint32_t w = w4[u][r];
+                    u32x4_t A;
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) A[p] = ((w >> (4 * p)) & 0x000F000Fu) | 0x43004300u;
+                    const float B = dot8r(A, xv[u], 0.f);
+                    const float sc = lo16(szv[u][r]), zr = hi16(szv[u][r]);
+                    acc[r] = fmaf(sc, B, acc[r]);
+                    acc[r] = fmaf(zr - 136.f * sc, xl, acc[r]);
+                }
             } else {
                 float xf[8];
 #pragma unroll
@@ -271,18 +324,22 @@ static void rowgemv_go(hipStream_t s, const RowGemvArgs& a, int U) {
 void launch_rowgemv(hipStream_t s, const RowGemvArgs& a0, int kind) {
     RowGemvArgs a = a0;
     a.dbg = fm_tuning().dbg;
-    const int qm = a.Wq ? 1 : 0;
+    const int qm = a.Wq4 ? 2 : (a.Wq ? 1 : 0);
     const int U = rowgemv_u(a.K, qm);
-    FMCHECK(U > 0 && (qm ? (a.Wq && a.wscale && !a.bias) : a.W != nullptr) && a.X,
-            "row GEMV: K a whole number of chunks (256 k, int8 512 k), at most 48 per wave; operands set");
+    FMCHECK(U > 0 && a.X &&
+                (qm == 2 ? (a.wsz && a.gs > 0 && a.gs % 8 == 0 && a.K % a.gs == 0 && !a.bias)
+                         : (qm == 1 ? (a.Wq && a.wscale && !a.bias) : a.W != nullptr)),
+            "row GEMV: K a whole number of chunks (256 k, int8 / int4 512 k), at most 48 per wave; operands set");
     if (kind == ROWGEMV_FIN) {
         FMCHECK(a.N % 2 == 0 && a.res && a.res_out, "row GEMV (fin): N even, residual rows set");
-        if (qm) rowgemv_go<2, false, true, 1>(s, a, U);
+        if (qm == 2) rowgemv_go<2, false, true, 2>(s, a, U);
+        else if (qm == 1) rowgemv_go<2, false, true, 1>(s, a, U);
         else rowgemv_go<2, false, true, 0>(s, a, U);
     } else {
         FMCHECK(kind == ROWGEMV_NORM_STORE && a.N % 8 == 0 && a.nw && a.Y && U <= 8,
                 "row GEMV (norm, store): N % 8 == 0, norm weight and output set");
-        if (qm) rowgemv_go<8, true, false, 1>(s, a, U);
+        if (qm == 2) rowgemv_go<8, true, false, 2>(s, a, U);
+        else if (qm == 1) rowgemv_go<8, true, false, 1>(s, a, U);
         else rowgemv_go<8, true, false, 0>(s, a, U);
     }
 }

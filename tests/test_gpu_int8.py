@@ -103,10 +103,23 @@ def test_int8_batched_slots_match_single(n, bstream, golden):
         np.testing.assert_array_equal(got, single[s])
 
 
-def test_int8_wide_real_widths_vs_reference(golden):
+@pytest.mark.parametrize("rowgemv", [1, 0])
+def test_int8_wide_real_widths_vs_reference(golden, rowgemv):
     """S2-Pro widths (d=2560, I=9728, 32/8x128 heads, V=155776, cb=4096) at reduced depth, int8 from
     the synthetic bf16 weights quantized on the device, bf16 production decode path teacher-forced
-    with the reference int8 model's columns: within BF16_RATIO x its own bf16 error."""
+    with the reference int8 model's columns: within BF16_RATIO x its own bf16 error -- with wo / w2
+    on the int8 row-block GEMV (fm_rowgemv.hip QM 1, the default) and on the 16-row tiles."""
+    from fishmi import native
+    from fishmi.llm import DualARModel
+
+    native.tune("rowgemv", rowgemv)
+    try:
+        _int8_wide(golden)
+    finally:
+        native.tune("rowgemv", 3)
+
+
+def _int8_wide(golden):
     from fishmi.llm import DualARModel
 
     path = os.path.join(GOLDEN, "llm_wide_int8_bf16.npz")
