@@ -298,7 +298,8 @@ struct FmTuning {
     int fw_cheap = 0;        // fattn_wo: FattnWoArgs::cheap
     int fw_prio = 0;         // fattn_wo: FattnWoArgs::prio
     int fattn_wo = 1;        // 1: batch-1 bf16 fast-model attention + wo as one launch (fm_rowgemv.hip fattn_wo_kernel)
-    int rowgemv = 3;         // batch-1 bf16 on the row-block GEMV (fm_rowgemv.hip): bit 0 wo / w2, bit 1 wqkv (0: 16-row MFMA tiles)
+    int rowgemv_q4 = 7;      // rowgemv's bits for weight-only int4 models (w1 || w3 too: int4 frame 3.06 -> 3.01 ms; bf16 4.07 -> 4.10, int8 3.11 -> 3.20 with it)
+    int rowgemv = 3;         // batch-1 decode linears on the row-block GEMV (fm_rowgemv.hip): bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3 (0: 16-row MFMA tiles)
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
     int pass_prepare = 0;    // 1: build the persistent pass's weight copy at finalize even with pass_fast 0
     int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1), 5 (12 x 8, 4: K / V from the cache, 96 KiB ring), 6 (no loader: stream waves with PASS_SR-fragment register rings)
@@ -323,7 +324,9 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
 //                      consumer: GemvArgs::ss_gran = 1)
 //   ROWGEMV_NORM_STORE (wqkv, RP 8): x' = RMSNorm(x) * nw in the prologue, y = round(W x' + bias) into
 //                      Y, optional KV prefetch (GemvArgs::pf_kc semantics)
-enum { ROWGEMV_FIN = 0, ROWGEMV_NORM_STORE = 1 };
+//   ROWGEMV_NORM_SWIGLU (w1 || w3, RP 8: rows 8b .. 8b+3 = W1 rows 4b .. 4b+3, rows 8b+4 .. 8b+7 the same
+//                      rows of W3): x' = RMSNorm(x) * nw, y[4b + t] = round(silu(round(g))) * round(u) into Y
+enum { ROWGEMV_FIN = 0, ROWGEMV_NORM_STORE = 1, ROWGEMV_NORM_SWIGLU = 2 };
 struct RowGemvArgs {
     const bf16_t* W;
     const int8_t* Wq;         // weight-only int8 (instead of W): row-major codes, output round(round(acc) * wscale)

@@ -103,7 +103,7 @@ static int pick_ksb(int N, int K, int R, size_t esz) {
 struct LayerW {
     void *wqkv = nullptr, *bqkv = nullptr, *wo = nullptr, *bo = nullptr, *qn = nullptr, *kn = nullptr;
     void *w13 = nullptr, *w2 = nullptr, *an = nullptr, *fn = nullptr;  // w13: row-interleaved W1||W3
-    void *wo_rm = nullptr, *w2_rm = nullptr, *wqkv_rm = nullptr;  // bf16 row-major as well (fm_rowgemv.hip)
+    void *wo_rm = nullptr, *w2_rm = nullptr, *wqkv_rm = nullptr, *w13_rm = nullptr;  // row-major as well (fm_rowgemv.hip)
 };
 
 struct StackDims {
@@ -192,8 +192,10 @@ struct fm_llm {
     std::map<const void*, QInfo> qmap;
     std::map<const void*, void*> rowmajor;  // packed wo / w2 / wqkv -> row-major bf16 copy (int8 / int4: codes)
     std::map<const void*, const void*> rowsz;  // int4: packed -> its row-major (scale, zero) table
+    std::map<const void*, const void*> rowscale;  // int8 w1 || w3: packed -> its row-block interleaved scales
     bool row_ok = false;                    // every layer of both stacks has wo / w2 row-major
     bool row_qkv_ok = false;                //                         ... and wqkv
+    bool row_w13_ok = false;                //                         ... and w1 || w3
     uint32_t* fxt = nullptr;                // fused fast attention + wo: tagged attention words [nh * hd]
     int32_t* fiota = nullptr;               // [16]: fiota[c] = c - 1 (the fast KV prefetch's last cached row)
     const QInfo* qinfo(const void* W) const {
@@ -746,17 +748,28 @@ template <typename T> struct Run {
     }
     // batch-1 bf16 wo / w2 on the row-block GEMV (fm_rowgemv.hip: one block per pair of rows, every
     // CU busy); their RMSNorm consumers then take the statistic from the row they stage (ss_gran 1)
+    // the row-block GEMV's enabled linears (fm_tune rowgemv; int4 models: rowgemv_q4)
+    int row_bits() const {
+        const FmTuning& t = fm_tuning();
+        return m->quant == FM_QUANT_INT4 ? t.rowgemv_q4 : t.rowgemv;
+    }
     bool row_fin(int n) const {
         const FmTuning& t = fm_tuning();
-        return sizeof(T) == 2 && n == 1 && m->row_ok && (t.rowgemv & 1) && !t.gemv_chain && !t.attn_wo &&
+        return sizeof(T) == 2 && n == 1 && m->row_ok && (row_bits() & 1) && !t.gemv_chain && !t.attn_wo &&
                (m->quant != FM_QUANT_INT4 || t.int4_stream);
     }
     // ... and wqkv (norm prologue, 8 rows per block)
     bool row_qkv(int n) const {
         const FmTuning& t = fm_tuning();
         // (int8: the tile kernel's wqkv measured as fast, 3.12 vs 3.14 ms per frame)
-        return sizeof(T) == 2 && n == 1 && m->row_qkv_ok && m->quant != FM_QUANT_INT8 && (t.rowgemv & 2) &&
+        return sizeof(T) == 2 && n == 1 && m->row_qkv_ok && m->quant != FM_QUANT_INT8 && (row_bits() & 2) &&
                !t.gemv_chain && (m->quant != FM_QUANT_INT4 || t.int4_stream);
+    }
+    // ... and w1 || w3 (norm prologue, SwiGLU epilogue, 4 + 4 rows per block)
+    bool row_w13(int n) const {
+        const FmTuning& t = fm_tuning();
+        return sizeof(T) == 2 && n == 1 && m->row_w13_ok && (row_bits() & 4) && !t.gemv_chain &&
+               (m->quant != FM_QUANT_INT4 || t.int4_stream);
     }
     void rowgemv(const RowGemvArgs& a, int kind) {
         chain_flush();
@@ -819,7 +832,8 @@ template <typename T> struct Run {
                 r.gs = m->q4_gs;
             } else if (m->quant) {
                 r.Wq = (const int8_t*)rm;
-                r.wscale = (const bf16_t*)m->qinfo(packed)->scale;
+                auto it = m->rowscale.find(packed);
+                r.wscale = (const bf16_t*)(it != m->rowscale.end() ? it->second : m->qinfo(packed)->scale);
             } else {
                 r.W = (const bf16_t*)rm;
             }
@@ -1014,7 +1028,17 @@ template <typename T> struct Run {
             }
         }
         // W1/W3 (+ ffn_norm) -> SwiGLU act
-        {
+        if (row_w13(n)) {
+            RowGemvArgs r{};
+            row_w(r, L.w13_rm, L.w13);
+            r.X = (const bf16_t*)hb;
+            r.nw = (const bf16_t*)L.fn;
+            r.eps = m->c.norm_eps;
+            r.Y = (bf16_t*)m->act;
+            r.N = 2 * d.inter;
+            r.K = d.dim;
+            rowgemv(r, ROWGEMV_NORM_SWIGLU);
+        } else {
             GemvArgs<T> a = ga();
             a.W = (const T*)L.w13;
             a.nw = (const T*)L.fn;
@@ -1602,6 +1626,39 @@ static void* pack_w13(fm_llm* m, const std::string& p, int inter, int dim) {
     HIPCHK(hipMemcpy2DAsync((char*)tmp + 8 * rb, 16 * rb, t3.p, 8 * rb, 8 * rb, inter / 8, hipMemcpyDeviceToDevice,
                             m->stream));
     void* pk = pack_dev(m, tmp, 2 * inter, dim);
+    // the row-block GEMV's copy (fm_rowgemv.hip ROWGEMV_NORM_SWIGLU): row-major, rows 4b .. 4b+3 of W1
+    // then the same rows of W3, per 8-row block (bf16 rows, or int8 codes + scales, or int4 packed
+    // code words + (scale, zero) rows)
+    const int qm = m->quant == FM_QUANT_INT8 ? 1 : (m->quant == FM_QUANT_INT4 ? 2 : 0);
+    const bool rk = m->prec == FM_PREC_BF16 && inter % 4 == 0 && rowgemv_u(dim, qm) > 0 && rowgemv_u(dim, qm) <= 8 &&
+                    (qm != 2 || (m->q4_gs % 8 == 0 && dim % m->q4_gs == 0));
+    auto il4 = [&](const void* a1, const void* a3, size_t rb4) -> void* {  // rb4: bytes per row
+        void* d = m->dalloc(2 * (size_t)inter * rb4, false);
+        HIPCHK(hipMemcpy2DAsync(d, 8 * rb4, a1, 4 * rb4, 4 * rb4, inter / 4, hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpy2DAsync((char*)d + 4 * rb4, 8 * rb4, a3, 4 * rb4, 4 * rb4, inter / 4, hipMemcpyDeviceToDevice,
+                                m->stream));
+        return d;
+    };
+    if (rk && qm == 0) m->rowmajor[pk] = il4(t1.p, t3.p, rb);
+    if (rk && qm == 1) {
+        m->rowmajor[pk] = il4(t1.q, t3.q, (size_t)dim);
+        m->rowscale[pk] = il4(t1.s, t3.s, E);
+    }
+    if (rk && qm == 2) {
+        void* codes = nullptr;  // one byte per code, interleaved, then packed to row words
+        HIPCHK(hipMalloc(&codes, 2 * (size_t)inter * dim));
+        HIPCHK(hipMemcpy2DAsync(codes, 8 * (size_t)dim, t1.q, 4 * (size_t)dim, 4 * (size_t)dim, inter / 4,
+                                hipMemcpyDeviceToDevice, m->stream));
+        HIPCHK(hipMemcpy2DAsync((char*)codes + 4 * (size_t)dim, 8 * (size_t)dim, t3.q, 4 * (size_t)dim, 4 * (size_t)dim,
+                                inter / 4, hipMemcpyDeviceToDevice, m->stream));
+        void* words = m->dalloc((size_t)inter * dim, false);
+        launch_pack_q4_rows(m->stream, (const uint8_t*)codes, 2 * inter, dim, (uint32_t*)words);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(m->stream));
+        HIPCHK(hipFree(codes));
+        m->rowmajor[pk] = words;
+        m->rowsz[pk] = il4(t1.s, t3.s, (size_t)(dim / m->q4_gs) * 4);
+    }
     if (m->quant == FM_QUANT_INT4) {  // the same interleave of the code rows and of the (scale, zero) rows
         const size_t gb = (size_t)(dim / m->q4_gs) * 4;
         void* qt = nullptr;
@@ -1792,6 +1849,7 @@ static void finalize(fm_llm* m) {
             L.wo_rm = rm(L.wo);
             L.w2_rm = rm(L.w2);
             L.wqkv_rm = rm(L.wqkv);
+            L.w13_rm = rm(L.w13);
         }
     };
     stack("layers.", m->sd, m->slow);
@@ -1804,11 +1862,12 @@ static void finalize(fm_llm* m) {
     }
     if (m->prec == FM_PREC_BF16 && !m->quant)
         m->fxt = (uint32_t*)m->dalloc((size_t)m->fdm.nh * m->fdm.hd * sizeof(uint32_t));  // tags 0: never current
-    m->row_ok = m->row_qkv_ok = true;
+    m->row_ok = m->row_qkv_ok = m->row_w13_ok = true;
     for (auto* st : {&m->slow, &m->fast})
         for (const LayerW& L : *st) {
             m->row_ok = m->row_ok && L.wo_rm && L.w2_rm;
             m->row_qkv_ok = m->row_qkv_ok && L.wqkv_rm;
+            m->row_w13_ok = m->row_w13_ok && L.w13_rm;
         }
     pass_tables(m);
     if (m->quant) {  // WeightOnlyInt8Linear has no bias (quantize.py:206-229): the checkpoint's are unused
@@ -2689,8 +2748,11 @@ int fm_tune(const char* key, int value) {
             t.fw_cheap = value != 0;
         } else if (k == "fattn_wo") {
             t.fattn_wo = value != 0;
+        } else if (k == "rowgemv_q4") {
+            FMCHECK(value >= 0 && value <= 7, "rowgemv_q4 must be 0..7");
+            t.rowgemv_q4 = value;
         } else if (k == "rowgemv") {
-            FMCHECK(value >= 0 && value <= 3, "rowgemv must be 0..3 (bit 0 wo / w2, bit 1 wqkv)");
+            FMCHECK(value >= 0 && value <= 7, "rowgemv must be 0..7 (bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3)");
             t.rowgemv = value;
         } else if (k == "pass_prepare") {
             t.pass_prepare = value != 0;

@@ -82,9 +82,12 @@ template <int QM> struct RowT {
     static constexpr int WPL = QM == 2 ? 1 : 2;  // 32-bit words of weights per lane per row per chunk
 };
 
-template <int U, int RP, bool PRENORM, bool FIN, bool G, int QM>
+// EPI: 0 STORE (wqkv), 1 FIN (wo / w2), 2 SWIGLU (w1 || w3: rows 4b .. 4b+3 of W1 then of W3 per
+// block, outputs y = round(silu(round(g))) * round(u), FeedForward.forward, llama.py:978-986)
+template <int U, int RP, bool PRENORM, int EPI, bool G, int QM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RP == 2 ? 5 : 3)))
 void rowgemv_kernel(RowGemvArgs a) {
+    constexpr bool FIN = EPI == 1;
     using R = RowT<QM>;
     using XV = typename R::XV;
     constexpr int EPL = R::EPL, NW = EPL / 2;  // NW: 32-bit words of x per lane per chunk
@@ -119,9 +122,9 @@ void rowgemv_kernel(RowGemvArgs a) {
     }
     // KV prefetch (STORE form, wqkv of the slow model): slot and position ride the first round trip
     constexpr int PF = 2;
-    const bool pf_on = !FIN && a.pf_kc != nullptr;
+    const bool pf_on = EPI == 0 && a.pf_kc != nullptr;
     int pf_s = 0, pf_p = 0;
-    if constexpr (!FIN) {
+    if constexpr (EPI == 0) {
         pf_s = *(pf_on ? a.pf_slot : reinterpret_cast<const int32_t*>(a.X));
         pf_p = *(pf_on ? a.pf_pos : reinterpret_cast<const int32_t*>(a.X));
     }
@@ -159,7 +162,7 @@ void rowgemv_kernel(RowGemvArgs a) {
     }
     asm volatile("" ::: "memory");
     float pfw[PF];
-    if constexpr (!FIN) {  // GemvArgs::pf_kc: one 4-byte load per 64-B sector, after the weights
+    if constexpr (EPI == 0) {  // GemvArgs::pf_kc: one 4-byte load per 64-B sector, after the weights
         // byte offsets from the K cache (integer selects only: a per-lane pointer select or a
         // load under a branch makes the compiler drain vmcnt)
         const char* kcb = reinterpret_cast<const char*>(pf_on ? a.pf_kc : a.X);
@@ -256,7 +259,7 @@ void rowgemv_kernel(RowGemvArgs a) {
             }
         }
     }
-    if constexpr (!FIN) {  // keep the prefetch loads (retired with the weights)
+    if constexpr (EPI == 0) {  // keep the prefetch loads (retired with the weights)
 #pragma unroll
         for (int q = 0; q < PF; ++q) asm volatile("" ::"v"(pfw[q]));
     }
@@ -281,6 +284,12 @@ void rowgemv_kernel(RowGemvArgs a) {
         if (a.bias) v += bf2f(bv);
         if constexpr (FIN) {
             a.res_out[er] = f2bf(bfround(bf2f(rv) + bfround(v)));
+        } else if constexpr (EPI == 2) {  // gate rows t < RP / 2, up rows t >= RP / 2 (same wave)
+            const float up = __shfl_down(v, RP / 2, 64);
+            if (t < RP / 2) {
+                const float g = bfround(v);
+                a.Y[blockIdx.x * (RP / 2) + t] = f2bf(bfround(g / (1.0f + expf(-g))) * bfround(up));
+            }
         } else {
             a.Y[er] = f2bf(v);
         }
@@ -301,13 +310,13 @@ int rowgemv_u(int K, int qm) {
     return 0;
 }
 
-template <int RP, bool PRENORM, bool FIN, int QM>
+template <int RP, bool PRENORM, int EPI, int QM>
 static void rowgemv_go(hipStream_t s, const RowGemvArgs& a, int U) {
     const dim3 grid(a.N / RP), block(256);
     auto go = [&](void (*plain)(RowGemvArgs), void (*gathered)(RowGemvArgs)) {
-        (FIN && a.residx ? gathered : plain)<<<grid, block, 0, s>>>(a);
+        (EPI == 1 && a.residx ? gathered : plain)<<<grid, block, 0, s>>>(a);
     };
-#define RG(u) go(rowgemv_kernel<u, RP, PRENORM, FIN, false, QM>, rowgemv_kernel<u, RP, PRENORM, FIN, FIN, QM>)
+#define RG(u) go(rowgemv_kernel<u, RP, PRENORM, EPI, false, QM>, rowgemv_kernel<u, RP, PRENORM, EPI, EPI == 1, QM>)
     switch (U) {
         case 2: RG(2); break;
         case 3: RG(3); break;
@@ -332,15 +341,21 @@ void launch_rowgemv(hipStream_t s, const RowGemvArgs& a0, int kind) {
             "row GEMV: K a whole number of chunks (256 k, int8 / int4 512 k), at most 48 per wave; operands set");
     if (kind == ROWGEMV_FIN) {
         FMCHECK(a.N % 2 == 0 && a.res && a.res_out, "row GEMV (fin): N even, residual rows set");
-        if (qm == 2) rowgemv_go<2, false, true, 2>(s, a, U);
-        else if (qm == 1) rowgemv_go<2, false, true, 1>(s, a, U);
-        else rowgemv_go<2, false, true, 0>(s, a, U);
+        if (qm == 2) rowgemv_go<2, false, 1, 2>(s, a, U);
+        else if (qm == 1) rowgemv_go<2, false, 1, 1>(s, a, U);
+        else rowgemv_go<2, false, 1, 0>(s, a, U);
+    } else if (kind == ROWGEMV_NORM_SWIGLU) {
+        FMCHECK(a.N % 8 == 0 && a.nw && a.Y && U <= 8 && !a.bias,
+                "row GEMV (norm, swiglu): N % 8 == 0 (4 + 4 interleaved rows), norm weight and output set");
+        if (qm == 2) rowgemv_go<8, true, 2, 2>(s, a, U);
+        else if (qm == 1) rowgemv_go<8, true, 2, 1>(s, a, U);
+        else rowgemv_go<8, true, 2, 0>(s, a, U);
     } else {
         FMCHECK(kind == ROWGEMV_NORM_STORE && a.N % 8 == 0 && a.nw && a.Y && U <= 8,
                 "row GEMV (norm, store): N % 8 == 0, norm weight and output set");
-        if (qm == 2) rowgemv_go<8, true, false, 2>(s, a, U);
-        else if (qm == 1) rowgemv_go<8, true, false, 1>(s, a, U);
-        else rowgemv_go<8, true, false, 0>(s, a, U);
+        if (qm == 2) rowgemv_go<8, true, 0, 2>(s, a, U);
+        else if (qm == 1) rowgemv_go<8, true, 0, 1>(s, a, U);
+        else rowgemv_go<8, true, 0, 0>(s, a, U);
     }
 }
 

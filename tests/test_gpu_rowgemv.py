@@ -45,7 +45,7 @@ def _row_blocks_ran(m, step, tag=ROW_TAG):
     return int(((rec[:, 0] >> 32) == tag).sum())
 
 
-@pytest.mark.parametrize("mode,fused", [(1, 0), (2, 0), (3, 0), (1, 1), (3, 1)])
+@pytest.mark.parametrize("mode,fused", [(1, 0), (2, 0), (3, 0), (4, 0), (1, 1), (3, 1), (7, 1)])
 def test_rowgemv_full_depth_bf16_vs_reference(golden, rowgemv_mode, mode, fused):
     """Config 2 at full depth (36 + 4 layers, S2-Pro shapes), graph-replayed frames, with wo / w2
     (bit 0), wqkv (bit 1) or both on the row-block GEMV, the fast model's attention + wo fused or
@@ -72,7 +72,8 @@ def test_rowgemv_full_depth_bf16_vs_reference(golden, rowgemv_mode, mode, fused)
     # the fused launch when on); wqkv of 35 slow + 10 x 3 fast layers at 768 blocks (bit 1; first
     # layers keep their gather); fused: 32 attention waves x 39 fast layers
     fw = fused and (mode & 1)
-    want = (1280 * (2 * 36 + 39 + (0 if fw else 39)) if mode & 1 else 0) + (768 * (35 + 30) if mode & 2 else 0)
+    want = (1280 * (2 * 36 + 39 + (0 if fw else 39)) if mode & 1 else 0) + (768 * (35 + 30) if mode & 2 else 0) + \
+        (2432 * (36 + 39) if mode & 4 else 0)
     assert nrec == want, (nrec, want)
     assert nfw == (32 * 39 if fw else 0), nfw
     st = bf16_vs_golden(slow, fast, g, rows=g["slow_rows"])
@@ -96,7 +97,7 @@ def _biased_cfg():
 
 
 def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
-    """Teacher-forced frames of a biased model, row-block GEMV (rowgemv 3) vs the 16-row MFMA tiles
+    """Teacher-forced frames of a biased model, row-block GEMV (rowgemv 7) vs the 16-row MFMA tiles
     (rowgemv 0): logits agree to bf16 rounding-order level (relative RMS < 2e-2, argmax equal where
     the margin is clear), the row path really ran, and its graph replay equals its eager frame bit
     for bit."""
@@ -114,7 +115,7 @@ def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
     sp = DualARModel.sampling(top_k=1)
     try:
         out = {}
-        for slot, mode in ((0, 0), (1, 3)):
+        for slot, mode in ((0, 0), (1, 7)):
             rowgemv_mode(mode, 1 if mode else 0)
             sl, fl = [], []
             for k in range(cols.shape[1]):
@@ -127,7 +128,7 @@ def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
                 sl.append(s)
                 fl.append(f)
             out[mode] = (np.stack(sl), np.stack(fl))
-        for a, b in zip(out[0], out[3]):
+        for a, b in zip(out[0], out[7]):
             fin = np.isfinite(a)  # (the constrained head's masked rows are -inf in both)
             assert np.array_equal(fin, np.isfinite(b))
             rel = np.sqrt(np.mean((a[fin] - b[fin]) ** 2)) / np.sqrt(np.mean(a[fin] ** 2))
@@ -135,7 +136,7 @@ def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
             srt = np.sort(a, axis=-1)
             clear = (srt[..., -1] - srt[..., -2]) > 0.1
             assert np.array_equal(np.argmax(a, -1)[clear], np.argmax(b, -1)[clear])
-        rowgemv_mode(3, 1)
+        rowgemv_mode(7, 1)
         m.force(1, cols[:, 1])
         assert _row_blocks_ran(m, lambda: m.decode([1])) > 0
         m.force(1, cols[:, 2])
