@@ -298,8 +298,9 @@ struct FmTuning {
     int fw_cheap = 0;        // fattn_wo: FattnWoArgs::cheap
     int fw_prio = 0;         // fattn_wo: FattnWoArgs::prio
     int fattn_wo = 1;        // 1: batch-1 bf16 fast-model attention + wo as one launch (fm_rowgemv.hip fattn_wo_kernel)
-    int rowgemv_q4 = 7;      // rowgemv's bits for weight-only int4 models (w1 || w3 too: int4 frame 3.06 -> 3.01 ms; bf16 4.07 -> 4.10, int8 3.11 -> 3.20 with it)
-    int rowgemv = 3;         // batch-1 decode linears on the row-block GEMV (fm_rowgemv.hip): bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3 (0: 16-row MFMA tiles)
+    int rowgemv_q4 = 31;     // rowgemv's bits for weight-only int4 models (w1 || w3 too: int4 frame 3.06 -> 3.01 ms; bf16 4.07 -> 4.10, int8 3.11 -> 3.20 with it)
+    int rowgemv = 27;        // batch-1 decode linears on the row-block GEMV (fm_rowgemv.hip): bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3,
+                             // bit 3 the codebook head, bit 4 the first layers' wqkv (0: 16-row MFMA tiles; 3 -> 27: 4.066 -> 4.032 ms)
     int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
     int pass_prepare = 0;    // 1: build the persistent pass's weight copy at finalize even with pass_fast 0
     int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1), 5 (12 x 8, 4: K / V from the cache, 96 KiB ring), 6 (no loader: stream waves with PASS_SR-fragment register rings)
@@ -326,7 +327,8 @@ template <typename T> void launch_gemv(hipStream_t s, const GemvArgs<T>& a, int 
 //                      Y, optional KV prefetch (GemvArgs::pf_kc semantics)
 //   ROWGEMV_NORM_SWIGLU (w1 || w3, RP 8: rows 8b .. 8b+3 = W1 rows 4b .. 4b+3, rows 8b+4 .. 8b+7 the same
 //                      rows of W3): x' = RMSNorm(x) * nw, y[4b + t] = round(silu(round(g))) * round(u) into Y
-enum { ROWGEMV_FIN = 0, ROWGEMV_NORM_STORE = 1, ROWGEMV_NORM_SWIGLU = 2 };
+//   ROWGEMV_NORM_F32   (a head, RP 8): x' = RMSNorm(x) * nw, Yf[n] = fp32 holding round(W x')
+enum { ROWGEMV_FIN = 0, ROWGEMV_NORM_STORE = 1, ROWGEMV_NORM_SWIGLU = 2, ROWGEMV_NORM_F32 = 3 };
 struct RowGemvArgs {
     const bf16_t* W;
     const int8_t* Wq;         // weight-only int8 (instead of W): row-major codes, output round(round(acc) * wscale)
@@ -334,7 +336,10 @@ struct RowGemvArgs {
     const uint32_t* Wq4;      // weight-only int4 (instead of W): packed row-major codes [N][K / 8] (launch_pack_q4_rows)
     const uint32_t* wsz;      // int4: (scale, zero) bf16 pairs [N][K / gs]
     int gs;                   // int4: group size
-    const bf16_t* X;          // [K]
+    const bf16_t* X;          // [K] (or a table [.][ldx] gathered by xidx[xcol], clamped to xrows; not FIN)
+    int ldx;                  // (0: K)
+    const int32_t* xidx;
+    int xcol, xrows;
     const bf16_t* bias;       // [N] or null
     const bf16_t* nw;         // NORM: norm weight [K]
     float eps;
@@ -343,7 +348,8 @@ struct RowGemvArgs {
     const int32_t* residx;
     int res_col, res_rows;
     bf16_t* res_out;          // FIN: [N]
-    bf16_t* Y;                // STORE: [N]
+    bf16_t* Y;                // STORE / SWIGLU: [N] ([N / 2])
+    float* Yf;                // F32: [N]
     int N, K;
     const bf16_t* pf_kc;      // STORE: KV prefetch (null: off), as GemvArgs
     const bf16_t* pf_vc;

@@ -197,6 +197,7 @@ struct fm_llm {
     bool row_qkv_ok = false;                //                         ... and wqkv
     bool row_w13_ok = false;                //                         ... and w1 || w3
     uint32_t* fxt = nullptr;                // fused fast attention + wo: tagged attention words [nh * hd]
+    void* fout_rm = nullptr;                // the codebook head row-major (int8 / int4: codes), row-block GEMV
     int32_t* fiota = nullptr;               // [16]: fiota[c] = c - 1 (the fast KV prefetch's last cached row)
     const QInfo* qinfo(const void* W) const {
         auto it = qmap.find(W);
@@ -877,18 +878,18 @@ template <typename T> struct Run {
                 a.pf_hd = d.hd;
             }
             const int epi = EPI_STORE;
-            if (first) {
-                a.X = (const T*)x_in;
-                a.ldx = ldx_in;
-                a.xidx = xidx;
-                a.xidx_ld = C1;
-                a.xidx_col = xcol;
-                a.xidx_rows = xidx ? m->cb : 0;
-                gemv(a, PRO_NORM, epi, 1, "linear");
-            } else if (row_qkv(n)) {
+            if (row_qkv(n) && (!first || (row_bits() & 16))) {
                 RowGemvArgs r{};
                 row_w(r, L.wqkv_rm, L.wqkv);
-                r.X = (const bf16_t*)xb;
+                if (first) {  // the layer's input row itself (a table row gathered by xidx[xcol] at codebook > 0)
+                    r.X = (const bf16_t*)x_in;
+                    r.ldx = ldx_in;
+                    r.xidx = xidx;
+                    r.xcol = xcol;
+                    r.xrows = xidx ? m->cb : 0;
+                } else {
+                    r.X = (const bf16_t*)xb;
+                }
                 r.bias = (const bf16_t*)L.bqkv;
                 r.nw = (const bf16_t*)L.an;
                 r.eps = m->c.norm_eps;
@@ -905,6 +906,14 @@ template <typename T> struct Run {
                 r.pf_nkv = a.pf_nkv;
                 r.pf_hd = a.pf_hd;
                 rowgemv(r, ROWGEMV_NORM_STORE);
+            } else if (first) {
+                a.X = (const T*)x_in;
+                a.ldx = ldx_in;
+                a.xidx = xidx;
+                a.xidx_ld = C1;
+                a.xidx_col = xcol;
+                a.xidx_rows = xidx ? m->cb : 0;
+                gemv(a, PRO_NORM, epi, 1, "linear");
             } else {
                 a.X = (const T*)xb;
                 a.ldx = d.dim;
@@ -1236,7 +1245,30 @@ template <typename T> struct Run {
             block_small(m->fdm, m->fast[l], n, first, xin, c.fast_dim, xidx, cc, xbuf(m->fx, m->fx2, l), m->fh, true,
                         cc, l, kp, xbuf(m->fx, m->fx2, l + 1), kv_only);
         }
-        if (with_head) {
+        if (with_head && sizeof(T) == 2 && n == 1 && m->fout_rm && (row_bits() & 8) && !fm_tuning().gemv_chain &&
+            (m->quant != FM_QUANT_INT4 || fm_tuning().int4_stream)) {
+            RowGemvArgs r{};  // the codebook head on the row-block GEMV (norm prologue, fp32 logits)
+            auto row_w = [&](RowGemvArgs& rr, void* rm, const void* packed) {
+                if (m->quant == FM_QUANT_INT4) {
+                    rr.Wq4 = (const uint32_t*)rm;
+                    rr.wsz = (const uint32_t*)m->rowsz.at(packed);
+                    rr.gs = m->q4_gs;
+                } else if (m->quant) {
+                    rr.Wq = (const int8_t*)rm;
+                    rr.wscale = (const bf16_t*)m->qinfo(packed)->scale;
+                } else {
+                    rr.W = (const bf16_t*)rm;
+                }
+            };
+            row_w(r, m->fout_rm, m->fout);
+            r.X = (const bf16_t*)xbuf(m->fx, m->fx2, m->fdm.n_layer);
+            r.nw = (const bf16_t*)m->fnorm;
+            r.eps = c.norm_eps;
+            r.Yf = m->flogits;
+            r.N = m->cb;
+            r.K = c.fast_dim;
+            rowgemv(r, ROWGEMV_NORM_F32);
+        } else if (with_head) {
             GemvArgs<T> a = ga();
             a.W = (const T*)m->fout;
             a.nw = (const T*)m->fnorm;
@@ -1600,6 +1632,7 @@ static bool row_keep(fm_llm* m, const std::string& n, int rows, int cols) {
     if (m->prec != FM_PREC_BF16 || rowgemv_u(cols, qm) == 0) return false;
     if (qm == 2 && (m->q4_gs % 8 || cols % m->q4_gs)) return false;
     if (ends("attention.wo.weight") || ends("feed_forward.w2.weight")) return rows % 2 == 0;
+    if (n == "fast_output.weight") return rows % 8 == 0 && rowgemv_u(cols, qm) <= 8;
     return ends("attention.wqkv.weight") && rows % 8 == 0 && rowgemv_u(cols, qm) <= 8;
 }
 
@@ -1882,6 +1915,10 @@ static void finalize(fm_llm* m) {
     m->femb = W(m, "fast_embeddings.weight");
     m->fnorm = W(m, "fast_norm.weight");
     m->fout = W(m, "fast_output.weight");
+    {
+        auto it = m->rowmajor.find(m->fout);
+        m->fout_rm = it == m->rowmajor.end() ? nullptr : it->second;
+    }
     // constrained head (inference.py:308-320): only the semantic rows + <|im_end|> can be
     // finite after the bias, so the LM head streams exactly those rows.
     const void* outw = c.tie_word_embeddings ? m->emb : W(m, "output.weight");
@@ -2749,10 +2786,10 @@ int fm_tune(const char* key, int value) {
         } else if (k == "fattn_wo") {
             t.fattn_wo = value != 0;
         } else if (k == "rowgemv_q4") {
-            FMCHECK(value >= 0 && value <= 7, "rowgemv_q4 must be 0..7");
+            FMCHECK(value >= 0 && value <= 31, "rowgemv_q4 must be 0..31");
             t.rowgemv_q4 = value;
         } else if (k == "rowgemv") {
-            FMCHECK(value >= 0 && value <= 7, "rowgemv must be 0..7 (bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3)");
+            FMCHECK(value >= 0 && value <= 31, "rowgemv must be 0..31 (bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3, bit 3 fast head, bit 4 first-layer wqkv)");
             t.rowgemv = value;
         } else if (k == "pass_prepare") {
             t.pass_prepare = value != 0;

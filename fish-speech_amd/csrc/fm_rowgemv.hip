@@ -83,7 +83,9 @@ template <int QM> struct RowT {
 };
 
 // EPI: 0 STORE (wqkv), 1 FIN (wo / w2), 2 SWIGLU (w1 || w3: rows 4b .. 4b+3 of W1 then of W3 per
-// block, outputs y = round(silu(round(g))) * round(u), FeedForward.forward, llama.py:978-986)
+// block, outputs y = round(silu(round(g))) * round(u), FeedForward.forward, llama.py:978-986),
+// 3 F32 (a head's logits: fp32 holding the T-rounded value).  G: FIN gathers its residual row,
+// the other forms their x row (RowGemvArgs::xidx: the fast model's first layer, codebook > 0).
 template <int U, int RP, bool PRENORM, int EPI, bool G, int QM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RP == 2 ? 5 : 3)))
 void rowgemv_kernel(RowGemvArgs a) {
@@ -101,17 +103,20 @@ void rowgemv_kernel(RowGemvArgs a) {
     // first round trip, unconditional (a load under a branch drains vmcnt): the epilogue's residual,
     // bias and (int8) scale elements of row n0 + (thread % RP), then x (and the norm weight)
     const int er = n0 + (int)(threadIdx.x % RP);
-    int ri = 0;
-    if constexpr (G) {
+    int ri = 0, xi = 0;
+    if constexpr (G && FIN) {
         const int32_t iv = a.residx[a.res_col];
         ri = iv < 0 ? 0 : (iv >= a.res_rows ? a.res_rows - 1 : iv);
+    } else if constexpr (G) {
+        const int32_t iv = a.xidx[a.xcol];
+        xi = iv < 0 ? 0 : (iv >= a.xrows ? a.xrows - 1 : iv);
     }
     bf16_t rv = 0;
     if constexpr (FIN) rv = a.res[(size_t)ri * a.ldr + er];
     const bf16_t bv = *(a.bias ? a.bias + er : a.X);
     bf16_t sv = 0;
     if constexpr (QM == 1) sv = a.wscale[er];
-    const XV* xp = reinterpret_cast<const XV*>(a.X) + (size_t)wa * 64 + lane;
+    const XV* xp = reinterpret_cast<const XV*>(a.X + (size_t)xi * a.ldx) + (size_t)wa * 64 + lane;
     const XV* gp = reinterpret_cast<const XV*>(PRENORM ? a.nw : a.X) + (size_t)wa * 64 + lane;
     XV xv[U], gv[PRENORM ? U : 1];
 #pragma unroll
@@ -284,6 +289,8 @@ void rowgemv_kernel(RowGemvArgs a) {
         if (a.bias) v += bf2f(bv);
         if constexpr (FIN) {
             a.res_out[er] = f2bf(bfround(bf2f(rv) + bfround(v)));
+        } else if constexpr (EPI == 3) {
+            a.Yf[er] = bfround(v);
         } else if constexpr (EPI == 2) {  // gate rows t < RP / 2, up rows t >= RP / 2 (same wave)
             const float up = __shfl_down(v, RP / 2, 64);
             if (t < RP / 2) {
@@ -314,9 +321,9 @@ template <int RP, bool PRENORM, int EPI, int QM>
 static void rowgemv_go(hipStream_t s, const RowGemvArgs& a, int U) {
     const dim3 grid(a.N / RP), block(256);
     auto go = [&](void (*plain)(RowGemvArgs), void (*gathered)(RowGemvArgs)) {
-        (EPI == 1 && a.residx ? gathered : plain)<<<grid, block, 0, s>>>(a);
+        ((EPI == 1 ? a.residx != nullptr : a.xidx != nullptr) ? gathered : plain)<<<grid, block, 0, s>>>(a);
     };
-#define RG(u) go(rowgemv_kernel<u, RP, PRENORM, EPI, false, QM>, rowgemv_kernel<u, RP, PRENORM, EPI, EPI == 1, QM>)
+#define RG(u) go(rowgemv_kernel<u, RP, PRENORM, EPI, false, QM>, rowgemv_kernel<u, RP, PRENORM, EPI, true, QM>)
     switch (U) {
         case 2: RG(2); break;
         case 3: RG(3); break;
@@ -333,6 +340,7 @@ static void rowgemv_go(hipStream_t s, const RowGemvArgs& a, int U) {
 void launch_rowgemv(hipStream_t s, const RowGemvArgs& a0, int kind) {
     RowGemvArgs a = a0;
     a.dbg = fm_tuning().dbg;
+    if (!a.ldx) a.ldx = a.K;
     const int qm = a.Wq4 ? 2 : (a.Wq ? 1 : 0);
     const int U = rowgemv_u(a.K, qm);
     FMCHECK(U > 0 && a.X &&
@@ -344,6 +352,11 @@ void launch_rowgemv(hipStream_t s, const RowGemvArgs& a0, int kind) {
         if (qm == 2) rowgemv_go<2, false, 1, 2>(s, a, U);
         else if (qm == 1) rowgemv_go<2, false, 1, 1>(s, a, U);
         else rowgemv_go<2, false, 1, 0>(s, a, U);
+    } else if (kind == ROWGEMV_NORM_F32) {
+        FMCHECK(a.N % 8 == 0 && a.nw && a.Yf && U <= 8 && !a.xidx, "row GEMV (norm, f32): N % 8 == 0, norm weight and output set");
+        if (qm == 2) rowgemv_go<8, true, 3, 2>(s, a, U);
+        else if (qm == 1) rowgemv_go<8, true, 3, 1>(s, a, U);
+        else rowgemv_go<8, true, 3, 0>(s, a, U);
     } else if (kind == ROWGEMV_NORM_SWIGLU) {
         FMCHECK(a.N % 8 == 0 && a.nw && a.Y && U <= 8 && !a.bias,
                 "row GEMV (norm, swiglu): N % 8 == 0 (4 + 4 interleaved rows), norm weight and output set");

@@ -37,7 +37,7 @@ def chain():
     native.tune("fattn_wo", 0)
     yield put
     native.tune("gemv_chain", 0)
-    native.tune("rowgemv", 3)
+    native.tune("rowgemv", 27)
     native.tune("fattn_wo", 1)
 
 

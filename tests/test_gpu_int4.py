@@ -59,12 +59,13 @@ def test_q4_gemv_equals_dequantized_linear(R):
     assert np.sqrt(np.mean((y4 - yb) ** 2)) <= 4e-3 * np.sqrt(np.mean(yb ** 2))
 
 
-@pytest.mark.parametrize("rowgemv", [7, 0, 3])
+@pytest.mark.parametrize("rowgemv", [31, 0, 3])
 def test_int4_model_stream_matches_dequantized_model(golden, rowgemv):
     """S2-Pro widths (llm_wide: 2 slow + 1 fast layers), int4 with group size 128, teacher-forced
     frames through the production decode graph: the streamed 4-bit GEMVs (fm_tune int4_stream 1;
-    wo / w2 / wqkv / w1 || w3 on the int4 row-block GEMV, fm_rowgemv.hip QM 2, with rowgemv_q4 7, the
-    default, w1 || w3 on the tiles with 3, all on the 16-row tiles with 0) against the same model on its dequantised bf16 weights
+    wo / w2 / wqkv / w1 || w3 on the int4 row-block GEMV, fm_rowgemv.hip QM 2, with rowgemv_q4 31 (also the
+    first layers' wqkv and the codebook head), the default, w1 || w3 on the tiles with 3, all on the
+    16-row tiles with 0) against the same model on its dequantised bf16 weights
     (int4_stream 0) -- logits equal up to
     the rounding of the dequantised weights (the streamed form applies the affine map exactly, the
     copy holds it rounded to bf16); and the int4 model tracks the bf16 model (quantization error only)."""
@@ -92,7 +93,7 @@ def test_int4_model_stream_matches_dequantized_model(golden, rowgemv):
             out[st] = m.teacher_decode(g["prompt"], cols)
     finally:
         native.tune("int4_stream", 1)
-        native.tune("rowgemv_q4", 7)
+        native.tune("rowgemv_q4", 31)
         m.close()
     mb = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 1)
     try:

@@ -26,7 +26,7 @@ def rowgemv_mode():
         native.tune("fattn_wo", fused)
 
     yield set_
-    native.tune("rowgemv", 3)
+    native.tune("rowgemv", 27)
     native.tune("fattn_wo", 1)
 
 
@@ -45,7 +45,7 @@ def _row_blocks_ran(m, step, tag=ROW_TAG):
     return int(((rec[:, 0] >> 32) == tag).sum())
 
 
-@pytest.mark.parametrize("mode,fused", [(1, 0), (2, 0), (3, 0), (4, 0), (1, 1), (3, 1), (7, 1)])
+@pytest.mark.parametrize("mode,fused", [(1, 0), (2, 0), (3, 0), (4, 0), (1, 1), (3, 1), (7, 1), (8, 0), (18, 0), (31, 1)])
 def test_rowgemv_full_depth_bf16_vs_reference(golden, rowgemv_mode, mode, fused):
     """Config 2 at full depth (36 + 4 layers, S2-Pro shapes), graph-replayed frames, with wo / w2
     (bit 0), wqkv (bit 1) or both on the row-block GEMV, the fast model's attention + wo fused or
@@ -69,11 +69,14 @@ def test_rowgemv_full_depth_bf16_vs_reference(golden, rowgemv_mode, mode, fused)
         m.close()
     # per frame: wo + w2 of 36 slow layers and 10 x 4 - 1 fast layers at 1280 blocks each (bit 0;
     # codebook 0's last fast layer stops after its K / V write, fm_tune fast_tail; the fast wo inside
-    # the fused launch when on); wqkv of 35 slow + 10 x 3 fast layers at 768 blocks (bit 1; first
-    # layers keep their gather); fused: 32 attention waves x 39 fast layers
+    # the fused launch when on); wqkv of 35 slow + 10 x 3 fast layers at 768 blocks (bit 1; the
+    # first layers' too with bit 4, the fast one gathering its row at codebook > 0); w1 || w3 of
+    # 36 + 39 layers at 2432 blocks (bit 2); the 9 codebook heads at 512 blocks (bit 3); fused: 32
+    # attention waves x 39 fast layers
     fw = fused and (mode & 1)
-    want = (1280 * (2 * 36 + 39 + (0 if fw else 39)) if mode & 1 else 0) + (768 * (35 + 30) if mode & 2 else 0) + \
-        (2432 * (36 + 39) if mode & 4 else 0)
+    want = (1280 * (2 * 36 + 39 + (0 if fw else 39)) if mode & 1 else 0) + \
+        (768 * (35 + 30 + (1 + 10 if mode & 16 else 0)) if mode & 2 else 0) + \
+        (2432 * (36 + 39) if mode & 4 else 0) + (512 * 9 if mode & 8 else 0)
     assert nrec == want, (nrec, want)
     assert nfw == (32 * 39 if fw else 0), nfw
     st = bf16_vs_golden(slow, fast, g, rows=g["slow_rows"])
@@ -97,7 +100,7 @@ def _biased_cfg():
 
 
 def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
-    """Teacher-forced frames of a biased model, row-block GEMV (rowgemv 7) vs the 16-row MFMA tiles
+    """Teacher-forced frames of a biased model, row-block GEMV (rowgemv 31) vs the 16-row MFMA tiles
     (rowgemv 0): logits agree to bf16 rounding-order level (relative RMS < 2e-2, argmax equal where
     the margin is clear), the row path really ran, and its graph replay equals its eager frame bit
     for bit."""
@@ -115,7 +118,7 @@ def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
     sp = DualARModel.sampling(top_k=1)
     try:
         out = {}
-        for slot, mode in ((0, 0), (1, 7)):
+        for slot, mode in ((0, 0), (1, 31)):
             rowgemv_mode(mode, 1 if mode else 0)
             sl, fl = [], []
             for k in range(cols.shape[1]):
@@ -128,7 +131,7 @@ def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
                 sl.append(s)
                 fl.append(f)
             out[mode] = (np.stack(sl), np.stack(fl))
-        for a, b in zip(out[0], out[7]):
+        for a, b in zip(out[0], out[31]):
             fin = np.isfinite(a)  # (the constrained head's masked rows are -inf in both)
             assert np.array_equal(fin, np.isfinite(b))
             rel = np.sqrt(np.mean((a[fin] - b[fin]) ** 2)) / np.sqrt(np.mean(a[fin] ** 2))
@@ -136,7 +139,7 @@ def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
             srt = np.sort(a, axis=-1)
             clear = (srt[..., -1] - srt[..., -2]) > 0.1
             assert np.array_equal(np.argmax(a, -1)[clear], np.argmax(b, -1)[clear])
-        rowgemv_mode(7, 1)
+        rowgemv_mode(31, 1)
         m.force(1, cols[:, 1])
         assert _row_blocks_ran(m, lambda: m.decode([1])) > 0
         m.force(1, cols[:, 2])
