@@ -1497,7 +1497,34 @@ __global__ __launch_bounds__(256) void sample_fast_kernel(SampleArgs a) {
     int K = sp.top_k < 1 ? 1 : (sp.top_k > 64 ? 64 : sp.top_k);
     if (K > Nl) K = Nl;
     SFTS(2)
-    const uint32_t kth = sf_radix_kth<SF_PER>(key, (uint32_t)K, fkey(mloc), (uint32_t)SF_CAP);
+    // fast threshold: the K-th largest of the 64 lane maxima t0 has at least K wave keys >= it (the
+    // K lanes' maxima), so it is a valid wave threshold whenever those keys fit the candidate cap;
+    // a 64-lane bitonic sort of the maxima finds it (else the radix search below)
+    uint32_t kth;
+    {
+        uint32_t lm = 0;
+#pragma unroll
+        for (int i = 0; i < SF_PER; ++i) lm = key[i] > lm ? key[i] : lm;
+        uint32_t v = lm;
+#pragma unroll
+        for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const uint32_t o = (uint32_t)__shfl_xor((int)v, j, 64);
+                const bool lower = (lane & j) == 0, desc = (lane & k) == 0;
+                // descending overall: the lower lane of a descending pair keeps the larger key
+                v = (lower == desc) ? (o > v ? o : v) : (o < v ? o : v);
+            }
+        }
+        const uint32_t t0 = (uint32_t)__shfl((int)v, K - 1, 64);
+        uint32_t cl = 0;
+#pragma unroll
+        for (int i = 0; i < SF_PER; ++i) cl += key[i] >= t0 ? 1u : 0u;
+        const uint32_t cnt = sf_wave_count<sf_bits(SF_PER)>(cl, nullptr);
+        kth = (a.kth_fast && t0 != 0u && cnt >= (uint32_t)K && cnt <= (uint32_t)SF_CAP)
+                  ? t0
+                  : sf_radix_kth<SF_PER>(key, (uint32_t)K, fkey(mloc), (uint32_t)SF_CAP);
+    }
     SFTS(3)
     if (lane == 0) wthr[wave] = kth;
     __syncthreads();
@@ -1744,10 +1771,13 @@ template <typename T> void launch_sample_radix(hipStream_t s, const SampleArgs& 
     // 160 KiB (sample_init, run at model finalize outside any capture)
     const size_t lds = std::max(sizeof(float) * a.Nl, sizeof(uint64_t) * (size_t)sw_pow2(a.Nl));
     FMCHECK(lds + 8 * 1024 <= 160 * 1024, "sampler: vocabulary too wide for the LDS row");
-    if (a.Nl <= 256 * SF_PER && fm_tuning().sampler_fast)
-        sample_fast_kernel<T><<<R, 256, lds, s>>>(a);
-    else
+    if (a.Nl <= 256 * SF_PER && fm_tuning().sampler_fast) {
+        SampleArgs b = a;
+        b.kth_fast = fm_tuning().sampler_kth;
+        sample_fast_kernel<T><<<R, 256, lds, s>>>(b);
+    } else {
         sample_radix_kernel<T><<<R, 256, lds, s>>>(a);
+    }
 }
 template void launch_attn_decode2<bf16_t>(hipStream_t, const AttnDecArgs<bf16_t>&, int);
 template void launch_attn_decode2<float>(hipStream_t, const AttnDecArgs<float>&, int);

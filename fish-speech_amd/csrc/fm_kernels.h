@@ -127,6 +127,7 @@ struct SampleArgs {
     const int32_t* force_cols;
     float* tap;
     int tap_ld;
+    int kth_fast;  // sample_fast_kernel: try the lane-maxima threshold before the radix search (launcher: fm_tune sampler_kth)
 };
 
 template <typename T>
@@ -241,6 +242,7 @@ struct FmTuning {
     int gemv_nt = 1;         // 1: non-temporal weight loads (each weight byte is read once a frame)
     int gemv_u = 8;          // weight fragments in flight per wave (2, 4 or 8)
     int gemv_wpb = 4;        // waves per block (4 or 8) sharing one 16-row tile
+    int sampler_kth = 1;     // sample_fast_kernel: the K-th lane maximum as the wave threshold when its candidates fit (else the radix search)
     int sampler_fast = 1;    // 1: two-stage register top-K sampler, 0: LDS radix-select sampler
     int attn_cap = 32;       // slow decode attention rows per block cap (0: the LDS-budget maximum)
     int attn_wo = 0;         // 1: fast-model attention recomputed in the Wo GEMV's prologue (PRO_FATT, R == 1; measured 0.37 ms/frame slower)
@@ -298,6 +300,7 @@ struct FmTuning {
     int fw_cheap = 0;        // fattn_wo: FattnWoArgs::cheap
     int fw_prio = 0;         // fattn_wo: FattnWoArgs::prio
     int fattn_wo = 1;        // 1: batch-1 bf16 fast-model attention + wo as one launch (fm_rowgemv.hip fattn_wo_kernel)
+    int row_qkv_rp = 8;      // developer: rows per block of the bf16 row-block wqkv (4, 8 or 16)
     int rowgemv_q4 = 31;     // rowgemv's bits for weight-only int4 models (w1 || w3 too: int4 frame 3.06 -> 3.01 ms; bf16 4.07 -> 4.10, int8 3.11 -> 3.20 with it)
     int rowgemv = 27;        // batch-1 decode linears on the row-block GEMV (fm_rowgemv.hip): bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3,
                              // bit 3 the codebook head, bit 4 the first layers' wqkv (0: 16-row MFMA tiles; 3 -> 27: 4.066 -> 4.032 ms)
@@ -361,7 +364,7 @@ struct RowGemvArgs {
 };
 int rowgemv_u(int K, int qm);  // per-wave chunk depth for K (qm 1: int8 codes; 0: not eligible)
 void launch_rowgemv(hipStream_t s, const RowGemvArgs& a, int kind);
-// batch-1 bf16 fast-model attention + wo in one launch (fm_rowgemv.hip fattn_wo_kernel): the
+// batch-1 fast-model attention + wo in one launch (fm_rowgemv.hip fattn_wo_kernel; wo in bf16, int8 or int4): the
 // attention blocks store their output as tagged words (bf16 << 16 | gen) into xt [nh * hd]; the wo
 // row-pair blocks (RowGemvArgs FIN; its X is unused) poll them.  gen: 1..65535, unique among
 // consecutive launches on the same xt; err: set when a wait timed out.
@@ -376,7 +379,7 @@ struct FattnWoArgs {
     int prio;                 // 1: attention waves at s_setprio 3 (fm_tune fw_prio)
     unsigned long long* dbg;  // developer records (launcher: fm_tune debug_ts)
 };
-bool fattn_wo_ok(int nh, int nkv, int hd, int cpos, int N, int K);
+bool fattn_wo_ok(int nh, int nkv, int hd, int cpos, int N, int K, int qm);
 void launch_fattn_wo(hipStream_t s, const FattnWoArgs& a);
 // batch-1 GEMV chain (fm_gemv.hip gemv_chain_kernel): 2..GEMV_CHAIN_MAX dependent GEMVs in one launch,
 // whole K per block, one row.  Stage kinds: wo / w2 (PRO_PLAIN, EPI_SLABFIN; the residual may be a

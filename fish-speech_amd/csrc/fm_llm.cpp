@@ -840,8 +840,9 @@ template <typename T> struct Run {
             }
         };
         // fast model, batch 1: attention and wo as one launch (fm_rowgemv.hip fattn_wo_kernel)
-        const bool fw = is_fast && !kv_only && rf && !m->quant && fm_tuning().fattn_wo && m->fxt && m->fdm.n_layer * m->C >= 2 &&
-                        fattn_wo_ok(d.nh, d.nkv, d.hd, cpos, d.dim, d.nq());
+        const int fq = m->quant == FM_QUANT_INT8 ? 1 : (m->quant == FM_QUANT_INT4 ? 2 : 0);
+        const bool fw = is_fast && !kv_only && rf && fm_tuning().fattn_wo && m->fxt && m->fdm.n_layer * m->C >= 2 &&
+                        fattn_wo_ok(d.nh, d.nkv, d.hd, cpos, d.dim, d.nq(), fq);
         const bool att_wo = is_fast && !kv_only && fm_tuning().attn_wo && !m->quant && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
                             d.hd <= 128 && d.nh % d.nkv == 0 && (d.nq() / kp.wo) % d.hd == 0 && d.nqkv() % 8 == 0;
         // QKV (+ attention_norm)
@@ -956,7 +957,7 @@ template <typename T> struct Run {
             A.at = *reinterpret_cast<const FastFusedArgs<bf16_t>*>(&fa);
             A.at.dbg = nullptr;
             RowGemvArgs& r = A.wo;
-            r.W = (const bf16_t*)L.wo_rm;
+            row_w(r, L.wo_rm, L.wo);
             r.X = (const bf16_t*)m->att;  // (unused: x comes from the tagged words)
             r.bias = (const bf16_t*)L.bo;
             if (first) {
@@ -979,7 +980,8 @@ template <typename T> struct Run {
             A.cheap = fm_tuning().fw_cheap;
             A.prio = fm_tuning().fw_prio;
             chain_flush();
-            const int64_t bytes = (int64_t)r.N * r.K * 2;
+            const int64_t bytes = r.Wq4 ? (int64_t)r.N * r.K / 2 + (int64_t)r.N * (r.K / r.gs) * 4
+                                  : (r.Wq ? (int64_t)r.N * r.K + (int64_t)r.N * 2 : (int64_t)r.N * r.K * 2);
             hipStream_t st = s;
             auto go = [st, A] { launch_fattn_wo(st, A); };
             m->prof.record("attn_wo", bytes, go);  // (not "linear": attention + GEMV, reported apart)
@@ -1893,7 +1895,7 @@ static void finalize(fm_llm* m) {
         m->fiota = (int32_t*)m->dalloc(sizeof(io), false);
         HIPCHK(hipMemcpy(m->fiota, io, sizeof(io), hipMemcpyHostToDevice));
     }
-    if (m->prec == FM_PREC_BF16 && !m->quant)
+    if (m->prec == FM_PREC_BF16)
         m->fxt = (uint32_t*)m->dalloc((size_t)m->fdm.nh * m->fdm.hd * sizeof(uint32_t));  // tags 0: never current
     m->row_ok = m->row_qkv_ok = m->row_w13_ok = true;
     for (auto* st : {&m->slow, &m->fast})
@@ -2785,6 +2787,11 @@ int fm_tune(const char* key, int value) {
             t.fw_cheap = value != 0;
         } else if (k == "fattn_wo") {
             t.fattn_wo = value != 0;
+        } else if (k == "sampler_kth") {
+            t.sampler_kth = value != 0;
+        } else if (k == "row_qkv_rp") {
+            FMCHECK(value == 4 || value == 8 || value == 16, "row_qkv_rp must be 4, 8 or 16");
+            t.row_qkv_rp = value;
         } else if (k == "rowgemv_q4") {
             FMCHECK(value >= 0 && value <= 31, "rowgemv_q4 must be 0..31");
             t.rowgemv_q4 = value;

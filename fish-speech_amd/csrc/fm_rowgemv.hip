@@ -86,16 +86,20 @@ template <int QM> struct RowT {
 // block, outputs y = round(silu(round(g))) * round(u), FeedForward.forward, llama.py:978-986),
 // 3 F32 (a head's logits: fp32 holding the T-rounded value).  G: FIN gathers its residual row,
 // the other forms their x row (RowGemvArgs::xidx: the fast model's first layer, codebook > 0).
-template <int U, int RP, bool PRENORM, int EPI, bool G, int QM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RP == 2 ? 5 : 3)))
-void rowgemv_kernel(RowGemvArgs a) {
+// TX (tagged x, fattn_wo_kernel): x is read after the weights, from 32-bit words (bf16 << 16 | gen)
+// that a producer in the same launch stores write-through; the wave re-reads its words (sc1) until
+// every tag equals gen (bounded; *err set on timeout).  blk: the row block's index.
+template <int U, int RP, bool PRENORM, int EPI, bool G, int QM, bool TX>
+__device__ __forceinline__ void rowgemv_body(const RowGemvArgs& a, const int blk, const uint32_t* xt, const uint32_t gen,
+                                             int* err) {
+    static_assert(!TX || (!PRENORM && EPI == 1), "tagged x: the residual form only");
     constexpr bool FIN = EPI == 1;
     using R = RowT<QM>;
     using XV = typename R::XV;
     constexpr int EPL = R::EPL, NW = EPL / 2;  // NW: 32-bit words of x per lane per chunk
     __shared__ float red[4 * RP + 8];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int n0 = blockIdx.x * RP;
+    const int n0 = blk * RP;
     const int nch = a.K / R::CE;
     const int wa = (wave * nch) >> 2, nmy = (((wave + 1) * nch) >> 2) - wa;
     const int last = nmy > 0 ? nmy - 1 : 0;
@@ -119,11 +123,13 @@ void rowgemv_kernel(RowGemvArgs a) {
     const XV* xp = reinterpret_cast<const XV*>(a.X + (size_t)xi * a.ldx) + (size_t)wa * 64 + lane;
     const XV* gp = reinterpret_cast<const XV*>(PRENORM ? a.nw : a.X) + (size_t)wa * 64 + lane;
     XV xv[U], gv[PRENORM ? U : 1];
+    if constexpr (!TX) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int j = (u < last ? u : last) * 64;
-        xv[u] = xp[j];
-        if constexpr (PRENORM) gv[u] = gp[j];
+        for (int u = 0; u < U; ++u) {
+            const int j = (u < last ? u : last) * 64;
+            xv[u] = xp[j];
+            if constexpr (PRENORM) gv[u] = gp[j];
+        }
     }
     // KV prefetch (STORE form, wqkv of the slow model): slot and position ride the first round trip
     constexpr int PF = 2;
@@ -166,6 +172,40 @@ void rowgemv_kernel(RowGemvArgs a) {
         }
     }
     asm volatile("" ::: "memory");
+    if constexpr (TX) {
+        // EPL tagged words per lane per chunk (sc1 loads, 16 B each), re-read until all are current
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)xt, (short)0, a.K * 4, 0x00020000);
+        u32x4_t xw[U][EPL / 4];
+        for (unsigned it = 0;; ++it) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int jc = u < last ? u : last;
+#pragma unroll
+                for (int q = 0; q < EPL / 4; ++q)
+                    xw[u][q] = __builtin_amdgcn_raw_buffer_load_b128(xr, ((wa + jc) * R::CE + EPL * lane + 4 * q) * 4, 0, 16);
+            }
+            bool ok = true;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int q = 0; q < EPL / 4; ++q)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) ok = ok && ((xw[u][q][e] & 0xffffu) == gen);
+            if (__all(ok)) break;
+            if (it >= (1u << 14)) {  // bounded: the host sees err and fails the frame
+                if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int h = 0; h < NW; ++h) {
+                const uint32_t w0 = xw[u][(2 * h) >> 2][(2 * h) & 3], w1 = xw[u][(2 * h + 1) >> 2][(2 * h + 1) & 3];
+                xv[u][h] = (w0 >> 16) | (w1 & 0xffff0000u);
+            }
+    }
     float pfw[PF];
     if constexpr (EPI == 0) {  // GemvArgs::pf_kc: one 4-byte load per 64-B sector, after the weights
         // byte offsets from the K cache (integer selects only: a per-lane pointer select or a
@@ -303,8 +343,14 @@ void rowgemv_kernel(RowGemvArgs a) {
     }
     if (a.dbg && threadIdx.x == 0) {
         const unsigned long long t[7] = {ts0, ts1, __builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0};
-        dbg_record(a.dbg, 0xFFFA, (unsigned)blockIdx.x, t);
+        dbg_record(a.dbg, TX ? 0xFFF8u : 0xFFFAu, (unsigned)blk, t);
     }
+}
+
+template <int U, int RP, bool PRENORM, int EPI, bool G, int QM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RP == 2 ? 5 : 3)))
+void rowgemv_kernel(RowGemvArgs a) {
+    rowgemv_body<U, RP, PRENORM, EPI, G, QM, false>(a, blockIdx.x, nullptr, 0u, nullptr);
 }
 
 // smallest instantiated depth covering a wave's share of the K chunks (0: not eligible)
@@ -368,6 +414,8 @@ void launch_rowgemv(hipStream_t s, const RowGemvArgs& a0, int kind) {
                 "row GEMV (norm, store): N % 8 == 0, norm weight and output set");
         if (qm == 2) rowgemv_go<8, true, 0, 2>(s, a, U);
         else if (qm == 1) rowgemv_go<8, true, 0, 1>(s, a, U);
+        else if (fm_tuning().row_qkv_rp == 4) rowgemv_go<4, true, 0, 0>(s, a, U);
+        else if (fm_tuning().row_qkv_rp == 16) rowgemv_go<16, true, 0, 0>(s, a, U);
         else rowgemv_go<8, true, 0, 0>(s, a, U);
     }
 }
@@ -390,7 +438,7 @@ void launch_rowgemv(hipStream_t s, const RowGemvArgs& a0, int kind) {
 constexpr int FW_MAXJ = 15;   // cached rows staged in LDS (cpos < 16)
 constexpr int FW_MAXHD = 128;
 
-template <int U, bool G>
+template <int U, bool G, int QM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6)))
 void fattn_wo_kernel(FattnWoArgs A) {
     __shared__ __attribute__((aligned(16))) bf16_t kvs[2 * FW_MAXJ * FW_MAXHD];
@@ -542,104 +590,12 @@ void fattn_wo_kernel(FattnWoArgs A) {
         }
         return;
     }
-    // ---------------- wo rows 2p, 2p + 1 (rowgemv_kernel FIN, x from the tagged words) --------
-    const RowGemvArgs& a = A.wo;
-    const int p = blockIdx.x - at.nkv, n0 = 2 * p;
-    const int nch = a.K >> 8;
-    const int wa = (wave * nch) >> 2, nmy = (((wave + 1) * nch) >> 2) - wa;
-    const int last = nmy > 0 ? nmy - 1 : 0;
-    const int er = n0 + (int)(threadIdx.x & 1);
-    int ri = 0;
-    if constexpr (G) {
-        const int32_t iv = a.residx[a.res_col];
-        ri = iv < 0 ? 0 : (iv >= a.res_rows ? a.res_rows - 1 : iv);
-    }
-    const bf16_t rv = a.res[(size_t)ri * a.ldr + er];
-    const bf16_t bv = *(a.bias ? a.bias + er : a.res);
-    // optional head start for the attention's dependent round trips (FattnWoArgs::delay, 10-ns
-    // ticks): the weight flood otherwise queues ahead of them
-    if (A.delay > 0) {
-        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t < (unsigned long long)A.delay) __builtin_amdgcn_s_sleep(2);
-    }
-    asm volatile("" ::: "memory");
-    const u32x2_t* wp = reinterpret_cast<const u32x2_t*>(a.W + (size_t)n0 * a.K) + (size_t)wa * 64 + lane;
-    const size_t rs4 = (size_t)(a.K >> 2);
-    u32x2_t wv[U][2];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int j = (u < last ? u : last) * 64;
-        wv[u][0] = __builtin_nontemporal_load(wp + j);
-        wv[u][1] = __builtin_nontemporal_load(wp + rs4 + j);
-    }
-    asm volatile("" ::: "memory");
-    const unsigned long long ts1 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    // x: 4 tagged words per lane per chunk, sc1 loads, re-read until every tag is this launch's
-    // (FattnWoArgs::cheap: first poll one word per 32-element group until all are current)
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)A.xt, (short)0, a.K * 4, 0x00020000);
-    unsigned it = 0;
-    if (A.cheap) {
-        const int span = (last + 1) * 256;  // elements of the wave's run
-        const int pw = wa * 256 + ((lane * 32) % span) + 31;  // the last word of lane's 32-element group
-        for (;; ++it) {
-            const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(xr, pw * 4, 0, 16);
-            if (__all((w & 0xffffu) == gen) || it >= (1u << 14)) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    const unsigned long long ts2 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    u32x4_t xw[U];
-    for (;; ++it) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int j = u < last ? u : last;
-            xw[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, ((wa + j) * 256 + 4 * lane) * 4, 0, 16);
-        }
-        bool ok = true;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) ok = ok && ((xw[u][e] & 0xffffu) == gen);
-        if (__all(ok)) break;
-        if (it >= (1u << 14)) {  // bounded: the host sees err and fails the frame
-            if (lane == 0) __hip_atomic_store(A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    const unsigned long long ts3 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    float acc0 = 0.f, acc1 = 0.f;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        if (u < nmy) {
-            u32x2_t xv;
-            xv[0] = (xw[u][0] >> 16) | (xw[u][1] & 0xffff0000u);
-            xv[1] = (xw[u][2] >> 16) | (xw[u][3] & 0xffff0000u);
-            acc0 = dot4(wv[u][0], xv, acc0);
-            acc1 = dot4(wv[u][1], xv, acc1);
-        }
-    }
-    acc0 = wave_sum(acc0);
-    acc1 = wave_sum(acc1);
-    if (lane == 0) {
-        red[2 * wave] = acc0;
-        red[2 * wave + 1] = acc1;
-    }
-    __syncthreads();
-    if (threadIdx.x < 2) {
-        const int t = threadIdx.x;
-        float v = ((red[t] + red[2 + t]) + red[4 + t]) + red[6 + t];
-        if (a.bias) v += bf2f(bv);
-        a.res_out[er] = f2bf(bfround(bf2f(rv) + bfround(v)));
-    }
-    if (A.dbg && threadIdx.x == 0 && (p & 63) == 0) {  // sampled wo block (tag 0xFFF8)
-        const unsigned long long t[7] = {ts0, ts1, ts2, ts3, __builtin_amdgcn_s_memrealtime(), 0, 0};
-        dbg_record(A.dbg, 0xFFF8, it, t);
-    }
+    // ---------------- wo rows 2p, 2p + 1: rowgemv_body FIN with x from the tagged words --------
+    rowgemv_body<U, 2, false, 1, G, QM, true>(A.wo, (int)blockIdx.x - at.nkv, A.xt, gen, A.err);
 }
 
-bool fattn_wo_ok(int nh, int nkv, int hd, int cpos, int N, int K) {
-    const int U = rowgemv_u(K, 0);
+bool fattn_wo_ok(int nh, int nkv, int hd, int cpos, int N, int K, int qm) {
+    const int U = rowgemv_u(K, qm);
     return nkv > 0 && nh % nkv == 0 && nh / nkv <= 4 && hd % 2 == 0 && hd <= FW_MAXHD && cpos >= 0 &&
            cpos < FW_MAXJ + 1 && K == nh * hd && N % 2 == 0 && U > 0 && U <= 8;
 }
@@ -647,17 +603,26 @@ bool fattn_wo_ok(int nh, int nkv, int hd, int cpos, int N, int K) {
 void launch_fattn_wo(hipStream_t s, const FattnWoArgs& A0) {
     FattnWoArgs A = A0;
     A.dbg = fm_tuning().dbg;
+    A.wo.dbg = A.dbg;
     const FastFusedArgs<bf16_t>& at = A.at;
-    FMCHECK(fattn_wo_ok(at.nh, at.nkv, at.hd, at.cpos, A.wo.N, A.wo.K) && A.xt && A.err && A.gen > 0 && A.gen < 65536 &&
-                A.wo.res && A.wo.res_out && A.wo.W,
+    const int qm = A.wo.Wq4 ? 2 : (A.wo.Wq ? 1 : 0);
+    FMCHECK(fattn_wo_ok(at.nh, at.nkv, at.hd, at.cpos, A.wo.N, A.wo.K, qm) && A.xt && A.err && A.gen > 0 && A.gen < 65536 &&
+                A.wo.res && A.wo.res_out &&
+                (qm == 2 ? (A.wo.wsz && A.wo.gs % 8 == 0 && !A.wo.bias) : (qm == 1 ? (A.wo.wscale && !A.wo.bias) : A.wo.W != nullptr)),
             "fused fast attention + wo: shapes, tag and buffers");
     const dim3 grid(at.nkv + A.wo.N / 2), block(256);
     const bool G = A.wo.residx != nullptr;
-    switch (rowgemv_u(A.wo.K, 0)) {
+    auto go = [&](auto q) {
+        constexpr int Q = decltype(q)::value;
+        switch (rowgemv_u(A.wo.K, Q)) {
 #define FW(u) \
-    case u: (G ? fattn_wo_kernel<u, true> : fattn_wo_kernel<u, false>)<<<grid, block, 0, s>>>(A); break;
-        FW(2) FW(3) FW(4) FW(5) FW(6)
-        default: (G ? fattn_wo_kernel<8, true> : fattn_wo_kernel<8, false>)<<<grid, block, 0, s>>>(A); break;
+    case u: (G ? fattn_wo_kernel<u, true, Q> : fattn_wo_kernel<u, false, Q>)<<<grid, block, 0, s>>>(A); break;
+            FW(2) FW(3) FW(4) FW(5) FW(6)
+            default: (G ? fattn_wo_kernel<8, true, Q> : fattn_wo_kernel<8, false, Q>)<<<grid, block, 0, s>>>(A); break;
 #undef FW
-    }
+        }
+    };
+    if (qm == 2) go(std::integral_constant<int, 2>{});
+    else if (qm == 1) go(std::integral_constant<int, 1>{});
+    else go(std::integral_constant<int, 0>{});
 }
