@@ -21,8 +21,9 @@ from collections import defaultdict
 
 def is_decode_linear(name):
     """bench.py's roofline kernel family: the bf16 decode GEMVs (gemv_kernel QM = 0, rowgemv_kernel)."""
-    return (name.startswith("void gemv_kernel") and re.search(r", 0>\(", name) is not None) or \
-        name.startswith("void rowgemv_kernel")
+    # bf16 instantiations only: both templates end in QM (0 bf16, 1 int8, 2 int4)
+    return (name.startswith("void gemv_kernel") or name.startswith("void rowgemv_kernel")) and \
+        re.search(r", 0>\(", name) is not None
 
 
 def load_dispatches(path):
