@@ -187,6 +187,7 @@ template <typename T> struct FastFusedArgs {
     const float* qslab = nullptr;
     int qslab_kp = 1;
     const T* qbias = nullptr;
+    const int* row_pos = nullptr;  // fattn_wo_kernel: the frame's position (its hand-off tag)
 };
 template <typename T> struct GemvArgs {
     const T* W;
@@ -366,8 +367,9 @@ int rowgemv_u(int K, int qm);  // per-wave chunk depth for K (qm 1: int8 codes; 
 void launch_rowgemv(hipStream_t s, const RowGemvArgs& a, int kind);
 // batch-1 fast-model attention + wo in one launch (fm_rowgemv.hip fattn_wo_kernel; wo in bf16, int8 or int4): the
 // attention blocks store their output as tagged words (bf16 << 16 | gen) into xt [nh * hd]; the wo
-// row-pair blocks (RowGemvArgs FIN; its X is unused) poll them.  gen: 1..65535, unique among
-// consecutive launches on the same xt; err: set when a wait timed out.
+// row-pair blocks (RowGemvArgs FIN; its X is unused) poll them.  gen: the launch's index in the
+// frame, 1..40; the tag is (row_pos[0] * 41 + gen) % 65535 + 1 (at.row_pos: the frame's position);
+// err: set when a wait timed out.
 struct FattnWoArgs {
     FastFusedArgs<bf16_t> at;
     RowGemvArgs wo;

@@ -842,6 +842,7 @@ template <typename T> struct Run {
         // fast model, batch 1: attention and wo as one launch (fm_rowgemv.hip fattn_wo_kernel)
         const int fq = m->quant == FM_QUANT_INT8 ? 1 : (m->quant == FM_QUANT_INT4 ? 2 : 0);
         const bool fw = is_fast && !kv_only && rf && fm_tuning().fattn_wo && m->fxt && m->fdm.n_layer * m->C >= 2 &&
+                        m->fdm.n_layer * m->C <= 40 &&
                         fattn_wo_ok(d.nh, d.nkv, d.hd, cpos, d.dim, d.nq(), fq);
         const bool att_wo = is_fast && !kv_only && fm_tuning().attn_wo && !m->quant && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
                             d.hd <= 128 && d.nh % d.nkv == 0 && (d.nq() / kp.wo) % d.hd == 0 && d.nqkv() % 8 == 0;
@@ -956,6 +957,7 @@ template <typename T> struct Run {
             FattnWoArgs A{};
             A.at = *reinterpret_cast<const FastFusedArgs<bf16_t>*>(&fa);
             A.at.dbg = nullptr;
+            A.at.row_pos = m->frame_pos;
             RowGemvArgs& r = A.wo;
             row_w(r, L.wo_rm, L.wo);
             r.X = (const bf16_t*)m->att;  // (unused: x comes from the tagged words)
@@ -974,7 +976,7 @@ template <typename T> struct Run {
             r.N = d.dim;
             r.K = d.nq();
             A.xt = m->fxt;
-            A.gen = 1 + layer + m->fdm.n_layer * cpos;
+            A.gen = 1 + layer + m->fdm.n_layer * cpos;  // <= 40 (fattn_wo_ok: cpos < 16, n_layer * C checked)
             A.err = m->chain_err;
             A.delay = fm_tuning().fw_delay;
             A.cheap = fm_tuning().fw_cheap;

@@ -445,7 +445,10 @@ void fattn_wo_kernel(FattnWoArgs A) {
     __shared__ float red[8];
     const FastFusedArgs<bf16_t>& at = A.at;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t gen = (uint32_t)A.gen;
+    // the tag: the frame's position (device, constant through the frame's fast passes) times 41
+    // plus the launch's index in the frame (1 .. 40): distinct for any two launches less than ~1600
+    // frames apart, across requests and slots too, so a stale word never passes for a fresh one
+    const uint32_t gen = ((uint32_t)A.at.row_pos[0] * 41u + (uint32_t)A.gen) % 65535u + 1u;
     const unsigned long long ts0 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     if ((int)blockIdx.x < at.nkv) {
         // ---------------- attention: kv group kvh, q head kvh * g + wave ----------------------
@@ -606,7 +609,7 @@ void launch_fattn_wo(hipStream_t s, const FattnWoArgs& A0) {
     A.wo.dbg = A.dbg;
     const FastFusedArgs<bf16_t>& at = A.at;
     const int qm = A.wo.Wq4 ? 2 : (A.wo.Wq ? 1 : 0);
-    FMCHECK(fattn_wo_ok(at.nh, at.nkv, at.hd, at.cpos, A.wo.N, A.wo.K, qm) && A.xt && A.err && A.gen > 0 && A.gen < 65536 &&
+    FMCHECK(fattn_wo_ok(at.nh, at.nkv, at.hd, at.cpos, A.wo.N, A.wo.K, qm) && A.xt && A.err && A.gen > 0 && A.gen <= 40 && at.row_pos &&
                 A.wo.res && A.wo.res_out &&
                 (qm == 2 ? (A.wo.wsz && A.wo.gs % 8 == 0 && !A.wo.bias) : (qm == 1 ? (A.wo.wscale && !A.wo.bias) : A.wo.W != nullptr)),
             "fused fast attention + wo: shapes, tag and buffers");

@@ -159,3 +159,47 @@ def test_rowgemv_matches_tile_path_with_biases(rowgemv_mode):
             m.force(s, None)
         m.use_graph(True)
         m.close()
+
+
+def test_fused_fast_attention_tags_stay_fresh_across_toggles(rowgemv_mode):
+    """The fused fast attention + wo hands its attention rows over by tagged words (fattn_wo_kernel):
+    teacher-forced frames with the fusion switched on, off and on again between frames (the words
+    left in the buffer by an earlier frame must never pass for the current one) track the same
+    frames without the fusion -- logits within bf16 rounding-order level, argmax equal where clear."""
+    from fishmi.llm import DualARModel
+
+    cfg = _biased_cfg()
+    m = DualARModel.synthetic(cfg, 12, 5, 0, "bf16", 1)
+    rng = np.random.default_rng(5)
+    C1 = cfg.num_codebooks + 1
+    prompt = np.zeros((C1, 10), np.int32)
+    prompt[0] = rng.integers(16, cfg.semantic_begin_id, 10)
+    nf = 7
+    cols = np.zeros((C1, nf), np.int32)
+    cols[0] = rng.integers(cfg.semantic_begin_id, cfg.semantic_end_id + 1, nf)
+    cols[1:] = rng.integers(0, cfg.codebook_size, (C1 - 1, nf))
+    sp = DualARModel.sampling(top_k=1)
+    try:
+        out = {}
+        for run, plan in (("off", [0] * nf), ("toggled", [1, 1, 0, 0, 1, 0, 1])):
+            fl = []
+            for k in range(nf):
+                rowgemv_mode(27, plan[k])
+                m.use_graph(True)  # re-capture the frame under the knob
+                m.force(0, cols[:, k])
+                if k == 0:
+                    m.prefill(0, prompt, sp)
+                else:
+                    m.decode([0])
+                fl.append(m.read_logits(0)[1])
+            out[run] = np.stack(fl)
+        a, b = out["off"], out["toggled"]
+        rel = np.sqrt(np.mean((a - b) ** 2)) / np.sqrt(np.mean(a ** 2))
+        assert rel < 2e-2, rel
+        srt = np.sort(a, axis=-1)
+        clear = (srt[..., -1] - srt[..., -2]) > 0.1
+        assert np.array_equal(np.argmax(a, -1)[clear], np.argmax(b, -1)[clear])
+    finally:
+        m.force(0, None)
+        m.use_graph(True)
+        m.close()
