@@ -301,10 +301,6 @@ struct FmTuning {
     int fw_cheap = 0;        // fattn_wo: FattnWoArgs::cheap
     int fw_prio = 0;         // fattn_wo: FattnWoArgs::prio
     int fattn_wo = 1;        // 1: batch-1 bf16 fast-model attention + wo as one launch (fm_rowgemv.hip fattn_wo_kernel)
-    int fattn_slow = 0;      // 1: batch-1 slow-model attention + wo as one launch (fm_rowgemv.hip fattn_slow_wo_kernel;
-                             //    opt-in: 4.028 vs 4.027 ms per frame at best)
-    int fws_cap = 256;       // fattn_slow: minimum positions per attention split (>= 16)
-    int fws_rp = 2;          // fattn_slow: wo rows per block (2 or 4)
     int row_qkv_rp = 8;      // developer: rows per block of the bf16 row-block wqkv (4, 8 or 16)
     int rowgemv_q4 = 31;     // rowgemv's bits for weight-only int4 models (w1 || w3 too: int4 frame 3.06 -> 3.01 ms; bf16 4.07 -> 4.10, int8 3.11 -> 3.20 with it)
     int rowgemv = 27;        // batch-1 decode linears on the row-block GEMV (fm_rowgemv.hip): bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3,
@@ -582,18 +578,6 @@ constexpr int FD_NSP = 16;
 inline bool attn_fd_ok(int hd, int g) { return (hd == 32 || hd == 64 || hd == 128) && g >= 1 && g <= 4; }
 template <typename T> void launch_attn_fd(hipStream_t s, const AttnDecArgs<T>& a, int R);
 template <typename T> void launch_attn_decode3(hipStream_t s, const AttnDecArgs<T>& a, int R);
-// batch-1 slow-model attention + wo in one launch (fm_rowgemv.hip fattn_slow_wo_kernel): attn_fd's
-// body (4-wave blocks, splits of at least at.cap positions, the output as tagged words in xt) in
-// blocks 0 .. nkv * maxsplit - 1, the wo row-pair blocks (rowgemv FIN, bf16 / int8 / int4) after them
-struct FattnSlowWoArgs {
-    AttnDecArgs<bf16_t> at;  // row 0 only; cap, cnt, part set (maxsplit set by the launcher)
-    RowGemvArgs wo;
-    uint32_t* xt;             // [nh * hd] tagged words (bf16 << 16 | tag), zero-initialised
-    int gen;                  // the launch's index in the frame, 1 .. 40 (the tag mixes in row_pos[0])
-    int* err;                 // set on a timed-out wait
-};
-bool fattn_slow_ok(int nh, int nkv, int hd, int N, int K, int qm);
-void launch_fattn_slow_wo(hipStream_t s, const FattnSlowWoArgs& a);
 template <typename T> void launch_fast_attn_fused(hipStream_t s, const FastFusedArgs<T>& a, int R);
 // fast-model attention, one wave per q head (cpos < 16 cached rows, hd <= 256)
 template <typename T> void launch_fast_attn2(hipStream_t s, const FastFusedArgs<T>& a, int R);

@@ -197,7 +197,6 @@ struct fm_llm {
     bool row_qkv_ok = false;                //                         ... and wqkv
     bool row_w13_ok = false;                //                         ... and w1 || w3
     uint32_t* fxt = nullptr;                // fused fast attention + wo: tagged attention words [nh * hd]
-    uint32_t* sxt = nullptr;                // fused slow attention + wo: tagged attention words [nh * hd]
     void* fout_rm = nullptr;                // the codebook head row-major (int8 / int4: codes), row-block GEMV
     int32_t* fiota = nullptr;               // [16]: fiota[c] = c - 1 (the fast KV prefetch's last cached row)
     const QInfo* qinfo(const void* W) const {
@@ -845,9 +844,6 @@ template <typename T> struct Run {
         const bool fw = is_fast && !kv_only && rf && fm_tuning().fattn_wo && m->fxt && m->fdm.n_layer * m->C >= 2 &&
                         m->fdm.n_layer * m->C <= 40 &&
                         fattn_wo_ok(d.nh, d.nkv, d.hd, cpos, d.dim, d.nq(), fq);
-        // slow model, batch 1: attention and wo as one launch (fm_rowgemv.hip fattn_slow_wo_kernel)
-        const bool fws = !is_fast && !kv_only && rf && fm_tuning().fattn_slow && fm_tuning().attn_fd && m->sxt &&
-                         layer < 40 && !(first && xidx) && fattn_slow_ok(d.nh, d.nkv, d.hd, d.dim, d.nq(), fq);
         const bool att_wo = is_fast && !kv_only && fm_tuning().attn_wo && !m->quant && n == 1 && cpos < 16 && d.hd % 16 == 0 &&
                             d.hd <= 128 && d.nh % d.nkv == 0 && (d.nq() / kp.wo) % d.hd == 0 && d.nqkv() % 8 == 0;
         // QKV (+ attention_norm)
@@ -928,19 +924,17 @@ template <typename T> struct Run {
                 gemv(a, PRO_PRENORM, epi, 1, "linear");
             }
         }
-        AttnDecArgs<T> aa{(const T*)m->qkv, d.nqkv(), m->frame_slot, m->frame_pos, d.nh, d.nkv, d.hd,
-                          d.qk_norm, m->c.norm_eps, (const T*)L.qn, (const T*)L.kn, m->rope, (T*)m->kc,
-                          (T*)m->vc, m->slot_stride, (size_t)layer * m->layer_stride, m->S,
-                          m->maxsplit, scale, m->part};
-        aa.cap = attn2_cap(d.hd, d.nh / d.nkv, E);
-        if (fm_tuning().attn_cap) aa.cap = std::min(aa.cap, fm_tuning().attn_cap);
-        aa.maxsplit = FM_CEIL(m->S, aa.cap);
-        aa.cnt = m->attn_cnt;
-        aa.dbg = fm_tuning().dbg;
-        aa.out = (T*)m->att;
-        if (fws) {
-            // (attention inside the wo launch below)
-        } else if (!is_fast) {
+        if (!is_fast) {
+            AttnDecArgs<T> aa{(const T*)m->qkv, d.nqkv(), m->frame_slot, m->frame_pos, d.nh, d.nkv, d.hd,
+                              d.qk_norm, m->c.norm_eps, (const T*)L.qn, (const T*)L.kn, m->rope, (T*)m->kc,
+                              (T*)m->vc, m->slot_stride, (size_t)layer * m->layer_stride, m->S,
+                              m->maxsplit, scale, m->part};
+            aa.cap = attn2_cap(d.hd, d.nh / d.nkv, E);
+            if (fm_tuning().attn_cap) aa.cap = std::min(aa.cap, fm_tuning().attn_cap);
+            aa.maxsplit = FM_CEIL(m->S, aa.cap);
+            aa.cnt = m->attn_cnt;
+            aa.dbg = fm_tuning().dbg;
+            aa.out = (T*)m->att;
             hipStream_t st = s;
             auto go = [st, aa, n] { attn_slow_on(st, aa, n); };
             m->prof.record("attn_slow", 0, go);  // the slow model's launches alone (fm_llm_kernel_bench)
@@ -959,31 +953,7 @@ template <typename T> struct Run {
         // wrote them to the cache); its wo / feed-forward output would be discarded
         if (kv_only) return;
         // wo, split-K; the last block of each tile finalises h = x + wo(att) and its sums of squares
-        if (fws) {
-            FattnSlowWoArgs A{};
-            A.at = *reinterpret_cast<const AttnDecArgs<bf16_t>*>(&aa);
-            A.at.out = nullptr;
-            A.at.cap = std::max(16, fm_tuning().fws_cap);
-            RowGemvArgs& r = A.wo;
-            row_w(r, L.wo_rm, L.wo);
-            r.X = (const bf16_t*)m->att;  // (unused: x comes from the tagged words)
-            r.bias = (const bf16_t*)L.bo;
-            r.res = (const bf16_t*)(first ? x_in : xb);
-            r.ldr = first ? ldx_in : d.dim;
-            r.res_out = (bf16_t*)hb;
-            r.N = d.dim;
-            r.K = d.nq();
-            A.xt = m->sxt;
-            A.gen = 1 + layer;  // <= 40 (fws: layer < 40)
-            A.err = m->chain_err;
-            chain_flush();
-            const int64_t bytes = r.Wq4 ? (int64_t)r.N * r.K / 2 + (int64_t)r.N * (r.K / r.gs) * 4
-                                  : (r.Wq ? (int64_t)r.N * r.K + (int64_t)r.N * 2 : (int64_t)r.N * r.K * 2);
-            hipStream_t st = s;
-            auto go = [st, A] { launch_fattn_slow_wo(st, A); };
-            m->prof.record("attn_wo", bytes, go);
-            m->prof.run(s, "attn", bytes, 2.0 * r.N * r.K, go);
-        } else if (fw) {
+        if (fw) {
             FattnWoArgs A{};
             A.at = *reinterpret_cast<const FastFusedArgs<bf16_t>*>(&fa);
             A.at.dbg = nullptr;
@@ -1927,10 +1897,8 @@ static void finalize(fm_llm* m) {
         m->fiota = (int32_t*)m->dalloc(sizeof(io), false);
         HIPCHK(hipMemcpy(m->fiota, io, sizeof(io), hipMemcpyHostToDevice));
     }
-    if (m->prec == FM_PREC_BF16) {
+    if (m->prec == FM_PREC_BF16)
         m->fxt = (uint32_t*)m->dalloc((size_t)m->fdm.nh * m->fdm.hd * sizeof(uint32_t));  // tags 0: never current
-        m->sxt = (uint32_t*)m->dalloc((size_t)m->sd.nh * m->sd.hd * sizeof(uint32_t));
-    }
     m->row_ok = m->row_qkv_ok = m->row_w13_ok = true;
     for (auto* st : {&m->slow, &m->fast})
         for (const LayerW& L : *st) {
@@ -2159,7 +2127,7 @@ static void upload_frame_rows(fm_llm* m, const int32_t* slots, int n) {
 // host's stream sync, a timed-out hand-off wait (a hang avoided) resets the counters and fails
 static void chain_err_async(fm_llm* m) {
     if (fm_tuning().gemv_chain || (m->pass_ok && fm_tuning().pass_fast) || fm_tuning().fin_split > 1 ||
-        (m->fxt && (fm_tuning().fattn_wo || fm_tuning().fattn_slow)))
+        (m->fxt && fm_tuning().fattn_wo))
         HIPCHK(hipMemcpyAsync(m->h_chain_err, m->chain_err, sizeof(int), hipMemcpyDeviceToHost, m->stream));
 }
 static void chain_err_check(fm_llm* m) {
@@ -2821,14 +2789,6 @@ int fm_tune(const char* key, int value) {
             t.fw_cheap = value != 0;
         } else if (k == "fattn_wo") {
             t.fattn_wo = value != 0;
-        } else if (k == "fattn_slow") {
-            t.fattn_slow = value != 0;
-        } else if (k == "fws_rp") {
-            FMCHECK(value == 2 || value == 4, "fws_rp: 2 or 4");
-            t.fws_rp = (int)value;
-        } else if (k == "fws_cap") {
-            FMCHECK(value >= 16 && value <= 4096, "fws_cap: 16 .. 4096");
-            t.fws_cap = (int)value;
         } else if (k == "sampler_kth") {
             t.sampler_kth = value != 0;
         } else if (k == "row_qkv_rp") {

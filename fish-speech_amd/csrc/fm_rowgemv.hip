@@ -27,7 +27,6 @@
 #include "fm_common.h"
 #include "fm_kernels.h"
 #include "fm_runtime.h"
-#include "fm_attn_fd.h"
 #include <type_traits>
 
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
@@ -629,70 +628,4 @@ void launch_fattn_wo(hipStream_t s, const FattnWoArgs& A0) {
     if (qm == 2) go(std::integral_constant<int, 2>{});
     else if (qm == 1) go(std::integral_constant<int, 1>{});
     else go(std::integral_constant<int, 0>{});
-}
-
-// =========================================================================================
-// Slow-model attention + wo in ONE launch (batch 1; fm_tune fattn_slow).
-//
-// The slow model's attention (llama.py:883-975 at one query row, 32 q / 8 kv heads, a context of
-// up to max_seq_len positions) is latency-bound: attn_fd_kernel takes ~12 us on 8 of 256 CUs over
-// the bench's positions, while the wo GEMV after it is a 21 MB weight stream.  Here blocks
-// 0 .. nkv * maxsplit - 1 run attn_fd's body (fm_attn_fd.h; 4-wave blocks, split sp of kv head
-// kvh at block sp * nkv + kvh, so the blocks of the first split dispatch first; unused splits exit)
-// and write the output row as tagged words, and the wo row-pair blocks after them stream their
-// weights and then poll their x words (rowgemv_body TX), as in fattn_wo_kernel.  The split combine
-// keeps attn_fd's last-arriver ticket (no block waits for another attention block), so the hand-off
-// is deadlock-free by dispatch order even when the grid does not fit at once.  RP (fm_tune fws_rp):
-// wo rows per block, 2 (as rowgemv_kernel) or 4 (half the blocks, the grid nearer one resident
-// round at the 4 blocks per CU the attention body's registers allow).
-template <int U, int HD, int QM, int RP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-void fattn_slow_wo_kernel(FattnSlowWoArgs A) {
-    const uint32_t gen = ((uint32_t)A.at.row_pos[0] * 41u + (uint32_t)A.gen) % 65535u + 1u;
-    const int natt = A.at.nkv * A.at.maxsplit;
-    if ((int)blockIdx.x < natt) {
-        const int kvh = (int)blockIdx.x % A.at.nkv, sp = (int)blockIdx.x / A.at.nkv;
-        attn_fd_body<bf16_t, HD, 4, true>(A.at, 0, kvh, sp, 1, A.at.maxsplit, A.xt, gen);
-        return;
-    }
-    rowgemv_body<U, RP, false, 1, false, QM, true>(A.wo, (int)blockIdx.x - natt, A.xt, gen, A.err);
-}
-
-bool fattn_slow_ok(int nh, int nkv, int hd, int N, int K, int qm) {
-    const int U = rowgemv_u(K, qm);
-    return (hd == 64 || hd == 128) && attn_fd_ok(hd, nkv > 0 ? nh / nkv : 0) && nkv > 0 && nh % nkv == 0 &&
-           K == nh * hd && N % 4 == 0 && U >= 2 && U <= 8;
-}
-
-void launch_fattn_slow_wo(hipStream_t s, const FattnSlowWoArgs& A0) {
-    FattnSlowWoArgs A = A0;
-    A.at.dbg = fm_tuning().dbg;
-    A.wo.dbg = A.at.dbg;
-    const AttnDecArgs<bf16_t>& at = A.at;
-    const int qm = A.wo.Wq4 ? 2 : (A.wo.Wq ? 1 : 0);
-    FMCHECK(fattn_slow_ok(at.nh, at.nkv, at.hd, A.wo.N, A.wo.K, qm) && A.xt && A.err && A.gen > 0 && A.gen <= 40 &&
-                at.row_pos && at.cap >= 16 && at.cnt && at.part && !at.qslab && A.wo.res && A.wo.res_out &&
-                !A.wo.residx &&
-                (qm == 2 ? (A.wo.wsz && A.wo.gs % 8 == 0 && !A.wo.bias) : (qm == 1 ? (A.wo.wscale && !A.wo.bias) : A.wo.W != nullptr)),
-            "fused slow attention + wo: shapes, tag and buffers");
-    A.at.maxsplit = std::min(FD_NSP, FM_CEIL(at.S, at.cap));
-    const int rp = fm_tuning().fws_rp;
-    const dim3 grid(at.nkv * A.at.maxsplit + A.wo.N / rp), block(256);
-    auto go = [&](auto q, auto h) {
-        constexpr int Q = decltype(q)::value, H = decltype(h)::value;
-        switch (rowgemv_u(A.wo.K, Q)) {
-#define FS(u) \
-    case u: (rp == 4 ? fattn_slow_wo_kernel<u, H, Q, 4> : fattn_slow_wo_kernel<u, H, Q, 2>)<<<grid, block, 0, s>>>(A); break;
-            FS(2) FS(3) FS(4) FS(5) FS(6)
-            default: (rp == 4 ? fattn_slow_wo_kernel<8, H, Q, 4> : fattn_slow_wo_kernel<8, H, Q, 2>)<<<grid, block, 0, s>>>(A); break;
-#undef FS
-        }
-    };
-    auto goh = [&](auto q) {
-        if (at.hd == 64) go(q, std::integral_constant<int, 64>{});
-        else go(q, std::integral_constant<int, 128>{});
-    };
-    if (qm == 2) goh(std::integral_constant<int, 2>{});
-    else if (qm == 1) goh(std::integral_constant<int, 1>{});
-    else goh(std::integral_constant<int, 0>{});
 }

@@ -18,11 +18,10 @@ pytestmark = pytest.mark.gpu
 DEFAULTS = {"attn3": 1, "attn_fd": 1, "fd_min": 32, "fd_nw": 8, "fd_min16": 256, "gemv_chain": 0, "gemv_nt": 1, "gemv_u": 8, "gemv_wpb": 4,
             "ksb_balance": 0, "ksb_blocks": 512, "attn_cap": 32, "prefill_attn": 1, "prompt_gemm": 1,
             "conv2": 1, "conv_splitk": 1, "kv_prefetch": 1, "fin_ksb": 0, "gemv_dummy": 2, "rowgemv": 27, "rowgemv_q4": 31, "sampler_kth": 1, "row_qkv_rp": 8,
-            "fattn_wo": 1, "fw_cheap": 0, "fw_delay": 0, "fattn_slow": 0, "fws_cap": 256, "fws_rp": 2}
+            "fattn_wo": 1, "fw_cheap": 0, "fw_delay": 0}
 
 DECODE_KNOBS = [{"attn3": 0}, {"attn3": 0, "attn_fd": 0}, {"fd_nw": 4}, {"fd_nw": 4, "fd_min": 16}, {"fd_nw": 16},
-                {"fd_min16": 16}, {"fd_nw": 16, "fd_min16": 16}, {"fattn_slow": 1}, {"fattn_slow": 1, "fws_cap": 16},
-                {"fattn_slow": 1, "fws_rp": 4}, {"fattn_slow": 1, "fws_cap": 16, "fws_rp": 4}, {"gemv_chain": 1}, {"gemv_nt": 0}, {"gemv_u": 4},
+                {"fd_min16": 16}, {"fd_nw": 16, "fd_min16": 16}, {"gemv_chain": 1}, {"gemv_nt": 0}, {"gemv_u": 4},
                 {"gemv_u": 2}, {"gemv_wpb": 8}, {"ksb_balance": 1}, {"ksb_blocks": 64}, {"attn_cap": 0},
                 {"kv_prefetch": 0}, {"fin_ksb": 4}, {"gemv_dummy": 0}, {"gemv_dummy": 1}, {"rowgemv": 0},
                 {"rowgemv": 1}, {"rowgemv": 2}, {"rowgemv": 3}, {"rowgemv": 7}, {"rowgemv": 31}, {"fattn_wo": 0}, {"fw_cheap": 1}, {"fw_delay": 100},
