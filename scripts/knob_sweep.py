@@ -1,7 +1,8 @@
 """Frame-time sweep of fm_tune knobs at S2-Pro shapes (B=1, graph-replayed frames).
 QUANT=int8|int4 quantizes the linears; each config also reports the decode GEMVs' average launch.
-Usage: python scripts/knob_sweep.py 'k1=v1,k2=v2' 'k1=v3' ...   (each arg is one config; the
-knobs of a config are reset to the first config's values before the next one is applied)."""
+Usage: python scripts/knob_sweep.py 'k1=v1,k2=v2' 'k1=v3' ...   (each arg is one config; every
+knob any config touches is reset before each config to the first config's value, or to its
+FmTuning default when the first config leaves it out)."""
 import os
 import sys
 import time
@@ -22,11 +23,22 @@ p = np.zeros((cfg.num_codebooks + 1, 64), np.int32)
 p[0] = np.random.default_rng(1).integers(16, cfg.semantic_begin_id, 64)
 sp = DualARModel.sampling(mask_im_end=True)
 confs = [dict(kv.split("=") for kv in a.split(",") if kv) for a in sys.argv[1:]] or [{}]
-base = {}
+# FmTuning's defaults (fm_kernels.h) for the knobs sweeps touch; a knob the first config sets takes
+# that value as its baseline instead
+DEFAULTS = {"attn3": 1, "attn_fd": 1, "fd_min": 32, "fd_nw": 8, "fd_min16": 256, "kv_prefetch": 1, "gemv_u": 8,
+            "gemv_wpb": 4, "fin_ksb": 0, "gemv_dummy": 2, "rowgemv": 27, "rowgemv_q4": 31, "sampler_kth": 1,
+            "row_qkv_rp": 8, "fattn_wo": 1, "fw_cheap": 0, "fw_delay": 0, "fw_prio": 0, "fast_tail": 1,
+            "fkv_prefetch": 0, "q_u": 4}
+base = {k: int(v) for k, v in confs[0].items()}
+touched = {k for c in confs for k in c}
+missing = sorted(k for k in touched if k not in base and k not in DEFAULTS)
+if missing:
+    sys.exit(f"no baseline for {missing}: give them in the first config")
 for rep in range(2):
     for c in confs:
+        for k in touched:  # every config starts from the baseline
+            native.tune(k, base.get(k, DEFAULTS.get(k)))
         for k, v in c.items():
-            base.setdefault(k, None)
             native.tune(k, int(v))
         m.use_graph(True)
         m.prefill(0, p, sp)
