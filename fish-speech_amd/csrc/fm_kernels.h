@@ -305,7 +305,11 @@ struct FmTuning {
     int rowgemv_q4 = 31;     // rowgemv's bits for weight-only int4 models (w1 || w3 too: int4 frame 3.06 -> 3.01 ms; bf16 4.07 -> 4.10, int8 3.11 -> 3.20 with it)
     int rowgemv = 27;        // batch-1 decode linears on the row-block GEMV (fm_rowgemv.hip): bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3,
                              // bit 3 the codebook head, bit 4 the first layers' wqkv (0: 16-row MFMA tiles; 3 -> 27: 4.066 -> 4.032 ms)
-    int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip)
+    int row_copies = 1;      // 1: fm_llm_finalize keeps a row-major copy of every linear the row-block GEMV can take, so any
+                             // rowgemv bits work later (bf16 S2-Pro: ~3.7 GB beside the packed tiles); 0: only the copies the
+                             // rowgemv / rowgemv_q4 bits in force at finalize select (w1 || w3 bf16 / int8: ~3.6 GB saved)
+    int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip); must be
+                             //    set (or pass_prepare) BEFORE fm_llm_finalize, which builds the pass weights
     int pass_prepare = 0;    // 1: build the persistent pass's weight copy at finalize even with pass_fast 0
     int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1), 5 (12 x 8, 4: K / V from the cache, 96 KiB ring), 6 (no loader: stream waves with PASS_SR-fragment register rings)
     int pass_mode = 0;       // developer: PassArgs::mode

@@ -1154,7 +1154,15 @@ template <typename T> struct Run {
     // one persistent launch for the whole fast pass (fm_pass.hip): batch 1, bf16, fm_tune pass_fast
     bool fast_pass_persistent(int n, int cc, bool with_head, const void* hidden) {
         if constexpr (sizeof(T) != 2) return false;
-        if (n != 1 || !m->pass_ok || !fm_tuning().pass_fast) return false;
+        if (n != 1 || !fm_tuning().pass_fast) return false;
+        if (!m->pass_ok) {  // pass_fast set after this model was finalised: its pass weights do not exist
+            static bool warned = false;
+            if (!warned)
+                fprintf(stderr, "fishmi: fm_tune pass_fast 1 has no effect on a model finalised without it "
+                                "(set pass_fast or pass_prepare before fm_llm_finalize); running the launch chain\n");
+            warned = true;
+            return false;
+        }
         const fm_model_config& c = m->c;
         const StackDims& f = m->fdm;
         PassArgs a{};
@@ -1626,6 +1634,11 @@ static void* pack_dev(fm_llm* m, const void* src, int rows, int cols) {
 
 // bf16 wo / w2 / wqkv whose shapes the row-block GEMV takes keep their row-major copy
 // (fm_rowgemv.hip; ~3.7 GB at S2-Pro beside the packed tiles the batched paths read)
+// fm_tune row_copies 0: a row-major copy only where the rowgemv bits in force at finalize use it
+static bool row_bits(fm_llm* m, int bits) {
+    const FmTuning& t = fm_tuning();
+    return t.row_copies || ((m->quant == FM_QUANT_INT4 ? t.rowgemv_q4 : t.rowgemv) & bits) != 0;
+}
 static bool row_keep(fm_llm* m, const std::string& n, int rows, int cols) {
     auto ends = [&](const char* suf) {
         const size_t L = strlen(suf);
@@ -1635,9 +1648,9 @@ static bool row_keep(fm_llm* m, const std::string& n, int rows, int cols) {
     const int qm = m->quant == FM_QUANT_INT8 ? 1 : (m->quant == FM_QUANT_INT4 ? 2 : 0);
     if (m->prec != FM_PREC_BF16 || rowgemv_u(cols, qm) == 0) return false;
     if (qm == 2 && (m->q4_gs % 8 || cols % m->q4_gs)) return false;
-    if (ends("attention.wo.weight") || ends("feed_forward.w2.weight")) return rows % 2 == 0;
-    if (n == "fast_output.weight") return rows % 8 == 0 && rowgemv_u(cols, qm) <= 8;
-    return ends("attention.wqkv.weight") && rows % 8 == 0 && rowgemv_u(cols, qm) <= 8;
+    if (ends("attention.wo.weight") || ends("feed_forward.w2.weight")) return rows % 2 == 0 && row_bits(m, 1);
+    if (n == "fast_output.weight") return rows % 8 == 0 && rowgemv_u(cols, qm) <= 8 && row_bits(m, 8);
+    return ends("attention.wqkv.weight") && rows % 8 == 0 && rowgemv_u(cols, qm) <= 8 && row_bits(m, 2 | 16);
 }
 
 static bool is_ffn_w13(const std::string& n) {
@@ -1668,7 +1681,7 @@ static void* pack_w13(fm_llm* m, const std::string& p, int inter, int dim) {
     // code words + (scale, zero) rows)
     const int qm = m->quant == FM_QUANT_INT8 ? 1 : (m->quant == FM_QUANT_INT4 ? 2 : 0);
     const bool rk = m->prec == FM_PREC_BF16 && inter % 4 == 0 && rowgemv_u(dim, qm) > 0 && rowgemv_u(dim, qm) <= 8 &&
-                    (qm != 2 || (m->q4_gs % 8 == 0 && dim % m->q4_gs == 0));
+                    (qm != 2 || (m->q4_gs % 8 == 0 && dim % m->q4_gs == 0)) && row_bits(m, 4);
     auto il4 = [&](const void* a1, const void* a3, size_t rb4) -> void* {  // rb4: bytes per row
         void* d = m->dalloc(2 * (size_t)inter * rb4, false);
         HIPCHK(hipMemcpy2DAsync(d, 8 * rb4, a1, 4 * rb4, 4 * rb4, inter / 4, hipMemcpyDeviceToDevice, m->stream));
@@ -2797,6 +2810,8 @@ int fm_tune(const char* key, int value) {
         } else if (k == "rowgemv_q4") {
             FMCHECK(value >= 0 && value <= 31, "rowgemv_q4 must be 0..31");
             t.rowgemv_q4 = value;
+        } else if (k == "row_copies") {
+            t.row_copies = value != 0;
         } else if (k == "rowgemv") {
             FMCHECK(value >= 0 && value <= 31, "rowgemv must be 0..31 (bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3, bit 3 fast head, bit 4 first-layer wqkv)");
             t.rowgemv = value;
@@ -2976,6 +2991,11 @@ int fm_llm_debug_vec(fm_llm* m, const char* name, int index, float* out, int64_t
         }
         void* p = k == "qkv" ? m->qkv : k == "att" ? m->att : k == "fh" ? m->fh : k == "act" ? m->act
                 : k == "fx" ? m->fx : k == "fx2" ? m->fx2 : k == "xl" ? m->xl : k == "xnl" ? m->xnl : nullptr;
+        if (k == "kc" || k == "vc") {  // slot 0's slow-layer `index` cache: [nkv][S][hd]
+            FMCHECK(index >= 0 && index < m->sd.n_layer, "layer out of range");
+            FMCHECK(n <= (int64_t)m->layer_stride, "n past the layer's cache");
+            p = (char*)(k == "kc" ? m->kc : m->vc) + (size_t)index * m->layer_stride * m->esz;
+        }
         FMCHECK(p, "unknown buffer: " + k);
         if (m->esz == 4) {
             HIPCHK(hipMemcpy(out, p, (size_t)n * 4, hipMemcpyDeviceToHost));

@@ -186,11 +186,22 @@ class _Vocoder:
             if it is None:
                 return
             v, w, done = it
+            # every item goes back on `ready` whatever happens, so the backlog drains and the
+            # request's done marker is delivered (a dead thread would leave this rank busy forever)
             if done:
-                v.close()
+                try:
+                    v.close()
+                except Exception as e:  # the stream's close failing ends nothing but its own context
+                    log.error("closing a vocoder stream failed: %r", e)
                 self.ready.put((v, None))
                 continue
-            self.ready.put((v, v.vocode(self.codec, w)))
+            try:
+                out = v.vocode(self.codec, w)
+            except Exception as e:
+                log.error("vocoder item failed: %r", e)
+                v.failed = True
+                out = WrappedGenerateResponse(status="error", response=e)
+            self.ready.put((v, out))
 
 
 class _Vocoding:
@@ -208,11 +219,11 @@ class _Vocoding:
     def vocode(self, codec, w):
         """(vocoder thread) the response with its PCM; after a codec error, the error once and the
         request's later samples dropped (its caller has its answer)"""
+        if self.failed:  # the caller has its error: nothing more of this request reaches it
+            return _DROP
         if w is None or w.status != "success" or not isinstance(w.response, GenerateResponse) \
                 or w.response.action != "sample" or w.response.codes is None:
             return w
-        if self.failed:
-            return _DROP
         r = w.response
         try:
             codes = np.asarray(r.codes)
@@ -226,7 +237,10 @@ class _Vocoding:
         except Exception as e:
             log.error("vocoding failed: %r", e)
             self.failed = True
-            self.close()
+            try:
+                self.close()
+            except Exception as e2:
+                log.error("closing the failed request's codec stream failed: %r", e2)
             return WrappedGenerateResponse(status="error", response=e)
         return WrappedGenerateResponse(status="success", response=dataclasses.replace(
             r, audio=np.ascontiguousarray(pcm, dtype=np.float32)))

@@ -187,8 +187,10 @@ def generate_long(*, model, text: str, tokenizer: Optional[P.FishTokenizer] = No
     the longest prefix its new prompt shares with what the slot already ran (the previous prompt
     plus the columns fed back while generating), and prefills only the rest (fm_llm_generate_at).
     The prompt tokens are the same, so the codes are the same up to the fp32 accumulation order of
-    the reused positions (decode-path vs prefill-path kernels; tests/test_gpu_engine.py).  It is
-    opt-in: the default is the reference's own re-prefill flow.
+    the reused positions: the decode GEMVs and the prompt GEMM sum K in different orders, so a
+    reused K / V row can differ from the re-prefilled one by an ulp (bf16).  The tests hold both
+    flows to the reference's own bf16 generate_long (tests/test_gpu_engine.py).  It is opt-in: the
+    default is the reference's own re-prefill flow.
 
     stream_frames > 0 (BASELINE config 5's streamed vocoder): each batch's codes are yielded as they
     are decoded, `stream_frames` columns at a time (GenerateResponse.stream = chunk index), instead of

@@ -299,6 +299,18 @@ class DualARModel:
             self.force(slot, None)
         return slow, fast
 
+    def read_cache(self, layer: int):
+        """Slot 0's slow-layer KV cache rows (developer hook fm_llm_debug_vec "kc" / "vc"):
+        k, v as float arrays (n_local_heads, max_seq_len, head_dim) of the stored values."""
+        c = self.cfg
+        n = c.n_local_heads * c.max_seq_len * c.head_dim
+        out = []
+        for name in (b"kc", b"vc"):
+            a = np.zeros(n, np.float32)
+            native.check(native.lib().fm_llm_debug_vec(self.h, name, int(layer), native.f32p(a), n))
+            out.append(a.reshape(c.n_local_heads, c.max_seq_len, c.head_dim))
+        return out[0], out[1]
+
     # ---- accounting / profiling --------------------------------------------------------
     def frame_bytes(self, n: int, pos: int) -> int:
         return int(native.lib().fm_llm_frame_bytes(self.h, n, pos))

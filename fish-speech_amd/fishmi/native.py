@@ -79,10 +79,16 @@ def lib():
     L = ctypes.CDLL(LIB_PATH)
     # build provenance: the library must have been compiled from the sources in this tree
     L.fm_source_hash.restype = ctypes.c_char_p
-    built, tree = L.fm_source_hash().decode(), tree_source_hash()
-    if built != tree and not os.environ.get("FISHMI_ALLOW_STALE"):
-        raise FishMIError(f"{LIB_PATH} was built from other sources (hash {built}, tree {tree}): "
-                          "rebuild it with `make -C fish-speech_amd`")
+    if not os.environ.get("FISHMI_ALLOW_STALE"):  # (the escape hatch skips the sources entirely)
+        built = L.fm_source_hash().decode()
+        try:
+            tree = tree_source_hash()
+        except OSError as e:
+            raise FishMIError(f"cannot check {LIB_PATH} against its sources ({e}): deploy the package with "
+                              "its Makefile, csrc/ and include/, or set FISHMI_ALLOW_STALE=1") from e
+        if built != tree:
+            raise FishMIError(f"{LIB_PATH} was built from other sources (hash {built}, tree {tree}): "
+                              "rebuild it with `make -C fish-speech_amd`")
     vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64
     f32 = ctypes.c_float
     pi32 = ctypes.POINTER(ctypes.c_int32)

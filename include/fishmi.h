@@ -181,8 +181,10 @@ int fm_llm_kernel_bench(fm_llm* h, const char* kernel_class, int reps, double* a
                         int64_t* launches, int64_t* bytes);
 int fm_llm_use_graph(fm_llm* h, int enable);
 /* developer hook: row 0 of an activation buffer of the decode path ("qkv", "att", "fh", "act",
-   "fx", "fx2", "xl", "xnl": bf16/fp32 storage as floats) or, for name "gran", op `index`'s vector
-   of the last persistent fast pass (fm_pass.hip exchange granules; n = its length) */
+   "fx", "fx2", "xl", "xnl": bf16/fp32 storage as floats), slot 0's KV cache of slow layer `index`
+   ("kc" / "vc": [n_local_heads][S][head_dim], n <= its size; the prefix-reuse identity tests) or,
+   for name "gran", op `index`'s vector of the last persistent fast pass (fm_pass.hip exchange
+   granules; n = its length) */
 int fm_llm_debug_vec(fm_llm* h, const char* name, int index, float* out, int64_t n);
 /* Teacher forcing on the PRODUCTION decode path (parity with the reference's own teacher-forced
    forward_generate / forward_generate_fast, llama.py:390-466, 798-827): while a slot is forced,
@@ -202,7 +204,9 @@ int fm_llm_read_logits(fm_llm* h, int slot, float* slow_logits, float* fast_logi
    "fd_nw_batched" 4|8|16, "attn_wo" 0|1,
    "batched_fused_attn" 0|1; batched linears "bstream" 0|1, "bstream_acc" 0|1, "bstream_chain" 0|1, "bstream_kparts" n, "bstream_nw" n, "bs_dummy" 0|1|2, "bs_qkv_slab" 0|1,
    "linear_u32" n, "linear_fill" n; prompt "prefill_attn", "prompt_gemm"; codec "conv2",
-   "conv_splitk"; "sampler_fast" 0|1, "rmsnorm_block" 0|1, "debug_ts" n.  They apply to launches
+   "conv_splitk"; "sampler_fast" 0|1, "rmsnorm_block" 0|1, "debug_ts" n; batch-1 row-block GEMV
+   "rowgemv" / "rowgemv_q4" bits, "row_copies" 0|1 (0: finalize keeps only the row-major weight
+   copies those bits select).  They apply to launches
    recorded after the call (graphs captured earlier keep theirs). */
 int fm_tune(const char* key, int value);
 /* developer hook ("debug_ts" armed): per-block records of 8 words {tag = N<<32 | blockIdx.y<<16 |

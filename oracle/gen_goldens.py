@@ -1066,6 +1066,60 @@ def cmd_engine():
     print("engine:", [o.action for o in outs], [res[k].shape for k in res if k.startswith("codes_")])
 
 
+def cmd_engine_bf16():
+    """generate_long (inference.py:523-733) in bf16 -- the reference's production precision -- on
+    the engine golden's request, recording what each batch's generate() saw: the encoded whole
+    conversation (its prompt) and every emitted column.  Each batch is then replayed teacher-forced
+    (teacher_forced above: the reference's own prefill + decode_one_token_ar forwards with its emitted
+    columns) by the bf16 model and by the fp32 model on the same columns, so the test can hold the
+    native reused-prefix flow (fm_llm_generate_at) to the reference's own bf16-vs-fp32 error batch by
+    batch, instead of to bit-identity with another native flow."""
+    import copy as _copy
+
+    from fish_speech.models.text2semantic import inference
+    from fish_speech.tokenizer import FishTokenizer
+
+    cfg = _copy.deepcopy(LLM_A_CONFIG)
+    cfg["text_config"]["max_seq_len"] = 2560
+    g = np.load(os.path.join(GOLD, "engine.npz"))
+    tok = FishTokenizer(os.path.join(GOLD, "tok_tiny"))
+    model = build_llm(cfg, None, seed=11, log2_half=3).to(torch.bfloat16)
+    model.tokenizer = tok
+    seen = []
+    real_generate = inference.generate
+
+    def recording_generate(*, model, prompt, **kw):  # instrumentation only: the reference's generate runs
+        y = real_generate(model=model, prompt=prompt, **kw)
+        seen.append((prompt.clone(), y.clone()))
+        return y
+
+    inference.generate = recording_generate
+    try:
+        outs = list(inference.generate_long(
+            model=model, device="cpu", decode_one_token=inference.decode_one_token_ar, text=str(g["text"]),
+            max_new_tokens=7, top_p=0.9, top_k=1, temperature=0.7, chunk_length=30,
+            prompt_text=["ref a", "<|speaker:1|>ref b"],
+            prompt_tokens=[torch.from_numpy(g["ptok0"]), torch.from_numpy(g["ptok1"])]))
+    finally:
+        inference.generate = real_generate
+    m32 = build_llm(cfg, None, seed=11, log2_half=3).to(torch.float32)
+    res = {"actions": np.array(json.dumps([o.action for o in outs])), "n_batches": len(seen)}
+    for i, (prompt, y) in enumerate(seen):
+        T = prompt.shape[1]
+        n = y.shape[1] - T
+        slow, fast, _ = teacher_forced(model, y, T, n, torch.bfloat16)
+        s32, f32, _ = teacher_forced(m32, y, T, n, torch.float32)
+        res[f"prompt_{i}"] = prompt.numpy().astype(np.int32)
+        res[f"cols_{i}"] = y[:, T:].numpy().astype(np.int32)
+        res[f"slow_{i}"], res[f"fast_{i}"] = slow, fast
+        res[f"slow32_{i}"], res[f"fast32_{i}"] = s32, f32
+    for i, o in enumerate([o for o in outs if o.action == "sample"]):
+        res[f"codes_{i}"] = o.codes.numpy().astype(np.int32)
+    np.savez_compressed(os.path.join(GOLD, "engine_bf16.npz"), **res)
+    print("engine_bf16:", [o.action for o in outs],
+          [(res[f"prompt_{i}"].shape[1], res[f"cols_{i}"].shape[1]) for i in range(len(seen))])
+
+
 def cmd_engine_clone():
     """BASELINE config 5's chain at tiny shapes: reference audio -> the reference's own DAC.encode
     (codec_enc_tiny weights, fp32; vq_manager.py:24-52) -> those codes as the voice-clone prompt of
@@ -1104,7 +1158,7 @@ if __name__ == "__main__":
     cmds = sys.argv[1:] or ["all"]
     if cmds == ["all"]:
         cmds = ["ops", "llm", "codec", "codec_full", "codec_long", "codec_enc", "codec_enc_full",
-                "codec_enc_long", "codec_keys", "llm_wide", "llm_int8", "llm_wide_int8", "prompt", "engine",
+                "codec_enc_long", "codec_keys", "llm_wide", "llm_int8", "llm_wide_int8", "prompt", "engine", "engine_bf16",
                 "engine_clone"]
     for c in cmds:
         globals()[f"cmd_{c}"]()

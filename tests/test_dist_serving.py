@@ -256,3 +256,68 @@ def test_wire_roundtrip():
     e = response_from_wire(unpack(pack(response_to_wire(engine.WrappedGenerateResponse("error", ValueError("x"))))))
     assert e.status == "error" and isinstance(e.response, ValueError) and str(e.response) == "x"
     assert response_from_wire(unpack(pack(response_to_wire(None)))) is None
+
+
+def test_vocoder_thread_survives_failing_stream_close():
+    """the per-rank vocoder thread must deliver every item even when a codec stream's
+    close() raises (on the request's done marker, and again after a decode error): the backlog drains
+    to 0, each done marker arrives, the thread stays alive, and after an error nothing more of that
+    request reaches its caller."""
+    from fishmi import engine
+    from fishmi.dist_serving import _DROP, _Vocoder, _Vocoding
+
+    class BadCloseVocoder(ScriptedVocoder):
+        def open_stream(self):
+            voc = self
+
+            class _S:
+                def decode_chunk(self, codes):
+                    return voc.decode_codes(codes)
+
+                def close(self):
+                    raise RuntimeError("injected close failure")
+
+            return _S()
+
+    def sample(stream, k):
+        return engine.WrappedGenerateResponse("success", engine.GenerateResponse(
+            "sample", np.full((3, 2), k, np.int32), "t", stream))
+
+    voc = _Vocoder(BadCloseVocoder(fail_at=5))
+    got = {}
+
+    class Sink:
+        def __init__(self, name):
+            self.name = name
+
+        def put(self, w):
+            got.setdefault(self.name, []).append(w)
+
+    a, b = _Vocoding(Sink("a"), voc), _Vocoding(Sink("b"), voc)
+    for k in range(3):  # a: a 3-chunk stream, then its done marker (its close raises)
+        a.put(sample(k, k))
+    voc.submit(a, None, done=True)
+    for k in range(3):  # b: chunk 1 hits the failing decode (call 5), its later chunks are dropped
+        b.put(sample(k, 10 + k))
+    b.put(engine.WrappedGenerateResponse("success", engine.GenerateResponse("next")))
+    voc.submit(b, None, done=True)
+    finished = []
+
+    def deliver(v, w):
+        if w is None:
+            finished.append(v)
+        elif w is not _DROP:
+            v.inner.put(w)
+
+    t0 = time.time()
+    while voc.drain(deliver) > 0:
+        assert time.time() - t0 < 10, "vocoder backlog never drained"
+        time.sleep(0.01)
+    assert finished == [a, b]
+    assert voc.th.is_alive()
+    assert [w.status for w in got["a"]] == ["success"] * 3
+    assert [w.status for w in got["b"]] == ["success", "error"]
+    assert "injected codec failure" in str(got["b"][1].response)
+    voc.close()
+    voc.th.join(timeout=5)
+    assert not voc.th.is_alive()
