@@ -465,6 +465,45 @@ def pmc_gemv_traffic(timeout_s=150):
         f"{vals['WRITE_SIZE'] / 1e6:.3f} MB written per decode-linear launch (gemv_kernel, rowgemv_kernel)")
 
 
+def pmc_codec_mfma(codec_ms, timeout_s=120):
+    """MFMA utilisation of the codec decode from the hardware counters, measured in this run: one
+    rocprofv3 --pmc pass (SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_MOPS_BF16, SQ_ACTIVE_INST_VALU,
+    SQ_WAVE_CYCLES, GRBM_GUI_ACTIVE) over scripts/codec_pmc_probe.py (config 2's 216-frame decode) in
+    a child process.  mfma_busy is rocprofiler-compute's MfmaUtil: busy MFMA cycles over (elapsed
+    cycles x 1024 SIMDs), per kernel family; it is set beside the FLOP-derived frac (see note)."""
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import codec_pmc_probe as P
+
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return {"note": "rocprofv3 not on PATH"}
+    d = tempfile.mkdtemp(prefix="fishmi_cpmc_", dir="/tmp")
+    cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", *P.COUNTERS, "--output-format", "csv", "-d", d,
+           "-o", "pmc", "--", sys.executable, os.path.join(ROOT, "scripts", "codec_pmc_probe.py")]
+    r = subprocess.run(cmd, cwd="/tmp", stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    csvs = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if r.returncode != 0 or not csvs:
+        return {"note": f"rocprofv3 --pmc failed (rc {r.returncode}): {r.stderr[-300:].decode(errors='replace')}"}
+    fams = P.summarise(csvs[0])
+    shutil.rmtree(d, ignore_errors=True)
+    a = fams.get("all", {})
+    el_ms = a.get("elapsed_Mcycles", 0) * 1e6 / 2.4e9 * 1e3
+    return {"mfma_busy": a.get("mfma_busy"), "per_kernel": {k: v for k, v in fams.items() if k != "all"},
+            "bf16_mfma_gflop_counted": a.get("bf16_mfma_gflop"),
+            "elapsed_ms_at_2.4GHz": round(el_ms, 3),
+            "note": "mfma_busy = sum SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) over one "
+                    "config-2 codec decode (rocprofiler-compute MfmaUtil).  Busy cycles = MOPS x 512 / 1024 "
+                    "(1024 bf16 flop per busy cycle per SIMD, the dense peak rate).  It reads below the "
+                    "FLOP-derived frac because GRBM_GUI_ACTIVE spans each counter-serialised dispatch's ramp "
+                    f"and tail ({el_ms:.2f} ms at 2.4 GHz vs {codec_ms:.2f} ms unprofiled) and above it by the "
+                    "padded MFMA work (counted vs analytic flops)"}
+
+
 def stream_peak_gbps(nbytes=2 << 30, reps=10):
     """Measured HBM stream peak (SURVEY.md §8d's STREAM-like figure beside the vendor 8 TB/s):
     libfishmi's fm_stream_peak: the best of several non-temporal read streams (register float4 and
@@ -594,6 +633,9 @@ def main():
     codec.decode_codes(np.zeros((ccfg.n_codebooks + 1, args.frames), np.int32))
     ms1, n1, fl1 = codec.profile()
     codec_tflops = (fl1 - fl0) / ((ms1 - ms0) * 1e-3) / 1e12
+    codec_pmc = {"mfma_busy": None, "note": "not measured (--no-pmc or N>1)"}
+    if rank == 0 and world == 1 and not args.no_pmc:
+        codec_pmc = pmc_codec_mfma(ms1 - ms0)
 
     thr = throughput_leg(llm, codec, cfg, args.batch, args.batch_frames, args.waves, sync, dist, world) \
         if args.batch > 0 else None
@@ -670,7 +712,7 @@ def main():
                                "eager_event_class_ms_per_frame": {k: round(v, 4) for k, v in cls_ms.items()}},
             "codec_roofline": {"bound": "mfma", "achieved": round(codec_tflops, 2),
                                "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
-                               "frac": round(codec_tflops / BF16_DENSE_TFLOPS, 4)},
+                               "frac": round(codec_tflops / BF16_DENSE_TFLOPS, 4), **codec_pmc},
             "throughput": thr,
             "encode": enc,
             "longform": longf,
