@@ -183,36 +183,42 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
         const T* dsrc = a.W + (a.dummy_tail == 2 ? (size_t)((blockIdx.x * 8 + wave) & 255) % ((size_t)T_ * S) * 512 : 0);
         fa[(t % TPI) * SPW + j] = F::template load_w<true>(past ? dsrc : wbase + ((size_t)tt * S + jj) * 512, lane);
     };
+    // X operands.  PRO_PRENORM also loads the norm weight and the producer's per-tile sums of squares
+    // here, laid out [R][K/16] by bsacc's EPI_SLABFIN (rows w + NW * i of wave w, tiles lane + 64 * jj;
+    // host: R <= 32, NW == 8, K / 16 <= 192).  a.xfirst (default): these go out before the weight ring,
+    // so the first MFMA waits for the first weight fragment, not for the whole ring (in-order vmcnt):
+    // B=32 frame 6.48 -> 6.36 ms.  (A per-tile epilogue by each tile's last-arriving wave instead of
+    // the one barrier + block epilogue measured 7.8 ms: one wave's stores are issue-bound.)
+    typename F::f xa[SPW], xb[SPW], wn[PRO == PRO_PRENORM ? SPW : 1];
+    float ssv[PRO == PRO_PRENORM ? 12 : 1];
+    auto load_x = [&]() {
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int jj = j < nst ? j : nst - 1;
+            const size_t k = (size_t)(wa + jj) * 32 + 8 * g;
+            xa[j] = F::load(a.X + (size_t)ra * a.ldx + k);
+            xb[j] = F::load(a.X + (size_t)rb * a.ldx + k);
+            if constexpr (PRO == PRO_PRENORM) wn[j] = F::load(a.nw + k);
+        }
+        if constexpr (PRO == PRO_PRENORM) {
+            const int nt = a.K >> 4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int jj = 0; jj < 3; ++jj) {
+                    const int row = wave + 8 * i, t = lane + 64 * jj;
+                    const bool ok = row < a.R && t < nt;
+                    const float v = a.ss_in[(size_t)(row < a.R ? row : 0) * nt + (ok ? t : 0)];  // [R][K/16]: coalesced
+                    ssv[i * 3 + jj] = ok ? v : 0.f;
+                }
+        }
+    };
+    if (a.xfirst) load_x();
 #pragma unroll
     for (int t = 0; t < TPI; ++t)
 #pragma unroll
         for (int j = 0; j < SPW; ++j) issue(t, j);
-    // X operands (issued before or after the weight ring: no measurable difference).  PRO_PRENORM also
-    // loads the norm weight and the producer's per-tile sums of squares here, laid out [R][K/16] by
-    // bsacc's EPI_SLABFIN (rows w + NW * i of wave w, tiles lane + 64 * jj; host: R <= 32, NW == 8,
-    // K / 16 <= 192)
-    typename F::f xa[SPW], xb[SPW], wn[PRO == PRO_PRENORM ? SPW : 1];
-#pragma unroll
-    for (int j = 0; j < SPW; ++j) {
-        const int jj = j < nst ? j : nst - 1;
-        const size_t k = (size_t)(wa + jj) * 32 + 8 * g;
-        xa[j] = F::load(a.X + (size_t)ra * a.ldx + k);
-        xb[j] = F::load(a.X + (size_t)rb * a.ldx + k);
-        if constexpr (PRO == PRO_PRENORM) wn[j] = F::load(a.nw + k);
-    }
-    float ssv[PRO == PRO_PRENORM ? 12 : 1];
-    if constexpr (PRO == PRO_PRENORM) {
-        const int nt = a.K >> 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 3; ++jj) {
-                const int row = wave + 8 * i, t = lane + 64 * jj;
-                const bool ok = row < a.R && t < nt;
-                const float v = a.ss_in[(size_t)(row < a.R ? row : 0) * nt + (ok ? t : 0)];  // [R][K/16]: coalesced
-                ssv[i * 3 + jj] = ok ? v : 0.f;
-            }
-    }
+    if (!a.xfirst) load_x();
     if constexpr (PRO == PRO_PRENORM) {
         // 1/rms of each X row (wave w: rows w, w + 8, w + 16, w + 24), then every lane's two rows from LDS
         __shared__ float rs_s[32];
@@ -281,7 +287,63 @@ __global__ __launch_bounds__(512) void bsacc_kernel(BstreamArgs<T> a) {
         }
     };
     // epilogue over the block's tiles: C/D map of a 16x16 accumulator: row = 4*(lane>>4)+i, col = lane&15
-    if constexpr (EPI == EPI_SWIGLU8) {
+    // a.vec_epi: one item = 4 consecutive rows (one accumulator register quad) of one column: NW
+    // 16-byte LDS reads (consecutive lanes, consecutive quads: no bank conflict) summed elementwise in
+    // wave order (the scalar form's fp32 order: bit-identical), one 8 / 16-byte store
+    const bool vec = a.vec_epi && EPI != EPI_SLABFIN && (a.N & 15) == 0 && (a.ldy & 3) == 0;
+    auto quad = [&](int t, int cg, int ln) {
+        f32x4_t v = bred[((t * NW) * 2 + cg) * 64 + ln];
+        for (int w = 1; w < NW; ++w) {
+            const f32x4_t p = bred[((t * NW + w) * 2 + cg) * 64 + ln];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] += p[i];
+        }
+        return v;
+    };
+    if (vec && EPI == EPI_SWIGLU8) {
+        const int no = ntl * 64;  // (tile, column group, gate quad, column)
+        for (int o = threadIdx.x; o < no; o += blockDim.x) {
+            const int t = o >> 6, cg = (o >> 5) & 1, gq = (o >> 4) & 1, c16 = o & 15, col = 16 * cg + c16;
+            if (col >= a.R) continue;
+            f32x4_t vg = quad(t, cg, 16 * gq + c16), vu = quad(t, cg, 16 * (gq + 2) + c16);
+            const int tile = t0 + t;
+            float y[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float g_ = vg[i], u_ = vu[i];
+                if (a.wscale) {
+                    g_ = rnd<T>(rnd<T>(g_) * ld(a.wscale, tile * 16 + 4 * gq + i));
+                    u_ = rnd<T>(rnd<T>(u_) * ld(a.wscale, tile * 16 + 8 + 4 * gq + i));
+                }
+                y[i] = rnd<T>(silu_b(rnd<T>(g_))) * rnd<T>(u_);
+            }
+            store4<T>(a.Y + (size_t)col * a.ldy + tile * 8 + 4 * gq, y);
+        }
+    } else if (vec) {
+        const int no = ntl * 128;  // (tile, column group, row quad, column)
+        for (int o = threadIdx.x; o < no; o += blockDim.x) {
+            const int t = o >> 7, cg = (o >> 6) & 1, q = (o >> 4) & 3, c16 = o & 15, col = 16 * cg + c16;
+            if (col >= a.R) continue;
+            const f32x4_t v = quad(t, cg, 16 * q + c16);
+            const int n = (t0 + t) * 16 + 4 * q;
+            if constexpr (EPI == EPI_SLAB) {
+                *reinterpret_cast<f32x4_t*>(a.Yf + ((size_t)kp * a.R + col) * a.ldy + n) = v;
+            } else {
+                float y[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float x = v[i];
+                    if (a.wscale) x = rnd<T>(rnd<T>(x) * ld(a.wscale, n + i));
+                    if (a.bias) x += ld(a.bias, n + i);
+                    y[i] = EPI == EPI_STORE ? x : rnd<T>(x);
+                }
+                if constexpr (EPI == EPI_STORE)
+                    store4<T>(a.Y + (size_t)col * a.ldy + n, y);
+                else
+                    *reinterpret_cast<f32x4_t*>(a.Yf + (size_t)col * a.ldy + n) = (f32x4_t){y[0], y[1], y[2], y[3]};
+            }
+        }
+    } else if constexpr (EPI == EPI_SWIGLU8) {
         const int no = ntl * 8 * a.R;
         for (int o = threadIdx.x; o < no; o += blockDim.x) {
             const int t = o / (8 * a.R), oo = o - t * 8 * a.R;
@@ -688,6 +750,8 @@ template <typename T> bool launch_bstream(hipStream_t s, const BstreamArgs<T>& a
     BstreamArgs<T> a = a0;
     a.kparts = p.kparts;
     a.dummy_tail = fm_tuning().bs_dummy;
+    a.xfirst = fm_tuning().bs_xfirst;
+    a.vec_epi = fm_tuning().bs_vec_epi;
     if (p.acc) {
         if constexpr (sizeof(T) == 2) {
             FMCHECK(epi != EPI_SWIGLU8 || a.N % 16 == 0, "bsacc: SwiGLU8 needs whole interleaved tiles");

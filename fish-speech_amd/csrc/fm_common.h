@@ -43,6 +43,17 @@ template <typename T> __device__ __forceinline__ void st(T* p, size_t i, float v
     else p[i] = v;
 }
 
+// 4 consecutive elements rounded to T (8 B for bf16, 16 B for float), p aligned to that size
+template <typename T> __device__ __forceinline__ void store4(T* p, const float (&v)[4]) {
+    if constexpr (is_bf16<T>::value) {
+        const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+    } else {
+        *reinterpret_cast<f32x4_t*>(p) = (f32x4_t){v[0], v[1], v[2], v[3]};
+    }
+}
+
 // 8 consecutive elements (16 B for bf16, 32 B for float), p 16-byte aligned
 template <typename T> __device__ __forceinline__ void load8(const T* p, float (&o)[8]) {
     if constexpr (is_bf16<T>::value) {

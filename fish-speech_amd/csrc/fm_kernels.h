@@ -292,6 +292,8 @@ struct FmTuning {
     int chain_max = 4;       // gemv_chain: GEMVs per launch at most (2..4)
     int chain_sleep = 4;     // gemv_chain: s_sleep argument between a waiting block's polls (1, 4 or 16)
     int gemv_chain = 0;      // 1: batch-1 decode runs wo -> w1||w3 -> w2 -> next qkv as one launch (gemv_chain_kernel)
+    int bs_xfirst = 1;       // bsacc: X operands before the weight ring (B=32 frame 6.48 -> 6.36 ms)
+    int bs_vec_epi = 1;      // bsacc: 4-row epilogue items (bit-identical to the scalar epilogue; B=32 frame 6.31 -> 6.18 ms)
     int bsacc_kparts = 0;    // developer: force the K parts of the batched split-K (slab) linears (0: bsacc_plan's pick)
     int q_u = 4;             // int8 / int4 decode GEMV: ring units in flight per wave (2, 4, 8, 16; int8 frame 3.79 -> 3.59 ms at 8 -> 4)
     int fin8 = 1;            // finalize_norm: all eight K parts' slab loads in one round trip (0: two batches of four)
@@ -497,6 +499,8 @@ template <typename T> struct BstreamArgs {
     float* ss_out = nullptr;
     int* tickets = nullptr;
     int dummy_tail = 0;  // bsacc: ring slots past the block's tiles / steps load one cached fragment
+    int xfirst = 1;      // bsacc: X (and the PRENORM operands) issued before the weight ring (fm_tune bs_xfirst)
+    int vec_epi = 1;     // bsacc: epilogue items of 4 rows (16-byte LDS reads, 8 / 16-byte stores; fm_tune bs_vec_epi)
 };
 struct BstreamPlan {
     bool ok = false;

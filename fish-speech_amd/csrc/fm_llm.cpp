@@ -2778,6 +2778,10 @@ int fm_tune(const char* key, int value) {
         } else if (k == "bstream_nw") {
             FMCHECK(value >= 0 && value <= 16, "bstream_nw must be in [0, 16]");
             t.bstream_nw = value;
+        } else if (k == "bs_xfirst") {
+            t.bs_xfirst = value != 0;
+        } else if (k == "bs_vec_epi") {
+            t.bs_vec_epi = value != 0;
         } else if (k == "bsacc_kparts") {
             FMCHECK(value == 0 || value == 1 || value == 2 || value == 4 || value == 8, "bsacc_kparts must be 0, 1, 2, 4 or 8");
             t.bsacc_kparts = value;

@@ -89,6 +89,12 @@ def lib():
         if built != tree:
             raise FishMIError(f"{LIB_PATH} was built from other sources (hash {built}, tree {tree}): "
                               "rebuild it with `make -C fish-speech_amd`")
+    # developer: FISHMI_TUNE="key=value,..." applies fm_tune knobs at load (run a test suite under a variant)
+    for kv in filter(None, os.environ.get("FISHMI_TUNE", "").split(",")):
+        k, v = kv.split("=")
+        L.fm_tune.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        if L.fm_tune(k.strip().encode(), int(v)) != 0:
+            raise FishMIError(f"FISHMI_TUNE: fm_tune({k}, {v}) failed")
     vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64
     f32 = ctypes.c_float
     pi32 = ctypes.POINTER(ctypes.c_int32)

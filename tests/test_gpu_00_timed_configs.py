@@ -124,6 +124,9 @@ def test_long_context_4_layers_bf16_vs_reference(golden):
     _teacher_case("llm_long4_bf16.npz", golden)
 
 
+_RAGGED_LOGITS = {}  # (prefill, chain, slab) -> the default forms' logits (the older-forms case compares)
+
+
 @pytest.fixture
 def knob():
     from fishmi import native
@@ -139,19 +142,24 @@ def knob():
         native.tune(k, d)
 
 
-@pytest.mark.parametrize("prefill,chain,slab", [("batch", 0, 1), ("single", 0, 1), ("batch", 1, 1), ("batch", 0, 0)])
-def test_config3_ragged_32_slots_bf16_vs_reference(prefill, chain, slab, golden, knob):
+@pytest.mark.parametrize("prefill,chain,slab,older", [("batch", 0, 1, 0), ("single", 0, 1, 0), ("batch", 1, 1, 0),
+                                                      ("batch", 0, 0, 0), ("batch", 0, 1, 1)])
+def test_config3_ragged_32_slots_bf16_vs_reference(prefill, chain, slab, older, golden, knob):
     """32 distinct prompts (16..256 tokens) in permuted slots: first frame from prefill_batch (the
     serving tick's path) or per-slot prefill, then batched decode frames (bsacc_kernel linears,
     finalize_norm, attn_fd at 32 different positions), every slot teacher-forced with its own
     reference columns.  Pooled over slots, the error is within BF16_RATIO x the reference's.
     chain = 1: the fm_tune bstream_chain variant (bsacc SLABFIN / PRENORM, no finalize_norm);
     slab = 0: the QKV projection's own STORE epilogue instead of K-part slabs summed by the attention
-    (fm_tune bs_qkv_slab)."""
+    (fm_tune bs_qkv_slab); older = 1: bsacc's round-5 forms (X loaded after the weight ring, the
+    one-output-per-thread epilogue: fm_tune bs_xfirst 0, bs_vec_epi 0), whose logits must equal the
+    default's bit for bit (same loads, same fp32 sums in the same order)."""
     from fishmi.llm import DualARModel
 
     knob("bstream_chain", chain, 0)
     knob("bs_qkv_slab", slab, 1)
+    knob("bs_xfirst", 1 - older, 1)
+    knob("bs_vec_epi", 1 - older, 1)
     g = golden("llm_ragged_bf16.npz")
     cfg = _cfg(g)
     B = int(g["lens"].size)
@@ -184,6 +192,12 @@ def test_config3_ragged_32_slots_bf16_vs_reference(prefill, chain, slab, golden,
             m.force(s, None)
         m.close()
     rows = g["slow_rows"]
+    key = (prefill, chain, slab)
+    if older:  # the default forms' logits of the same run, bit for bit
+        np.testing.assert_array_equal(slow, _RAGGED_LOGITS[key][0])
+        np.testing.assert_array_equal(fast, _RAGGED_LOGITS[key][1])
+    else:
+        _RAGGED_LOGITS[key] = (slow, fast)
     st = bf16_vs_reference(slow.reshape(B * n, -1)[:, rows], fast[:, :, -1:].reshape(B * n, 1, -1),
                            bits_to_f32(g["slow_logits_bits"]).reshape(B * n, -1),
                            bits_to_f32(g["fast_last_bits"]).reshape(B * n, 1, -1),
