@@ -310,14 +310,6 @@ struct FmTuning {
     int row_copies = 1;      // 1: fm_llm_finalize keeps a row-major copy of every linear the row-block GEMV can take, so any
                              // rowgemv bits work later (bf16 S2-Pro: ~3.7 GB beside the packed tiles); 0: only the copies the
                              // rowgemv / rowgemv_q4 bits in force at finalize select (w1 || w3 bf16 / int8: ~3.6 GB saved)
-    int pass_fast = 0;       // 1: batch-1 bf16 fast-model passes as one persistent launch each (fm_pass.hip); must be
-                             //    set (or pass_prepare) BEFORE fm_llm_finalize, which builds the pass weights
-    int pass_prepare = 0;    // 1: build the persistent pass's weight copy at finalize even with pass_fast 0
-    int pass_cfg = 0;        // pass_kernel ring: 0 (8 slots x 8 KiB, 4 fills in flight), 1 (4 x 16, 2), 2 (8 x 8, 5), 3 (8 x 8, 3), 4 (4 x 16, 1), 5 (12 x 8, 4: K / V from the cache, 96 KiB ring), 6 (no loader: stream waves with PASS_SR-fragment register rings)
-    int pass_mode = 0;       // developer: PassArgs::mode
-    int pass_nap = 2;        // PassArgs::sweep_nap
-    int pass_prefetch = 12;  // PassArgs::prefetch
-    int pass_spin = 0;       // developer: hand-off poll bound exponent (0: default 2^20 polls)
     unsigned long long* dbg = nullptr;  // device buffer of per-block phase timestamps (debug_ts)
 };
 FmTuning& fm_tuning();
@@ -409,67 +401,6 @@ template <typename T> struct GemvChainArgs {
     int sleep;  // s_sleep between polls (fm_tune chain_sleep)
 };
 template <typename T> void launch_gemv_chain(hipStream_t s, const GemvChainArgs<T>& c);
-
-// ---- persistent batch-1 decode pass (fm_pass.hip) --------------------------------------------
-// One launch runs a whole stack pass at batch 1 -- every layer's QKV, attention, Wo, W1||W3, W2
-// (TransformerBlock.forward, llama.py:838-843) and the head -- with one workgroup per CU.  Each op
-// is split by output rows over the workgroups (whole rows, no split K); a loader wave streams the
-// workgroup's rows (row-major copies, 1 KiB fragments of one row) by LDS-DMA into a ring of 16 KiB
-// slots that runs ahead ACROSS op boundaries, consumer waves take the dot products from the ring,
-// and exchange waves swap each op's output vector between workgroups (8-byte {tag, bf16 pair}
-// granules, write-through, one flat sweep) and build the next op's input row in LDS.
-struct PassLayer {
-    const bf16_t *bqkv, *bo, *an, *fn, *qn, *kn;  // biases (or null) and norm weights
-};
-struct PassArgs {
-    // weights: one allocation, layer l at wbase + l * w_layer: wqkv [nqkv][dim], then wo [dim][nq] at
-    // off_wo, w13 [2 * inter][dim] at off_w13 (rows w1_j, w3_j interleaved), w2 [dim][inter] at off_w2
-    // (elements; address arithmetic only, so the streaming waves never load a pointer)
-    const bf16_t* wbase;
-    size_t w_layer, off_wo, off_w13, off_w2;
-    const PassLayer* layers;  // device table [nlayer] (read by the exchange waves only)
-    int nlayer, dim, nq, nqkv, inter, nh, nkv, hd, qk_norm, nhead;
-    float eps, scale;
-    int nop;        // ops run: 4 per layer (+ 1 head); the last layer of a head-less pass stops after QKV
-    int tail_attn;  // the pass ends in a QKV: workgroup 0 still runs that layer's attention (KV store)
-    const bf16_t* x_in;       // input row, or a table gathered by xidx[xidx_col] (clamped to xidx_rows)
-    const int32_t* xidx;
-    int xidx_col, xidx_rows;
-    const bf16_t* head;       // [nhead][dim] row-major (null: no head)
-    const bf16_t* hnorm;
-    float* logits;            // [nhead]: round(head . norm(x)) as fp32
-    bf16_t *kc, *vc;          // fast cache [slot][layer][kv][S][hd]
-    size_t slot_stride, layer_stride;
-    int S, cpos;
-    const int* row_slot;
-    const float* rope;        // [S][hd/2][2]
-    unsigned long long* gran; // [ops][gran_stride] exchange granules
-    int gran_stride;
-    unsigned* sync;           // [0] generation, [32] arrival counter (both survive launches)
-    int* err;                 // set when a hand-off wait timed out
-    int nwg;                  // workgroups (one per CU)
-    int spin_log2;            // each hand-off wait gives up after 2^spin_log2 polls (0: 2^16)
-    int sweep_nap;            // s_sleep between a sweep's polls of the granules still missing (1 .. 32)
-    int mode;                 // developer timing modes (fm_tune pass_mode; results wrong): 1 consumers skip the
-                              // input-row wait, 2 consumers skip the dot products too
-    unsigned long long* dbg;  // developer phase stamps (fm_tune debug_ts) or null
-    int off_ring, off_xbuf, off_resx, off_resh, off_raw, off_kvs, off_red, off_sc, off_opt, off_lyt, off_attc,
-        off_flg, off_junk, off_dbg, off_wtab;  // LDS byte offsets (pass_lds)
-    int prefetch;  // fills past the ring pulled into L2 while the ring is full (0: none)
-};
-constexpr int PASS_NWM = 4;    // exchange waves per workgroup
-constexpr int PASS_NC = 4;     // consumer waves per workgroup (plus one loader wave)
-constexpr int PASS_RING_KB = 64;  // LDS weight ring (fm_tune pass_cfg picks its slots x fill size)
-constexpr int PASS_SR = 48;       // pass_cfg 6: register-ring fragments per stream wave
-struct PassLds {
-    int ring, xbuf, resx, resh, raw, kvs, red, sc, opt, lyt, attc, flg, junk, dbg, wtab;
-    size_t bytes;
-};
-PassLds pass_lds(int kmax, int dim, int nqkv, int nkv, int S, int hd, int maxrows, int nop);
-int pass_maxrows_for(int nqkv, int dim, int inter, int nhead, int nwg);
-bool pass_shapes_ok(int dim, int nq, int nqkv, int inter, int nhead, int nh, int nkv, int hd, int S, int nwg);
-void pass_init();  // kernel attributes (> 64 KiB LDS), outside any capture
-void launch_pass(hipStream_t s, const PassArgs& a);
 
 // ---- batched decode weight streaming with register-resident X, 8 < R <= 32 (fm_bstream.hip) ---
 template <typename T> struct BstreamArgs {

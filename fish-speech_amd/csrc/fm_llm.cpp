@@ -138,18 +138,6 @@ struct fm_llm {
     unsigned* chain_cnt = nullptr;  // [GEMV_CHAIN_WORDS] arrival counters (zeroed; each launch re-zeroes them)
     int* chain_err = nullptr;       // a chain wait timed out
     int* h_chain_err = nullptr;     // pinned copy, read after the host's stream sync
-    // persistent batch-1 fast passes (fm_pass.hip): the fast stack's linears once more, row-major,
-    // one allocation [layer][wqkv | wo | w13 as (w1_j, w3_j) row pairs | w2], the codebook head,
-    // the per-layer norm / bias table, the exchange granules and the generation word
-    bf16_t* pw = nullptr;
-    size_t pw_layer = 0, pw_off_wo = 0, pw_off_w13 = 0, pw_off_w2 = 0;
-    bf16_t* phead = nullptr;
-    PassLayer* players = nullptr;
-    unsigned long long* pgran = nullptr;
-    int pgran_stride = 0;
-    unsigned* psync = nullptr;
-    int pnwg = 0;
-    bool pass_ok = false;
     void* plast = nullptr;  // batched prefill: the last prompt row of each request [max_slots][dim]
     float *part = nullptr, *logits = nullptr, *flogits = nullptr;
     void* act2 = nullptr;  // batched path: [R][2 * inter] output of the interleaved W1||W3
@@ -1151,100 +1139,7 @@ template <typename T> struct Run {
         return hid;
     }
 
-    // one persistent launch for the whole fast pass (fm_pass.hip): batch 1, bf16, fm_tune pass_fast
-    bool fast_pass_persistent(int n, int cc, bool with_head, const void* hidden) {
-        if constexpr (sizeof(T) != 2) return false;
-        if (n != 1 || !fm_tuning().pass_fast) return false;
-        if (!m->pass_ok) {  // pass_fast set after this model was finalised: its pass weights do not exist
-            static bool warned = false;
-            if (!warned)
-                fprintf(stderr, "fishmi: fm_tune pass_fast 1 has no effect on a model finalised without it "
-                                "(set pass_fast or pass_prepare before fm_llm_finalize); running the launch chain\n");
-            warned = true;
-            return false;
-        }
-        const fm_model_config& c = m->c;
-        const StackDims& f = m->fdm;
-        PassArgs a{};
-        a.wbase = m->pw;
-        a.w_layer = m->pw_layer;
-        a.off_wo = m->pw_off_wo;
-        a.off_w13 = m->pw_off_w13;
-        a.off_w2 = m->pw_off_w2;
-        a.layers = m->players;
-        a.nlayer = f.n_layer;
-        a.dim = f.dim;
-        a.nq = f.nh * f.hd;
-        a.nqkv = f.nqkv();
-        a.inter = f.inter;
-        a.nh = f.nh;
-        a.nkv = f.nkv;
-        a.hd = f.hd;
-        a.qk_norm = f.qk_norm;
-        a.nhead = m->cb;
-        a.eps = c.norm_eps;
-        a.scale = 1.0f / sqrtf((float)f.hd);
-        // a head-less pass (codebook 0: its logits are discarded) only needs the last layer's K/V
-        a.nop = with_head ? 4 * f.n_layer + 1 : 4 * (f.n_layer - 1) + 1;
-        a.tail_attn = !with_head;
-        a.x_in = (const bf16_t*)(cc == 0 ? hidden : m->femb);
-        a.xidx = cc == 0 ? nullptr : m->cols;
-        a.xidx_col = cc;
-        a.xidx_rows = m->cb;
-        a.head = with_head ? m->phead : nullptr;
-        a.hnorm = (const bf16_t*)m->fnorm;
-        a.logits = m->flogits;
-        a.kc = (bf16_t*)m->fkc;
-        a.vc = (bf16_t*)m->fvc;
-        a.slot_stride = m->fslot_stride;
-        a.layer_stride = m->flayer_stride;
-        a.S = m->C;
-        a.cpos = cc;
-        a.row_slot = m->frame_slot;
-        a.rope = m->frope;
-        a.gran = m->pgran;
-        a.gran_stride = m->pgran_stride;
-        a.sync = m->psync;
-        a.err = m->chain_err;
-        a.nwg = m->pnwg;
-        a.spin_log2 = fm_tuning().pass_spin;
-        a.mode = fm_tuning().pass_mode;
-        a.sweep_nap = fm_tuning().pass_nap;
-        a.dbg = fm_tuning().dbg;
-        const PassLds L = pass_lds(std::max({a.dim, a.nq, a.inter}), a.dim, a.nqkv, a.nkv, a.S, a.hd,
-                                   pass_maxrows_for(a.nqkv, a.dim, a.inter, a.nhead, a.nwg), a.nop);
-        a.off_ring = L.ring;
-        a.off_xbuf = L.xbuf;
-        a.off_resx = L.resx;
-        a.off_resh = L.resh;
-        a.off_raw = L.raw;
-        a.off_kvs = L.kvs;
-        a.off_red = L.red;
-        a.off_sc = L.sc;
-        a.off_opt = L.opt;
-        a.off_lyt = L.lyt;
-        a.off_attc = L.attc;
-        a.off_flg = L.flg;
-        a.off_junk = L.junk;
-        a.prefetch = fm_tuning().pass_prefetch;
-        a.off_dbg = L.dbg;
-        a.off_wtab = L.wtab;
-        int64_t bytes = 0;  // weight bytes streamed
-        for (int o = 0; o < a.nop; ++o) {
-            const int k = o >= 4 * f.n_layer ? 4 : (o & 3);
-            const int64_t N = k == 0 ? a.nqkv : (k == 2 ? 2 * a.inter : (k == 4 ? a.nhead : a.dim));
-            const int64_t K = k == 1 ? a.nq : (k == 3 ? a.inter : a.dim);
-            bytes += N * K * 2;
-        }
-        hipStream_t st = s;
-        auto go = [st, a] { launch_pass(st, a); };
-        m->prof.record("pass", bytes, go);
-        run_("pass", bytes, 2.0 * (double)bytes / 2, go);
-        return true;
-    }
-
     void fast_small(int n, int cc, bool with_head, const void* hidden) {
-        if (fast_pass_persistent(n, cc, with_head, hidden)) return;
         const fm_model_config& c = m->c;
         const KsbPlan kp = plan(m->fdm, n);
         for (int l = 0; l < m->fdm.n_layer; ++l) {
@@ -1755,79 +1650,6 @@ static void* pack_w13(fm_llm* m, const std::string& p, int inter, int dim) {
     return pk;
 }
 
-// ---- persistent fast pass (fm_pass.hip): eligibility and its row-major weight copy ----------
-static bool pass_eligible(fm_llm* m, int* nwg_out) {
-    const StackDims& f = m->fdm;
-    if (m->prec != FM_PREC_BF16 || m->quant || f.n_layer < 1) return false;
-    int ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device) != hipSuccess || ncu <= 0)
-        return false;
-    const int nq = f.nh * f.hd;
-    if (!pass_shapes_ok(f.dim, nq, f.nqkv(), f.inter, m->cb, f.nh, f.nkv, f.hd, m->C, ncu)) return false;
-    // the exchange granules of one op: P = N / 2 pairs, P * nwg must stay in int range
-    if ((long long)std::max({f.nqkv(), f.dim, f.inter, m->cb}) / 2 * ncu >= (1ll << 31)) return false;
-    const int nop = 4 * f.n_layer + 1;
-    const PassLds L = pass_lds(std::max({f.dim, nq, f.inter}), f.dim, f.nqkv(), f.nkv, m->C, f.hd,
-                               pass_maxrows_for(f.nqkv(), f.dim, f.inter, m->cb, ncu), nop);
-    if (L.bytes > 160 * 1024 || nop >= 255) return false;
-    *nwg_out = ncu;
-    return true;
-}
-
-static void pass_prepare(fm_llm* m) {
-    // the row-major copy of the fast stack (~0.8 GB at S2-Pro) only for a model that may run the
-    // persistent pass: pass_fast (or pass_prepare) set when the model is finalised
-    if (!fm_tuning().pass_fast && !fm_tuning().pass_prepare) return;
-    int nwg = 0;
-    if (!pass_eligible(m, &nwg)) return;
-    const StackDims& f = m->fdm;
-    const size_t E = 2, D = f.dim, nq = (size_t)f.nh * f.hd, I = f.inter;
-    m->pw_off_wo = (size_t)f.nqkv() * D;
-    m->pw_off_w13 = m->pw_off_wo + D * nq;
-    m->pw_off_w2 = m->pw_off_w13 + 2 * I * D;
-    m->pw_layer = m->pw_off_w2 + D * I;
-    m->pw = (bf16_t*)m->dalloc(m->pw_layer * f.n_layer * E, false);
-    const size_t rb = D * E;
-    for (int l = 0; l < f.n_layer; ++l) {
-        const std::string p = "fast_layers." + std::to_string(l) + ".";
-        bf16_t* base = m->pw + (size_t)l * m->pw_layer;
-        auto src = [&](const char* n) { return m->w.at(p + n).p; };
-        HIPCHK(hipMemcpyAsync(base, src("attention.wqkv.weight"), (size_t)f.nqkv() * rb, hipMemcpyDeviceToDevice, m->stream));
-        HIPCHK(hipMemcpyAsync(base + m->pw_off_wo, src("attention.wo.weight"), D * nq * E, hipMemcpyDeviceToDevice,
-                              m->stream));
-        HIPCHK(hipMemcpy2DAsync(base + m->pw_off_w13, 2 * rb, src("feed_forward.w1.weight"), rb, rb, I,
-                                hipMemcpyDeviceToDevice, m->stream));
-        HIPCHK(hipMemcpy2DAsync(base + m->pw_off_w13 + D, 2 * rb, src("feed_forward.w3.weight"), rb, rb, I,
-                                hipMemcpyDeviceToDevice, m->stream));
-        HIPCHK(hipMemcpyAsync(base + m->pw_off_w2, src("feed_forward.w2.weight"), D * I * E, hipMemcpyDeviceToDevice,
-                              m->stream));
-    }
-    m->phead = (bf16_t*)m->dalloc((size_t)m->cb * rb, false);
-    HIPCHK(hipMemcpyAsync(m->phead, m->w.at("fast_output.weight").p, (size_t)m->cb * rb, hipMemcpyDeviceToDevice,
-                          m->stream));
-    const int nop = 4 * f.n_layer + 1;
-    m->pgran_stride = (std::max({f.nqkv(), f.dim, f.inter, m->cb}) / 2 + 15) / 16 * 16;
-    m->pgran = (unsigned long long*)m->dalloc((size_t)nop * m->pgran_stride * 8);
-    m->psync = (unsigned*)m->dalloc(64 * sizeof(unsigned));
-    m->pnwg = nwg;
-    pass_init();
-    HIPCHK(hipStreamSynchronize(m->stream));
-}
-
-// the per-layer norm / bias table (after the stacks' pointers are final)
-static void pass_tables(fm_llm* m) {
-    if (!m->pw) return;
-    std::vector<PassLayer> t(m->fdm.n_layer);
-    for (int l = 0; l < m->fdm.n_layer; ++l) {
-        const LayerW& L = m->fast[l];
-        t[l] = PassLayer{(const bf16_t*)L.bqkv, (const bf16_t*)L.bo, (const bf16_t*)L.an,
-                         (const bf16_t*)L.fn, (const bf16_t*)L.qn, (const bf16_t*)L.kn};
-    }
-    m->players = (PassLayer*)m->dalloc(t.size() * sizeof(PassLayer), false);
-    HIPCHK(hipMemcpy(m->players, t.data(), t.size() * sizeof(PassLayer), hipMemcpyHostToDevice));
-    m->pass_ok = true;
-}
-
 static void finalize(fm_llm* m) {
     if (m->finalized) return;
     const fm_model_config& c = m->c;
@@ -1835,7 +1657,6 @@ static void finalize(fm_llm* m) {
     sample_init();
     for (auto& kv : m->w) FMCHECK(kv.second.set || kv.second.optional, "tensor not set: " + kv.first);
     if (m->quant) quantize_linears(m);
-    pass_prepare(m);  // (row-major copies: before the linears are packed)
     for (auto& kv : m->w) {
         if (!is_linear_weight(kv.first) || is_ffn_w13(kv.first)) continue;  // W1/W3: pack_w13 below
         DTensor& t = kv.second;
@@ -1919,7 +1740,6 @@ static void finalize(fm_llm* m) {
             m->row_qkv_ok = m->row_qkv_ok && L.wqkv_rm;
             m->row_w13_ok = m->row_w13_ok && L.w13_rm;
         }
-    pass_tables(m);
     if (m->quant) {  // WeightOnlyInt8Linear has no bias (quantize.py:206-229): the checkpoint's are unused
         for (auto* st : {&m->slow, &m->fast})
             for (LayerW& L : *st) L.bqkv = L.bo = nullptr;
@@ -2139,7 +1959,7 @@ static void upload_frame_rows(fm_llm* m, const int32_t* slots, int n) {
 // gemv chain health: the error word travels to pinned memory behind the frames; after the
 // host's stream sync, a timed-out hand-off wait (a hang avoided) resets the counters and fails
 static void chain_err_async(fm_llm* m) {
-    if (fm_tuning().gemv_chain || (m->pass_ok && fm_tuning().pass_fast) || fm_tuning().fin_split > 1 ||
+    if (fm_tuning().gemv_chain || fm_tuning().fin_split > 1 ||
         (m->fxt && fm_tuning().fattn_wo))
         HIPCHK(hipMemcpyAsync(m->h_chain_err, m->chain_err, sizeof(int), hipMemcpyDeviceToHost, m->stream));
 }
@@ -2150,7 +1970,7 @@ static void chain_err_check(fm_llm* m) {
     HIPCHK(hipMemset(m->chain_err, 0, 16 * sizeof(int)));
     if (m->fin_cnt) HIPCHK(hipMemset(m->fin_cnt, 0, (size_t)std::max(m->max_slots, 64) * 2 * sizeof(int)));
     throw FmError{FM_ERR_STATE,
-                  "in-launch hand-off wait timed out (gemv chain / persistent pass / split finalize / fused fast "
+                  "in-launch hand-off wait timed out (gemv chain / split finalize / fused fast "
                   "attention + wo; counters reset)"};
 }
 
@@ -2795,8 +2615,6 @@ int fm_tune(const char* key, int value) {
             t.fin_split = value;
         } else if (k == "int4_stream") {
             t.int4_stream = value != 0;
-        } else if (k == "pass_fast") {
-            t.pass_fast = value != 0;
         } else if (k == "fw_delay") {
             FMCHECK(value >= 0 && value <= 1000, "fw_delay must be 0..1000 (10-ns ticks)");
             t.fw_delay = value;
@@ -2819,23 +2637,6 @@ int fm_tune(const char* key, int value) {
         } else if (k == "rowgemv") {
             FMCHECK(value >= 0 && value <= 31, "rowgemv must be 0..31 (bit 0 wo / w2, bit 1 wqkv, bit 2 w1 || w3, bit 3 fast head, bit 4 first-layer wqkv)");
             t.rowgemv = value;
-        } else if (k == "pass_prepare") {
-            t.pass_prepare = value != 0;
-        } else if (k == "pass_cfg") {
-            FMCHECK(value >= 0 && value <= 9, "pass_cfg must be 0..9");
-            t.pass_cfg = value;
-        } else if (k == "pass_mode") {
-            FMCHECK(value >= 0 && value <= 31, "pass_mode must be 0..31");
-            t.pass_mode = value;
-        } else if (k == "pass_nap") {
-            FMCHECK(value >= 1 && value <= 32, "pass_nap must be 1..32");
-            t.pass_nap = value;
-        } else if (k == "pass_prefetch") {
-            FMCHECK(value >= 0 && value <= 64, "pass_prefetch must be 0..64");
-            t.pass_prefetch = value;
-        } else if (k == "pass_spin") {
-            FMCHECK(value >= 0 && value < 28, "pass_spin must be 0 (default) or a poll-bound exponent < 28");
-            t.pass_spin = value;
         } else if (k == "rmsnorm_block") {
             t.rmsnorm_block = value != 0;
         } else if (k == "debug_ts") {  // (re)arm the per-block timestamp buffer; 0 frees it
@@ -2981,18 +2782,6 @@ int fm_llm_debug_vec(fm_llm* m, const char* name, int index, float* out, int64_t
         HIPCHK(hipSetDevice(m->device));
         HIPCHK(hipStreamSynchronize(m->stream));
         const std::string k = name;
-        if (k == "gran") {
-            FMCHECK(m->pgran && index >= 0 && index <= 4 * m->fdm.n_layer, "no persistent pass granules");
-            FMCHECK(n <= 2 * (int64_t)m->pgran_stride, "n past the granule region");
-            std::vector<unsigned long long> g((size_t)(n + 1) / 2);
-            HIPCHK(hipMemcpy(g.data(), m->pgran + (size_t)index * m->pgran_stride, g.size() * 8, hipMemcpyDeviceToHost));
-            for (int64_t i = 0; i < n; ++i) {
-                const uint32_t w = (uint32_t)g[(size_t)i / 2], b = (i & 1) ? (w >> 16) : (w & 0xffffu);
-                const uint32_t u = b << 16;
-                memcpy(out + i, &u, 4);
-            }
-            return;
-        }
         void* p = k == "qkv" ? m->qkv : k == "att" ? m->att : k == "fh" ? m->fh : k == "act" ? m->act
                 : k == "fx" ? m->fx : k == "fx2" ? m->fx2 : k == "xl" ? m->xl : k == "xnl" ? m->xnl : nullptr;
         if (k == "kc" || k == "vc") {  // slot 0's slow-layer `index` cache: [nkv][S][hd]

@@ -32,7 +32,7 @@
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
 
-// acc += w . x over 4 bf16 (two v_dot2c_f32_bf16); whole-vector bit casts (see fm_pass.hip dot8)
+// acc += w . x over 4 bf16 (two v_dot2c_f32_bf16); whole-vector bit casts, so the compiler emits v_dot2c_f32_bf16 on the loaded registers
 __device__ __forceinline__ float dot4(u32x2_t w, u32x2_t x, float acc) {
     const bf16x4_t wb = __builtin_bit_cast(bf16x4_t, w), xb = __builtin_bit_cast(bf16x4_t, x);
     acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(wb, wb, 0, 1), __builtin_shufflevector(xb, xb, 0, 1),
@@ -43,7 +43,7 @@ __device__ __forceinline__ float dot4(u32x2_t w, u32x2_t x, float acc) {
 }
 __device__ __forceinline__ float lo16(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi16(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
-// acc += w . x over 8 bf16 pairs (v_dot2c_f32_bf16); whole-vector bit casts (fm_pass.hip dot8)
+// acc += w . x over 8 bf16 pairs (v_dot2c_f32_bf16); whole-vector bit casts
 __device__ __forceinline__ float dot8r(u32x4_t w, u32x4_t x, float acc) {
     const bf16x8_t wb = __builtin_bit_cast(bf16x8_t, w), xb = __builtin_bit_cast(bf16x8_t, x);
     acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(wb, wb, 0, 1), __builtin_shufflevector(xb, xb, 0, 1),

@@ -181,10 +181,8 @@ int fm_llm_kernel_bench(fm_llm* h, const char* kernel_class, int reps, double* a
                         int64_t* launches, int64_t* bytes);
 int fm_llm_use_graph(fm_llm* h, int enable);
 /* developer hook: row 0 of an activation buffer of the decode path ("qkv", "att", "fh", "act",
-   "fx", "fx2", "xl", "xnl": bf16/fp32 storage as floats), slot 0's KV cache of slow layer `index`
-   ("kc" / "vc": [n_local_heads][S][head_dim], n <= its size; the prefix-reuse identity tests) or,
-   for name "gran", op `index`'s vector of the last persistent fast pass (fm_pass.hip exchange
-   granules; n = its length) */
+   "fx", "fx2", "xl", "xnl": bf16/fp32 storage as floats) or slot 0's KV cache of slow layer `index`
+   ("kc" / "vc": [n_local_heads][S][head_dim], n <= its size; the prefix-reuse identity tests) */
 int fm_llm_debug_vec(fm_llm* h, const char* name, int index, float* out, int64_t n);
 /* Teacher forcing on the PRODUCTION decode path (parity with the reference's own teacher-forced
    forward_generate / forward_generate_fast, llama.py:390-466, 798-827): while a slot is forced,
