@@ -465,6 +465,41 @@ def pmc_gemv_traffic(timeout_s=150):
         f"{vals['WRITE_SIZE'] / 1e6:.3f} MB written per decode-linear launch (gemv_kernel, rowgemv_kernel)")
 
 
+def trace_decode_kernels(timeout_s=150):
+    """Per-launch durations of the decode kernels from a rocprofv3 --kernel-trace pass over
+    scripts/pmc_probe.py (a child process; prefill + 4 batch-1 frames at S2-Pro shapes): the decode
+    linear class and the fused fast attention + wo (fattn_wo_kernel), which streams the fast model's
+    wo weights but sits outside the "linear" class.  Returns {name: (launches, avg_us)} or a note."""
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from rocprof_summary import is_decode_linear, load_dispatches
+
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return {"note": "rocprofv3 not on PATH"}
+    d = tempfile.mkdtemp(prefix="fishmi_tr_", dir="/tmp")
+    cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--kernel-trace", "--output-format", "csv", "-d", d, "-o",
+           "tr", "--", sys.executable, os.path.join(ROOT, "scripts", "pmc_probe.py")]
+    r = subprocess.run(cmd, cwd="/tmp", stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    csvs = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if r.returncode != 0 or not csvs:
+        return {"note": f"rocprofv3 --kernel-trace failed (rc {r.returncode}): {r.stderr[-300:].decode(errors='replace')}"}
+    disp = load_dispatches(csvs[0])
+    shutil.rmtree(d, ignore_errors=True)
+    lin = [ns for n, ns, _ in disp if is_decode_linear(n)]
+    fw = [ns for n, ns, _ in disp if n.startswith("void fattn_wo_kernel")]
+    out = {}
+    if lin:
+        out["linear"] = (len(lin), sum(lin) / len(lin) / 1e3)
+    if fw:
+        out["fattn_wo"] = (len(fw), sum(fw) / len(fw) / 1e3)
+    return out
+
+
 def pmc_codec_mfma(codec_ms, timeout_s=120):
     """MFMA utilisation of the codec decode from the hardware counters, measured in this run: one
     rocprofv3 --pmc pass (SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_MOPS_BF16, SQ_ACTIVE_INST_VALU,
@@ -651,8 +686,29 @@ def main():
     stream_gbps = stream_peak_gbps() if rank == 0 else (None, None)
     box = box_identity() if rank == 0 else None
     traffic, traffic_note = None, "not measured (--no-pmc or N>1)"
+    fused_wo = {"note": "not measured (--no-pmc or N>1)"}
     if rank == 0 and world == 1 and not args.no_pmc:
         traffic, traffic_note = pmc_gemv_traffic()
+        tr = trace_decode_kernels()
+        if "fattn_wo" in tr and "linear" in tr:
+            # the fused fast attention + wo (fm_rowgemv.hip fattn_wo_kernel): its wo weights count as
+            # decode-linear bytes; one launch per fast layer and codebook, less codebook 0's last layer
+            # (fast_tail: only its K / V rows are needed)
+            fw_n = cfg.num_codebooks * cfg.n_fast_layer - 1
+            fw_bytes = 2 * cfg.fast_dim * cfg.fast_n_head * cfg.fast_head_dim
+            fw_us, lin_tr_us = tr["fattn_wo"][1], tr["linear"][1]
+            both = (lin_bytes + fw_n * fw_bytes) / (lin_n * lin_tr_us + fw_n * fw_us) / 1e3  # GB/s
+            fused_wo = {"launches_per_frame": fw_n, "bytes_per_launch": fw_bytes,
+                        "avg_launch_us_rocprof": round(fw_us, 3),
+                        "achieved": round(fw_bytes / fw_us / 1e3, 1), "unit": "GB/s",
+                        "frac": round(fw_bytes / fw_us / 1e3 / HBM_PEAK_GBPS, 4),
+                        "linear_avg_launch_us_rocprof": round(lin_tr_us, 3),
+                        "linear_incl_fused_wo_frac": round(both / HBM_PEAK_GBPS, 4),
+                        "method": "rocprofv3 --kernel-trace pass over scripts/pmc_probe.py in this run (prefill + 4 "
+                                  "batch-1 frames): per-launch durations; bytes = the fast model's wo weights "
+                                  "(the attention's <= 10 cached K / V rows are not counted)"}
+        else:
+            fused_wo = tr
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -702,6 +758,7 @@ def main():
                                                             "(16 / 32 KiB in flight per wave); best of two "
                                                             "float4 copies (read + write bytes); 2 GiB "
                                                             "buffers, 10 launches each, HIP events"},
+                         "fused_fast_wo": fused_wo,
                          "bytes_per_launch": int(per_launch),
                          "avg_launch_us": round(avg_us, 3), "launches_per_frame": int(lin_n),
                          "method": "one frame's GEMV launches replayed x20 as a graph, HIP events on "
