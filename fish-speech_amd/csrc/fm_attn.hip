@@ -1673,15 +1673,19 @@ __global__ __launch_bounds__(256) void sample_fast_kernel(SampleArgs a) {
     SFTS(5)
     const uint64_t step = (uint64_t)sp.step;
     int32_t* col = a.cols + (size_t)r * a.ldc;
-    if (a.dbg && lane == 0) {
-        tsx[6] = __builtin_amdgcn_s_memrealtime();
-        const unsigned long long slot2 = atomicAdd(a.dbg, 1ull);
-        if (slot2 < (1ull << 20)) {
-            unsigned long long* q = a.dbg + 8 + slot2 * 8;
-            q[0] = (0xFFFFull << 32) | (unsigned)(ncand[0] + ncand[1] + ncand[2] + ncand[3]) | ((unsigned long long)overflow << 16);
-            for (int z = 0; z < 7; ++z) q[1 + z] = tsx[z];
+    // developer stamps {start, values in, max, threshold, candidates, ranks, end} (wave 0, at the end)
+    auto record = [&]() {
+        if (a.dbg && lane == 0) {
+            tsx[6] = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long slot2 = atomicAdd(a.dbg, 1ull);
+            if (slot2 < (1ull << 20)) {
+                unsigned long long* q = a.dbg + 8 + slot2 * 8;
+                q[0] = (0xFFFFull << 32) | (unsigned)(ncand[0] + ncand[1] + ncand[2] + ncand[3]) |
+                       ((unsigned long long)overflow << 16) | ((unsigned long long)a.slow << 17);
+                for (int z = 0; z < 7; ++z) q[1 + z] = tsx[z];
+            }
         }
-    }
+    };
     if (a.slow) {
         int tok = sample_top<T>(cv, cid, K, M, den, sp.temperature, sp.top_p, sp.top_k, sp.seed, step, 0, lane);
         const int hi = sample_top<T>(cv, cid, K, M, den, 1.0f, 0.9f, sp.top_k, sp.seed, step, 1, lane);
@@ -1709,6 +1713,7 @@ __global__ __launch_bounds__(256) void sample_fast_kernel(SampleArgs a) {
             col[a.col_idx] = sp.force ? a.force_cols[(size_t)slot * a.ldc + a.col_idx]
                                       : ((code >= 0 && code < a.cb) ? code : 0);
     }
+    record();
 }
 
 // ---------------------------------------------------------------------------------------
