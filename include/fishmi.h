@@ -201,6 +201,7 @@ int fm_llm_read_logits(fm_llm* h, int slot, float* slow_logits, float* fast_logi
    "attn_cap" n, "attn_cap_batched" n, "fd_min" n, "fd_min_batched" n, "fd_nw" 4|8|16, "fd_min16" n,
    "fd_nw_batched" 4|8|16, "attn_wo" 0|1,
    "batched_fused_attn" 0|1; batched linears "bstream" 0|1, "bstream_acc" 0|1, "bstream_chain" 0|1, "bstream_kparts" n, "bstream_nw" n, "bs_dummy" 0|1|2, "bs_qkv_slab" 0|1,
+   "bs_xfirst" 0|1, "bs_vec_epi" 0|1,
    "linear_u32" n, "linear_fill" n; prompt "prefill_attn", "prompt_gemm"; codec "conv2",
    "conv_splitk"; "sampler_fast" 0|1, "rmsnorm_block" 0|1, "debug_ts" n; batch-1 row-block GEMV
    "rowgemv" / "rowgemv_q4" bits, "row_copies" 0|1 (0: finalize keeps only the row-major weight
