@@ -51,6 +51,12 @@ def parse():
     ap.add_argument("--batch", type=int, default=32,
                     help="throughput leg (BASELINE config 3): concurrent streams per GPU (0: skip)")
     ap.add_argument("--batch-frames", type=int, default=512, help="throughput leg: frames per request")
+    ap.add_argument("--serial-vocode", action="store_true",
+                    help="config 2: vocode each chunk before decoding the next (default: on a host thread, "
+                         "overlapped with the next chunk's decode)")
+    ap.add_argument("--vocode-chunk", type=int, default=128,
+                    help="throughput leg: frames per streamed codec chunk, vocoded on a host thread of its "
+                         "own while the decode goes on (0: each stream vocoded at its end, serially)")
     ap.add_argument("--waves", type=int, default=1,
                     help="throughput leg: requests = batch x GPUs x waves, pulled from rank 0's tick queue")
     ap.add_argument("--longform-turns", type=int, default=4,
@@ -74,48 +80,76 @@ def make_prompt(cfg, T, seed):
     return p
 
 
-def utterance(llm, codec, prompt, sp, frames, first_chunk):
+def utterance(llm, codec, prompt, sp, frames, first_chunk, voc=None):
     """Request -> PCM for one stream.  Returns (pcm, timings in seconds).  The vocoder streams:
     each chunk of frames is vocoded as soon as its frames exist -- first_chunk frames, then chunks
     growing 4x, so a chunk's generation (4^k frames at ~10x real time) takes less time than the
     audio already delivered (>= 4^k frames) takes to play -- continuing one codec stream (carried
     causal state, fm_codec_decode_chunk), so no frame is vocoded twice and the waveform is
-    bit-identical to a one-shot decode (tests/test_gpu_codec_stream.py)."""
+    bit-identical to a one-shot decode (tests/test_gpu_codec_stream.py).  With voc (a
+    scheduler.StreamVocoder), the chunks after the first are vocoded on its host thread, on the
+    codec's own HIP stream, while the next chunk decodes; the first chunk's PCM is waited for (the
+    first-sample latency), the rest at the end.  timings: decode = host time in decode_frames,
+    codec = time inside the codec calls after the first chunk."""
     t0 = time.perf_counter()
     col0 = llm.prefill(0, prompt, sp)
     t1 = time.perf_counter()
-    codec.stream_reset()
-    pcm, done, n = [], 0, min(first_chunk, frames)
+    durs = []
+
+    def vocode(codes):
+        ta = time.perf_counter()
+        out = codec.decode_chunk(codes)
+        durs.append(time.perf_counter() - ta)
+        return out
+
+    if voc is None:
+        codec.stream_reset()
+    else:
+        voc.submit(codec.stream_reset)
+    pcm, jobs, done, n = [], [], 0, min(first_chunk, frames)
     cols = col0[None]
-    first = decode = vocode = 0.0
+    first = decode = 0.0
     while done < frames:
         ta = time.perf_counter()
         if n > cols.shape[0]:
             cols = np.concatenate([cols, llm.decode_frames([0], n - cols.shape[0])[:, 0, :]], axis=0)
         tb = time.perf_counter()
-        pcm.append(codec.decode_chunk(np.ascontiguousarray(cols[:, 1:].T)))
+        codes = np.ascontiguousarray(cols[:, 1:].T)
+        if voc is None:
+            pcm.append(vocode(codes))
+        else:
+            ev, box = voc.submit(lambda c=codes: vocode(c))
+            jobs.append((ev, box))
+            if done == 0:
+                ev.wait()
         tc = time.perf_counter()
         if done == 0:
             first = tc - t0
         else:
             decode += tb - ta
-            vocode += tc - tb
         done += n
         cols = cols[:0]
         n = min(4 * n, frames - done)
+    for ev, box in jobs:
+        ev.wait()
+        if isinstance(box[0], BaseException):
+            raise box[0]
+        pcm.append(box[0])
     t4 = time.perf_counter()
     return np.concatenate(pcm), dict(first=first, prefill=t1 - t0, head=first - (t1 - t0), decode=decode,
-                                     codec=vocode, total=t4 - t0)
+                                     codec=float(sum(durs[1:])), total=t4 - t0)
 
 
-def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world):
+def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world, vocode_chunk=128):
     """BASELINE config 3 at N=1 (32 concurrent prompts per GPU) and config 4 at N=8 (256 requests
     over 8 GPUs), end to end: rank 0 owns batch x world x waves requests (prompt lengths uniform in
     [16, 256], seed 2; `frames` frames each) and hands them out through the tick queue
     (fishmi/scheduler.py). Each rank prefills its requests into KV slots and decodes them together,
     one batched Dual-AR frame per graph replay (slow pass + 10 fast passes + samplers of every
-    stream). It vocodes each finished stream through the streamed codec, and the int16 PCM is
-    gathered to rank 0 over RCCL. Value = audio seconds of PCM gathered at rank 0 / wall time
+    stream). It vocodes each stream through the streamed codec -- with vocode_chunk > 0 on a
+    host thread of its own (scheduler.StreamVocoder), each live stream's finished columns in chunks
+    of vocode_chunk frames while the next tick decodes; 0: each stream at its end, serially -- and
+    the int16 PCM is gathered to rank 0 over RCCL. Value = audio seconds of PCM gathered at rank 0 / wall time
     (max over ranks)."""
     from fishmi import dp
     from fishmi import scheduler as S
@@ -161,7 +195,12 @@ def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world):
     def step(slots, n):
         return timed("decode", lambda: llm.decode_frames(slots, n))
 
+    voc = S.StreamVocoder(codec, vocode_chunk) if vocode_chunk > 0 else None
+
     def finish(slot, req, cols):
+        if voc is not None:  # the rest of the stream; earlier chunks were vocoded during the decode
+            return timed("codec", lambda: dp.pcm_to_int16(voc.finish(slot, req, cols)))
+
         def vocode():
             codec.stream_reset()
             mx = codec.max_frames
@@ -172,9 +211,13 @@ def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world):
     sync()
     t0 = time.perf_counter()
     q = S.TickQueue(reqs, C1)
-    stats = S.serve(q, batch, start, step, finish, tick_frames=32, start_batch=start_batch)
+    stats = S.serve(q, batch, start, step, finish, tick_frames=32, start_batch=start_batch,
+                    progress=voc.progress if voc is not None else None)
     sync()
     dt = time.perf_counter() - t0
+    codec_busy = voc.busy_s if voc is not None else phase["codec"]
+    if voc is not None:
+        voc.close()
     if dist is not None:
         import torch
 
@@ -198,6 +241,7 @@ def throughput_leg(llm, codec, cfg, batch, frames, waves, sync, dist, world):
             "value": round(audio_s / dt, 2), "unit": "audio-sec/wall-sec", "wall_s": round(dt, 3),
             "decode_frames_rank0": stats["frames"], "ticks": stats["ticks"],
             "phase_s_rank0": {k: round(v, 3) for k, v in phase.items()},
+            "vocode_chunk": vocode_chunk, "codec_busy_s_rank0": round(codec_busy, 3),
             "per_stream_rtf": round(audio_s / len(q.results) / dt, 3)}
 
 
@@ -234,7 +278,7 @@ def encode_leg(ccfg, device, seconds, seed):
                          "unit": "TFLOP/s", "frac": round(tflops / BF16_DENSE_TFLOPS, 4)}}
 
 
-def longform_leg(ccfg, device, turns, frames_per_turn, seed):
+def longform_leg(ccfg, device, turns, frames_per_turn, seed, serial=False):
     """BASELINE config 5 on one GPU: voice clone from 30 s of reference audio (codec encode), then
     `turns` speaker turns of `frames_per_turn` frames through the native generate_long (conversation
     growing with each turn's codes, prefix KV reused), codes streamed into the causal streamed
@@ -271,28 +315,49 @@ def longform_leg(ccfg, device, turns, frames_per_turn, seed):
     words = "the quick brown fox jumps over a lazy dog while the river runs past the old mill "
     text = " ".join(f"<|speaker:{i % 2}|>" + (words * 2)[: 150 + 7 * i] for i in range(turns))
 
+    from fishmi import scheduler as S
+
+    # chunks after a turn's first go to the vocoder thread (codec HIP stream) while the generator
+    # decodes on; a turn's first chunk is waited for (its latency is the turn's first-chunk time)
+    voc = None if serial else S.StreamVocoder(codec)
+
     def run():
         t0 = time.perf_counter()
         ptok = codec.encode_audio(audio)
-        firsts, samples, turn_t0 = [], 0, t0
+        firsts, samples, turn_t0, jobs = [], 0, t0, []
         for o in E.generate_long(model=llm, text=text, max_new_tokens=frames_per_turn, top_p=0.8, top_k=30,
                                  temperature=0.8, chunk_length=200, prompt_text=["a thirty second reference"],
                                  prompt_tokens=[ptok], seed=seed, stream_frames=1, stream_growth=4,
                                  stream_max=64, mask_im_end=True, reuse_prefix=True):
             if o.action != "sample":
                 continue
-            if o.stream == 0:
-                codec.stream_reset()
-            pcm = codec.decode_chunk(o.codes)
-            samples += pcm.size
+            if voc is None:
+                if o.stream == 0:
+                    codec.stream_reset()
+                samples += codec.decode_chunk(o.codes).size
+            else:
+                if o.stream == 0:
+                    voc.submit(codec.stream_reset)
+                ev, box = voc.submit(lambda c=o.codes: codec.decode_chunk(c))
+                jobs.append((ev, box))
+                if o.stream == 0:
+                    ev.wait()
             now = time.perf_counter()
             if o.stream == 0:
-                firsts.append(now - turn_t0)  # turn start (previous turn's last PCM) -> first PCM
+                # turn start (the previous turn's last chunk vocoded, or handed to the vocoder) -> first PCM
+                firsts.append(now - turn_t0)
             turn_t0 = now
+        for ev, box in jobs:
+            ev.wait()
+            if isinstance(box[0], BaseException):
+                raise box[0]
+            samples += box[0].size
         return time.perf_counter() - t0, firsts, samples, ptok.shape[1]
 
     run()  # warm-up: graph capture, tokenizer, allocation
     wall, firsts, samples, ref_codes = run()
+    if voc is not None:
+        voc.close()
     llm.close()
     codec.close()
     audio_s = samples / ccfg.sample_rate
@@ -302,7 +367,8 @@ def longform_leg(ccfg, device, turns, frames_per_turn, seed):
                         f"through generate_long (prefix KV reused across turns), codes streamed in chunks of 1, 4, 16, "
                         f"then 64 frames into the causal streamed vocoder; bf16, synthetic weights + tokenizer",
             "value": round(audio_s / wall, 3), "unit": "audio-sec/wall-sec", "audio_s": round(audio_s, 2),
-            "wall_s": round(wall, 3), "first_sample_ms": round(float(f[0]), 2),
+            "wall_s": round(wall, 3), "vocoder": "serial" if serial else "host thread, overlapped with generation",
+            "first_sample_ms": round(float(f[0]), 2),
             "turn_first_chunk_ms_p50": round(float(np.median(f)), 2),
             "turn_first_chunk_ms_p90": round(float(np.percentile(f, 90)), 2)}
 
@@ -624,11 +690,14 @@ def main():
             prompt = make_prompt(cfg, args.prompt_len, 1000 * step)
         sp = DualARModel.sampling(temperature=0.8, top_p=0.8, top_k=30, seed=7919 * step + rank,
                                   mask_im_end=True)
-        pcm, tm = utterance(llm, codec, prompt, sp, args.frames, args.first_chunk)
+        pcm, tm = utterance(llm, codec, prompt, sp, args.frames, args.first_chunk, voc2)
         if dist is not None:
             dp.gather_pcm(dp.pcm_to_int16(pcm))
         return tm
 
+    from fishmi import scheduler as S
+
+    voc2 = None if args.serial_vocode else S.StreamVocoder(codec)
     for w in range(args.warmup):
         one_step(-1 - w)
     sync()
@@ -636,6 +705,8 @@ def main():
     tms = [one_step(k) for k in range(args.steps)]
     sync()
     elapsed = time.perf_counter() - t0
+    if voc2 is not None:
+        voc2.close()
     firsts = np.array([t["first"] for t in tms], np.float64)
     if dist is not None:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -672,10 +743,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_pmc:
         codec_pmc = pmc_codec_mfma(ms1 - ms0)
 
-    thr = throughput_leg(llm, codec, cfg, args.batch, args.batch_frames, args.waves, sync, dist, world) \
+    thr = throughput_leg(llm, codec, cfg, args.batch, args.batch_frames, args.waves, sync, dist, world,
+                         args.vocode_chunk) \
         if args.batch > 0 else None
     enc = encode_leg(ccfg, local, args.encode_seconds, args.seed) if args.encode_seconds > 0 else None
-    longf = longform_leg(ccfg, local, args.longform_turns, args.longform_frames, args.seed) \
+    longf = longform_leg(ccfg, local, args.longform_turns, args.longform_frames, args.seed,
+                         args.serial_vocode) \
         if args.longform_turns > 0 and rank == 0 else None
 
     q8 = q4 = None
@@ -737,6 +810,8 @@ def main():
                                    f"+ codec decode [1,10,{args.frames}] -> {args.frames * 2048} samples",
                        "global_batch": world, "frames": args.frames, "prompt_len": args.prompt_len,
                        "first_chunk_frames": args.first_chunk, "vocoder_chunks": "first_chunk_frames, then growing 4x",
+                       "vocoder": "serial" if args.serial_vocode else
+                                  "host thread, codec HIP stream overlapped with the next chunk's decode",
                        "parallelism": f"dp{world}"},
             "p50_first_sample_ms": round(float(np.median(firsts)) * 1e3, 2),
             "p90_first_sample_ms": round(float(np.percentile(firsts, 90)) * 1e3, 2),

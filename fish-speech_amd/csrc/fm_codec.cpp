@@ -1011,7 +1011,7 @@ int fm_codec_open(const fm_codec_config* cfg, int device, int precision, int max
         m->prec = precision;
         m->esz = precision == FM_PREC_BF16 ? 2 : 4;
         m->max_frames = max_frames;
-        HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+        HIPCHK(fm_stream_create(&m->stream, 1));
         build_inventory(m.get());
         *out = m.release();
     });
@@ -1158,6 +1158,17 @@ int fm_codec_stream_open(fm_codec* m, int* sid) {
         HIPCHK(hipStreamSynchronize(m->stream));
         m->sctx.emplace(id, std::move(ctx));
         *sid = id;
+    });
+}
+
+int fm_codec_stream_rewind(fm_codec* m, int sid) {
+    return fm_guard([&] {
+        FMCHECK(m && sid > 0, "bad stream id (0 is the handle's own stream: stream_reset)");
+        FMCHECK(m->sctx.count(sid), "unknown codec stream id " + std::to_string(sid));
+        HIPCHK(hipSetDevice(m->device));
+        finalize(m);
+        m->activate(sid);
+        stream_zero(m);
     });
 }
 

@@ -211,6 +211,10 @@ class CodecStream:
                                                           native.f32p(out)))
         return out
 
+    def rewind(self):
+        """Back to zero state for the next request (fm_codec_stream_rewind: no reallocation)."""
+        native.check(native.lib().fm_codec_stream_rewind(self.codec.h, self.sid))
+
     def close(self):
         if self.sid and getattr(self.codec, "h", None):
             native.check(native.lib().fm_codec_stream_close(self.codec.h, self.sid))

@@ -26,7 +26,7 @@ ABI_SYMBOLS = [
     "fm_llm_frame_bytes", "fm_llm_profile", "fm_llm_profile_read", "fm_llm_kernel_bench", "fm_llm_use_graph", "fm_llm_debug_vec", "fm_tune", "fm_debug_ts_read",
     "fm_llm_close", "fm_source_hash", "fm_codec_open", "fm_codec_set_tensor", "fm_codec_synth_tensor",
     "fm_codec_finalize", "fm_codec_decode", "fm_codec_stream_reset", "fm_codec_decode_chunk",
-    "fm_codec_stream_open", "fm_codec_stream_decode", "fm_codec_stream_close",
+    "fm_codec_stream_open", "fm_codec_stream_decode", "fm_codec_stream_rewind", "fm_codec_stream_close",
     "fm_codec_profile_read", "fm_codec_debug_read", "fm_codec_enable_encoder", "fm_codec_encode",
     "fm_codec_close", "fm_llm_force", "fm_llm_read_logits", "fm_op_rmsnorm", "fm_op_qk_rope", "fm_op_decode_attn", "fm_op_prompt_attn",
     "fm_op_embed", "fm_op_quant4", "fm_rope_table",
@@ -152,6 +152,7 @@ def lib():
         L.fm_codec_decode_chunk.argtypes = [vp, pi32, i32, pf32]
         L.fm_codec_stream_open.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
         L.fm_codec_stream_decode.argtypes = [vp, i32, pi32, i32, pf32]
+        L.fm_codec_stream_rewind.argtypes = [vp, i32]
         L.fm_codec_stream_close.argtypes = [vp, i32]
         L.fm_codec_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_int64),

@@ -28,6 +28,9 @@ tick queue does not.
 from __future__ import annotations
 
 import dataclasses
+import queue as _queue
+import threading
+import time
 from typing import Callable, Dict, List, Optional, Sequence
 
 import numpy as np
@@ -266,3 +269,105 @@ def serve(queue: TickQueue, max_concurrent: int, start: Callable[[int, Request],
             free_slots.append(slot)
             served += 1
     return {"frames": frames, "served": served, "ticks": queue.ticks}
+
+
+class _VocState:
+    __slots__ = ("ctx", "sent", "pcm", "err")
+
+    def __init__(self):
+        self.ctx, self.sent, self.pcm, self.err = None, 0, [], None
+
+
+class StreamVocoder:
+    """serve()'s vocoder off the decode's critical path.  The codec runs on a host thread of its
+    own, on the codec handle's HIP stream (separate from the LLM's), so a tick's vocoding overlaps
+    the next tick's decode frames on the GPU (ctypes calls release the GIL).  `progress` streams
+    each live request's finished columns (all but the newest) in chunks of `chunk` frames through a
+    causal codec stream context of that request (fm_codec_stream_decode: the chunks' PCM is the
+    one-shot decode's, bit for bit); `finish` vocodes the rest and returns the request's float32
+    PCM.  Contexts are pooled and rewound (fm_codec_stream_rewind) instead of freed per request.
+    Every codec call runs on the one thread, in submission order (the handle is single-threaded).
+    busy_s: the thread's time inside codec calls."""
+
+    def __init__(self, codec, chunk: int = 128):
+        self.codec = codec
+        self.chunk = max(1, min(int(chunk), codec.max_frames))
+        self.fifo: "_queue.Queue" = _queue.Queue()
+        self.live: Dict[int, _VocState] = {}
+        self.pool: list = []   # rewound contexts (vocoder thread only)
+        self.ctxs: list = []   # every context opened (closed by close())
+        self.busy_s = 0.0
+        self.th = threading.Thread(target=self._run, daemon=True)
+        self.th.start()
+
+    def submit(self, fn):
+        """Run fn() on the vocoder thread after everything submitted before; returns (event,
+        box): box holds fn's result, or the exception it raised, once the event is set."""
+        ev, box = threading.Event(), []
+        self.fifo.put((fn, ev, box))
+        return ev, box
+
+    def _run(self):
+        while True:
+            it = self.fifo.get()
+            if it is None:
+                return
+            fn, ev, box = it
+            t = time.perf_counter()
+            try:
+                box.append(fn())
+            except BaseException as e:  # handed to the waiter, the thread lives on
+                box.append(e)
+            self.busy_s += time.perf_counter() - t
+            ev.set()
+
+    def _chunk(self, v: _VocState, codes: np.ndarray):
+        if v.err is not None:
+            return None
+        try:
+            if v.ctx is None:
+                if self.pool:
+                    v.ctx = self.pool.pop()
+                else:
+                    v.ctx = self.codec.open_stream()
+                    self.ctxs.append(v.ctx)
+            v.pcm.append(v.ctx.decode_chunk(codes))
+        except BaseException as e:
+            v.err = e
+        return None
+
+    def _release(self, v: _VocState):
+        if v.ctx is not None:
+            ctx, v.ctx = v.ctx, None
+            ctx.rewind()
+            self.pool.append(ctx)
+
+    def progress(self, slot: int, req: Request, cols: List[np.ndarray]):
+        v = self.live.setdefault(req.id, _VocState())
+        ready = len(cols) - 1  # the newest column may be the dropped last one
+        while ready - v.sent >= self.chunk:
+            codes = np.ascontiguousarray(np.stack(cols[v.sent: v.sent + self.chunk], 1)[1:])
+            self.submit(lambda v=v, c=codes: self._chunk(v, c))
+            v.sent += self.chunk
+
+    def finish(self, slot: int, req: Request, cols: np.ndarray) -> np.ndarray:
+        """cols (C+1, N), the last column already dropped -> float32 PCM (2048 N,)."""
+        v = self.live.pop(req.id, None) or _VocState()
+        mx = self.codec.max_frames
+        for t in range(v.sent, cols.shape[1], mx):
+            codes = np.ascontiguousarray(cols[1:, t: t + mx])
+            self.submit(lambda v=v, c=codes: self._chunk(v, c))
+        ev, box = self.submit(lambda v=v: self._release(v))
+        ev.wait()
+        if v.err is not None:
+            raise v.err
+        if box and isinstance(box[0], BaseException):
+            raise box[0]
+        return np.concatenate(v.pcm) if v.pcm else np.zeros(0, np.float32)
+
+    def close(self):
+        self.fifo.put(None)
+        self.th.join()
+        for ctx in self.ctxs:
+            ctx.close()
+        self.ctxs, self.pool = [], []

@@ -290,12 +290,14 @@ int fm_codec_decode(fm_codec* h, const int32_t* codes, int T, float* pcm);
    frames (T <= max_frames) and returns their 2048*T samples.  Concurrent streams (one per
    streamed request, several requests on one handle): stream_open gives a new context with its own
    carried rows and position (starting at zero, like a reset), stream_decode appends to it,
-   stream_close frees it.  Calls on one handle are serialised by the caller (one host thread at a
-   time); a context switch rebinds pointers only. */
+   stream_close frees it; stream_rewind zeroes a context for the next request (a context pool
+   needs no allocation, and no hipFree device sync, per request).  Calls on one handle are
+   serialised by the caller (one host thread at a time); a context switch rebinds pointers only. */
 int fm_codec_stream_reset(fm_codec* h);
 int fm_codec_decode_chunk(fm_codec* h, const int32_t* codes, int T, float* pcm);
 int fm_codec_stream_open(fm_codec* h, int* stream_id);
 int fm_codec_stream_decode(fm_codec* h, int stream_id, const int32_t* codes, int T, float* pcm);
+int fm_codec_stream_rewind(fm_codec* h, int stream_id);
 int fm_codec_stream_close(fm_codec* h, int stream_id);
 int fm_codec_profile_read(fm_codec* h, double* total_ms, int64_t* launches, double* flops);
 /* test hook: intermediate of the last decode as fp32, time-major (1 transformer out [T][latent],

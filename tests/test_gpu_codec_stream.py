@@ -87,3 +87,45 @@ def test_interleaved_stream_contexts_equal_one_shot(golden):
     ctx[0].close()
     ctx[1].close()
     m.close()
+
+
+def test_rewound_context_and_stream_vocoder_equal_one_shot(golden):
+    """A rewound context (fm_codec_stream_rewind) starts from zero state like a fresh one, and
+    scheduler.StreamVocoder -- chunks on its own host thread, contexts pooled and rewound between
+    requests -- gives each request the one-shot waveform bit for bit, whatever the chunk size and
+    however the requests' progress calls interleave."""
+    from fishmi import scheduler as S
+
+    m = _codec(golden, "bf16", 160)
+    rng = np.random.default_rng(33)
+    C1, T = m.cfg.n_codebooks + 2, 150  # a frame column: the main token, then the codec's rows
+    streams = []
+    for _ in range(4):
+        c = np.zeros((C1, T + 1), np.int32)  # + the column serve() drops at the end
+        c[0] = rng.integers(0, 1000, T + 1)
+        c[1] = rng.integers(0, m.cfg.semantic_codebook_size, T + 1)
+        c[2:] = rng.integers(0, m.cfg.codebook_size, (C1 - 2, T + 1))
+        streams.append(c)
+    full = [m.decode_codes(np.ascontiguousarray(c[1:, :T])) for c in streams]
+    ctx = m.open_stream()
+    ctx.decode_chunk(np.ascontiguousarray(streams[0][1:, :40]))
+    ctx.rewind()
+    np.testing.assert_array_equal(ctx.decode_chunk(np.ascontiguousarray(streams[1][1:, :T - 60])),
+                                  full[1][: (T - 60) * m.frame_length])
+    ctx.close()
+    for chunk in (1, 32, 96):
+        voc = S.StreamVocoder(m, chunk)
+        for w0 in (0, 2):  # the second wave reuses the first wave's contexts
+            wave = streams[w0:w0 + 2]
+            reqs = [S.Request(i, np.zeros((C1, 1), np.int32), T, 0) for i in range(len(wave))]
+            cols = [[] for _ in wave]
+            for t in range(0, T + 1, 17):  # a tick: 17 new columns per live stream
+                for i, c in enumerate(wave):
+                    cols[i] += [c[:, j] for j in range(t, min(t + 17, T + 1))]
+                    voc.progress(i, reqs[i], cols[i])
+            for i, c in enumerate(wave):
+                pcm = voc.finish(i, reqs[i], np.stack(cols[i], 1)[:, :-1])
+                np.testing.assert_array_equal(pcm, full[w0 + i])
+        assert len(voc.ctxs) == 2
+        voc.close()
+    m.close()
