@@ -51,9 +51,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=32,
                     help="throughput leg (BASELINE config 3): concurrent streams per GPU (0: skip)")
     ap.add_argument("--batch-frames", type=int, default=512, help="throughput leg: frames per request")
-    ap.add_argument("--serial-vocode", action="store_true",
-                    help="config 2: vocode each chunk before decoding the next (default: on a host thread, "
-                         "overlapped with the next chunk's decode)")
+    ap.add_argument("--overlap-vocode", action="store_true",
+                    help="configs 2 and 5: vocode the chunks after the first on a host thread, overlapped with "
+                         "the next chunk's decode (default: each chunk before decoding the next; measured "
+                         "neutral, profiles/r06_vocoder_overlap_ab.txt)")
     ap.add_argument("--vocode-chunk", type=int, default=128,
                     help="throughput leg: frames per streamed codec chunk, vocoded on a host thread of its "
                          "own while the decode goes on (0: each stream vocoded at its end, serially)")
@@ -697,7 +698,7 @@ def main():
 
     from fishmi import scheduler as S
 
-    voc2 = None if args.serial_vocode else S.StreamVocoder(codec)
+    voc2 = S.StreamVocoder(codec) if args.overlap_vocode else None
     for w in range(args.warmup):
         one_step(-1 - w)
     sync()
@@ -748,7 +749,7 @@ def main():
         if args.batch > 0 else None
     enc = encode_leg(ccfg, local, args.encode_seconds, args.seed) if args.encode_seconds > 0 else None
     longf = longform_leg(ccfg, local, args.longform_turns, args.longform_frames, args.seed,
-                         args.serial_vocode) \
+                         not args.overlap_vocode) \
         if args.longform_turns > 0 and rank == 0 else None
 
     q8 = q4 = None
@@ -810,7 +811,7 @@ def main():
                                    f"+ codec decode [1,10,{args.frames}] -> {args.frames * 2048} samples",
                        "global_batch": world, "frames": args.frames, "prompt_len": args.prompt_len,
                        "first_chunk_frames": args.first_chunk, "vocoder_chunks": "first_chunk_frames, then growing 4x",
-                       "vocoder": "serial" if args.serial_vocode else
+                       "vocoder": "serial" if not args.overlap_vocode else
                                   "host thread, codec HIP stream overlapped with the next chunk's decode",
                        "parallelism": f"dp{world}"},
             "p50_first_sample_ms": round(float(np.median(firsts)) * 1e3, 2),

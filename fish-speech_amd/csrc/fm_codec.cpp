@@ -1011,7 +1011,7 @@ int fm_codec_open(const fm_codec_config* cfg, int device, int precision, int max
         m->prec = precision;
         m->esz = precision == FM_PREC_BF16 ? 2 : 4;
         m->max_frames = max_frames;
-        HIPCHK(fm_stream_create(&m->stream, 1));
+        HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
         build_inventory(m.get());
         *out = m.release();
     });

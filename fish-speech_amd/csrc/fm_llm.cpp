@@ -2032,7 +2032,7 @@ int fm_llm_open(const fm_model_config* cfg, int device, int precision, int max_s
         m->C = c.num_codebooks;
         m->C1 = c.num_codebooks + 1;
         m->cb = c.codebook_size;
-        HIPCHK(fm_stream_create(&m->stream, 0));
+        HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
         const char* g = getenv("FISHMI_GRAPH");  // FISHMI_GRAPH=0: eager launches (profilers)
         m->use_graph = !(g && g[0] == '0');
         build_inventory(m.get());

@@ -66,32 +66,6 @@ inline float host_bf16_round(float x) {
     return r;
 }
 
-// A handle's HIP stream (non-blocking).  Developer env knobs for running the codec beside the LLM
-// decode (the serving vocoder thread): FISHMI_STREAM_PRIO=1 gives the LLM stream the highest and the
-// codec stream the lowest dispatch priority; FISHMI_CODEC_CU_STRIDE=k (> 1) confines the codec stream
-// to every k-th CU (hipExtStreamCreateWithCUMask).  role: 0 LLM, 1 codec.
-inline hipError_t fm_stream_create(hipStream_t* s, int role) {
-    const char* ce = getenv("FISHMI_CODEC_CU_STRIDE");
-    const int k = ce ? atoi(ce) : 0;
-    if (role == 1 && k > 1) {
-        hipDeviceProp_t p;
-        hipError_t e = hipGetDeviceProperties(&p, 0);
-        if (e != hipSuccess) return e;
-        const int ncu = p.multiProcessorCount;
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int i = 0; i < ncu; i += k) mask[i / 32] |= 1u << (i % 32);
-        return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
-    }
-    const char* pe = getenv("FISHMI_STREAM_PRIO");
-    if (pe && pe[0] == '1') {
-        int lo = 0, hi = 0;
-        hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if (e != hipSuccess) return e;
-        return hipStreamCreateWithPriority(s, hipStreamNonBlocking, role == 0 ? hi : lo);
-    }
-    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-}
-
 // RoPE table exactly like llama.py:1003-1022 / modded_dac.py:442-452: fp32 freqs, fp32 angle,
 // (cos, sin) cast to bf16.  [S][hd/2][2] floats.
 inline std::vector<float> rope_table_host(int S, int hd, float base) {

@@ -6,8 +6,8 @@ cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 FAST="--no-int8 --no-cpu-baseline --no-pmc --encode-seconds 0"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_codec_stream.py -x -v --timeout 180 --timeout-method thread -m gpu \
     > gpurun_out/voc_tests.log 2>&1 && tail -2 gpurun_out/voc_tests.log &&
-timeout -k 10 400 python -u bench.py $FAST "$@" > gpurun_out/bench_voc_ov.log 2>&1 &&
-timeout -k 10 400 python -u bench.py $FAST --serial-vocode --vocode-chunk 0 "$@" > gpurun_out/bench_voc_se.log 2>&1 &&
+timeout -k 10 400 python -u bench.py $FAST --overlap-vocode "$@" > gpurun_out/bench_voc_ov.log 2>&1 &&
+timeout -k 10 400 python -u bench.py $FAST --vocode-chunk 0 "$@" > gpurun_out/bench_voc_se.log 2>&1 &&
 python3 - <<'PY'
 import json
 for tag in ("ov", "se"):
