@@ -672,9 +672,12 @@ __global__ __launch_bounds__(NW * 64) void attn_fd_kernel(AttnDecArgs<T> a) {
             for (int c = 0; c < VL; ++c) vb[it][c] = pv[c];
         }
     };
+    // the RoPE row of pos goes out ahead of pass 0's K / V (vmcnt retires in order: the q-side
+    // arithmetic waits for these two floats only, not for the pass's loads)
+    const float* tab = a.rope + (size_t)pos * HD;
+    const float2 rcs = *reinterpret_cast<const float2*>(tab + 2 * (lane < half ? lane : 0));
     issue(j0);
     // ---- q heads (+ new k / v in the owner): qk-norm (fp32 incl. weight, one rounding), RoPE
-    const float* tab = a.rope + (size_t)pos * HD;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
         const int it = wave + NW * i;
@@ -692,7 +695,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fd_kernel(AttnDecArgs<T> a) {
         if (lane < half) {
             float y0 = x0[i], y1 = x1[i];
             if (isq || isk) {
-                const float c = tab[2 * lane], sn = tab[2 * lane + 1];
+                const float c = rcs.x, sn = rcs.y;
                 y0 = rnd<T>(x0[i] * c - x1[i] * sn);
                 y1 = rnd<T>(x1[i] * c + x0[i] * sn);
             }
