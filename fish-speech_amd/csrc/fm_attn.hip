@@ -1017,9 +1017,11 @@ __device__ int sample_top(const float* cv, const int* cid, int K, float M, float
     const float v = lane < K ? cv[lane] : -INFINITY;
     const int id = lane < K ? cid[lane] : 0x7fffffff;
     const float p = (v == -INFINITY) ? 0.f : rnd<T>(expf(v - M) / den);
+    // the reference's cumsum in rank order: lane k's value read as a scalar (k is uniform), so each
+    // step is a readlane + add instead of an LDS-routed shuffle
     float cum = 0.f, mycum = 0.f;
     for (int k = 0; k < K; ++k) {
-        cum += __shfl(p, k, 64);
+        cum += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p), k));
         if (lane == k) mycum = rnd<T>(cum);
     }
     const float t = rnd<T>(temperature), tp = rnd<T>(top_p);
@@ -1038,16 +1040,17 @@ __device__ int sample_top(const float* cv, const int* cid, int K, float M, float
         score = rnd<T>(prob / qv);
         bid = id;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float os = __shfl_xor(score, o, 64);
-        const int oid = __shfl_xor(bid, o, 64);
-        if (cbetter(os, oid, score, bid)) {
-            score = os;
-            bid = oid;
-        }
+    // argmax of (score desc, id asc): the wave maximum by DPP, then the smallest id among the lanes
+    // holding it (one lane but for exact ties), read as scalars
+    const float best = wave_max(score);
+    uint64_t hit = __ballot(score == best);
+    int tok = 0x7fffffff;
+    while (hit) {
+        const int l = __ffsll((long long)hit) - 1;
+        tok = min(tok, __builtin_amdgcn_readlane(bid, l));
+        hit &= hit - 1;
     }
-    return bid;
+    return tok;
 }
 
 // ---- top_k > 64 (the reference's logits_to_probs takes any top_k, inference.py:54-77) ----------
@@ -1501,25 +1504,20 @@ __global__ __launch_bounds__(256) void sample_fast_kernel(SampleArgs a) {
     if (K > Nl) K = Nl;
     SFTS(2)
     // fast threshold: the K-th largest of the 64 lane maxima t0 has at least K wave keys >= it (the
-    // K lanes' maxima), so it is a valid wave threshold whenever those keys fit the candidate cap;
-    // a 64-lane bitonic sort of the maxima finds it (else the radix search below)
+    // K lanes' maxima), so it is a valid wave threshold whenever those keys fit the candidate cap
+    // (else the radix search below)
     uint32_t kth;
     {
         uint32_t lm = 0;
 #pragma unroll
         for (int i = 0; i < SF_PER; ++i) lm = key[i] > lm ? key[i] : lm;
-        uint32_t v = lm;
-#pragma unroll
-        for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                const uint32_t o = (uint32_t)__shfl_xor((int)v, j, 64);
-                const bool lower = (lane & j) == 0, desc = (lane & k) == 0;
-                // descending overall: the lower lane of a descending pair keeps the larger key
-                v = (lower == desc) ? (o > v ? o : v) : (o < v ? o : v);
-            }
+        // the K-th largest lane maximum by a binary search on its bits: one ballot + popcount per
+        // bit (scalar work) instead of a 21-step shuffle sort of the 64 maxima
+        uint32_t t0 = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t c = t0 | (1u << bit);
+            if ((uint32_t)__popcll(__ballot(lm >= c)) >= (uint32_t)K) t0 = c;
         }
-        const uint32_t t0 = (uint32_t)__shfl((int)v, K - 1, 64);
         uint32_t cl = 0;
 #pragma unroll
         for (int i = 0; i < SF_PER; ++i) cl += key[i] >= t0 ? 1u : 0u;

@@ -263,6 +263,8 @@ struct FmTuning {
                              // one block per kv head, no cross-block combine)
     int prefill_attn = 1;    // 1: prompt-chunk attention on attn_prefill_kernel (bf16, head_dim 128, flash form)
     int prompt_gemm = 1;     // 1: prompt-chunk linears (R > 32) on the codec's LDS-tiled GEMM kernels
+    int prompt_ks_tiles = 384;  // prompt GEMM: split K until ceil(R/128) ceil(N/128) ks reaches this ...
+    int prompt_ks_max = 8;      // ... or ks this (fp32 slabs + the conv split-K epilogue)
     int conv2 = 1;           // 1: codec GEMMs on the LDS-staged conv_gemm2_kernel, 0: conv_gemm_kernel
     int conv_splitk = 1;     // 1: small-grid codec GEMMs split K into fp32 slabs + a reduce/epilogue kernel
     int resunit_cfg = 1;     // resunit_kernel tile at 192 / 96 channels: 0 (BM 128 / 256, 8 time tiles per wave), 1 (BM 64 / 128, 4 tiles), 2 (128 / 128)

@@ -319,10 +319,12 @@ template <typename T> struct Run {
         c.out = Y;
         c.ldo = ldy;
         c.flags = CE_STORE | (bias ? CE_BIAS : 0) | (epi == EPI_RESID ? CE_RES : 0);
-        // split K (fp32 slabs + the conv split-K epilogue) until the 128 x 128 tiles number >= 384
+        // split K (fp32 slabs + the conv split-K epilogue) until the 128 x 128 tiles number >=
+        // prompt_ks_tiles (default 384)
         const long long t128 = (long long)FM_CEIL(R, 128) * FM_CEIL(N, 128);
         int ks = 1;
-        while (t128 * ks < 384 && ks < 8 && K / 32 >= 8 * ks * 2) ks *= 2;
+        while (t128 * ks < fm_tuning().prompt_ks_tiles && ks < fm_tuning().prompt_ks_max && K / 32 >= 8 * ks * 2)
+            ks *= 2;
         c.ksplit = ks;
         c.slab = m->skpart;
         c.slab_cap = (size_t)m->skpart_cap;
@@ -2500,6 +2502,12 @@ int fm_tune(const char* key, int value) {
             t.attn_cap = value;
         } else if (k == "prefill_attn") {
             t.prefill_attn = value != 0;
+        } else if (k == "prompt_ks_tiles") {
+            FMCHECK(value >= 1, "prompt_ks_tiles must be >= 1");
+            t.prompt_ks_tiles = value;
+        } else if (k == "prompt_ks_max") {
+            FMCHECK(value == 1 || value == 2 || value == 4 || value == 8, "prompt_ks_max must be 1, 2, 4 or 8");
+            t.prompt_ks_max = value;
         } else if (k == "prompt_gemm") {
             t.prompt_gemm = value != 0;
         } else if (k == "conv2") {
