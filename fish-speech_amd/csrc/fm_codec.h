@@ -88,6 +88,8 @@ struct RvqPtrs {
 };
 
 template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a);
+// the split-K epilogue alone over a.ksplit slabs in a.slab (the prompt skinny GEMM's finisher)
+template <typename T> void launch_conv_epi(hipStream_t s, const ConvArgs<T>& a);
 template <typename T> void launch_snake_inv(hipStream_t s, const T* alpha, int64_t n, float* ialpha);
 // encode side (fm_codec_encode)
 struct VqEncPtrs {

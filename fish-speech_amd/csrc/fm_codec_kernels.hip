@@ -844,6 +844,12 @@ template <typename T> static void conv_splitk_go(hipStream_t s, const ConvArgs<T
     }
 }
 
+template <typename T> void launch_conv_epi(hipStream_t s, const ConvArgs<T>& b) {
+    FMCHECK(b.ksplit >= 1 && b.slab && !(b.flags & CE_NORM) && b.Co % 8 == 0, "conv epilogue: slabs, Co % 8, no norm");
+    const size_t n = (size_t)b.nphase * b.Lq * (((b.flags & CE_SWIGLU) ? b.Co / 2 : b.Co) / 8);
+    conv_splitk_epi_kernel<T><<<(int)std::min<size_t>(FM_CEIL(n, 256), 4096), 256, 0, s>>>(b);
+}
+
 template <typename T> void launch_conv_gemm(hipStream_t s, const ConvArgs<T>& a0) {
     ConvArgs<T> a = a0;
     a.shift0 = a.shift[0];
@@ -1186,6 +1192,7 @@ void launch_conv_weight(hipStream_t s, const float* w, int kind, int Ci, int Co,
 
 #define CINST(T)                                                                                     \
     template void launch_conv_gemm<T>(hipStream_t, const ConvArgs<T>&);                              \
+    template void launch_conv_epi<T>(hipStream_t, const ConvArgs<T>&);                               \
     template void launch_silu_mul<T>(hipStream_t, const T*, T*, size_t);                             \
     template void launch_rvq_decode<T>(hipStream_t, const int32_t*, int, int, int, int, int,         \
                                        const RvqPtrs&, int, T*);                                     \

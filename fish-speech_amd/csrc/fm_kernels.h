@@ -263,6 +263,8 @@ struct FmTuning {
                              // one block per kv head, no cross-block combine)
     int prefill_attn = 1;    // 1: prompt-chunk attention on attn_prefill_kernel (bf16, head_dim 128, flash form)
     int prompt_gemm = 1;     // 1: prompt-chunk linears (R > 32) on the codec's LDS-tiled GEMM kernels
+    int prompt_skinny = 1;      // prompt linears at 32 < R <= 64 rows (bf16) on prompt_skinny_kernel ...
+    int prompt_skinny_blocks = 256;  // ... with K sliced until its 64-row blocks number >= this
     int prompt_ks_tiles = 384;  // prompt GEMM: split K until ceil(R/128) ceil(N/128) ks reaches this ...
     int prompt_ks_max = 8;      // ... or ks this (fp32 slabs + the conv split-K epilogue)
     int conv2 = 1;           // 1: codec GEMMs on the LDS-staged conv_gemm2_kernel, 0: conv_gemm_kernel
@@ -468,6 +470,19 @@ template <typename T> struct FinalizeArgs {
 template <typename T> void launch_finalize_norm(hipStream_t s, const FinalizeArgs<T>& a);
 
 // ---- fused decode attention / sampler (fm_attn.hip) ------------------------------------------
+// prompt-chunk linear at 32 < R <= 64 rows, bf16 (fm_prompt.hip): raw fp32 K-slice partials into the
+// conv split-K slab layout [ks][R][N]; the conv split-K epilogue finishes it
+struct PromptSkinnyArgs {
+    const bf16_t* w;   // packed weight [ceil(N/16)][K/32][512]
+    const bf16_t* x;   // activation rows [R][ldx]
+    int ldx, R, N, K;
+    float* slab;       // [ks][R][N]
+};
+void launch_prompt_skinny(hipStream_t s, const PromptSkinnyArgs& a, int ks);
+// K slices: the smallest divisor of K/32 with >= 8 k-steps per slice giving >= target blocks of 64
+// rows (the largest such when none does; 0 when K / 32 < 8)
+int prompt_skinny_ks(int N, int K, int target);
+
 template <typename T> struct AttnDecArgs {
     const T* qkv;        // raw projections [R][ldqkv] (q heads, k heads, v heads)
     int ldqkv;

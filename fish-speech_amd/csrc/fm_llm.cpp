@@ -319,6 +319,29 @@ template <typename T> struct Run {
         c.out = Y;
         c.ldo = ldy;
         c.flags = CE_STORE | (bias ? CE_BIAS : 0) | (epi == EPI_RESID ? CE_RES : 0);
+        hipStream_t st = s;
+        const int64_t bytes = (int64_t)N * K * E + (int64_t)R * K * E + (int64_t)R * N * E;
+        const double flops = 2.0 * R * N * K;
+        if constexpr (sizeof(T) == 2) {
+            // R <= 64: one weight pass for all rows (fm_prompt.hip), K slices finished by the conv
+            // split-K epilogue (the same roundings as below)
+            auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+            const int ks = prompt_skinny_ks(N, K, fm_tuning().prompt_skinny_blocks);
+            if (fm_tuning().prompt_skinny && ks > 0 && R <= 64 && ldx % 8 == 0 && al16(X) && al16(Y) && ldy % 8 == 0 &&
+                (!c.res || (al16(c.res) && ldr % 8 == 0)) && (long long)ks * R * N <= m->skpart_cap) {
+                c.ksplit = ks;
+                c.slab = m->skpart;
+                c.slab_cap = (size_t)m->skpart_cap;
+                const PromptSkinnyArgs p{(const bf16_t*)W, (const bf16_t*)X, ldx, R, N, K, m->skpart};
+                auto go = [st, c, p, ks] {
+                    launch_prompt_skinny(st, p, ks);
+                    launch_conv_epi<T>(st, c);
+                };
+                m->prof.record(cls, bytes, go);
+                run_(cls, bytes, flops, go);
+                return true;
+            }
+        }
         // split K (fp32 slabs + the conv split-K epilogue) until the 128 x 128 tiles number >=
         // prompt_ks_tiles (default 384)
         const long long t128 = (long long)FM_CEIL(R, 128) * FM_CEIL(N, 128);
@@ -328,9 +351,6 @@ template <typename T> struct Run {
         c.ksplit = ks;
         c.slab = m->skpart;
         c.slab_cap = (size_t)m->skpart_cap;
-        const int64_t bytes = (int64_t)N * K * E + (int64_t)R * K * E + (int64_t)R * N * E;
-        const double flops = 2.0 * R * N * K;
-        hipStream_t st = s;
         auto go = [st, c] { launch_conv_gemm<T>(st, c); };
         m->prof.record(cls, bytes, go);
         run_(cls, bytes, flops, go);
@@ -2502,6 +2522,11 @@ int fm_tune(const char* key, int value) {
             t.attn_cap = value;
         } else if (k == "prefill_attn") {
             t.prefill_attn = value != 0;
+        } else if (k == "prompt_skinny") {
+            t.prompt_skinny = value != 0;
+        } else if (k == "prompt_skinny_blocks") {
+            FMCHECK(value >= 1, "prompt_skinny_blocks must be >= 1");
+            t.prompt_skinny_blocks = value;
         } else if (k == "prompt_ks_tiles") {
             FMCHECK(value >= 1, "prompt_ks_tiles must be >= 1");
             t.prompt_ks_tiles = value;
