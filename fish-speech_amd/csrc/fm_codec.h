@@ -18,6 +18,9 @@ enum {
                       // output) at position t + rope_pos0, as rope_qk_kernel does it
     CE_NORM = 1024,   // split-K epilogue only (one phase, Co % 512 == 0, Co <= 2048): out2 = RMSNorm(y)
                       // with weight normw, the next layer's / stage's norm, as rmsnorm_wave_kernel does it
+    CE_SWIGLU8 = 2048,  // split-K epilogue only: CE_SWIGLU over the row-interleaved W1 || W3 (8 rows of
+                        // W1, then the same 8 of W3): out[t][8g + e] = round(round(silu(y[16g + e])) *
+                        // y[16g + 8 + e]), as swiglu_i8_kernel does it on the stored output (no bias)
 };
 
 // out[t_out][co] (time-major, ld = ldo) with t_out = tq * stride + phase, tq in [0, Lq):

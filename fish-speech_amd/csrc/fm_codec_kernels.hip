@@ -147,17 +147,21 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs<T> a) {
 // CE_SWIGLU: the GEMM's channels are [W1 rows | W3 rows]; thread (t, n) also sums the partials of
 // channel Co/2 + n and writes round(round(silu(g1)) * g3), g = round(sum) -- silu_mul_kernel's
 // roundings on the two GEMMs' stored outputs, so the result is bit-identical to the three launches.
+// CE_SWIGLU8: the same over the 8-row interleave of the LLM's packed W1 || W3 (thread: gate channels
+// 16 cc .. + 8, up channels 16 cc + 8 .. + 8, outputs 8 cc .. + 8), swiglu_i8_kernel's roundings.
 template <typename T>
 __global__ __launch_bounds__(256) void conv_splitk_epi_kernel(ConvArgs<T> a) {
     const int fl = a.flags;
-    const int half = (fl & CE_SWIGLU) ? a.Co >> 1 : 0;
-    const int cpr = (half ? half : a.Co) >> 3;
+    const bool sw8 = fl & CE_SWIGLU8;
+    // the up channel's offset from the gate's: Co/2 ([W1 | W3]) or 8 (8-row interleave)
+    const int half = (fl & CE_SWIGLU) ? a.Co >> 1 : (sw8 ? 8 : 0);
+    const int cpr = sw8 ? a.Co >> 4 : ((fl & CE_SWIGLU) ? half : a.Co) >> 3;
     const size_t n = (size_t)a.nphase * a.Lq * cpr;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
         const int cc = (int)(i % cpr);
         const size_t pt = i / cpr;  // phase * Lq + t
         const int t = (int)(pt % a.Lq), phase = (int)(pt / a.Lq);
-        const int co = 8 * cc;
+        const int co = sw8 ? 16 * cc : 8 * cc;
         float y[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         float u[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         for (int kz = 0; kz < a.ksplit; ++kz) {
@@ -185,7 +189,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epi_kernel(ConvArgs<T> a) {
                 const float g = rnd<T>(y[j]);
                 o[j] = rnd<T>(rnd<T>(g / (1.0f + expf(-g))) * rnd<T>(u[j]));
             }
-            store8(reinterpret_cast<T*>(a.out) + ((size_t)t * a.stride + phase) * a.ldo + co, o);
+            store8(reinterpret_cast<T*>(a.out) + ((size_t)t * a.stride + phase) * a.ldo + 8 * cc, o);
             continue;
         }
         float b[8];
@@ -846,7 +850,10 @@ template <typename T> static void conv_splitk_go(hipStream_t s, const ConvArgs<T
 
 template <typename T> void launch_conv_epi(hipStream_t s, const ConvArgs<T>& b) {
     FMCHECK(b.ksplit >= 1 && b.slab && !(b.flags & CE_NORM) && b.Co % 8 == 0, "conv epilogue: slabs, Co % 8, no norm");
-    const size_t n = (size_t)b.nphase * b.Lq * (((b.flags & CE_SWIGLU) ? b.Co / 2 : b.Co) / 8);
+    FMCHECK(!(b.flags & CE_SWIGLU8) || (b.Co % 16 == 0 && !(b.flags & (CE_SWIGLU | CE_BIAS))),
+            "conv epilogue: the interleaved SwiGLU needs Co % 16 == 0, no bias");
+    const size_t n = (size_t)b.nphase * b.Lq *
+                     ((b.flags & CE_SWIGLU8) ? b.Co / 16 : (((b.flags & CE_SWIGLU) ? b.Co / 2 : b.Co) / 8));
     conv_splitk_epi_kernel<T><<<(int)std::min<size_t>(FM_CEIL(n, 256), 4096), 256, 0, s>>>(b);
 }
 

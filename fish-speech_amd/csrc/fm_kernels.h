@@ -265,6 +265,7 @@ struct FmTuning {
     int prompt_gemm = 1;     // 1: prompt-chunk linears (R > 32) on the codec's LDS-tiled GEMM kernels
     int prompt_skinny = 1;      // prompt linears at 32 < R <= 64 rows (bf16) on prompt_skinny_kernel ...
     int prompt_skinny_blocks = 256;  // ... with K sliced until its 64-row blocks number >= this
+    int prompt_swiglu = 1;      // skinny w1 || w3: the SwiGLU in its split-K epilogue (no separate launch)
     int prompt_ks_tiles = 384;  // prompt GEMM: split K until ceil(R/128) ceil(N/128) ks reaches this ...
     int prompt_ks_max = 8;      // ... or ks this (fp32 slabs + the conv split-K epilogue)
     int conv2 = 1;           // 1: codec GEMMs on the LDS-staged conv_gemm2_kernel, 0: conv_gemm_kernel
@@ -477,6 +478,10 @@ struct PromptSkinnyArgs {
     const bf16_t* x;   // activation rows [R][ldx]
     int ldx, R, N, K;
     float* slab;       // [ks][R][N]
+    // one slice and act set: no slab, the interleaved SwiGLU of the row-interleaved W1 || W3 stored
+    // straight to act [R][lda] (swiglu_i8_kernel's roundings)
+    bf16_t* act = nullptr;
+    int lda = 0;
 };
 void launch_prompt_skinny(hipStream_t s, const PromptSkinnyArgs& a, int ks);
 // K slices: the smallest divisor of K/32 with >= 8 k-steps per slice giving >= target blocks of 64

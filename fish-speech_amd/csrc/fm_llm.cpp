@@ -299,8 +299,9 @@ template <typename T> struct Run {
     // The packed weight layout is the same; epilogues: round(acc + bias) and round(res + round(acc)).
     bool prompt_gemm(const void* W, const void* W2, const void* bias, const void* X, int ldx, int R, int N, int K,
                      void* Y, int ldy, const void* res, int ldr, int epi, const char* cls) {
-        if (R <= 32 || W2 || m->qinfo(W) || !fm_tuning().prompt_gemm || (epi != EPI_STORE && epi != EPI_RESID) ||
-            N % 16 || K % 32 || N < 96)
+        if (R <= 32 || W2 || m->qinfo(W) || !fm_tuning().prompt_gemm ||
+            (epi != EPI_STORE && epi != EPI_RESID && epi != EPI_SWIGLU8) || N % 16 || K % 32 || N < 96 ||
+            (epi == EPI_SWIGLU8 && (bias || N % 16)))
             return false;
         ConvArgs<T> c{};
         c.x = (const T*)X;
@@ -318,7 +319,8 @@ template <typename T> struct Run {
         c.ldr = ldr;
         c.out = Y;
         c.ldo = ldy;
-        c.flags = CE_STORE | (bias ? CE_BIAS : 0) | (epi == EPI_RESID ? CE_RES : 0);
+        c.flags = CE_STORE | (bias ? CE_BIAS : 0) | (epi == EPI_RESID ? CE_RES : 0) |
+                  (epi == EPI_SWIGLU8 ? CE_SWIGLU8 : 0);  // SWIGLU8: Y = act [R][N/2], ldy = N/2
         hipStream_t st = s;
         const int64_t bytes = (int64_t)N * K * E + (int64_t)R * K * E + (int64_t)R * N * E;
         const double flops = 2.0 * R * N * K;
@@ -332,16 +334,22 @@ template <typename T> struct Run {
                 c.ksplit = ks;
                 c.slab = m->skpart;
                 c.slab_cap = (size_t)m->skpart_cap;
-                const PromptSkinnyArgs p{(const bf16_t*)W, (const bf16_t*)X, ldx, R, N, K, m->skpart};
-                auto go = [st, c, p, ks] {
+                PromptSkinnyArgs p{(const bf16_t*)W, (const bf16_t*)X, ldx, R, N, K, m->skpart};
+                const bool direct = ks == 1 && epi == EPI_SWIGLU8;  // the kernel stores act itself
+                if (direct) {
+                    p.act = (bf16_t*)Y;
+                    p.lda = ldy;
+                }
+                auto go = [st, c, p, ks, direct] {
                     launch_prompt_skinny(st, p, ks);
-                    launch_conv_epi<T>(st, c);
+                    if (!direct) launch_conv_epi<T>(st, c);
                 };
                 m->prof.record(cls, bytes, go);
                 run_(cls, bytes, flops, go);
                 return true;
             }
         }
+        if (epi == EPI_SWIGLU8) return false;  // the conv GEMMs' own epilogues have no interleaved SwiGLU
         // split K (fp32 slabs + the conv split-K epilogue) until the 128 x 128 tiles number >=
         // prompt_ks_tiles (default 384)
         const long long t128 = (long long)FM_CEIL(R, 128) * FM_CEIL(N, 128);
@@ -640,11 +648,17 @@ template <typename T> struct Run {
         }
         if (!(bs && bs_linear(L.w13, nullptr, xnb, d.dim, R, 2 * d.inter, d.dim, m->act, d.inter, nullptr,
                               EPI_SWIGLU8))) {
-            linear(L.w13, nullptr, nullptr, xnb, d.dim, R, 2 * d.inter, d.dim, m->act2, 2 * d.inter, nullptr, 0,
-                   nullptr, EPI_STORE, "linear");
-            run_("other", 0, 0, [&] {
-                launch_swiglu_i8<T>(s, (const T*)m->act2, 2 * d.inter, (T*)m->act, d.inter, d.inter, R);
-            });
+            // a prompt chunk's w1 || w3 with the SwiGLU in its split-K epilogue (skinny path), else the
+            // stored output and the SwiGLU launch
+            if (!(fm_tuning().prompt_swiglu &&
+                  prompt_gemm(L.w13, nullptr, nullptr, xnb, d.dim, R, 2 * d.inter, d.dim, m->act, d.inter, nullptr, 0,
+                              EPI_SWIGLU8, "linear"))) {
+                linear(L.w13, nullptr, nullptr, xnb, d.dim, R, 2 * d.inter, d.dim, m->act2, 2 * d.inter, nullptr, 0,
+                       nullptr, EPI_STORE, "linear");
+                run_("other", 0, 0, [&] {
+                    launch_swiglu_i8<T>(s, (const T*)m->act2, 2 * d.inter, (T*)m->act, d.inter, d.inter, R);
+                });
+            }
         }
         if (bs && bs_linear(L.w2, nullptr, m->act, d.inter, R, d.dim, d.inter, nullptr, d.dim, m->bsB, EPI_SLAB, &kp)) {
             pend.on = true;  // x = h + w2(act): finalised by the next block's norm, or flush()
@@ -2522,6 +2536,8 @@ int fm_tune(const char* key, int value) {
             t.attn_cap = value;
         } else if (k == "prefill_attn") {
             t.prefill_attn = value != 0;
+        } else if (k == "prompt_swiglu") {
+            t.prompt_swiglu = value != 0;
         } else if (k == "prompt_skinny") {
             t.prompt_skinny = value != 0;
         } else if (k == "prompt_skinny_blocks") {

@@ -14,7 +14,8 @@
 // The K range is cut into ks slices (grid y) so the grid fills the chip; each slice writes raw fp32
 // partials to the conv split-K slab layout [ks][R][N], and conv_splitk_epi_kernel applies the
 // epilogue: round(sum of slices + bias), the residual, the store.  The fp32 sum over slices runs in
-// slice order, each slice's MFMA chain in k order.
+// slice order, each slice's MFMA chain in k order.  An unsliced w1 || w3 (act set) applies the
+// interleaved SwiGLU itself (no slab, no epilogue launch; swiglu_i8_kernel's roundings).
 //
 // Measured forms that lost (profiles/r06_prompt_skinny_v3_trace.md, 64-token prefill): loading the
 // activation chunks two ahead (6.88 vs 6.57 ms) and staging a whole <= 20-step slice at once with a
@@ -98,6 +99,26 @@ __global__ __launch_bounds__(256) void prompt_skinny_kernel(PromptSkinnyArgs a) 
     for (int c = 0; c < nch; c += 2) {
         chunk(wa, c);
         if (c + 1 < nch) chunk(wbq, c + 1);
+    }
+    if (a.act) {  // one slice: act[r][8 tile + 4 (lane >> 4) + j] = round(round(silu(g)) * u), g the gate
+        // row 16 tile + 4 (lane >> 4) + j (lanes 0-31), u the up row 8 further (lane + 32)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int r = 16 * t + (lane & 15);
+            float o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float g = rnd<bf16_t>(acc[t][j]);
+                const float u = rnd<bf16_t>(__shfl_xor(acc[t][j], 32));
+                o[j] = rnd<bf16_t>(rnd<bf16_t>(g / (1.0f + expf(-g))) * u);
+            }
+            if (live && lane < 32 && r < a.R) {
+                bf16_t* d = a.act + (size_t)r * a.lda + 8 * tile + 4 * (lane >> 4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) st(d, j, o[j]);
+            }
+        }
+        return;
     }
     if (!live) return;
     // lane: weight rows 16 tile + 4 (lane >> 4) + j, activation row 16 t + (lane & 15)
