@@ -364,6 +364,28 @@ template <typename T> struct Run {
         run_(cls, bytes, flops, go);
         return true;
     }
+    // A prompt chunk's wo / w2 (32 < R <= 64, bf16) as raw K-slice partials in m->skpart ([ks][R][N], the
+    // finalize_norm slab layout): the residual add, the bias and the next RMSNorm then run in one
+    // finalize_norm launch instead of the split-K epilogue + an RMSNorm launch.  false: not eligible.
+    bool prompt_slab(const void* W, const void* X, int ldx, int R, int N, int K, int* ks_out) {
+        if constexpr (sizeof(T) != 2) {
+            return false;
+        } else {
+            if (!fm_tuning().prompt_fin || !fm_tuning().prompt_skinny || !fm_tuning().prompt_gemm || R <= 32 ||
+                R > 64 || m->qinfo(W) || N % 16 || K % 32 || ldx % 8 || ((uintptr_t)X & 15))
+                return false;
+            const int ks = prompt_skinny_ks(N, K, fm_tuning().prompt_skinny_blocks);
+            if (ks <= 0 || (long long)ks * R * N > m->skpart_cap) return false;
+            const PromptSkinnyArgs p{(const bf16_t*)W, (const bf16_t*)X, ldx, R, N, K, m->skpart};
+            hipStream_t st = s;
+            auto go = [st, p, ks] { launch_prompt_skinny(st, p, ks); };
+            const int64_t bytes = (int64_t)N * K * E + (int64_t)R * K * E + (int64_t)ks * R * N * 4;
+            m->prof.record("linear", bytes, go);
+            run_("linear", bytes, 2.0 * R * N * K, go);
+            *ks_out = ks;
+            return true;
+        }
+    }
     void linear(const void* W, const void* W2, const void* bias, const void* X, int ldx, int R, int N,
                 int K, void* Y, int ldy, const void* res, int ldr, float* Yf, int epi, const char* cls) {
         if (bs_use(R, false) && !W2 && !res && (epi == EPI_F32 || epi == EPI_STORE) &&
@@ -547,10 +569,7 @@ template <typename T> struct Run {
                 linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
                        nullptr, EPI_STORE, "linear");
         } else {
-            flush();
-            run_("norm", 0, 0, [&] {
-                launch_rmsnorm<T>(s, (const T*)xb, d.dim, (const T*)L.an, d.dim, eps, (T*)xnb, d.dim, R);
-            });
+            bs_norm_in(d, L, R, xb, xnb);  // a prompt chunk's pending w2 (prompt_slab) finalised with this norm
             linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
                    nullptr, EPI_STORE, "linear");
         }
@@ -639,6 +658,8 @@ template <typename T> struct Run {
         }
         if (bs && bs_linear(L.wo, nullptr, m->att, d.nq(), R, d.dim, d.nq(), nullptr, d.dim, m->bsA, EPI_SLAB, &kp)) {
             finalize_norm(m->bsA, kp, L.bo, xb, hb, L.fn, xnb, d.dim, R, wscale(L.wo));  // h = x + wo(att); xn = ffn_norm(h)
+        } else if (!bs && prompt_slab(L.wo, m->att, d.nq(), R, d.dim, d.nq(), &kp)) {
+            finalize_norm(m->skpart, kp, L.bo, xb, hb, L.fn, xnb, d.dim, R, nullptr);  // h = x + wo(att); ffn_norm
         } else {
             linear(L.wo, nullptr, L.bo, m->att, d.nq(), R, d.dim, d.nq(), hb, d.dim, xb, d.dim, nullptr,
                    EPI_RESID, "linear");
@@ -669,6 +690,15 @@ template <typename T> struct Run {
             pend.res = hb;
             pend.out = xb;
             pend.sc = wscale(L.w2);
+        } else if (!bs && prompt_slab(L.w2, m->act, d.inter, R, d.dim, d.inter, &kp)) {
+            pend.on = true;  // x = h + w2(act): finalised with the next block's norm, or flush()
+            pend.slab = m->skpart;
+            pend.kparts = kp;
+            pend.d = d.dim;
+            pend.R = R;
+            pend.res = hb;
+            pend.out = xb;
+            pend.sc = nullptr;
         } else {
             linear(L.w2, nullptr, nullptr, m->act, d.inter, R, d.dim, d.inter, xb, d.dim, hb, d.dim, nullptr,
                    EPI_RESID, "linear");
@@ -2536,6 +2566,8 @@ int fm_tune(const char* key, int value) {
             t.attn_cap = value;
         } else if (k == "prefill_attn") {
             t.prefill_attn = value != 0;
+        } else if (k == "prompt_fin") {
+            t.prompt_fin = value != 0;
         } else if (k == "prompt_swiglu") {
             t.prompt_swiglu = value != 0;
         } else if (k == "prompt_skinny") {
