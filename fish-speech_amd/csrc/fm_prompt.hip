@@ -18,8 +18,10 @@
 // interleaved SwiGLU itself (no slab, no epilogue launch; swiglu_i8_kernel's roundings).
 //
 // Measured forms that lost (profiles/r06_prompt_skinny_v3_trace.md, 64-token prefill): loading the
-// activation chunks two ahead (6.88 vs 6.57 ms) and staging a whole <= 20-step slice at once with a
-// 16-deep ring (7.31 ms: 82 KiB of LDS leaves one block per CU).
+// activation chunks two ahead (6.88 vs 6.57 ms), staging a whole <= 20-step slice at once with a
+// 16-deep ring (7.31 ms: 82 KiB of LDS leaves one block per CU), and no LDS at all -- each wave
+// loading its 4 activation fragments per k-step from L2 beside its weight fragment (10.03 vs
+// 6.05 ms: 4x the weight bytes through L2; w1 || w3 92 vs 34 us, profiles/r06_prompt_skinny_l2direct_trace.md).
 #include "fm_codec.h"
 #include "fm_frag.h"
 #include "fm_kernels.h"
