@@ -22,8 +22,9 @@
 // 16-deep ring (7.31 ms: 82 KiB of LDS leaves one block per CU), and no LDS at all -- each wave
 // loading its 4 activation fragments per k-step from L2 beside its weight fragment (10.03 vs
 // 6.05 ms: 4x the weight bytes through L2; w1 || w3 92 vs 34 us, profiles/r06_prompt_skinny_l2direct_trace.md).
-// Neutral: 8-step chunks (6.15 vs 6.04 ms, profiles/r06_prompt_chunk8_trace.md) and grid targets of
-// 384-1024 blocks (6.04-6.30 ms, profiles/r06_prompt_blocks_sweep.txt).
+// Neutral or slower: 8-step chunks (6.15 vs 6.04 ms, profiles/r06_prompt_chunk8_trace.md), grid
+// targets of 384-1024 blocks (6.04-6.30 ms, profiles/r06_prompt_blocks_sweep.txt), and a third weight
+// set in the ring (6.25 vs 6.08 ms; w1 || w3 38.9 vs 34 us).
 #include "fm_codec.h"
 #include "fm_frag.h"
 #include "fm_kernels.h"
