@@ -570,8 +570,16 @@ template <typename T> struct Run {
                        nullptr, EPI_STORE, "linear");
         } else {
             bs_norm_in(d, L, R, xb, xnb);  // a prompt chunk's pending w2 (prompt_slab) finalised with this norm
-            linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
-                   nullptr, EPI_STORE, "linear");
+            int kq = 0;
+            // a prompt chunk's QKV as K-slice slabs, summed by qk_rope_cache_kernel itself (no epilogue launch)
+            if (!is_fast && !rows_distinct_slots && fm_tuning().prompt_qkv_slab &&
+                prompt_slab(L.wqkv, xnb, d.dim, R, d.nqkv(), d.dim, &kq)) {
+                qslab = m->skpart;
+                qslab_kp = kq;
+            } else {
+                linear(L.wqkv, nullptr, L.bqkv, xnb, d.dim, R, d.nqkv(), d.dim, m->qkv, d.nqkv(), nullptr, 0,
+                       nullptr, EPI_STORE, "linear");
+            }
         }
         const float scale = 1.0f / sqrtf((float)d.hd);
         // One row per slot (batched decode frames, every fast pass): the fused decode attention
@@ -609,6 +617,9 @@ template <typename T> struct Run {
         } else {
             QkArgs<T> qa{(const T*)m->qkv, d.nqkv(), rslot, rpos, fixed_pos, d.nh, d.nkv, d.hd, d.qk_norm,
                          eps, (const T*)L.qn, (const T*)L.kn, rope, (T*)m->q, (T*)kc, (T*)vc, sstride, loff, Sc};
+            qa.qslab = qslab;
+            qa.qslab_kp = qslab_kp;
+            qa.qbias = (const T*)L.bqkv;
             run_("rope", 0, 0, [&] { launch_qk_rope_cache<T>(s, qa, R); });
             if (!is_fast) {
                 // rows [r0, r0 + len) in pieces of <= ATTN_PIECE rows (rows are independent given the cache)
@@ -2566,6 +2577,8 @@ int fm_tune(const char* key, int value) {
             t.attn_cap = value;
         } else if (k == "prefill_attn") {
             t.prefill_attn = value != 0;
+        } else if (k == "prompt_qkv_slab") {
+            t.prompt_qkv_slab = value != 0;
         } else if (k == "prompt_fin") {
             t.prompt_fin = value != 0;
         } else if (k == "prompt_swiglu") {

@@ -515,8 +515,24 @@ __global__ __launch_bounds__(256) void qk_rope_cache_kernel(QkArgs<T> a) {
     float x0[2], x1[2];
     int np = 0;
     for (int p = lane; p < half; p += 64, ++np) {
-        x0[np] = ld(src, 2 * p);
-        x1[np] = ld(src, 2 * p + 1);
+        if (a.qslab) {  // round(sum of the K slices + bias): the split-K epilogue's one rounding
+            const size_t c = (size_t)head * hd + 2 * p;
+            float v0 = 0.f, v1 = 0.f;
+            for (int q = 0; q < a.qslab_kp; ++q) {
+                const float* sp = a.qslab + ((size_t)q * gridDim.x + r) * a.ldqkv + c;
+                v0 += sp[0];
+                v1 += sp[1];
+            }
+            if (a.qbias) {
+                v0 += ld(a.qbias, c);
+                v1 += ld(a.qbias, c + 1);
+            }
+            x0[np] = rnd<T>(v0);
+            x1[np] = rnd<T>(v1);
+        } else {
+            x0[np] = ld(src, 2 * p);
+            x1[np] = ld(src, 2 * p + 1);
+        }
     }
     if (kind < 2 && a.qk_norm) {
         float ss = 0.f;

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 DEFAULTS = {"attn3": 1, "attn_fd": 1, "fd_min": 32, "fd_nw": 8, "fd_min16": 256, "gemv_chain": 0, "gemv_nt": 1, "gemv_u": 8, "gemv_wpb": 4,
             "ksb_balance": 0, "ksb_blocks": 512, "attn_cap": 32, "prefill_attn": 1, "prompt_gemm": 1,
             "conv2": 1, "conv_splitk": 1, "kv_prefetch": 1, "fin_ksb": 0, "gemv_dummy": 2, "rowgemv": 27, "rowgemv_q4": 31, "sampler_kth": 1, "row_qkv_rp": 8,
-            "fattn_wo": 1, "fw_cheap": 0, "fw_delay": 0, "prompt_skinny": 1, "prompt_skinny_blocks": 256, "prompt_swiglu": 1, "prompt_fin": 1}
+            "fattn_wo": 1, "fw_cheap": 0, "fw_delay": 0, "prompt_skinny": 1, "prompt_skinny_blocks": 256, "prompt_swiglu": 1, "prompt_fin": 1, "prompt_qkv_slab": 0}
 
 DECODE_KNOBS = [{"attn3": 0}, {"attn3": 0, "attn_fd": 0}, {"fd_nw": 4}, {"fd_nw": 4, "fd_min": 16}, {"fd_nw": 16},
                 {"fd_min16": 16}, {"fd_nw": 16, "fd_min16": 16}, {"gemv_chain": 1}, {"gemv_nt": 0}, {"gemv_u": 4},
@@ -64,7 +64,8 @@ def test_fp32_decode_variants(knobs, golden, tune):
 
 @pytest.mark.parametrize("knobs", DECODE_KNOBS + [{"prefill_attn": 0}, {"prompt_gemm": 0}, {"prompt_skinny": 0},
                                                   {"prompt_skinny_blocks": 1}, {"prompt_skinny_blocks": 4096},
-                                                  {"prompt_swiglu": 0}, {"prompt_fin": 0}], ids=_ids)
+                                                  {"prompt_swiglu": 0}, {"prompt_fin": 0}, {"prompt_qkv_slab": 1}],
+                         ids=_ids)
 def test_wide_bf16_variants_vs_reference(knobs, golden, tune):
     from fishmi.llm import DualARModel
 
@@ -99,19 +100,21 @@ def test_codec_variants_vs_reference(prec, knobs, golden, tune):
         assert rms(wave - ref) <= 1.5 * ref_bf16_err + 1e-4, (rms(wave - ref), ref_bf16_err)
 
 
-@pytest.mark.parametrize("blocks", [1, 4096])
-def test_prompt_swiglu_epilogue_bit_identical(golden, tune, blocks):
-    """The skinny prompt GEMM's w1 || w3 with the interleaved SwiGLU fused -- stored by the kernel
-    itself when unsliced (blocks 1), in the split-K epilogue (CE_SWIGLU8) when sliced (blocks 4096)
-    -- gives the teacher-forced logits of the stored output + swiglu_i8_kernel bit for bit (the same
-    roundings on the same sums)."""
+@pytest.mark.parametrize("knob,blocks", [("prompt_swiglu", 1), ("prompt_swiglu", 4096), ("prompt_qkv_slab", 256),
+                                          ("prompt_qkv_slab", 4096)])
+def test_prompt_fusions_bit_identical(golden, tune, knob, blocks):
+    """The skinny prompt GEMM's fused epilogues give the teacher-forced logits of the unfused launches
+    bit for bit (the same roundings on the same sums): w1 || w3 with the interleaved SwiGLU -- stored
+    by the kernel itself when unsliced (blocks 1), in the split-K epilogue (CE_SWIGLU8) when sliced --
+    against the stored output + swiglu_i8_kernel; the QKV slices summed + biased + rounded by
+    qk_rope_cache_kernel against the split-K epilogue's stored projection."""
     from fishmi.llm import DualARModel
 
     g = golden("llm_wide_bf16.npz")
     cfg = _cfg("llm_wide")
     out = []
     for v in (1, 0):
-        tune({"prompt_swiglu": v, "prompt_skinny_blocks": blocks})
+        tune({knob: v, "prompt_skinny_blocks": blocks})
         m = DualARModel.synthetic(cfg, int(g["synth_seed"]), int(g["log2_half"]), 0, "bf16", 1)
         T = g["prompt"].shape[1]
         out.append(m.teacher_decode(g["prompt"], g["seq"][:, T:]))
