@@ -2579,6 +2579,8 @@ int fm_tune(const char* key, int value) {
             t.prefill_attn = value != 0;
         } else if (k == "prompt_qkv_slab") {
             t.prompt_qkv_slab = value != 0;
+        } else if (k == "prompt_unroll") {
+            t.prompt_unroll = value != 0;
         } else if (k == "prompt_fin") {
             t.prompt_fin = value != 0;
         } else if (k == "prompt_swiglu") {

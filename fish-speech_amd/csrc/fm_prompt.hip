@@ -135,6 +135,101 @@ __global__ __launch_bounds__(256) void prompt_skinny_kernel(PromptSkinnyArgs a) 
     }
 }
 
+// Fully unrolled form (fm_tune prompt_unroll): NCH chunks as straight-line code, so no load is pending
+// across a loop back edge (where the compiler drains vmcnt), with each chunk's activation rows
+// loaded two chunks ahead.  Same MFMA chains in the same k order: bit-identical partials.
+template <int NCH>
+__global__ __launch_bounds__(256) void prompt_skinny_unrolled_kernel(PromptSkinnyArgs a) {
+    using F = Frag<bf16_t>;
+    __shared__ __attribute__((aligned(16))) bf16_t xs[2][64][SK_XS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int ntile = (a.N + 15) / 16;
+    const int tile = blockIdx.x * 4 + wave;
+    const bool live = tile < ntile;
+    const int nks = a.K / 32;
+    const int kps = nks / (int)gridDim.y;  // host: (kps + 3) / 4 == NCH
+    const int s0 = (int)blockIdx.y * kps;
+    const bf16_t* wb = a.w + ((size_t)(live ? tile : ntile - 1) * nks + s0) * 512;
+    u32x4_t xr[2][4];
+    auto xload = [&](int set, int c) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int piece = (int)threadIdx.x + 256 * i;
+            const int row = piece >> 4, kq = piece & 15;
+            const int kl = 128 * c + 8 * kq;
+            const bool ok = row < a.R && kl < 32 * kps;
+            xr[set][i] = F::load_masked(a.x + (size_t)(ok ? row : 0) * a.ldx + 32 * s0 + (ok ? kl : 0), ok);
+        }
+    };
+    auto xstore = [&](int set, int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int piece = (int)threadIdx.x + 256 * i;
+            *reinterpret_cast<u32x4_t*>(&xs[buf][piece >> 4][8 * (piece & 15)]) = xr[set][i];
+        }
+    };
+    u32x4_t w[2][4];
+    auto wload = [&](int set, int c) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int st = 4 * c + q;
+            w[set][q] = F::load_w<true>(wb + (size_t)(st < kps ? st : 0) * 512, lane);
+        }
+    };
+    f32x4_t acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    xload(0, 0);
+    if (NCH > 1) xload(1, 1);
+    wload(0, 0);
+    if (NCH > 1) wload(1, 1);
+    xstore(0, 0);
+    lds_barrier();
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        if (c + 2 < NCH) xload(c & 1, c + 2);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (4 * c + q < kps) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const F::f xb = F::load(&xs[c & 1][16 * t + (lane & 15)][32 * q + 8 * (lane >> 4)]);
+                    acc[t] = F::mma(w[c & 1][q], xb, acc[t]);
+                }
+            }
+        }
+        if (c + 2 < NCH) wload(c & 1, c + 2);
+        if (c + 1 < NCH) xstore((c + 1) & 1, (c + 1) & 1);
+        lds_barrier();
+    }
+    if (a.act) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int r = 16 * t + (lane & 15);
+            float o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float g = rnd<bf16_t>(acc[t][j]);
+                const float u = rnd<bf16_t>(__shfl_xor(acc[t][j], 32));
+                o[j] = rnd<bf16_t>(rnd<bf16_t>(g / (1.0f + expf(-g))) * u);
+            }
+            if (live && lane < 32 && r < a.R) {
+                bf16_t* d = a.act + (size_t)r * a.lda + 8 * tile + 4 * (lane >> 4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) st(d, j, o[j]);
+            }
+        }
+        return;
+    }
+    if (!live) return;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int r = 16 * t + (lane & 15);
+        if (r < a.R)
+            *reinterpret_cast<f32x4_t*>(a.slab + ((size_t)blockIdx.y * a.R + r) * a.N + 16 * tile + 4 * (lane >> 4)) = acc[t];
+    }
+}
+
 }  // namespace
 
 int prompt_skinny_ks(int N, int K, int target) {
@@ -152,5 +247,16 @@ void launch_prompt_skinny(hipStream_t s, const PromptSkinnyArgs& a, int ks) {
     FMCHECK(a.R > 0 && a.R <= 64 && a.K % 32 == 0 && ks >= 1 && (a.K / 32) % ks == 0 && a.N % 16 == 0 && a.slab &&
                 a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0,
             "prompt skinny GEMM: R <= 64, K a multiple of 32 split evenly, N a multiple of 16, 16-B rows, slab set");
-    prompt_skinny_kernel<<<dim3((a.N + 63) / 64, ks), 256, 0, s>>>(a);
+    const dim3 grid((a.N + 63) / 64, ks);
+    const int nch = (a.K / 32 / ks + 3) / 4;
+    if (fm_tuning().prompt_unroll) {
+        switch (nch) {
+            case 4: prompt_skinny_unrolled_kernel<4><<<grid, 256, 0, s>>>(a); return;
+            case 5: prompt_skinny_unrolled_kernel<5><<<grid, 256, 0, s>>>(a); return;
+            case 10: prompt_skinny_unrolled_kernel<10><<<grid, 256, 0, s>>>(a); return;
+            case 20: prompt_skinny_unrolled_kernel<20><<<grid, 256, 0, s>>>(a); return;
+            default: break;
+        }
+    }
+    prompt_skinny_kernel<<<grid, 256, 0, s>>>(a);
 }
