@@ -270,7 +270,7 @@ struct FmTuning {
     int prompt_gemm = 1;     // 1: prompt-chunk linears (R > 32) on the codec's LDS-tiled GEMM kernels
     int prompt_skinny = 1;      // prompt linears at 32 < R <= 64 rows (bf16) on prompt_skinny_kernel ...
     int prompt_skinny_blocks = 256;  // ... with K sliced until its 64-row blocks number >= this
-    int prompt_unroll = 0;      // skinny prompt GEMM: the fully unrolled form (5 / 10 / 20-chunk slices)
+    int prompt_unroll = 1;      // skinny prompt GEMM: the fully unrolled form (5 / 10 / 20-chunk slices)
     int prompt_qkv_slab = 1;    // skinny QKV: slabs summed by qk_rope_cache_kernel (no epilogue launch)
     int prompt_fin = 1;         // skinny wo / w2: slabs finished by finalize_norm with the next RMSNorm
     int prompt_swiglu = 1;      // skinny w1 || w3: the SwiGLU in its split-K epilogue (no separate launch)

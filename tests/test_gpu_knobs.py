@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 DEFAULTS = {"attn3": 1, "attn_fd": 1, "fd_min": 32, "fd_nw": 8, "fd_min16": 256, "gemv_chain": 0, "gemv_nt": 1, "gemv_u": 8, "gemv_wpb": 4,
             "ksb_balance": 0, "ksb_blocks": 512, "attn_cap": 32, "prefill_attn": 1, "prompt_gemm": 1,
             "conv2": 1, "conv_splitk": 1, "kv_prefetch": 1, "fin_ksb": 0, "gemv_dummy": 2, "rowgemv": 27, "rowgemv_q4": 31, "sampler_kth": 1, "row_qkv_rp": 8,
-            "fattn_wo": 1, "fw_cheap": 0, "fw_delay": 0, "prompt_skinny": 1, "prompt_skinny_blocks": 256, "prompt_swiglu": 1, "prompt_fin": 1, "prompt_qkv_slab": 1, "prompt_unroll": 0}
+            "fattn_wo": 1, "fw_cheap": 0, "fw_delay": 0, "prompt_skinny": 1, "prompt_skinny_blocks": 256, "prompt_swiglu": 1, "prompt_fin": 1, "prompt_qkv_slab": 1, "prompt_unroll": 1}
 
 DECODE_KNOBS = [{"attn3": 0}, {"attn3": 0, "attn_fd": 0}, {"fd_nw": 4}, {"fd_nw": 4, "fd_min": 16}, {"fd_nw": 16},
                 {"fd_min16": 16}, {"fd_nw": 16, "fd_min16": 16}, {"gemv_chain": 1}, {"gemv_nt": 0}, {"gemv_u": 4},
